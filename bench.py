@@ -1,0 +1,179 @@
+#!/usr/bin/env python3
+"""bench.py -- trace(exp(A)) evaluations/s on the BASELINE.json metric config.
+
+Workload (BASELINE.json metric / configs[3]): synthetic Chung-Lu scale-free
+graph, n = 1,000,000, nnz = 10,000,000 (power law 2.5, unit weights, seeded),
+one evaluation = plain Hutchinson over N = 1024 Rademacher probes, each with
+m = 30 Lanczos steps + host Gauss quadrature.  A "step" is one evaluation.
+Multi-GPU (torchrun, one process per GPU): the 1024 probes of each
+evaluation are sharded over the ranks and one RCCL all-reduce of
+(sum q, sum q^2) gives the trace -- strong scaling of a fixed evaluation.
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="sf1m", choices=["sf1m", "er100k"])
+    ap.add_argument("--nprobes", type=int, default=None)
+    ap.add_argument("--m", type=int, default=30)
+    ap.add_argument("--block", type=int, default=0, help="probes per SpMM sweep (0 = auto)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="CPU-baseline time budget (rank 0, N=1 only); 0 disables")
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def make_graph(config):
+    from krylov_robustness_amd import graphs
+    if config == "sf1m":
+        return graphs.chung_lu(1_000_000, 10_000_000, gamma=2.5, seed=0), 1024, \
+            "chung_lu n=1M nnz=10M gamma=2.5 (BASELINE configs[3])"
+    return graphs.erdos_renyi(100_000, 500_000, seed=0), 128, \
+        "erdos_renyi n=100k nnz~1M (BASELINE configs[1])"
+
+
+def cpu_baseline(A, m, budget_s, nprobes_eval):
+    """Time the C restatement (oracle/slq_ref.c, OpenMP over probes) on a
+    bounded sample of the same workload; extrapolate to evals/s."""
+    from oracle import slq_ref
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    slq_ref.load()
+    done = 0
+    t0 = time.perf_counter()
+    batch = threads
+    while True:
+        slq_ref.slq_trace(A, batch, m, seed=12345, probe_offset=done, nthreads=threads)
+        done += batch
+        el = time.perf_counter() - t0
+        if el >= budget_s or done >= nprobes_eval:
+            break
+    probes_per_s = done / el
+    return {"value": probes_per_s / nprobes_eval, "unit": "evals/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{done} of the {nprobes_eval} probes of one evaluation (m={m}) in "
+                      f"{el:.1f} s with {threads} OpenMP threads, extrapolated"}
+
+
+def main():
+    args = parse()
+    import torch  # noqa: F401  -- load torch's HIP runtime first (one runtime per process)
+    import torch.distributed as dist
+
+    from krylov_robustness_amd import dist as kdist
+    rank, world, local_rank = kdist.env_rank()
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    import krylov_robustness_amd as kra
+    A, N, wl = make_graph(args.config)
+    if args.nprobes:
+        N = args.nprobes
+    m = args.m
+    n, nnz = A.shape[0], A.nnz
+    ctx = kra.Context(local_rank)
+    D = kra.DeviceMatrix(A, ctx)
+    off, cnt = kdist.probe_shard(N, rank, world)
+    P = args.block or _auto_block(n, cnt)
+
+    def step(seed):
+        s1, s2, _ = kra.slq_quadforms(D, cnt, m, seed=seed, probe_offset=off, block=P, ctx=ctx)
+        s1, s2 = kdist.allreduce_sums([s1, s2], device=dev)
+        return s1 / N, s2
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for w in range(args.warmup):
+        step(1000 + w)
+    if not args.no_profile:
+        ctx.profile_reset()
+        ctx.profile(True)
+    barrier()
+    t0 = time.perf_counter()
+    tr = None
+    for s in range(args.steps):
+        tr, _ = step(s)
+    barrier()
+    el = time.perf_counter() - t0
+    if not args.no_profile:
+        ctx.profile(False)
+    el_max = kdist.allreduce_max(el, device=dev)
+
+    ms_per_step = el_max * 1e3 / args.steps
+    value = args.steps / el_max
+    # algorithmic bytes: one K1 launch = one Lanczos step of one
+    # P-probe sweep: CSR (12 nnz + 4(n+1)) + gather source, v_{j-1}, y (8nP each)
+    k1_bytes = 12 * nnz + 4 * (n + 1) + 24 * n * P
+    sweeps = math.ceil(cnt / P)
+    b_eval_rank = m * (sweeps * (12 * nnz + 4 * (n + 1)) + 24 * n * cnt)
+    roof = None
+    extra = {}
+    if not args.no_profile:
+        l1, ms1 = ctx.profile_read(0)
+        l2, ms2 = ctx.profile_read(1)
+        if l1:
+            k1_ms = ms1 / l1
+            achieved = k1_bytes / (k1_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": f"k_spmm_gram<P={P}>", "avg_launch_us": round(k1_ms * 1e3, 2),
+                    "algorithmic_bytes_per_launch": k1_bytes}
+            extra["k2_update_avg_us"] = round(ms2 / max(l2, 1) * 1e3, 2)
+    eval_gbs = b_eval_rank / (ms_per_step * 1e-3) / 1e9
+    extra["eval_roofline"] = {"B_eval_bytes_per_rank": b_eval_rank, "achieved_GBs_per_rank":
+                              round(eval_gbs, 1), "frac": round(eval_gbs / HBM_PEAK_GBS, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(A, m, args.cpu_seconds, N)
+
+    if rank == 0:
+        out = {
+            "metric": "trace(exp(A)) evals/sec (+ achieved HBM GB/s), n=1M nnz=10M",
+            "value": round(value, 4), "unit": "evals/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": wl, "n": n, "nnz": nnz, "probes_per_eval": N, "lanczos_m": m,
+                       "probes_per_sweep": P, "fun": "exp", "parallelism": f"probes sharded x{world}"},
+            "roofline": roof, "cpu_baseline": cpu, "trace_estimate": tr, **extra,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _auto_block(n, cnt):
+    P = 128
+    while P > 8 and n * 8.0 * P > 96.0 * 1024 * 1024:
+        P //= 2
+    while P > 1 and P // 2 >= cnt:
+        P //= 2
+    return P
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,99 @@
+/* krylov_trace.h -- C ABI of libkrylov_hip.so, the MI355X trace(f(A)) evaluator.
+ *
+ * This is the drop-in boundary of SURVEY.md §8b.  The reference is MATLAB;
+ * its callers (Tests/ scripts, greedy_krylov.m, fmincon closures) resolve the
+ * functions below by name, so a MEX file of the same name placed in
+ * functions/ shadows the .m (krylov_robustness_amd/mex/).
+ * The MEX shim forwards mxArray data to these plain-pointer entry points; the
+ * ctypes binding in krylov_robustness_amd/_lib.py binds the same symbols for
+ * tests.
+ *
+ * Conventions
+ *   - All functions return an int status (KT_OK == 0).  On failure a
+ *     thread-local message is available from kt_last_error(); messages
+ *     reproduce the reference's error strings where one exists.
+ *   - Matrices: MATLAB sparse CSC (mwIndex = int64 jc[n+1], ir[nnz], 0-based;
+ *     double pr[nnz]).  A is symmetric on every hot path, so CSC == CSR.
+ *   - Dense arrays are column-major fp64 (MATLAB layout); Omega is 1-based.
+ *   - Inputs are borrowed (read-only); outputs are caller-allocated.
+ *   - A context is externally synchronised: no concurrent calls on one
+ *     context (MATLAB calls a MEX on its single interpreter thread).
+ *   - fun codes mirror fun_update.m:43-59's handle identities.
+ */
+#ifndef KRYLOV_TRACE_H
+#define KRYLOV_TRACE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KT_ABI_VERSION 1
+
+enum kt_status {
+    KT_OK = 0,
+    KT_ERR_ARG = 1,           /* bad argument (sizes, null pointers)            */
+    KT_ERR_HIP = 2,           /* HIP runtime failure                            */
+    KT_ERR_NOT_HERMITIAN = 3, /* fun_and_grad_krylov_exp.m:21-23                */
+    KT_ERR_NOT_SQUARE = 4,    /* lanczos_krylov.m:36-38                         */
+    KT_ERR_ALLOC = 5,         /* device allocation failed                       */
+    KT_ERR_UNSUPPORTED = 6    /* size / option outside what the build supports  */
+};
+
+enum kt_fun { /* fun_update.m:43-59 */
+    KT_FUN_EXP = 0,
+    KT_FUN_SINH = 1,
+    KT_FUN_COSH = 2,
+    KT_FUN_SIN = 3,
+    KT_FUN_COS = 4,
+    KT_FUN_LOG = 5,
+    KT_FUN_SQRT = 6
+};
+
+typedef struct kt_context_s* kt_context_t;
+typedef struct kt_matrix_s* kt_matrix_t;
+
+/* ---- runtime ------------------------------------------------------------ */
+int kt_abi_version(void);
+const char* kt_last_error(void);
+int kt_device_count(int* count);
+int kt_context_create(int device, kt_context_t* ctx);
+int kt_context_destroy(kt_context_t ctx);
+
+/* Device-resident A (SURVEY.md §7 hard part (e): fmincon and greedy call the
+ * shim repeatedly with the same A, so the CSR stays in HBM across calls).
+ * Replaces the sparse `A` argument of trace_exp.m:1, mc_trace.m:32-34,
+ * trace_fun_update.m:1, fun_update.m:1, fun_and_grad_krylov_exp.m:1,
+ * fun_and_grad_krylov_fun.m:1.  `check_symmetric` != 0 rejects a
+ * non-symmetric A with KT_ERR_NOT_HERMITIAN. */
+int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr,
+                         const int64_t* rowind, const double* vals, int check_symmetric,
+                         kt_matrix_t* A);
+int kt_matrix_destroy(kt_matrix_t A);
+int kt_matrix_info(kt_matrix_t A, int64_t* n, int64_t* nnz);
+
+/* ---- hot path: stochastic Lanczos quadrature ------------------------------
+ * For probes p in [probe_offset, probe_offset + nprobes) (Rademacher,
+ * splitmix64 stream keyed by the GLOBAL probe index, so any sharding over
+ * GPUs gives the same probes), run m steps of the single-vector
+ * lanczos_krylov recurrence (lanczos_krylov.m:73-115, bs = 1) and form
+ * q_p = ||z||^2 e1' f(T_m) e1.  Returns sum_p q_p and sum_p q_p^2 (for the
+ * all-reduce of partial traces and the variance), and optionally q[nprobes].
+ * `block` = probes per SpMM sweep (power of two 1..128; 0 = auto).
+ * This is the Afun of mc_trace.m:45-49 evaluated as quadratic forms and the
+ * plain-Hutchinson estimator of BASELINE.json configs 2-4. */
+int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_t probe_offset,
+                 int64_t nprobes, int block, double* sum_q, double* sum_q2, double* q);
+
+/* Per-kernel timing (HIP events recorded on the library's stream around each
+ * launch of the named kernel while enabled).  kernel: 0 = spmm_gram (K1),
+ * 1 = update_norm (K2).  Returns launch count and summed milliseconds. */
+int kt_profile_enable(kt_context_t ctx, int enable);
+int kt_profile_read(kt_context_t ctx, int kernel, int64_t* launches, double* total_ms);
+int kt_profile_reset(kt_context_t ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KRYLOV_TRACE_H */

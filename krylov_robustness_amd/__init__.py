@@ -1,0 +1,17 @@
+"""krylov_robustness_amd -- MI355X-native trace(f(A)) evaluator.
+
+Drop-in for the Krylov trace / matrix-function hot path of
+COMPiLELab/krylov_robustness (trace_exp, mc_trace, trace_fun_update,
+fun_update, fun_and_grad_krylov_{exp,fun}).  The compute lives
+in libkrylov_hip.so (HIP kernels for gfx950 + C++ host driver, C ABI in
+include/krylov_trace.h); this package is the Python mirror of the reference
+interface used by tests and bench.py.
+"""
+from ._lib import KrylovError, KrylovLibraryError, FUN_CODES, LIB_PATH
+from .core import (Context, DeviceMatrix, default_context, device_count, slq_quadforms,
+                   slq_trace)
+
+__all__ = [
+    "KrylovError", "KrylovLibraryError", "FUN_CODES", "LIB_PATH", "Context", "DeviceMatrix",
+    "default_context", "device_count", "slq_quadforms", "slq_trace",
+]

@@ -1,0 +1,85 @@
+"""ctypes binding of libkrylov_hip.so (the C ABI declared in include/krylov_trace.h).
+
+There is no fallback: if the in-tree shared library is missing or cannot be
+loaded, every entry point raises ``KrylovLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkrylov_hip.so")
+
+
+class KrylovLibraryError(RuntimeError):
+    pass
+
+
+class KrylovError(RuntimeError):
+    """A non-zero kt_status; .code holds the status, str() the library message."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+# kt_status
+KT_OK, KT_ERR_ARG, KT_ERR_HIP, KT_ERR_NOT_HERMITIAN, KT_ERR_NOT_SQUARE, KT_ERR_ALLOC, KT_ERR_UNSUPPORTED = range(7)
+# kt_fun (fun_update.m:43-59)
+FUN_CODES = {"exp": 0, "sinh": 1, "cosh": 2, "sin": 3, "cos": 4, "log": 5, "sqrt": 6}
+
+_ctx_p = C.c_void_p
+_mat_p = C.c_void_p
+_i64p = C.POINTER(C.c_int64)
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+
+# (name, restype, argtypes) -- every symbol include/krylov_trace.h declares
+SIGNATURES = [
+    ("kt_abi_version", C.c_int, []),
+    ("kt_last_error", C.c_char_p, []),
+    ("kt_device_count", C.c_int, [_ip]),
+    ("kt_context_create", C.c_int, [C.c_int, C.POINTER(_ctx_p)]),
+    ("kt_context_destroy", C.c_int, [_ctx_p]),
+    ("kt_matrix_create_csc", C.c_int, [_ctx_p, C.c_int64, _i64p, _i64p, _dp, C.c_int, C.POINTER(_mat_p)]),
+    ("kt_matrix_destroy", C.c_int, [_mat_p]),
+    ("kt_matrix_info", C.c_int, [_mat_p, _i64p, _i64p]),
+    ("kt_slq_trace", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int,
+                               _dp, _dp, _dp]),
+    ("kt_profile_enable", C.c_int, [_ctx_p, C.c_int]),
+    ("kt_profile_read", C.c_int, [_ctx_p, C.c_int, _i64p, _dp]),
+    ("kt_profile_reset", C.c_int, [_ctx_p]),
+]
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load (once) and return the CDLL; raise KrylovLibraryError if unavailable."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise KrylovLibraryError(
+                f"{LIB_PATH} not found: build it with `make -C krylov_robustness_amd/csrc` "
+                "or __graft_entry__.build() (no CPU fallback exists)")
+        try:
+            lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        except OSError as e:  # pragma: no cover - depends on the box
+            raise KrylovLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(status: int):
+    if status != KT_OK:
+        msg = load().kt_last_error()
+        raise KrylovError(status, msg.decode() if msg else f"kt status {status}")

@@ -1,0 +1,155 @@
+"""Host-side mirror of the reference's entry points over the C ABI.
+
+Names, argument meaning and error behaviour follow the MATLAB functions in
+/root/reference/functions (cited per function); device work happens in
+libkrylov_hip.so.  Nothing here computes on the CPU except argument marshalling.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+
+
+class Context:
+    """One HIP device + stream (kt_context_t)."""
+
+    def __init__(self, device: Optional[int] = None):
+        lib = _lib.load()
+        if device is None:
+            device = int(os.environ.get("KT_DEVICE", "0"))
+        h = C.c_void_p()
+        _lib.check(lib.kt_context_create(int(device), C.byref(h)))
+        self._h = h
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.load().kt_context_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- profiling (HIP events on the library stream) ----
+    def profile(self, enable: bool = True):
+        _lib.check(_lib.load().kt_profile_enable(self._h, 1 if enable else 0))
+
+    def profile_reset(self):
+        _lib.check(_lib.load().kt_profile_reset(self._h))
+
+    def profile_read(self, kernel: int):
+        n = C.c_int64()
+        ms = C.c_double()
+        _lib.check(_lib.load().kt_profile_read(self._h, kernel, C.byref(n), C.byref(ms)))
+        return int(n.value), float(ms.value)
+
+
+_default_ctx: Optional[Context] = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context()
+    return _default_ctx
+
+
+def device_count() -> int:
+    c = C.c_int()
+    _lib.check(_lib.load().kt_device_count(C.byref(c)))
+    return int(c.value)
+
+
+def _as_csc(A):
+    import scipy.sparse as sp
+    if not sp.issparse(A):
+        A = sp.csc_matrix(np.asarray(A, dtype=np.float64))
+    A = A.tocsc()
+    A.sort_indices()
+    if A.shape[0] != A.shape[1]:
+        raise _lib.KrylovError(_lib.KT_ERR_NOT_SQUARE, "The matrix A should be square")
+    return A
+
+
+class DeviceMatrix:
+    """Device-resident CSR/CSC of a symmetric A (kt_matrix_t)."""
+
+    def __init__(self, A, ctx: Optional[Context] = None, check_symmetric: bool = False):
+        self.ctx = ctx or default_context()
+        A = _as_csc(A)
+        self.n = A.shape[0]
+        self.nnz = A.nnz
+        colptr = np.ascontiguousarray(A.indptr, dtype=np.int64)
+        rowind = np.ascontiguousarray(A.indices, dtype=np.int64)
+        vals = np.ascontiguousarray(A.data, dtype=np.float64)
+        h = C.c_void_p()
+        lib = _lib.load()
+        _lib.check(lib.kt_matrix_create_csc(
+            self.ctx.handle, self.n,
+            colptr.ctypes.data_as(C.POINTER(C.c_int64)),
+            rowind.ctypes.data_as(C.POINTER(C.c_int64)),
+            vals.ctypes.data_as(C.POINTER(C.c_double)),
+            1 if check_symmetric else 0, C.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.load().kt_matrix_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _dev(A, ctx=None) -> DeviceMatrix:
+    return A if isinstance(A, DeviceMatrix) else DeviceMatrix(A, ctx)
+
+
+def _fun_code(fun) -> int:
+    if callable(fun):
+        fun = getattr(fun, "__name__", str(fun))
+    try:
+        return _lib.FUN_CODES[str(fun)]
+    except KeyError:
+        raise _lib.KrylovError(_lib.KT_ERR_UNSUPPORTED, f"unsupported function handle {fun!r}")
+
+
+def slq_quadforms(A, nprobes: int, m: int, seed: int = 0, fun="exp", probe_offset: int = 0,
+                  block: int = 0, ctx: Optional[Context] = None):
+    """Per-probe z_p' f(A) z_p for the global probe range [probe_offset,
+    probe_offset + nprobes) by m-step Lanczos quadrature (SURVEY.md §8a a10,
+    lanczos_krylov.m:73-115 with bs = 1).  Returns (sum, sum_sq, q[nprobes])."""
+    D = _dev(A, ctx)
+    q = np.zeros(max(int(nprobes), 1), dtype=np.float64)
+    s1 = C.c_double()
+    s2 = C.c_double()
+    _lib.check(_lib.load().kt_slq_trace(
+        D.handle, _fun_code(fun), int(m), int(seed) & 0xFFFFFFFFFFFFFFFF, int(probe_offset),
+        int(nprobes), int(block), C.byref(s1), C.byref(s2), q.ctypes.data_as(C.POINTER(C.c_double))))
+    return float(s1.value), float(s2.value), q[:nprobes]
+
+
+def slq_trace(A, nprobes: int, m: int, seed: int = 0, fun="exp", block: int = 0,
+              ctx: Optional[Context] = None):
+    """Plain-Hutchinson trace(f(A)) estimate with Lanczos quadrature."""
+    s1, _, q = slq_quadforms(A, nprobes, m, seed, fun, 0, block, ctx)
+    return s1 / max(nprobes, 1), q

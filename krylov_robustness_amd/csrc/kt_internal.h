@@ -1,0 +1,119 @@
+// kt_internal.h -- shared internals of libkrylov_hip.so (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/krylov_trace.h"
+
+namespace kt {
+
+void set_error(const std::string& msg);
+
+struct Status {  // exception carrying a kt_status; caught at the ABI edge
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] inline void fail(int code, const std::string& msg) { throw Status{code, msg}; }
+
+#define KT_HIP(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            ::kt::fail(KT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
+    } while (0)
+
+// Growable device buffer (bytes).
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t want) {
+        if (want <= bytes) return;
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&ptr, want);
+        if (e != hipSuccess) fail(KT_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+        bytes = want;
+    }
+    template <class T> T* as() { return static_cast<T*>(ptr); }
+    void release() {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+};
+
+struct PinnedBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    void ensure(size_t want) {
+        if (want <= bytes) return;
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+        hipError_t e = hipHostMalloc(&ptr, want, hipHostMallocDefault);
+        if (e != hipSuccess) fail(KT_ERR_ALLOC, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        bytes = want;
+    }
+    template <class T> T* as() { return static_cast<T*>(ptr); }
+    void release() {
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+};
+
+struct ProfSlot {
+    std::vector<hipEvent_t> ev;  // start/stop pairs
+    size_t used = 0;             // events used (2 per launch)
+    int64_t launches = 0;
+    double total_ms = 0.0;
+};
+
+enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_NSLOTS = 2 };
+
+struct Workspace {
+    DevBuf X0, X1, Y, partial, coef, scales, trec;
+    PinnedBuf host_trec;
+};
+
+}  // namespace kt
+
+struct kt_context_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int num_cu = 256;
+    bool profile = false;
+    kt::ProfSlot prof[kt::PROF_NSLOTS];
+    kt::Workspace ws;
+};
+
+struct kt_matrix_s {
+    kt_context_s* ctx = nullptr;
+    int64_t n = 0, nnz = 0;
+    int* d_rowptr = nullptr;
+    int* d_col = nullptr;
+    double* d_val = nullptr;
+    // host copy (CSR, int64 pointers) for host-side algorithms and checks
+    std::vector<int64_t> h_rowptr;
+    std::vector<int32_t> h_col;
+    std::vector<double> h_val;
+};
+
+namespace kt {
+
+// profiling helpers (no-ops unless ctx->profile)
+void prof_begin(kt_context_s* ctx, int slot);
+void prof_end(kt_context_s* ctx, int slot);
+void prof_collect(kt_context_s* ctx);  // after stream sync: fold events into totals
+
+// dense host helpers (kt_dense.cpp)
+double fscalar(int fun, double x);
+// Gauss quadrature e1' f(T) e1 for symmetric tridiagonal T (m x m).
+double tridiag_quadrature(int m, const double* alpha, const double* off, int fun);
+
+}  // namespace kt

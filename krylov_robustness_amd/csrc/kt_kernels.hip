@@ -1,0 +1,439 @@
+// kt_kernels.hip -- CDNA4 (gfx950) kernels for the block-Krylov trace path.
+//
+// Data layout in HBM:
+//   A      : CSR, int32 row_ptr[n+1], int32 col[nnz], fp64 val[nnz]
+//            (the reference's CSC of a symmetric matrix, read as CSR)
+//   blocks : n x P fp64, ROW-MAJOR ("probe-contiguous"): row i of a probe
+//            block is P consecutive doubles, so every nonzero a_ic gathers
+//            one contiguous 8P-byte row X[c, 0:P] -- a fully coalesced
+//            16 B/lane load by P/2 lanes.
+//
+// Wave mapping: a wave64 is split into GPW = 64/LPR "row groups" of
+// LPR = P/2 lanes; each group owns one matrix row, each lane two probe
+// columns.  P = 128 -> one row per wave (1 KiB gathers); P = 16 -> 8 rows
+// per wave (128 B gathers = one cache line).
+//
+// Hot recurrence (lanczos_krylov.m:73-115 with
+// bs = 1 per probe column).  Stored vectors are UNNORMALISED, u_j, with a
+// per-probe scale s_j so that v_j = s_j u_j; this lets the normalisation
+// 1/beta be applied inside the next SpMM for free:
+//   K1 spmm_gram : y = s_j A u_j, Gram partials of [v_{j-1}, v_j, y]
+//   coef         : CGS2 coefficients from the Gram (= two classical passes,
+//                  lanczos_krylov.m:109-115, computed algebraically)
+//   K2 update    : u_{j+1} = y - c0 v_{j-1} - c1 v_j, partial ||u_{j+1}||^2
+//   norm         : beta = ||u_{j+1}||, s_{j+1} = 1/beta, lucky if < 1e-8
+// All reductions are deterministic: per-block partial slabs reduced in a
+// fixed order (no float atomics).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+namespace kt {
+
+__device__ __forceinline__ uint64_t sm64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+template <int P> struct Geo {
+    static constexpr int VEC = (P >= 2) ? 2 : 1;     // doubles per lane
+    static constexpr int LPR = P / VEC;              // lanes per row group
+    static constexpr int GPW = 64 / LPR;             // row groups per wave
+};
+
+template <int VEC> struct VecT;
+template <> struct VecT<1> {
+    using T = double;
+    __device__ static __forceinline__ T load(const double* p) { return *p; }
+    __device__ static __forceinline__ void store(double* p, const T& v) { *p = v; }
+    __device__ static __forceinline__ double get(const T& v, int) { return v; }
+};
+template <> struct VecT<2> {
+    using T = double2;
+    __device__ static __forceinline__ T load(const double* p) {
+        return *reinterpret_cast<const double2*>(p);
+    }
+    __device__ static __forceinline__ void store(double* p, const T& v) {
+        *reinterpret_cast<double2*>(p) = v;
+    }
+    __device__ static __forceinline__ double get(const T& v, int e) { return e ? v.y : v.x; }
+};
+
+// ---------------------------------------------------------------------------
+// Rademacher probe block: X[i, p] = +-1 from splitmix64(key(seed, base+p) + i)
+// (same stream as oracle/krylov_oracle.py:rademacher and oracle/slq_ref.c).
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ __launch_bounds__(256) void k_rademacher(int n, uint64_t seed, int64_t probe_base,
+                                                    double* __restrict__ X) {
+    __shared__ uint64_t keys[P];
+    for (int p = threadIdx.x; p < P; p += blockDim.x)
+        keys[p] = sm64(sm64(seed) + (uint64_t)(probe_base + p));
+    __syncthreads();
+    const int64_t total = (int64_t)n * P;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = t / P;
+        const int p = (int)(t % P);
+        X[t] = (sm64(keys[p] + (uint64_t)i) >> 63) ? -1.0 : 1.0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K1: y = s_cur * (A u_cur); Gram partials per probe column:
+//   [0] v0.y  [1] v1.y  [2] v0.v0  [3] v0.v1  [4] v1.v1
+// where v0 = s_prev * u_prev (absent on the first step), v1 = s_cur * u_cur.
+// partial layout: [gridDim.x][5][P].
+// ---------------------------------------------------------------------------
+constexpr int NG = 5;
+
+template <int P, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_spmm_gram(
+    const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
+    int n, const double* __restrict__ ucur, const double* __restrict__ uprev,
+    const double* __restrict__ scale_cur, const double* __restrict__ scale_prev, int first,
+    double* __restrict__ y, double* __restrict__ partial) {
+    using G = Geo<P>;
+    using V = VecT<G::VEC>;
+    constexpr int WAVES = BLOCK / 64;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int sub = lane % G::LPR;
+    const int grp = lane / G::LPR;
+    const int p0 = sub * G::VEC;
+
+    double sc[G::VEC], sp[G::VEC];
+#pragma unroll
+    for (int e = 0; e < G::VEC; ++e) {
+        sc[e] = scale_cur[p0 + e];
+        sp[e] = first ? 0.0 : scale_prev[p0 + e];
+    }
+    double acc[NG][G::VEC];
+#pragma unroll
+    for (int q = 0; q < NG; ++q)
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) acc[q][e] = 0.0;
+
+    const int groups_total = gridDim.x * WAVES * G::GPW;
+    for (int row = (blockIdx.x * WAVES + wave) * G::GPW + grp; row < n; row += groups_total) {
+        const int beg = row_ptr[row];
+        const int end = row_ptr[row + 1];
+        double s[G::VEC];
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+        int k = beg;
+        // 4 independent gathers in flight per lane
+        for (; k + 4 <= end; k += 4) {
+            const int c0 = col[k], c1 = col[k + 1], c2 = col[k + 2], c3 = col[k + 3];
+            const double a0 = val[k], a1 = val[k + 1], a2 = val[k + 2], a3 = val[k + 3];
+            const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
+            const typename V::T x1 = V::load(ucur + (int64_t)c1 * P + p0);
+            const typename V::T x2 = V::load(ucur + (int64_t)c2 * P + p0);
+            const typename V::T x3 = V::load(ucur + (int64_t)c3 * P + p0);
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) {
+                s[e] = fma(a0, V::get(x0, e), s[e]);
+                s[e] = fma(a1, V::get(x1, e), s[e]);
+                s[e] = fma(a2, V::get(x2, e), s[e]);
+                s[e] = fma(a3, V::get(x3, e), s[e]);
+            }
+        }
+        for (; k < end; ++k) {
+            const int c0 = col[k];
+            const double a0 = val[k];
+            const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) s[e] = fma(a0, V::get(x0, e), s[e]);
+        }
+        const int64_t off = (int64_t)row * P + p0;
+        const typename V::T ui = V::load(ucur + off);
+        typename V::T yo;
+        double* yp = reinterpret_cast<double*>(&yo);
+        if (first) {
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) {
+                const double yv = s[e] * sc[e];
+                const double v1 = V::get(ui, e) * sc[e];
+                yp[e] = yv;
+                acc[1][e] = fma(v1, yv, acc[1][e]);
+                acc[4][e] = fma(v1, v1, acc[4][e]);
+            }
+        } else {
+            const typename V::T pi = V::load(uprev + off);
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) {
+                const double yv = s[e] * sc[e];
+                const double v1 = V::get(ui, e) * sc[e];
+                const double v0 = V::get(pi, e) * sp[e];
+                yp[e] = yv;
+                acc[0][e] = fma(v0, yv, acc[0][e]);
+                acc[1][e] = fma(v1, yv, acc[1][e]);
+                acc[2][e] = fma(v0, v0, acc[2][e]);
+                acc[3][e] = fma(v0, v1, acc[3][e]);
+                acc[4][e] = fma(v1, v1, acc[4][e]);
+            }
+        }
+        V::store(y + off, yo);
+    }
+
+    // reduce over the row groups of this wave (lanes sharing `sub`)
+#pragma unroll
+    for (int o = G::LPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int q = 0; q < NG; ++q)
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) acc[q][e] += __shfl_xor(acc[q][e], o, 64);
+
+    __shared__ double red[WAVES][NG][P];
+    if (grp == 0) {
+#pragma unroll
+        for (int q = 0; q < NG; ++q)
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) red[wave][q][p0 + e] = acc[q][e];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < NG * P; t += BLOCK) {
+        const int q = t / P, p = t % P;
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) v += red[w][q][p];
+        partial[(int64_t)blockIdx.x * NG * P + t] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Reduce [nblk][NQ][P] partial slabs in block order (deterministic).
+// One workgroup; thread t owns slot t % (NQ*P) and a chunk of blocks, then an
+// LDS combine over chunks in chunk order.
+// ---------------------------------------------------------------------------
+template <int NQ, int P>
+__device__ __forceinline__ void reduce_slabs(const double* __restrict__ partial, int nblk,
+                                             double* __restrict__ out /* LDS [NQ*P] */) {
+    constexpr int SLOTS = NQ * P;
+    constexpr int CH = (1024 / SLOTS) > 0 ? (1024 / SLOTS) : 1;  // chunks
+    __shared__ double tmp[CH][SLOTS];
+    const int t = threadIdx.x;
+    for (int s = t; s < CH * SLOTS; s += blockDim.x) {
+        const int slot = s % SLOTS, ch = s / SLOTS;
+        const int b0 = (int)((int64_t)nblk * ch / CH), b1 = (int)((int64_t)nblk * (ch + 1) / CH);
+        double v = 0.0;
+        for (int b = b0; b < b1; ++b) v += partial[(int64_t)b * SLOTS + slot];
+        tmp[ch][slot] = v;
+    }
+    __syncthreads();
+    for (int s = t; s < SLOTS; s += blockDim.x) {
+        double v = 0.0;
+        for (int ch = 0; ch < CH; ++ch) v += tmp[ch][s];
+        out[s] = v;
+    }
+    __syncthreads();
+}
+
+// coef: CGS2 against the window [v0, v1] from the Gram matrix.
+//   pass 1: h = [v0.y, v1.y];  pass 2: h' = V'(y - V h) = h - (V'V) h
+//   c = h + h'  ->  H(j-1,j) = c0, H(j,j) = c1   (lanczos_krylov.m:88,109-115)
+// Writes coef[2][P] and the T-record rows alpha (=c1) and up (=c0).
+template <int P>
+__global__ __launch_bounds__(1024) void k_coef_cgs2(const double* __restrict__ partial, int nblk,
+                                                     int first, double* __restrict__ coef,
+                                                     double* __restrict__ t_alpha,
+                                                     double* __restrict__ t_up) {
+    __shared__ double g[NG * P];
+    reduce_slabs<NG, P>(partial, nblk, g);
+    for (int p = threadIdx.x; p < P; p += blockDim.x) {
+        double g0 = g[0 * P + p], g1 = g[1 * P + p];
+        double G00 = g[2 * P + p], G01 = g[3 * P + p], G11 = g[4 * P + p];
+        if (first) { g0 = 0.0; G00 = 0.0; G01 = 0.0; }
+        const double h0p = g0 - (G00 * g0 + G01 * g1);
+        const double h1p = g1 - (G01 * g0 + G11 * g1);
+        const double c0 = g0 + h0p, c1 = g1 + h1p;
+        coef[p] = c0;
+        coef[P + p] = c1;
+        t_alpha[p] = c1;
+        t_up[p] = c0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2: u_next = y - c0 * s_prev * u_prev - c1 * s_cur * u_cur  (in place over
+// u_prev), partial ||u_next||^2 per probe -> partial [gridDim.x][P].
+// Pure streaming: rows are contiguous, so lanes cover 16 B each.
+// ---------------------------------------------------------------------------
+template <int P, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_update_norm(
+    int n, const double* __restrict__ y, double* __restrict__ uprev,
+    const double* __restrict__ ucur, const double* __restrict__ scale_cur,
+    const double* __restrict__ scale_prev, const double* __restrict__ coef, int first,
+    double* __restrict__ partial) {
+    using G = Geo<P>;
+    using V = VecT<G::VEC>;
+    constexpr int WAVES = BLOCK / 64;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int sub = lane % G::LPR;
+    const int grp = lane / G::LPR;
+    const int p0 = sub * G::VEC;
+    double a0[G::VEC], a1[G::VEC], acc[G::VEC];
+#pragma unroll
+    for (int e = 0; e < G::VEC; ++e) {
+        a0[e] = first ? 0.0 : coef[p0 + e] * scale_prev[p0 + e];
+        a1[e] = coef[P + p0 + e] * scale_cur[p0 + e];
+        acc[e] = 0.0;
+    }
+    const int groups_total = gridDim.x * WAVES * G::GPW;
+    for (int row = (blockIdx.x * WAVES + wave) * G::GPW + grp; row < n; row += groups_total) {
+        const int64_t off = (int64_t)row * P + p0;
+        const typename V::T yv = V::load(y + off);
+        const typename V::T cv = V::load(ucur + off);
+        typename V::T o;
+        double* op = reinterpret_cast<double*>(&o);
+        if (first) {
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) {
+                const double u = fma(-a1[e], V::get(cv, e), V::get(yv, e));
+                op[e] = u;
+                acc[e] = fma(u, u, acc[e]);
+            }
+        } else {
+            const typename V::T pv = V::load(uprev + off);
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) {
+                double u = fma(-a0[e], V::get(pv, e), V::get(yv, e));
+                u = fma(-a1[e], V::get(cv, e), u);
+                op[e] = u;
+                acc[e] = fma(u, u, acc[e]);
+            }
+        }
+        V::store(uprev + off, o);
+    }
+#pragma unroll
+    for (int o = G::LPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
+    __shared__ double red[WAVES][P];
+    if (grp == 0) {
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) red[wave][p0 + e] = acc[e];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < P; t += BLOCK) {
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) v += red[w][t];
+        partial[(int64_t)blockIdx.x * P + t] = v;
+    }
+}
+
+// norm: beta = ||u_next||; s_next = 1/beta (0 after a lucky breakdown,
+// lanczos_krylov.m:91-93 with lucky_tol = 1e-8); T-record row `low` = beta.
+template <int P>
+__global__ __launch_bounds__(1024) void k_norm(const double* __restrict__ partial, int nblk,
+                                                double* __restrict__ scale_next,
+                                                double* __restrict__ t_low) {
+    __shared__ double g[P];
+    reduce_slabs<1, P>(partial, nblk, g);
+    for (int p = threadIdx.x; p < P; p += blockDim.x) {
+        const double beta = sqrt(g[p]);
+        t_low[p] = beta;
+        scale_next[p] = (beta < 1e-8) ? 0.0 : 1.0 / beta;
+    }
+}
+
+// initial scale of a Rademacher block: ||z|| = sqrt(n)
+__global__ void k_fill(double* __restrict__ x, int count, double v) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < count) x[t] = v;
+}
+
+}  // namespace kt
+
+// ---------------------------------------------------------------------------
+// host-side launchers (C++ linkage, used by kt_runtime.cpp)
+// ---------------------------------------------------------------------------
+#include "kt_launch.h"
+
+namespace kt {
+
+static constexpr int kBlock = 512;
+
+int spmm_grid(int n, int P, int max_blocks) {
+    const int gpw = (P >= 2) ? 64 / (P / 2) : 64;
+    const int rows_per_block = (kBlock / 64) * gpw;
+    int g = (n + rows_per_block - 1) / rows_per_block;
+    if (g > max_blocks) g = max_blocks;
+    if (g < 1) g = 1;
+    return g;
+}
+
+template <class F>
+static hipError_t dispatch_p(int P, F&& f) {
+    switch (P) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    case 16: f(std::integral_constant<int, 16>{}); break;
+    case 32: f(std::integral_constant<int, 32>{}); break;
+    case 64: f(std::integral_constant<int, 64>{}); break;
+    case 128: f(std::integral_constant<int, 128>{}); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_rademacher(int P, int n, uint64_t seed, int64_t probe_base, double* X,
+                             hipStream_t st) {
+    int64_t total = (int64_t)n * P;
+    int grid = (int)((total + 255) / 256);
+    if (grid > 8192) grid = 8192;
+    if (grid < 1) grid = 1;
+    return dispatch_p(P, [&](auto c) {
+        k_rademacher<decltype(c)::value><<<grid, 256, 0, st>>>(n, seed, probe_base, X);
+    });
+}
+
+hipError_t launch_spmm_gram(int P, int grid, const int* rp, const int* ci, const double* va,
+                            int n, const double* ucur, const double* uprev, const double* sc,
+                            const double* sp, int first, double* y, double* partial,
+                            hipStream_t st) {
+    return dispatch_p(P, [&](auto c) {
+        k_spmm_gram<decltype(c)::value, kBlock><<<grid, kBlock, 0, st>>>(
+            rp, ci, va, n, ucur, uprev, sc, sp, first, y, partial);
+    });
+}
+
+hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, double* coef,
+                            double* t_alpha, double* t_up, hipStream_t st) {
+    return dispatch_p(P, [&](auto c) {
+        k_coef_cgs2<decltype(c)::value><<<1, 1024, 0, st>>>(partial, nblk, first, coef, t_alpha,
+                                                            t_up);
+    });
+}
+
+hipError_t launch_update_norm(int P, int grid, int n, const double* y, double* uprev,
+                              const double* ucur, const double* sc, const double* sp,
+                              const double* coef, int first, double* partial, hipStream_t st) {
+    return dispatch_p(P, [&](auto c) {
+        k_update_norm<decltype(c)::value, kBlock><<<grid, kBlock, 0, st>>>(
+            n, y, uprev, ucur, sc, sp, coef, first, partial);
+    });
+}
+
+hipError_t launch_norm(int P, const double* partial, int nblk, double* scale_next, double* t_low,
+                       hipStream_t st) {
+    return dispatch_p(P, [&](auto c) {
+        k_norm<decltype(c)::value><<<1, 1024, 0, st>>>(partial, nblk, scale_next, t_low);
+    });
+}
+
+hipError_t launch_fill(double* x, int count, double v, hipStream_t st) {
+    int grid = (count + 255) / 256;
+    if (grid < 1) grid = 1;
+    k_fill<<<grid, 256, 0, st>>>(x, count, v);
+    return hipGetLastError();
+}
+
+}  // namespace kt

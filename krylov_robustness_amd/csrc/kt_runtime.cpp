@@ -1,0 +1,245 @@
+// kt_runtime.cpp -- contexts, device-resident matrices, errors, profiling.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <thread>
+
+#include "kt_internal.h"
+
+namespace kt {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+void prof_begin(kt_context_s* ctx, int slot) {
+    if (!ctx->profile) return;
+    ProfSlot& s = ctx->prof[slot];
+    if (s.used + 2 > s.ev.size()) {
+        for (int i = 0; i < 512; ++i) {
+            hipEvent_t e;
+            KT_HIP(hipEventCreate(&e));
+            s.ev.push_back(e);
+        }
+    }
+    KT_HIP(hipEventRecord(s.ev[s.used], ctx->stream));
+}
+
+void prof_end(kt_context_s* ctx, int slot) {
+    if (!ctx->profile) return;
+    ProfSlot& s = ctx->prof[slot];
+    KT_HIP(hipEventRecord(s.ev[s.used + 1], ctx->stream));
+    s.used += 2;
+}
+
+void prof_collect(kt_context_s* ctx) {
+    for (int k = 0; k < PROF_NSLOTS; ++k) {
+        ProfSlot& s = ctx->prof[k];
+        for (size_t i = 0; i + 1 < s.used; i += 2) {
+            float ms = 0.f;
+            KT_HIP(hipEventElapsedTime(&ms, s.ev[i], s.ev[i + 1]));
+            s.total_ms += ms;
+            s.launches += 1;
+        }
+        s.used = 0;
+    }
+}
+
+}  // namespace kt
+
+using namespace kt;
+
+#define KT_GUARD_BEGIN try {
+#define KT_GUARD_END                                   \
+    }                                                  \
+    catch (const kt::Status& s) {                      \
+        kt::set_error(s.msg);                          \
+        return s.code;                                 \
+    }                                                  \
+    catch (const std::bad_alloc&) {                    \
+        kt::set_error("host allocation failed");       \
+        return KT_ERR_ALLOC;                           \
+    }                                                  \
+    catch (const std::exception& e) {                  \
+        kt::set_error(e.what());                       \
+        return KT_ERR_ARG;                             \
+    }                                                  \
+    return KT_OK;
+
+extern "C" {
+
+int kt_abi_version(void) { return KT_ABI_VERSION; }
+
+const char* kt_last_error(void) { return kt::g_last_error.c_str(); }
+
+int kt_device_count(int* count) {
+    KT_GUARD_BEGIN
+    if (!count) fail(KT_ERR_ARG, "count is NULL");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    *count = c;
+    KT_GUARD_END
+}
+
+int kt_context_create(int device, kt_context_t* out) {
+    KT_GUARD_BEGIN
+    if (!out) fail(KT_ERR_ARG, "ctx out is NULL");
+    int c = 0;
+    KT_HIP(hipGetDeviceCount(&c));
+    if (device < 0 || device >= c) fail(KT_ERR_ARG, "device index out of range");
+    KT_HIP(hipSetDevice(device));
+    auto* ctx = new kt_context_s();
+    ctx->device = device;
+    hipDeviceProp_t prop;
+    KT_HIP(hipGetDeviceProperties(&prop, device));
+    ctx->num_cu = prop.multiProcessorCount;
+    KT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    *out = ctx;
+    KT_GUARD_END
+}
+
+int kt_context_destroy(kt_context_t ctx) {
+    KT_GUARD_BEGIN
+    if (!ctx) return KT_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& s : ctx->prof)
+        for (auto e : s.ev) (void)hipEventDestroy(e);
+    Workspace& w = ctx->ws;
+    w.X0.release(); w.X1.release(); w.Y.release(); w.partial.release();
+    w.coef.release(); w.scales.release(); w.trec.release(); w.host_trec.release();
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    KT_GUARD_END
+}
+
+int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr, const int64_t* rowind,
+                         const double* vals, int check_symmetric, kt_matrix_t* out) {
+    KT_GUARD_BEGIN
+    if (!ctx || !out || !colptr || (!rowind && n > 0)) fail(KT_ERR_ARG, "NULL argument");
+    if (n < 0) fail(KT_ERR_ARG, "negative dimension");
+    const int64_t nnz = colptr[n];
+    if (n >= (int64_t(1) << 31) || nnz >= (int64_t(1) << 31))
+        fail(KT_ERR_UNSUPPORTED, "n and nnz must be < 2^31 (int32 device indices)");
+    for (int64_t j = 0; j < n; ++j)
+        if (colptr[j + 1] < colptr[j]) fail(KT_ERR_ARG, "column pointers not monotone");
+    for (int64_t k = 0; k < nnz; ++k)
+        if (rowind[k] < 0 || rowind[k] >= n) fail(KT_ERR_ARG, "row index out of range");
+
+    auto* A = new kt_matrix_s();
+    A->ctx = ctx;
+    A->n = n;
+    A->nnz = nnz;
+    // CSC of a symmetric matrix == CSR; keep the column-sorted host copy.
+    A->h_rowptr.assign(colptr, colptr + n + 1);
+    A->h_col.resize(nnz);
+    A->h_val.resize(nnz);
+    for (int64_t k = 0; k < nnz; ++k) {
+        A->h_col[k] = (int32_t)rowind[k];
+        A->h_val[k] = vals ? vals[k] : 1.0;
+    }
+    // sort indices within each row (MATLAB keeps them sorted; be defensive)
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t b = A->h_rowptr[i], e = A->h_rowptr[i + 1];
+        bool sorted = true;
+        for (int64_t k = b + 1; k < e; ++k)
+            if (A->h_col[k] < A->h_col[k - 1]) { sorted = false; break; }
+        if (!sorted) {
+            std::vector<std::pair<int32_t, double>> t(e - b);
+            for (int64_t k = b; k < e; ++k) t[k - b] = {A->h_col[k], A->h_val[k]};
+            std::sort(t.begin(), t.end(),
+                      [](const auto& x, const auto& y) { return x.first < y.first; });
+            for (int64_t k = b; k < e; ++k) { A->h_col[k] = t[k - b].first; A->h_val[k] = t[k - b].second; }
+        }
+    }
+    if (check_symmetric) {
+        // transpose by counting sort and compare entry by entry
+        std::vector<int64_t> tp(n + 1, 0);
+        for (int64_t k = 0; k < nnz; ++k) tp[A->h_col[k] + 1]++;
+        for (int64_t i = 0; i < n; ++i) tp[i + 1] += tp[i];
+        std::vector<int32_t> tc(nnz);
+        std::vector<double> tv(nnz);
+        std::vector<int64_t> pos(tp.begin(), tp.end() - 1);
+        for (int64_t i = 0; i < n; ++i)
+            for (int64_t k = A->h_rowptr[i]; k < A->h_rowptr[i + 1]; ++k) {
+                int64_t d = pos[A->h_col[k]]++;
+                tc[d] = (int32_t)i;
+                tv[d] = A->h_val[k];
+            }
+        bool sym = std::equal(tp.begin(), tp.end(), A->h_rowptr.begin()) &&
+                   std::equal(tc.begin(), tc.end(), A->h_col.begin()) &&
+                   std::equal(tv.begin(), tv.end(), A->h_val.begin());
+        if (!sym) {
+            delete A;
+            fail(KT_ERR_NOT_HERMITIAN, "FUN_AND_GRAD_KRYLOV:: matrix A is not Hermitian");
+        }
+    }
+    try {
+        KT_HIP(hipSetDevice(ctx->device));
+        std::vector<int32_t> rp32(n + 1);
+        for (int64_t i = 0; i <= n; ++i) rp32[i] = (int32_t)A->h_rowptr[i];
+        KT_HIP(hipMalloc(&A->d_rowptr, sizeof(int) * (n + 1)));
+        KT_HIP(hipMalloc(&A->d_col, sizeof(int) * std::max<int64_t>(nnz, 1)));
+        KT_HIP(hipMalloc(&A->d_val, sizeof(double) * std::max<int64_t>(nnz, 1)));
+        KT_HIP(hipMemcpy(A->d_rowptr, rp32.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice));
+        if (nnz) {
+            KT_HIP(hipMemcpy(A->d_col, A->h_col.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
+            KT_HIP(hipMemcpy(A->d_val, A->h_val.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+        }
+    } catch (...) {
+        if (A->d_rowptr) (void)hipFree(A->d_rowptr);
+        if (A->d_col) (void)hipFree(A->d_col);
+        if (A->d_val) (void)hipFree(A->d_val);
+        delete A;
+        throw;
+    }
+    *out = A;
+    KT_GUARD_END
+}
+
+int kt_matrix_destroy(kt_matrix_t A) {
+    KT_GUARD_BEGIN
+    if (!A) return KT_OK;
+    (void)hipSetDevice(A->ctx->device);
+    (void)hipStreamSynchronize(A->ctx->stream);
+    if (A->d_rowptr) (void)hipFree(A->d_rowptr);
+    if (A->d_col) (void)hipFree(A->d_col);
+    if (A->d_val) (void)hipFree(A->d_val);
+    delete A;
+    KT_GUARD_END
+}
+
+int kt_matrix_info(kt_matrix_t A, int64_t* n, int64_t* nnz) {
+    KT_GUARD_BEGIN
+    if (!A) fail(KT_ERR_ARG, "A is NULL");
+    if (n) *n = A->n;
+    if (nnz) *nnz = A->nnz;
+    KT_GUARD_END
+}
+
+int kt_profile_enable(kt_context_t ctx, int enable) {
+    KT_GUARD_BEGIN
+    if (!ctx) fail(KT_ERR_ARG, "ctx is NULL");
+    ctx->profile = enable != 0;
+    KT_GUARD_END
+}
+
+int kt_profile_read(kt_context_t ctx, int kernel, int64_t* launches, double* total_ms) {
+    KT_GUARD_BEGIN
+    if (!ctx || kernel < 0 || kernel >= PROF_NSLOTS) fail(KT_ERR_ARG, "bad profile query");
+    if (launches) *launches = ctx->prof[kernel].launches;
+    if (total_ms) *total_ms = ctx->prof[kernel].total_ms;
+    KT_GUARD_END
+}
+
+int kt_profile_reset(kt_context_t ctx) {
+    KT_GUARD_BEGIN
+    if (!ctx) fail(KT_ERR_ARG, "ctx is NULL");
+    for (auto& s : ctx->prof) { s.launches = 0; s.total_ms = 0.0; s.used = 0; }
+    KT_GUARD_END
+}
+
+}  // extern "C"

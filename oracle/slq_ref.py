@@ -1,0 +1,56 @@
+"""ctypes wrapper of oracle/libslq_ref.so (TEST INFRASTRUCTURE ONLY)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PATH = os.path.join(_HERE, "libslq_ref.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_PATH):
+            build()
+        lib = C.CDLL(_PATH)
+        lib.slq_ref_trace.restype = C.c_double
+        lib.slq_ref_trace.argtypes = [C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                      C.c_int64, C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_void_p]
+        lib.slq_ref_rademacher.restype = C.c_double
+        lib.slq_ref_rademacher.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
+        lib.slq_ref_tridiag_quad.restype = C.c_double
+        lib.slq_ref_tridiag_quad.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        lib.slq_ref_max_threads.restype = C.c_int
+        _lib = lib
+    return _lib
+
+
+FUN = {"exp": 0, "sinh": 1, "cosh": 2, "sin": 3, "cos": 4, "log": 5, "sqrt": 6}
+
+
+def slq_trace(A, nprobes, m, seed=0, fun="exp", probe_offset=0, nthreads=0):
+    """Returns (mean of quadforms, quadforms) for probes [offset, offset+nprobes)."""
+    import scipy.sparse as sp
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    rp = np.ascontiguousarray(A.indptr, dtype=np.int64)
+    ci = np.ascontiguousarray(A.indices, dtype=np.int32)
+    va = np.ascontiguousarray(A.data, dtype=np.float64)
+    q = np.zeros(max(nprobes, 1))
+    mean = load().slq_ref_trace(A.shape[0], rp.ctypes.data, ci.ctypes.data, va.ctypes.data,
+                                int(nprobes), int(probe_offset), int(m), int(seed), FUN[fun],
+                                int(nthreads), q.ctypes.data)
+    return float(mean), q[:nprobes]
+
+
+def max_threads():
+    return int(load().slq_ref_max_threads())

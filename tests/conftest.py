@@ -1,0 +1,42 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs via gpurun)")
+
+
+def load_graph(name):
+    z = np.load(os.path.join(GOLDEN, "graphs.npz"))
+    n = int(z[name + "__n"][0])
+    return sp.csr_matrix((z[name + "__data"], z[name + "__indices"], z[name + "__indptr"]),
+                         shape=(n, n))
+
+
+def golden_values():
+    with open(os.path.join(GOLDEN, "values.json")) as f:
+        return json.load(f)
+
+
+GRAPHS = ["oregon_A0", "anaheim", "rome", "denmark", "austria", "india"]
+
+
+@pytest.fixture(scope="session")
+def values():
+    return golden_values()
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    import krylov_robustness_amd as kra
+    return kra.Context(0)

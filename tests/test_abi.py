@@ -1,0 +1,62 @@
+"""CPU: the C-ABI library builds, loads and exports every symbol that
+include/krylov_trace.h declares; argument errors come back as statuses."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "krylov_trace.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(kt_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_declares_entry_points():
+    fns = declared_functions()
+    assert "kt_slq_trace" in fns and "kt_matrix_create_csc" in fns
+    assert len(fns) >= 10
+
+
+def test_library_exports_every_declared_symbol():
+    from krylov_robustness_amd import _lib
+    lib = _lib.load()
+    bound = {name for name, _, _ in _lib.SIGNATURES}
+    for name in declared_functions():
+        assert hasattr(lib, name), f"{name} not exported by {_lib.LIB_PATH}"
+        assert name in bound, f"{name} has no ctypes signature in _lib.SIGNATURES"
+
+
+def test_abi_version_and_null_arguments():
+    from krylov_robustness_amd import _lib
+    lib = _lib.load()
+    assert lib.kt_abi_version() == 1
+    h = C.c_void_p()
+    # NULL context -> KT_ERR_ARG with a message, never a crash
+    st = lib.kt_matrix_create_csc(None, 0, None, None, None, 0, C.byref(h))
+    assert st == _lib.KT_ERR_ARG
+    assert b"NULL" in lib.kt_last_error()
+    assert lib.kt_slq_trace(None, 0, 10, 0, 0, 1, 0, None, None, None) == _lib.KT_ERR_ARG
+    assert lib.kt_context_destroy(None) == _lib.KT_OK
+
+
+def test_no_gpu_fails_loudly():
+    """With no device the library reports an error instead of computing on CPU."""
+    import krylov_robustness_amd as kra
+    if kra.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(kra.KrylovError):
+        kra.Context(0)
+
+
+def test_missing_library_raises(monkeypatch, tmp_path):
+    from krylov_robustness_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(_lib.KrylovLibraryError):
+        _lib.load()

@@ -1,0 +1,98 @@
+"""GPU parity for the hot path: kt_slq_trace (HIP) vs the C oracle on the same
+probes.  Tolerance: per-probe quadratic forms agree to rtol 1e-8 (fp64; the
+device forms the CGS2 coefficients from a Gram matrix and sums in a different
+order than the oracle's explicit two-pass CGS2, lanczos_krylov.m:109-115)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import GRAPHS, load_graph
+from oracle import slq_ref
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-8
+
+
+@pytest.fixture(scope="module")
+def kra():
+    import krylov_robustness_amd as kra
+    return kra
+
+
+@pytest.mark.parametrize("name", GRAPHS)
+@pytest.mark.parametrize("fun", ["exp", "sinh"])
+def test_slq_matches_oracle_golden(kra, gpu_ctx, values, name, fun):
+    A = load_graph(name)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    gold = np.array(values[name][f"oracle_slq_{fun}_seed7_m20"])
+    s1, s2, q = kra.slq_quadforms(D, 16, 20, seed=7, fun=fun, ctx=gpu_ctx)
+    np.testing.assert_allclose(q, gold, rtol=RTOL)
+    assert s1 == pytest.approx(gold.sum(), rel=RTOL)
+    assert s2 == pytest.approx((gold ** 2).sum(), rel=RTOL)
+
+
+@pytest.mark.parametrize("block", [1, 2, 4, 8, 16, 32, 64, 128])
+def test_slq_every_block_width(kra, gpu_ctx, block):
+    """Every probe-block width P (kernel template) gives the oracle's answer,
+    with a ragged probe count (21 is not a multiple of P)."""
+    A = load_graph("rome")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    _, q_ref = slq_ref.slq_trace(A, 21, 25, seed=3, fun="exp", probe_offset=5)
+    _, _, q = kra.slq_quadforms(D, 21, 25, seed=3, fun="exp", probe_offset=5, block=block,
+                                ctx=gpu_ctx)
+    np.testing.assert_allclose(q, q_ref, rtol=RTOL)
+
+
+def test_slq_probe_sharding_invariant(kra, gpu_ctx):
+    """Probes are keyed by global index: shards sum to the unsharded result."""
+    A = load_graph("india")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    s_all, _, q_all = kra.slq_quadforms(D, 40, 20, seed=9, ctx=gpu_ctx)
+    parts = [kra.slq_quadforms(D, 10, 20, seed=9, probe_offset=o, ctx=gpu_ctx) for o in (0, 10, 20, 30)]
+    np.testing.assert_allclose(np.concatenate([p[2] for p in parts]), q_all, rtol=1e-12)
+    assert sum(p[0] for p in parts) == pytest.approx(s_all, rel=1e-12)
+
+
+def test_slq_deterministic(kra, gpu_ctx):
+    A = load_graph("oregon_A0")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    a = kra.slq_quadforms(D, 33, 30, seed=1, ctx=gpu_ctx)[2]
+    b = kra.slq_quadforms(D, 33, 30, seed=1, ctx=gpu_ctx)[2]
+    assert np.array_equal(a, b)
+
+
+def test_slq_lucky_breakdown_small_graph(kra, gpu_ctx):
+    """m larger than the Krylov dimension: lucky breakdown (lanczos_krylov.m:91-93)
+    stops the recurrence; the quadrature is then exact."""
+    A = sp.csr_matrix(np.array([[0, 1, 0, 0], [1, 0, 1, 0], [0, 1, 0, 1], [0, 0, 1, 0]], float))
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    _, _, q = kra.slq_quadforms(D, 8, 20, seed=2, ctx=gpu_ctx)
+    _, q_ref = slq_ref.slq_trace(A, 8, 20, seed=2)
+    np.testing.assert_allclose(q, q_ref, rtol=1e-10)
+    from oracle import krylov_oracle as ko
+    from scipy.linalg import expm
+    Z = ko.rademacher(4, np.arange(8), 2)
+    exact = np.einsum("ip,ij,jp->p", Z, expm(A.toarray()), Z)
+    np.testing.assert_allclose(q, exact, rtol=1e-10)
+
+
+def test_slq_empty_and_zero_matrix(kra, gpu_ctx):
+    A = sp.csr_matrix((5, 5))
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    s1, s2, q = kra.slq_quadforms(D, 3, 10, seed=0, ctx=gpu_ctx)
+    np.testing.assert_allclose(q, 5.0)            # z' exp(0) z = ||z||^2 = n
+    s1, s2, q = kra.slq_quadforms(D, 0, 10, seed=0, ctx=gpu_ctx)
+    assert s1 == 0 and q.size == 0
+
+
+def test_slq_full_size_config2_properties(kra, gpu_ctx):
+    """BASELINE.json config 2 size (ER n=100k, nnz~1M, m=30): size-independent
+    checks -- first probes match the C oracle, and block widths agree."""
+    from krylov_robustness_amd import graphs
+    A = graphs.erdos_renyi(100_000, 500_000, seed=0)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    _, _, q128 = kra.slq_quadforms(D, 128, 30, seed=0, block=128, ctx=gpu_ctx)
+    _, _, q16 = kra.slq_quadforms(D, 128, 30, seed=0, block=16, ctx=gpu_ctx)
+    np.testing.assert_allclose(q16, q128, rtol=1e-10)
+    _, q_ref = slq_ref.slq_trace(A, 4, 30, seed=0)
+    np.testing.assert_allclose(q128[:4], q_ref, rtol=RTOL)
