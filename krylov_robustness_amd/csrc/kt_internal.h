@@ -98,6 +98,10 @@ struct kt_matrix_s {
     int* d_rowptr = nullptr;
     int* d_col = nullptr;
     double* d_val = nullptr;
+    // rows with degree > long_thresh, hubs first (one wave per such row in K1)
+    int* d_long_rows = nullptr;
+    int n_long = 0;
+    int long_thresh = 64;
     // host copy (CSR, int64 pointers) for host-side algorithms and checks
     std::vector<int64_t> h_rowptr;
     std::vector<int32_t> h_col;

@@ -90,14 +90,94 @@ __global__ __launch_bounds__(256) void k_rademacher(int n, uint64_t seed, int64_
 // ---------------------------------------------------------------------------
 constexpr int NG = 5;
 
+// Row epilogue shared by both modes: y_i = s_cur * sum, Gram accumulation.
+template <int P>
+__device__ __forceinline__ void row_epilogue(int row, int p0, const double* s, const double* sc,
+                                             const double* sp, int first,
+                                             const double* __restrict__ ucur,
+                                             const double* __restrict__ uprev,
+                                             double* __restrict__ y, double (*acc)[Geo<P>::VEC]) {
+    using G = Geo<P>;
+    using V = VecT<G::VEC>;
+    const int64_t off = (int64_t)row * P + p0;
+    const typename V::T ui = V::load(ucur + off);
+    typename V::T yo;
+    double* yp = reinterpret_cast<double*>(&yo);
+    if (first) {
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) {
+            const double yv = s[e] * sc[e];
+            const double v1 = V::get(ui, e) * sc[e];
+            yp[e] = yv;
+            acc[1][e] = fma(v1, yv, acc[1][e]);
+            acc[4][e] = fma(v1, v1, acc[4][e]);
+        }
+    } else {
+        const typename V::T pi = V::load(uprev + off);
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) {
+            const double yv = s[e] * sc[e];
+            const double v1 = V::get(ui, e) * sc[e];
+            const double v0 = V::get(pi, e) * sp[e];
+            yp[e] = yv;
+            acc[0][e] = fma(v0, yv, acc[0][e]);
+            acc[1][e] = fma(v1, yv, acc[1][e]);
+            acc[2][e] = fma(v0, v0, acc[2][e]);
+            acc[3][e] = fma(v0, v1, acc[3][e]);
+            acc[4][e] = fma(v1, v1, acc[4][e]);
+        }
+    }
+    V::store(y + off, yo);
+}
+
+// Gather-accumulate nonzeros k = k0, k0 + stride, ... < end of one row.
+template <int P>
+__device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
+                                           const int* __restrict__ col,
+                                           const double* __restrict__ val,
+                                           const double* __restrict__ ucur, double* s) {
+    using G = Geo<P>;
+    using V = VecT<G::VEC>;
+    int k = k0;
+    for (; k + 3 * stride < end; k += 4 * stride) {  // 4 independent gathers in flight
+        const int c0 = col[k], c1 = col[k + stride], c2 = col[k + 2 * stride],
+                  c3 = col[k + 3 * stride];
+        const double a0 = val[k], a1 = val[k + stride], a2 = val[k + 2 * stride],
+                     a3 = val[k + 3 * stride];
+        const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
+        const typename V::T x1 = V::load(ucur + (int64_t)c1 * P + p0);
+        const typename V::T x2 = V::load(ucur + (int64_t)c2 * P + p0);
+        const typename V::T x3 = V::load(ucur + (int64_t)c3 * P + p0);
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) {
+            s[e] = fma(a0, V::get(x0, e), s[e]);
+            s[e] = fma(a1, V::get(x1, e), s[e]);
+            s[e] = fma(a2, V::get(x2, e), s[e]);
+            s[e] = fma(a3, V::get(x3, e), s[e]);
+        }
+    }
+    for (; k < end; k += stride) {
+        const int c0 = col[k];
+        const double a0 = val[k];
+        const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) s[e] = fma(a0, V::get(x0, e), s[e]);
+    }
+}
+
+// Two modes in one launch.  Blocks [0, long_blocks): one WAVE per long row
+// (degree > long_thresh, listed hubs-first in long_rows), its row groups
+// striding over the row's nonzeros, combined by wave shuffles -- so a hub
+// row costs deg/(4*GPW) dependent gather rounds instead of deg/4.  Other
+// blocks: one row GROUP per short row, rows in natural order (coalesced y).
 template <int P, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_spmm_gram(
     const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
     int n, const double* __restrict__ ucur, const double* __restrict__ uprev,
     const double* __restrict__ scale_cur, const double* __restrict__ scale_prev, int first,
-    double* __restrict__ y, double* __restrict__ partial) {
+    double* __restrict__ y, double* __restrict__ partial, const int* __restrict__ long_rows,
+    int n_long, int long_thresh, int long_blocks) {
     using G = Geo<P>;
-    using V = VecT<G::VEC>;
     constexpr int WAVES = BLOCK / 64;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -117,66 +197,34 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_gram(
 #pragma unroll
         for (int e = 0; e < G::VEC; ++e) acc[q][e] = 0.0;
 
-    const int groups_total = gridDim.x * WAVES * G::GPW;
-    for (int row = (blockIdx.x * WAVES + wave) * G::GPW + grp; row < n; row += groups_total) {
-        const int beg = row_ptr[row];
-        const int end = row_ptr[row + 1];
-        double s[G::VEC];
+    if ((int)blockIdx.x < long_blocks) {
+        for (int li = blockIdx.x * WAVES + wave; li < n_long; li += long_blocks * WAVES) {
+            const int row = long_rows[li];
+            const int beg = row_ptr[row];
+            const int end = row_ptr[row + 1];
+            double s[G::VEC];
 #pragma unroll
-        for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-        int k = beg;
-        // 4 independent gathers in flight per lane
-        for (; k + 4 <= end; k += 4) {
-            const int c0 = col[k], c1 = col[k + 1], c2 = col[k + 2], c3 = col[k + 3];
-            const double a0 = val[k], a1 = val[k + 1], a2 = val[k + 2], a3 = val[k + 3];
-            const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
-            const typename V::T x1 = V::load(ucur + (int64_t)c1 * P + p0);
-            const typename V::T x2 = V::load(ucur + (int64_t)c2 * P + p0);
-            const typename V::T x3 = V::load(ucur + (int64_t)c3 * P + p0);
+            for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+            row_gather<P>(beg + grp, end, G::GPW, p0, col, val, ucur, s);
 #pragma unroll
-            for (int e = 0; e < G::VEC; ++e) {
-                s[e] = fma(a0, V::get(x0, e), s[e]);
-                s[e] = fma(a1, V::get(x1, e), s[e]);
-                s[e] = fma(a2, V::get(x2, e), s[e]);
-                s[e] = fma(a3, V::get(x3, e), s[e]);
-            }
+            for (int o = G::LPR; o < 64; o <<= 1)
+#pragma unroll
+                for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
+            if (grp == 0) row_epilogue<P>(row, p0, s, sc, sp, first, ucur, uprev, y, acc);
         }
-        for (; k < end; ++k) {
-            const int c0 = col[k];
-            const double a0 = val[k];
-            const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
+    } else {
+        const int sb = blockIdx.x - long_blocks;
+        const int groups_total = (gridDim.x - long_blocks) * WAVES * G::GPW;
+        for (int row = (sb * WAVES + wave) * G::GPW + grp; row < n; row += groups_total) {
+            const int beg = row_ptr[row];
+            const int end = row_ptr[row + 1];
+            if (end - beg > long_thresh) continue;  // owned by a long-row wave
+            double s[G::VEC];
 #pragma unroll
-            for (int e = 0; e < G::VEC; ++e) s[e] = fma(a0, V::get(x0, e), s[e]);
+            for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+            row_gather<P>(beg, end, 1, p0, col, val, ucur, s);
+            row_epilogue<P>(row, p0, s, sc, sp, first, ucur, uprev, y, acc);
         }
-        const int64_t off = (int64_t)row * P + p0;
-        const typename V::T ui = V::load(ucur + off);
-        typename V::T yo;
-        double* yp = reinterpret_cast<double*>(&yo);
-        if (first) {
-#pragma unroll
-            for (int e = 0; e < G::VEC; ++e) {
-                const double yv = s[e] * sc[e];
-                const double v1 = V::get(ui, e) * sc[e];
-                yp[e] = yv;
-                acc[1][e] = fma(v1, yv, acc[1][e]);
-                acc[4][e] = fma(v1, v1, acc[4][e]);
-            }
-        } else {
-            const typename V::T pi = V::load(uprev + off);
-#pragma unroll
-            for (int e = 0; e < G::VEC; ++e) {
-                const double yv = s[e] * sc[e];
-                const double v1 = V::get(ui, e) * sc[e];
-                const double v0 = V::get(pi, e) * sp[e];
-                yp[e] = yv;
-                acc[0][e] = fma(v0, yv, acc[0][e]);
-                acc[1][e] = fma(v1, yv, acc[1][e]);
-                acc[2][e] = fma(v0, v0, acc[2][e]);
-                acc[3][e] = fma(v0, v1, acc[3][e]);
-                acc[4][e] = fma(v1, v1, acc[4][e]);
-            }
-        }
-        V::store(y + off, yo);
     }
 
     // reduce over the row groups of this wave (lanes sharing `sub`)
@@ -359,6 +407,12 @@ namespace kt {
 
 static constexpr int kBlock = 512;
 
+int long_blocks_for(int n_long, int max_blocks) {
+    const int waves = kBlock / 64;
+    int b = (n_long + waves - 1) / waves;
+    return b < max_blocks ? b : max_blocks;
+}
+
 int spmm_grid(int n, int P, int max_blocks) {
     const int gpw = (P >= 2) ? 64 / (P / 2) : 64;
     const int rows_per_block = (kBlock / 64) * gpw;
@@ -398,10 +452,12 @@ hipError_t launch_rademacher(int P, int n, uint64_t seed, int64_t probe_base, do
 hipError_t launch_spmm_gram(int P, int grid, const int* rp, const int* ci, const double* va,
                             int n, const double* ucur, const double* uprev, const double* sc,
                             const double* sp, int first, double* y, double* partial,
+                            const int* long_rows, int n_long, int long_thresh, int long_blocks,
                             hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
         k_spmm_gram<decltype(c)::value, kBlock><<<grid, kBlock, 0, st>>>(
-            rp, ci, va, n, ucur, uprev, sc, sp, first, y, partial);
+            rp, ci, va, n, ucur, uprev, sc, sp, first, y, partial, long_rows, n_long,
+            long_thresh, long_blocks);
     });
 }
 

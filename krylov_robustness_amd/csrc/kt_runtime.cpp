@@ -189,10 +189,22 @@ int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr, con
             KT_HIP(hipMemcpy(A->d_col, A->h_col.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
             KT_HIP(hipMemcpy(A->d_val, A->h_val.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
         }
+        // long-row list for K1's wave-per-row mode, heaviest first
+        std::vector<int32_t> lr;
+        for (int64_t i = 0; i < n; ++i)
+            if (A->h_rowptr[i + 1] - A->h_rowptr[i] > A->long_thresh) lr.push_back((int32_t)i);
+        std::stable_sort(lr.begin(), lr.end(), [&](int32_t a, int32_t b) {
+            return A->h_rowptr[a + 1] - A->h_rowptr[a] > A->h_rowptr[b + 1] - A->h_rowptr[b];
+        });
+        A->n_long = (int)lr.size();
+        KT_HIP(hipMalloc(&A->d_long_rows, sizeof(int) * std::max<size_t>(lr.size(), 1)));
+        if (!lr.empty())
+            KT_HIP(hipMemcpy(A->d_long_rows, lr.data(), sizeof(int) * lr.size(), hipMemcpyHostToDevice));
     } catch (...) {
         if (A->d_rowptr) (void)hipFree(A->d_rowptr);
         if (A->d_col) (void)hipFree(A->d_col);
         if (A->d_val) (void)hipFree(A->d_val);
+        if (A->d_long_rows) (void)hipFree(A->d_long_rows);
         delete A;
         throw;
     }
@@ -208,6 +220,7 @@ int kt_matrix_destroy(kt_matrix_t A) {
     if (A->d_rowptr) (void)hipFree(A->d_rowptr);
     if (A->d_col) (void)hipFree(A->d_col);
     if (A->d_val) (void)hipFree(A->d_val);
+    if (A->d_long_rows) (void)hipFree(A->d_long_rows);
     delete A;
     KT_GUARD_END
 }

@@ -46,7 +46,9 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         const int n = (int)n64;
         const int P = block ? block : auto_block(n64, nprobes);
         const int64_t nsweeps = (nprobes + P - 1) / P;
-        const int grid = spmm_grid(n, P, ctx->num_cu * 4);
+        const int grid = spmm_grid(n, P, ctx->num_cu * 4);           // K2 / short rows
+        const int lblocks = long_blocks_for(A->n_long, ctx->num_cu * 2);
+        const int grid1 = grid + lblocks;                             // K1 total
         KT_HIP(hipSetDevice(ctx->device));
         hipStream_t st = ctx->stream;
 
@@ -55,7 +57,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         w.X0.ensure(blk_bytes);
         w.X1.ensure(blk_bytes);
         w.Y.ensure(blk_bytes);
-        w.partial.ensure(sizeof(double) * (size_t)grid * (5 + 1) * P);
+        w.partial.ensure(sizeof(double) * (size_t)(grid1 * 5 + grid) * P);
         w.coef.ensure(sizeof(double) * 2 * P);
         w.scales.ensure(sizeof(double) * 3 * P);
         const size_t rec = (size_t)3 * m * P;  // [alpha | up | low][m][P]
@@ -63,7 +65,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         w.host_trec.ensure(sizeof(double) * rec * nsweeps);
 
         double* part1 = w.partial.as<double>();
-        double* part2 = part1 + (size_t)grid * 5 * P;
+        double* part2 = part1 + (size_t)grid1 * 5 * P;
         double* coef = w.coef.as<double>();
         double* trec = w.trec.as<double>();
         double* htrec = w.host_trec.as<double>();
@@ -79,10 +81,11 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
             for (int j = 0; j < m; ++j) {
                 const int first = (j == 0);
                 prof_begin(ctx, PROF_SPMM);
-                KT_HIP(launch_spmm_gram(P, grid, A->d_rowptr, A->d_col, A->d_val, n, ucur, uprev,
-                                        sc, sp, first, w.Y.as<double>(), part1, st));
+                KT_HIP(launch_spmm_gram(P, grid1, A->d_rowptr, A->d_col, A->d_val, n, ucur, uprev,
+                                        sc, sp, first, w.Y.as<double>(), part1, A->d_long_rows,
+                                        A->n_long, A->long_thresh, lblocks, st));
                 prof_end(ctx, PROF_SPMM);
-                KT_HIP(launch_coef_cgs2(P, part1, grid, first, coef, trec + (size_t)(0 * m + j) * P,
+                KT_HIP(launch_coef_cgs2(P, part1, grid1, first, coef, trec + (size_t)(0 * m + j) * P,
                                         trec + (size_t)(1 * m + j) * P, st));
                 prof_begin(ctx, PROF_UPDATE);
                 KT_HIP(launch_update_norm(P, grid, n, w.Y.as<double>(), uprev, ucur, sc, sp, coef,

@@ -96,3 +96,15 @@ def test_slq_full_size_config2_properties(kra, gpu_ctx):
     np.testing.assert_allclose(q16, q128, rtol=1e-10)
     _, q_ref = slq_ref.slq_trace(A, 4, 30, seed=0)
     np.testing.assert_allclose(q128[:4], q_ref, rtol=RTOL)
+
+
+@pytest.mark.parametrize("block", [4, 16, 128])
+def test_slq_hub_rows_long_mode(kra, gpu_ctx, block):
+    """Scale-free graph with hub rows (degree > 64 -> K1's wave-per-row mode)."""
+    from krylov_robustness_amd import graphs
+    A = graphs.chung_lu(20_000, 200_000, seed=4)
+    assert np.diff(A.indptr).max() > 64
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    _, _, q = kra.slq_quadforms(D, 6, 30, seed=8, block=block, ctx=gpu_ctx)
+    _, q_ref = slq_ref.slq_trace(A, 6, 30, seed=8)
+    np.testing.assert_allclose(q, q_ref, rtol=RTOL)
