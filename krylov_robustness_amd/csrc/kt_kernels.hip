@@ -89,6 +89,7 @@ __global__ __launch_bounds__(256) void k_rademacher(int n, uint64_t seed, int64_
 // partial layout: [gridDim.x][5][P].
 // ---------------------------------------------------------------------------
 constexpr int NG = 5;
+constexpr int GQ = 8;  // padded Gram slots per probe
 
 // Row epilogue shared by both modes: y_i = s_cur * sum, Gram accumulation.
 template <int P>
@@ -243,65 +244,79 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_gram(
             for (int e = 0; e < G::VEC; ++e) red[wave][q][p0 + e] = acc[q][e];
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < NG * P; t += BLOCK) {
-        const int q = t / P, p = t % P;
+    // slab layout [P][GQ] (GQ = 8 >= NG, zero padded) so that one probe's
+    // Gram entries are 8 adjacent slots in the reduction kernel
+    for (int t = threadIdx.x; t < GQ * P; t += BLOCK) {
+        const int p = t / GQ, q = t % GQ;
         double v = 0.0;
+        if (q < NG) {
 #pragma unroll
-        for (int w = 0; w < WAVES; ++w) v += red[w][q][p];
-        partial[(int64_t)blockIdx.x * NG * P + t] = v;
+            for (int w = 0; w < WAVES; ++w) v += red[w][q][p];
+        }
+        partial[(int64_t)blockIdx.x * GQ * P + t] = v;
     }
 }
 
 // ---------------------------------------------------------------------------
-// Reduce [nblk][NQ][P] partial slabs in block order (deterministic).
-// One workgroup; thread t owns slot t % (NQ*P) and a chunk of blocks, then an
-// LDS combine over chunks in chunk order.
+// Deterministic column reduction of per-block slabs [nblk][slots]: 64 slots
+// per workgroup (one per lane), 16 waves striding over the slabs in a fixed
+// order, LDS combine in wave order.  Returns the sum to every lane of wave 0.
 // ---------------------------------------------------------------------------
-template <int NQ, int P>
-__device__ __forceinline__ void reduce_slabs(const double* __restrict__ partial, int nblk,
-                                             double* __restrict__ out /* LDS [NQ*P] */) {
-    constexpr int SLOTS = NQ * P;
-    constexpr int CH = (1024 / SLOTS) > 0 ? (1024 / SLOTS) : 1;  // chunks
-    __shared__ double tmp[CH][SLOTS];
-    const int t = threadIdx.x;
-    for (int s = t; s < CH * SLOTS; s += blockDim.x) {
-        const int slot = s % SLOTS, ch = s / SLOTS;
-        const int b0 = (int)((int64_t)nblk * ch / CH), b1 = (int)((int64_t)nblk * (ch + 1) / CH);
-        double v = 0.0;
-        for (int b = b0; b < b1; ++b) v += partial[(int64_t)b * SLOTS + slot];
-        tmp[ch][slot] = v;
+__device__ __forceinline__ double reduce_cols(const double* __restrict__ partial, int nblk,
+                                              int slots, int slot) {
+    __shared__ double tmp[16][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double v = 0.0;
+    if (slot < slots) {
+        int b = wave;
+        for (; b + 48 < nblk; b += 64) {  // 4 loads in flight
+            const double x0 = partial[(int64_t)b * slots + slot];
+            const double x1 = partial[(int64_t)(b + 16) * slots + slot];
+            const double x2 = partial[(int64_t)(b + 32) * slots + slot];
+            const double x3 = partial[(int64_t)(b + 48) * slots + slot];
+            v += x0; v += x1; v += x2; v += x3;
+        }
+        for (; b < nblk; b += 16) v += partial[(int64_t)b * slots + slot];
     }
+    tmp[wave][lane] = v;
     __syncthreads();
-    for (int s = t; s < SLOTS; s += blockDim.x) {
-        double v = 0.0;
-        for (int ch = 0; ch < CH; ++ch) v += tmp[ch][s];
-        out[s] = v;
+    double r = 0.0;
+    if (wave == 0) {
+#pragma unroll
+        for (int w = 0; w < 16; ++w) r += tmp[w][lane];
     }
-    __syncthreads();
+    return r;
 }
 
 // coef: CGS2 against the window [v0, v1] from the Gram matrix.
 //   pass 1: h = [v0.y, v1.y];  pass 2: h' = V'(y - V h) = h - (V'V) h
 //   c = h + h'  ->  H(j-1,j) = c0, H(j,j) = c1   (lanczos_krylov.m:88,109-115)
-// Writes coef[2][P] and the T-record rows alpha (=c1) and up (=c0).
+// grid = ceil(8P/64) workgroups of 1024; writes coef[2][P], T-record rows.
 template <int P>
 __global__ __launch_bounds__(1024) void k_coef_cgs2(const double* __restrict__ partial, int nblk,
                                                      int first, double* __restrict__ coef,
                                                      double* __restrict__ t_alpha,
                                                      double* __restrict__ t_up) {
-    __shared__ double g[NG * P];
-    reduce_slabs<NG, P>(partial, nblk, g);
-    for (int p = threadIdx.x; p < P; p += blockDim.x) {
-        double g0 = g[0 * P + p], g1 = g[1 * P + p];
-        double G00 = g[2 * P + p], G01 = g[3 * P + p], G11 = g[4 * P + p];
-        if (first) { g0 = 0.0; G00 = 0.0; G01 = 0.0; }
-        const double h0p = g0 - (G00 * g0 + G01 * g1);
-        const double h1p = g1 - (G01 * g0 + G11 * g1);
-        const double c0 = g0 + h0p, c1 = g1 + h1p;
-        coef[p] = c0;
-        coef[P + p] = c1;
-        t_alpha[p] = c1;
-        t_up[p] = c0;
+    const int lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 64 + lane;
+    const double r = reduce_cols(partial, nblk, GQ * P, slot);
+    if (threadIdx.x < 64) {
+        // lanes 8k..8k+7 hold probe p's [g0 g1 G00 G01 G11 0 0 0]
+        const int base = lane & ~7;
+        double g0 = __shfl(r, base + 0, 64), g1 = __shfl(r, base + 1, 64);
+        double G00 = __shfl(r, base + 2, 64), G01 = __shfl(r, base + 3, 64);
+        const double G11 = __shfl(r, base + 4, 64);
+        const int p = slot / GQ;
+        if ((lane & 7) == 0 && p < P) {
+            if (first) { g0 = 0.0; G00 = 0.0; G01 = 0.0; }
+            const double h0p = g0 - (G00 * g0 + G01 * g1);
+            const double h1p = g1 - (G01 * g0 + G11 * g1);
+            const double c0 = g0 + h0p, c1 = g1 + h1p;
+            coef[p] = c0;
+            coef[P + p] = c1;
+            t_alpha[p] = c1;
+            t_up[p] = c0;
+        }
     }
 }
 
@@ -381,12 +396,12 @@ template <int P>
 __global__ __launch_bounds__(1024) void k_norm(const double* __restrict__ partial, int nblk,
                                                 double* __restrict__ scale_next,
                                                 double* __restrict__ t_low) {
-    __shared__ double g[P];
-    reduce_slabs<1, P>(partial, nblk, g);
-    for (int p = threadIdx.x; p < P; p += blockDim.x) {
-        const double beta = sqrt(g[p]);
-        t_low[p] = beta;
-        scale_next[p] = (beta < 1e-8) ? 0.0 : 1.0 / beta;
+    const int slot = blockIdx.x * 64 + (threadIdx.x & 63);
+    const double r = reduce_cols(partial, nblk, P, slot);
+    if (threadIdx.x < 64 && slot < P) {
+        const double beta = sqrt(r);
+        t_low[slot] = beta;
+        scale_next[slot] = (beta < 1e-8) ? 0.0 : 1.0 / beta;
     }
 }
 
@@ -464,8 +479,9 @@ hipError_t launch_spmm_gram(int P, int grid, const int* rp, const int* ci, const
 hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, double* coef,
                             double* t_alpha, double* t_up, hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
-        k_coef_cgs2<decltype(c)::value><<<1, 1024, 0, st>>>(partial, nblk, first, coef, t_alpha,
-                                                            t_up);
+        constexpr int PP = decltype(c)::value;
+        k_coef_cgs2<PP><<<(GQ * PP + 63) / 64, 1024, 0, st>>>(partial, nblk, first, coef,
+                                                             t_alpha, t_up);
     });
 }
 
@@ -481,7 +497,8 @@ hipError_t launch_update_norm(int P, int grid, int n, const double* y, double* u
 hipError_t launch_norm(int P, const double* partial, int nblk, double* scale_next, double* t_low,
                        hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
-        k_norm<decltype(c)::value><<<1, 1024, 0, st>>>(partial, nblk, scale_next, t_low);
+        constexpr int PP = decltype(c)::value;
+        k_norm<PP><<<(PP + 63) / 64, 1024, 0, st>>>(partial, nblk, scale_next, t_low);
     });
 }
 

@@ -57,7 +57,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         w.X0.ensure(blk_bytes);
         w.X1.ensure(blk_bytes);
         w.Y.ensure(blk_bytes);
-        w.partial.ensure(sizeof(double) * (size_t)(grid1 * 5 + grid) * P);
+        w.partial.ensure(sizeof(double) * (size_t)(grid1 * 8 + grid) * P);
         w.coef.ensure(sizeof(double) * 2 * P);
         w.scales.ensure(sizeof(double) * 3 * P);
         const size_t rec = (size_t)3 * m * P;  // [alpha | up | low][m][P]
@@ -65,7 +65,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         w.host_trec.ensure(sizeof(double) * rec * nsweeps);
 
         double* part1 = w.partial.as<double>();
-        double* part2 = part1 + (size_t)grid1 * 5 * P;
+        double* part2 = part1 + (size_t)grid1 * 8 * P;
         double* coef = w.coef.as<double>();
         double* trec = w.trec.as<double>();
         double* htrec = w.host_trec.as<double>();
