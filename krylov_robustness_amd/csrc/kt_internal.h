@@ -102,6 +102,12 @@ struct kt_matrix_s {
     int* d_long_rows = nullptr;
     int n_long = 0;
     int long_thresh = 64;
+    // Device rows are relabelled by descending degree (hubs first): device
+    // row r holds original row new2old[r].  Probes stay keyed by ORIGINAL
+    // index (d_perm = new2old), so results do not depend on the relabelling.
+    bool relabeled = false;
+    int* d_perm = nullptr;
+    std::vector<int32_t> new2old, old2new;
     // host copy (CSR, int64 pointers) for host-side algorithms and checks
     std::vector<int64_t> h_rowptr;
     std::vector<int32_t> h_col;

@@ -68,6 +68,7 @@ template <> struct VecT<2> {
 // ---------------------------------------------------------------------------
 template <int P>
 __global__ __launch_bounds__(256) void k_rademacher(int n, uint64_t seed, int64_t probe_base,
+                                                    const int* __restrict__ perm,
                                                     double* __restrict__ X) {
     __shared__ uint64_t keys[P];
     for (int p = threadIdx.x; p < P; p += blockDim.x)
@@ -76,9 +77,10 @@ __global__ __launch_bounds__(256) void k_rademacher(int n, uint64_t seed, int64_
     const int64_t total = (int64_t)n * P;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = t / P;
+        const int64_t r = t / P;
         const int p = (int)(t % P);
-        X[t] = (sm64(keys[p] + (uint64_t)i) >> 63) ? -1.0 : 1.0;
+        const uint64_t i = perm ? (uint64_t)perm[r] : (uint64_t)r;  // original row index
+        X[t] = (sm64(keys[p] + i) >> 63) ? -1.0 : 1.0;
     }
 }
 
@@ -453,14 +455,14 @@ static hipError_t dispatch_p(int P, F&& f) {
     return hipGetLastError();
 }
 
-hipError_t launch_rademacher(int P, int n, uint64_t seed, int64_t probe_base, double* X,
-                             hipStream_t st) {
+hipError_t launch_rademacher(int P, int n, uint64_t seed, int64_t probe_base, const int* perm,
+                             double* X, hipStream_t st) {
     int64_t total = (int64_t)n * P;
     int grid = (int)((total + 255) / 256);
     if (grid > 8192) grid = 8192;
     if (grid < 1) grid = 1;
     return dispatch_p(P, [&](auto c) {
-        k_rademacher<decltype(c)::value><<<grid, 256, 0, st>>>(n, seed, probe_base, X);
+        k_rademacher<decltype(c)::value><<<grid, 256, 0, st>>>(n, seed, probe_base, perm, X);
     });
 }
 

@@ -8,8 +8,8 @@ namespace kt {
 int spmm_grid(int n, int P, int max_blocks);
 int long_blocks_for(int n_long, int max_blocks);
 
-hipError_t launch_rademacher(int P, int n, uint64_t seed, int64_t probe_base, double* X,
-                             hipStream_t st);
+hipError_t launch_rademacher(int P, int n, uint64_t seed, int64_t probe_base, const int* perm,
+                             double* X, hipStream_t st);
 hipError_t launch_spmm_gram(int P, int grid, const int* rp, const int* ci, const double* va,
                             int n, const double* ucur, const double* uprev, const double* sc,
                             const double* sp, int first, double* y, double* partial,

@@ -1,5 +1,6 @@
 // kt_runtime.cpp -- contexts, device-resident matrices, errors, profiling.
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -179,22 +180,53 @@ int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr, con
     }
     try {
         KT_HIP(hipSetDevice(ctx->device));
-        std::vector<int32_t> rp32(n + 1);
-        for (int64_t i = 0; i <= n; ++i) rp32[i] = (int32_t)A->h_rowptr[i];
+        // degree-descending relabelling (stable, so ties keep original order)
+        const char* rl = getenv("KT_RELABEL");
+        A->relabeled = !(rl && rl[0] == '0');
+        A->new2old.resize(n);
+        A->old2new.resize(n);
+        for (int64_t i = 0; i < n; ++i) A->new2old[i] = (int32_t)i;
+        if (A->relabeled)
+            std::stable_sort(A->new2old.begin(), A->new2old.end(), [&](int32_t a, int32_t b) {
+                return A->h_rowptr[a + 1] - A->h_rowptr[a] > A->h_rowptr[b + 1] - A->h_rowptr[b];
+            });
+        for (int64_t r = 0; r < n; ++r) A->old2new[A->new2old[r]] = (int32_t)r;
+        std::vector<int32_t> rp32(n + 1), c32(nnz);
+        std::vector<double> v64(nnz);
+        rp32[0] = 0;
+        for (int64_t r = 0; r < n; ++r) {
+            const int64_t o = A->new2old[r];
+            rp32[r + 1] = rp32[r] + (int32_t)(A->h_rowptr[o + 1] - A->h_rowptr[o]);
+        }
+        std::vector<std::pair<int32_t, double>> tmp;
+        for (int64_t r = 0; r < n; ++r) {
+            const int64_t o = A->new2old[r];
+            tmp.clear();
+            for (int64_t k = A->h_rowptr[o]; k < A->h_rowptr[o + 1]; ++k)
+                tmp.push_back({A->old2new[A->h_col[k]], A->h_val[k]});
+            std::sort(tmp.begin(), tmp.end(),
+                      [](const auto& x, const auto& y) { return x.first < y.first; });
+            for (size_t t = 0; t < tmp.size(); ++t) {
+                c32[rp32[r] + t] = tmp[t].first;
+                v64[rp32[r] + t] = tmp[t].second;
+            }
+        }
         KT_HIP(hipMalloc(&A->d_rowptr, sizeof(int) * (n + 1)));
         KT_HIP(hipMalloc(&A->d_col, sizeof(int) * std::max<int64_t>(nnz, 1)));
         KT_HIP(hipMalloc(&A->d_val, sizeof(double) * std::max<int64_t>(nnz, 1)));
+        KT_HIP(hipMalloc(&A->d_perm, sizeof(int) * std::max<int64_t>(n, 1)));
         KT_HIP(hipMemcpy(A->d_rowptr, rp32.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice));
+        if (n) KT_HIP(hipMemcpy(A->d_perm, A->new2old.data(), sizeof(int) * n, hipMemcpyHostToDevice));
         if (nnz) {
-            KT_HIP(hipMemcpy(A->d_col, A->h_col.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
-            KT_HIP(hipMemcpy(A->d_val, A->h_val.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
+            KT_HIP(hipMemcpy(A->d_col, c32.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
+            KT_HIP(hipMemcpy(A->d_val, v64.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
         }
-        // long-row list for K1's wave-per-row mode, heaviest first
+        // long-row list (device numbering) for K1's wave-per-row mode, heaviest first
         std::vector<int32_t> lr;
-        for (int64_t i = 0; i < n; ++i)
-            if (A->h_rowptr[i + 1] - A->h_rowptr[i] > A->long_thresh) lr.push_back((int32_t)i);
+        for (int64_t r = 0; r < n; ++r)
+            if (rp32[r + 1] - rp32[r] > A->long_thresh) lr.push_back((int32_t)r);
         std::stable_sort(lr.begin(), lr.end(), [&](int32_t a, int32_t b) {
-            return A->h_rowptr[a + 1] - A->h_rowptr[a] > A->h_rowptr[b + 1] - A->h_rowptr[b];
+            return rp32[a + 1] - rp32[a] > rp32[b + 1] - rp32[b];
         });
         A->n_long = (int)lr.size();
         KT_HIP(hipMalloc(&A->d_long_rows, sizeof(int) * std::max<size_t>(lr.size(), 1)));
@@ -205,6 +237,7 @@ int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr, con
         if (A->d_col) (void)hipFree(A->d_col);
         if (A->d_val) (void)hipFree(A->d_val);
         if (A->d_long_rows) (void)hipFree(A->d_long_rows);
+        if (A->d_perm) (void)hipFree(A->d_perm);
         delete A;
         throw;
     }
@@ -221,6 +254,7 @@ int kt_matrix_destroy(kt_matrix_t A) {
     if (A->d_col) (void)hipFree(A->d_col);
     if (A->d_val) (void)hipFree(A->d_val);
     if (A->d_long_rows) (void)hipFree(A->d_long_rows);
+    if (A->d_perm) (void)hipFree(A->d_perm);
     delete A;
     KT_GUARD_END
 }

@@ -76,7 +76,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
             double* sc = w.scales.as<double>();
             double* sp = sc + P;
             double* sn = sc + 2 * P;
-            KT_HIP(launch_rademacher(P, n, seed, probe_offset + s * P, ucur, st));
+            KT_HIP(launch_rademacher(P, n, seed, probe_offset + s * P, A->d_perm, ucur, st));
             KT_HIP(launch_fill(sc, P, 1.0 / std::sqrt((double)n), st));
             for (int j = 0; j < m; ++j) {
                 const int first = (j == 0);

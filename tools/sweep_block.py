@@ -14,6 +14,7 @@ def main():
     ap.add_argument("--nprobes", type=int, default=256)
     ap.add_argument("--m", type=int, default=30)
     ap.add_argument("--blocks", default="4,8,16,32,64,128")
+    ap.add_argument("--variants", default="relabel", help="comma list: relabel,natural")
     a = ap.parse_args()
     import krylov_robustness_amd as kra
     from krylov_robustness_amd import graphs
@@ -24,25 +25,28 @@ def main():
         A = graphs.erdos_renyi(100_000, 500_000, seed=0)
     print(f"graph {a.config} n={A.shape[0]} nnz={A.nnz} gen {time.time()-t:.1f}s", flush=True)
     ctx = kra.Context(0)
-    D = kra.DeviceMatrix(A, ctx)
     n, nnz = A.shape[0], A.nnz
-    for P in [int(x) for x in a.blocks.split(",")]:
-        kra.slq_quadforms(D, P, 4, seed=0, block=P, ctx=ctx)  # warm
-        ctx.profile_reset(); ctx.profile(True)
-        t = time.perf_counter()
-        s1, _, q = kra.slq_quadforms(D, a.nprobes, a.m, seed=0, block=P, ctx=ctx)
-        el = time.perf_counter() - t
-        ctx.profile(False)
-        l1, ms1 = ctx.profile_read(0)
-        l2, ms2 = ctx.profile_read(1)
-        k1 = ms1 / max(l1, 1); k2 = ms2 / max(l2, 1)
-        k1_bytes = 12 * nnz + 4 * (n + 1) + 24 * n * P
-        k2_bytes = 32 * n * P
-        per_eval_1024 = el / a.nprobes * 1024
-        print(f"P={P:4d} total {el*1e3:9.1f} ms  ({1/per_eval_1024:7.3f} evals/s @1024 probes) "
-              f"K1 {k1*1e3:8.1f} us {k1_bytes/k1/1e6:7.0f} GB/s  K2 {k2*1e3:8.1f} us "
-              f"{k2_bytes/k2/1e6:7.0f} GB/s  launches {l1}  K1+K2 share {(ms1+ms2)/(el*1e3):.2f}  "
-              f"tr~{s1/a.nprobes:.4e}", flush=True)
+    for var in a.variants.split(","):
+      os.environ["KT_RELABEL"] = "0" if var == "natural" else "1"
+      D = kra.DeviceMatrix(A, ctx)
+      print(f"--- variant {var}", flush=True)
+      for P in [int(x) for x in a.blocks.split(",")]:
+          kra.slq_quadforms(D, P, 4, seed=0, block=P, ctx=ctx)  # warm
+          ctx.profile_reset(); ctx.profile(True)
+          t = time.perf_counter()
+          s1, _, q = kra.slq_quadforms(D, a.nprobes, a.m, seed=0, block=P, ctx=ctx)
+          el = time.perf_counter() - t
+          ctx.profile(False)
+          l1, ms1 = ctx.profile_read(0)
+          l2, ms2 = ctx.profile_read(1)
+          k1 = ms1 / max(l1, 1); k2 = ms2 / max(l2, 1)
+          k1_bytes = 12 * nnz + 4 * (n + 1) + 24 * n * P
+          k2_bytes = 32 * n * P
+          per_eval_1024 = el / a.nprobes * 1024
+          print(f"P={P:4d} total {el*1e3:9.1f} ms  ({1/per_eval_1024:7.3f} evals/s @1024 probes) "
+                f"K1 {k1*1e3:8.1f} us {k1_bytes/k1/1e6:7.0f} GB/s  K2 {k2*1e3:8.1f} us "
+                f"{k2_bytes/k2/1e6:7.0f} GB/s  launches {l1}  K1+K2 share {(ms1+ms2)/(el*1e3):.2f}  "
+                f"tr~{s1/a.nprobes:.4e}", flush=True)
 
 
 if __name__ == "__main__":
