@@ -77,7 +77,7 @@ struct ProfSlot {
 enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_NSLOTS = 2 };
 
 struct Workspace {
-    DevBuf X0, X1, Y, partial, coef, scales, trec;
+    DevBuf X0, X1, Y, partial, coef, scales, k2s, trec;
     PinnedBuf host_trec;
 };
 
@@ -88,6 +88,7 @@ struct kt_context_s {
     hipStream_t stream = nullptr;
     int num_cu = 256;
     bool profile = false;
+    int k1_flags = 0;  // KT_K1_FLAGS: bit 0 = non-temporal stream hints in K1
     kt::ProfSlot prof[kt::PROF_NSLOTS];
     kt::Workspace ws;
 };

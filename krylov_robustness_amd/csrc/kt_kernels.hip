@@ -1,29 +1,34 @@
-// kt_kernels.hip -- CDNA4 (gfx950) kernels for the block-Krylov trace path.
+// kt_kernels.hip -- CDNA4 (gfx950) kernels for the probe-Lanczos trace path.
 //
 // Data layout in HBM:
-//   A      : CSR, int32 row_ptr[n+1], int32 col[nnz], fp64 val[nnz]
-//            (the reference's CSC of a symmetric matrix, read as CSR)
+//   A      : CSR, int32 row_ptr[n+1], int32 col[nnz], fp64 val[nnz]; rows
+//            relabelled by descending degree (kt_runtime.cpp), hub rows first.
 //   blocks : n x P fp64, ROW-MAJOR ("probe-contiguous"): row i of a probe
 //            block is P consecutive doubles, so every nonzero a_ic gathers
-//            one contiguous 8P-byte row X[c, 0:P] -- a fully coalesced
-//            16 B/lane load by P/2 lanes.
+//            one contiguous 8P-byte row X[c, 0:P] -- a coalesced 16 B/lane
+//            load by P/2 lanes.
 //
 // Wave mapping: a wave64 is split into GPW = 64/LPR "row groups" of
 // LPR = P/2 lanes; each group owns one matrix row, each lane two probe
 // columns.  P = 128 -> one row per wave (1 KiB gathers); P = 16 -> 8 rows
-// per wave (128 B gathers = one cache line).
+// per wave (128 B gathers = one cache line).  Rows with degree > 64 are
+// instead owned by a whole wave whose groups stride over the nonzeros.
 //
-// Hot recurrence (lanczos_krylov.m:73-115 with
-// bs = 1 per probe column).  Stored vectors are UNNORMALISED, u_j, with a
-// per-probe scale s_j so that v_j = s_j u_j; this lets the normalisation
-// 1/beta be applied inside the next SpMM for free:
-//   K1 spmm_gram : y = s_j A u_j, Gram partials of [v_{j-1}, v_j, y]
-//   coef         : CGS2 coefficients from the Gram (= two classical passes,
-//                  lanczos_krylov.m:109-115, computed algebraically)
-//   K2 update    : u_{j+1} = y - c0 v_{j-1} - c1 v_j, partial ||u_{j+1}||^2
-//   norm         : beta = ||u_{j+1}||, s_{j+1} = 1/beta, lucky if < 1e-8
-// All reductions are deterministic: per-block partial slabs reduced in a
-// fixed order (no float atomics).
+// Recurrence (lanczos_krylov.m:73-115 with bs = 1
+// per probe column).  Stored vectors are UNNORMALISED, u_j, with a per-probe
+// scale s_j (v_j = s_j u_j), so 1/beta is applied inside the next SpMM.
+//   K1 spmm_dot  : y = s_j A u_j;             partial  v_j . y
+//   coef         : CGS2 against the window [v_{j-1}, v_j] from the Gram
+//                  (two classical passes, lanczos_krylov.m:109-115, formed
+//                  algebraically: c = 2h - G h)
+//   K2 update    : u_{j+1} = y - c0 v_{j-1} - c1 v_j (over u_{j-1});
+//                  partials ||u_{j+1}||^2, y . u_{j+1}, u_j . u_{j+1}
+//   norm         : beta = ||u_{j+1}||, s_{j+1} = 1/beta (lucky if < 1e-8)
+// By the symmetry of A, v_j . (A v_{j+1}) = (A v_j) . v_{j+1}: the K2 dot
+// y . u_{j+1} supplies next step's window coefficient, so K1 never reads
+// v_{j-1} (48 B of vector traffic per probe-row-step instead of 56).
+// All reductions are deterministic: per-block partial slabs summed in a fixed
+// order by column-reduction kernels (no float atomics).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -39,32 +44,58 @@ __device__ __forceinline__ uint64_t sm64(uint64_t x) {
 }
 
 template <int P> struct Geo {
-    static constexpr int VEC = (P >= 2) ? 2 : 1;     // doubles per lane
-    static constexpr int LPR = P / VEC;              // lanes per row group
-    static constexpr int GPW = 64 / LPR;             // row groups per wave
+    static constexpr int VEC = (P >= 2) ? 2 : 1;  // doubles per lane
+    static constexpr int LPR = P / VEC;           // lanes per row group
+    static constexpr int GPW = 64 / LPR;          // row groups per wave
 };
+
+// FLAGS bit 0: non-temporal hints on the streamed (read-once) traffic of K1
+// (CSR arrays, own-row vector read, y store) so it does not evict the
+// gathered probe block from L2.
+enum : int { KF_NT = 1 };
 
 template <int VEC> struct VecT;
 template <> struct VecT<1> {
     using T = double;
     __device__ static __forceinline__ T load(const double* p) { return *p; }
+    __device__ static __forceinline__ T load_nt(const double* p) {
+        return __builtin_nontemporal_load(p);
+    }
     __device__ static __forceinline__ void store(double* p, const T& v) { *p = v; }
+    __device__ static __forceinline__ void store_nt(double* p, const T& v) {
+        __builtin_nontemporal_store(v, p);
+    }
     __device__ static __forceinline__ double get(const T& v, int) { return v; }
 };
 template <> struct VecT<2> {
     using T = double2;
+    using N = __attribute__((ext_vector_type(2))) double;
     __device__ static __forceinline__ T load(const double* p) {
         return *reinterpret_cast<const double2*>(p);
+    }
+    __device__ static __forceinline__ T load_nt(const double* p) {
+        const N v = __builtin_nontemporal_load(reinterpret_cast<const N*>(p));
+        return double2(v[0], v[1]);
     }
     __device__ static __forceinline__ void store(double* p, const T& v) {
         *reinterpret_cast<double2*>(p) = v;
     }
+    __device__ static __forceinline__ void store_nt(double* p, const T& v) {
+        N w = {v.x, v.y};
+        __builtin_nontemporal_store(w, reinterpret_cast<N*>(p));
+    }
     __device__ static __forceinline__ double get(const T& v, int e) { return e ? v.y : v.x; }
 };
 
+template <int FLAGS, class T> __device__ __forceinline__ T ld_stream(const T* p) {
+    if constexpr (FLAGS & KF_NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
 // ---------------------------------------------------------------------------
-// Rademacher probe block: X[i, p] = +-1 from splitmix64(key(seed, base+p) + i)
-// (same stream as oracle/krylov_oracle.py:rademacher and oracle/slq_ref.c).
+// Rademacher probe block: X[r, p] = +-1 from splitmix64(key(seed, base+p) + i),
+// i = perm[r] the ORIGINAL row index (oracle/krylov_oracle.py:rademacher,
+// oracle/slq_ref.c produce the same stream).
 // ---------------------------------------------------------------------------
 template <int P>
 __global__ __launch_bounds__(256) void k_rademacher(int n, uint64_t seed, int64_t probe_base,
@@ -79,62 +110,16 @@ __global__ __launch_bounds__(256) void k_rademacher(int n, uint64_t seed, int64_
          t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = t / P;
         const int p = (int)(t % P);
-        const uint64_t i = perm ? (uint64_t)perm[r] : (uint64_t)r;  // original row index
+        const uint64_t i = perm ? (uint64_t)perm[r] : (uint64_t)r;
         X[t] = (sm64(keys[p] + i) >> 63) ? -1.0 : 1.0;
     }
 }
 
 // ---------------------------------------------------------------------------
-// K1: y = s_cur * (A u_cur); Gram partials per probe column:
-//   [0] v0.y  [1] v1.y  [2] v0.v0  [3] v0.v1  [4] v1.v1
-// where v0 = s_prev * u_prev (absent on the first step), v1 = s_cur * u_cur.
-// partial layout: [gridDim.x][5][P].
+// K1
 // ---------------------------------------------------------------------------
-constexpr int NG = 5;
-constexpr int GQ = 8;  // padded Gram slots per probe
-
-// Row epilogue shared by both modes: y_i = s_cur * sum, Gram accumulation.
-template <int P>
-__device__ __forceinline__ void row_epilogue(int row, int p0, const double* s, const double* sc,
-                                             const double* sp, int first,
-                                             const double* __restrict__ ucur,
-                                             const double* __restrict__ uprev,
-                                             double* __restrict__ y, double (*acc)[Geo<P>::VEC]) {
-    using G = Geo<P>;
-    using V = VecT<G::VEC>;
-    const int64_t off = (int64_t)row * P + p0;
-    const typename V::T ui = V::load(ucur + off);
-    typename V::T yo;
-    double* yp = reinterpret_cast<double*>(&yo);
-    if (first) {
-#pragma unroll
-        for (int e = 0; e < G::VEC; ++e) {
-            const double yv = s[e] * sc[e];
-            const double v1 = V::get(ui, e) * sc[e];
-            yp[e] = yv;
-            acc[1][e] = fma(v1, yv, acc[1][e]);
-            acc[4][e] = fma(v1, v1, acc[4][e]);
-        }
-    } else {
-        const typename V::T pi = V::load(uprev + off);
-#pragma unroll
-        for (int e = 0; e < G::VEC; ++e) {
-            const double yv = s[e] * sc[e];
-            const double v1 = V::get(ui, e) * sc[e];
-            const double v0 = V::get(pi, e) * sp[e];
-            yp[e] = yv;
-            acc[0][e] = fma(v0, yv, acc[0][e]);
-            acc[1][e] = fma(v1, yv, acc[1][e]);
-            acc[2][e] = fma(v0, v0, acc[2][e]);
-            acc[3][e] = fma(v0, v1, acc[3][e]);
-            acc[4][e] = fma(v1, v1, acc[4][e]);
-        }
-    }
-    V::store(y + off, yo);
-}
-
 // Gather-accumulate nonzeros k = k0, k0 + stride, ... < end of one row.
-template <int P>
+template <int P, int FLAGS>
 __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
                                            const int* __restrict__ col,
                                            const double* __restrict__ val,
@@ -143,10 +128,12 @@ __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
     using V = VecT<G::VEC>;
     int k = k0;
     for (; k + 3 * stride < end; k += 4 * stride) {  // 4 independent gathers in flight
-        const int c0 = col[k], c1 = col[k + stride], c2 = col[k + 2 * stride],
-                  c3 = col[k + 3 * stride];
-        const double a0 = val[k], a1 = val[k + stride], a2 = val[k + 2 * stride],
-                     a3 = val[k + 3 * stride];
+        const int c0 = ld_stream<FLAGS>(col + k), c1 = ld_stream<FLAGS>(col + k + stride);
+        const int c2 = ld_stream<FLAGS>(col + k + 2 * stride);
+        const int c3 = ld_stream<FLAGS>(col + k + 3 * stride);
+        const double a0 = ld_stream<FLAGS>(val + k), a1 = ld_stream<FLAGS>(val + k + stride);
+        const double a2 = ld_stream<FLAGS>(val + k + 2 * stride);
+        const double a3 = ld_stream<FLAGS>(val + k + 3 * stride);
         const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
         const typename V::T x1 = V::load(ucur + (int64_t)c1 * P + p0);
         const typename V::T x2 = V::load(ucur + (int64_t)c2 * P + p0);
@@ -160,24 +147,45 @@ __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
         }
     }
     for (; k < end; k += stride) {
-        const int c0 = col[k];
-        const double a0 = val[k];
+        const int c0 = ld_stream<FLAGS>(col + k);
+        const double a0 = ld_stream<FLAGS>(val + k);
         const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
 #pragma unroll
         for (int e = 0; e < G::VEC; ++e) s[e] = fma(a0, V::get(x0, e), s[e]);
     }
 }
 
+// y_r = s_cur * sum; accumulate v_cur . y.
+template <int P, int FLAGS>
+__device__ __forceinline__ void row_epilogue(int row, int p0, const double* s, const double* sc,
+                                             const double* __restrict__ ucur,
+                                             double* __restrict__ y, double* acc) {
+    using G = Geo<P>;
+    using V = VecT<G::VEC>;
+    const int64_t off = (int64_t)row * P + p0;
+    typename V::T ui;
+    if constexpr (FLAGS & KF_NT) ui = V::load_nt(ucur + off);
+    else ui = V::load(ucur + off);
+    typename V::T yo;
+    double* yp = reinterpret_cast<double*>(&yo);
+#pragma unroll
+    for (int e = 0; e < G::VEC; ++e) {
+        const double yv = s[e] * sc[e];
+        yp[e] = yv;
+        acc[e] = fma(V::get(ui, e) * sc[e], yv, acc[e]);
+    }
+    if constexpr (FLAGS & KF_NT) V::store_nt(y + off, yo);
+    else V::store(y + off, yo);
+}
+
 // Two modes in one launch.  Blocks [0, long_blocks): one WAVE per long row
-// (degree > long_thresh, listed hubs-first in long_rows), its row groups
-// striding over the row's nonzeros, combined by wave shuffles -- so a hub
-// row costs deg/(4*GPW) dependent gather rounds instead of deg/4.  Other
-// blocks: one row GROUP per short row, rows in natural order (coalesced y).
-template <int P, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_spmm_gram(
+// (degree > long_thresh, listed heaviest first), its row groups striding over
+// the row's nonzeros and combining by wave shuffles.  Other blocks: one row
+// GROUP per short row, rows in order (coalesced y).  partial: [grid][P].
+template <int P, int BLOCK, int FLAGS>
+__global__ __launch_bounds__(BLOCK) void k_spmm_dot(
     const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
-    int n, const double* __restrict__ ucur, const double* __restrict__ uprev,
-    const double* __restrict__ scale_cur, const double* __restrict__ scale_prev, int first,
+    int n, const double* __restrict__ ucur, const double* __restrict__ scale_cur,
     double* __restrict__ y, double* __restrict__ partial, const int* __restrict__ long_rows,
     int n_long, int long_thresh, int long_blocks) {
     using G = Geo<P>;
@@ -188,17 +196,12 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_gram(
     const int grp = lane / G::LPR;
     const int p0 = sub * G::VEC;
 
-    double sc[G::VEC], sp[G::VEC];
+    double sc[G::VEC], acc[G::VEC];
 #pragma unroll
     for (int e = 0; e < G::VEC; ++e) {
         sc[e] = scale_cur[p0 + e];
-        sp[e] = first ? 0.0 : scale_prev[p0 + e];
+        acc[e] = 0.0;
     }
-    double acc[NG][G::VEC];
-#pragma unroll
-    for (int q = 0; q < NG; ++q)
-#pragma unroll
-        for (int e = 0; e < G::VEC; ++e) acc[q][e] = 0.0;
 
     if ((int)blockIdx.x < long_blocks) {
         for (int li = blockIdx.x * WAVES + wave; li < n_long; li += long_blocks * WAVES) {
@@ -208,61 +211,51 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_gram(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            row_gather<P>(beg + grp, end, G::GPW, p0, col, val, ucur, s);
+            row_gather<P, FLAGS>(beg + grp, end, G::GPW, p0, col, val, ucur, s);
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
                 for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
-            if (grp == 0) row_epilogue<P>(row, p0, s, sc, sp, first, ucur, uprev, y, acc);
+            if (grp == 0) row_epilogue<P, FLAGS>(row, p0, s, sc, ucur, y, acc);
         }
     } else {
         const int sb = blockIdx.x - long_blocks;
         const int groups_total = (gridDim.x - long_blocks) * WAVES * G::GPW;
         for (int row = (sb * WAVES + wave) * G::GPW + grp; row < n; row += groups_total) {
-            const int beg = row_ptr[row];
-            const int end = row_ptr[row + 1];
+            const int beg = ld_stream<FLAGS>(row_ptr + row);
+            const int end = ld_stream<FLAGS>(row_ptr + row + 1);
             if (end - beg > long_thresh) continue;  // owned by a long-row wave
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            row_gather<P>(beg, end, 1, p0, col, val, ucur, s);
-            row_epilogue<P>(row, p0, s, sc, sp, first, ucur, uprev, y, acc);
+            row_gather<P, FLAGS>(beg, end, 1, p0, col, val, ucur, s);
+            row_epilogue<P, FLAGS>(row, p0, s, sc, ucur, y, acc);
         }
     }
 
-    // reduce over the row groups of this wave (lanes sharing `sub`)
+    // reduce over the row groups of this wave (lanes sharing `sub`), then waves
 #pragma unroll
     for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
-        for (int q = 0; q < NG; ++q)
-#pragma unroll
-            for (int e = 0; e < G::VEC; ++e) acc[q][e] += __shfl_xor(acc[q][e], o, 64);
-
-    __shared__ double red[WAVES][NG][P];
+        for (int e = 0; e < G::VEC; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
+    __shared__ double red[WAVES][P];
     if (grp == 0) {
 #pragma unroll
-        for (int q = 0; q < NG; ++q)
-#pragma unroll
-            for (int e = 0; e < G::VEC; ++e) red[wave][q][p0 + e] = acc[q][e];
+        for (int e = 0; e < G::VEC; ++e) red[wave][p0 + e] = acc[e];
     }
     __syncthreads();
-    // slab layout [P][GQ] (GQ = 8 >= NG, zero padded) so that one probe's
-    // Gram entries are 8 adjacent slots in the reduction kernel
-    for (int t = threadIdx.x; t < GQ * P; t += BLOCK) {
-        const int p = t / GQ, q = t % GQ;
+    for (int t = threadIdx.x; t < P; t += BLOCK) {
         double v = 0.0;
-        if (q < NG) {
 #pragma unroll
-            for (int w = 0; w < WAVES; ++w) v += red[w][q][p];
-        }
-        partial[(int64_t)blockIdx.x * GQ * P + t] = v;
+        for (int w = 0; w < WAVES; ++w) v += red[w][t];
+        partial[(int64_t)blockIdx.x * P + t] = v;
     }
 }
 
 // ---------------------------------------------------------------------------
 // Deterministic column reduction of per-block slabs [nblk][slots]: 64 slots
 // per workgroup (one per lane), 16 waves striding over the slabs in a fixed
-// order, LDS combine in wave order.  Returns the sum to every lane of wave 0.
+// order, LDS combine in wave order.  The sum lands in every lane of wave 0.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double reduce_cols(const double* __restrict__ partial, int nblk,
                                               int slots, int slot) {
@@ -290,45 +283,51 @@ __device__ __forceinline__ double reduce_cols(const double* __restrict__ partial
     return r;
 }
 
-// coef: CGS2 against the window [v0, v1] from the Gram matrix.
-//   pass 1: h = [v0.y, v1.y];  pass 2: h' = V'(y - V h) = h - (V'V) h
-//   c = h + h'  ->  H(j-1,j) = c0, H(j,j) = c1   (lanczos_krylov.m:88,109-115)
-// grid = ceil(8P/64) workgroups of 1024; writes coef[2][P], T-record rows.
+// k2s[4][P] carries the previous K2's sums: [0] ||u_cur||^2, [1] y_prev . u_cur,
+// [2] u_prev . u_cur, [3] ||u_prev||^2.  Window Gram (v = s u):
+//   g0 = v_prev.y = (A v_prev).v_cur = s_cur k2s[1]     (symmetry of A)
+//   g1 = v_cur.y  (K1 partials)
+//   G00 = s_prev^2 k2s[3], G01 = s_prev s_cur k2s[2], G11 = s_cur^2 k2s[0]
+// CGS2: h = (g0, g1), h' = h - G h, c = h + h' -> H(j-1,j) = c0, H(j,j) = c1.
 template <int P>
 __global__ __launch_bounds__(1024) void k_coef_cgs2(const double* __restrict__ partial, int nblk,
-                                                     int first, double* __restrict__ coef,
+                                                     int first, const double* __restrict__ k2s,
+                                                     const double* __restrict__ scale_cur,
+                                                     const double* __restrict__ scale_prev,
+                                                     double* __restrict__ coef,
                                                      double* __restrict__ t_alpha,
                                                      double* __restrict__ t_up) {
-    const int lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * 64 + lane;
-    const double r = reduce_cols(partial, nblk, GQ * P, slot);
-    if (threadIdx.x < 64) {
-        // lanes 8k..8k+7 hold probe p's [g0 g1 G00 G01 G11 0 0 0]
-        const int base = lane & ~7;
-        double g0 = __shfl(r, base + 0, 64), g1 = __shfl(r, base + 1, 64);
-        double G00 = __shfl(r, base + 2, 64), G01 = __shfl(r, base + 3, 64);
-        const double G11 = __shfl(r, base + 4, 64);
-        const int p = slot / GQ;
-        if ((lane & 7) == 0 && p < P) {
-            if (first) { g0 = 0.0; G00 = 0.0; G01 = 0.0; }
-            const double h0p = g0 - (G00 * g0 + G01 * g1);
-            const double h1p = g1 - (G01 * g0 + G11 * g1);
-            const double c0 = g0 + h0p, c1 = g1 + h1p;
-            coef[p] = c0;
-            coef[P + p] = c1;
-            t_alpha[p] = c1;
-            t_up[p] = c0;
+    const int p = blockIdx.x * 64 + (threadIdx.x & 63);
+    const double g1 = reduce_cols(partial, nblk, P, p);
+    if (threadIdx.x < 64 && p < P) {
+        const double sc = scale_cur[p];
+        const double G11 = sc * sc * k2s[0 * P + p];
+        double g0 = 0.0, G00 = 0.0, G01 = 0.0;
+        if (!first) {
+            const double sp = scale_prev[p];
+            g0 = sc * k2s[1 * P + p];
+            G01 = sp * sc * k2s[2 * P + p];
+            G00 = sp * sp * k2s[3 * P + p];
         }
+        const double h0p = g0 - (G00 * g0 + G01 * g1);
+        const double h1p = g1 - (G01 * g0 + G11 * g1);
+        const double c0 = g0 + h0p, c1 = g1 + h1p;
+        coef[p] = c0;
+        coef[P + p] = c1;
+        t_alpha[p] = c1;
+        t_up[p] = c0;
     }
 }
 
 // ---------------------------------------------------------------------------
-// K2: u_next = y - c0 * s_prev * u_prev - c1 * s_cur * u_cur  (in place over
-// u_prev), partial ||u_next||^2 per probe -> partial [gridDim.x][P].
+// K2: u_next = y - c0 s_prev u_prev - c1 s_cur u_cur (in place over u_prev);
+// partial slab [grid][P][4]: ||u_next||^2, y.u_next, u_cur.u_next, 0.
 // Pure streaming: rows are contiguous, so lanes cover 16 B each.
 // ---------------------------------------------------------------------------
+constexpr int KQ = 4;
+
 template <int P, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_update_norm(
+__global__ __launch_bounds__(BLOCK) void k_update(
     int n, const double* __restrict__ y, double* __restrict__ uprev,
     const double* __restrict__ ucur, const double* __restrict__ scale_cur,
     const double* __restrict__ scale_prev, const double* __restrict__ coef, int first,
@@ -341,73 +340,88 @@ __global__ __launch_bounds__(BLOCK) void k_update_norm(
     const int sub = lane % G::LPR;
     const int grp = lane / G::LPR;
     const int p0 = sub * G::VEC;
-    double a0[G::VEC], a1[G::VEC], acc[G::VEC];
+    double a0[G::VEC], a1[G::VEC], nn[G::VEC], yu[G::VEC], cu[G::VEC];
 #pragma unroll
     for (int e = 0; e < G::VEC; ++e) {
         a0[e] = first ? 0.0 : coef[p0 + e] * scale_prev[p0 + e];
         a1[e] = coef[P + p0 + e] * scale_cur[p0 + e];
-        acc[e] = 0.0;
+        nn[e] = yu[e] = cu[e] = 0.0;
     }
     const int groups_total = gridDim.x * WAVES * G::GPW;
     for (int row = (blockIdx.x * WAVES + wave) * G::GPW + grp; row < n; row += groups_total) {
         const int64_t off = (int64_t)row * P + p0;
         const typename V::T yv = V::load(y + off);
         const typename V::T cv = V::load(ucur + off);
+        typename V::T pv;
+        if (!first) pv = V::load(uprev + off);
         typename V::T o;
         double* op = reinterpret_cast<double*>(&o);
-        if (first) {
 #pragma unroll
-            for (int e = 0; e < G::VEC; ++e) {
-                const double u = fma(-a1[e], V::get(cv, e), V::get(yv, e));
-                op[e] = u;
-                acc[e] = fma(u, u, acc[e]);
-            }
-        } else {
-            const typename V::T pv = V::load(uprev + off);
-#pragma unroll
-            for (int e = 0; e < G::VEC; ++e) {
-                double u = fma(-a0[e], V::get(pv, e), V::get(yv, e));
-                u = fma(-a1[e], V::get(cv, e), u);
-                op[e] = u;
-                acc[e] = fma(u, u, acc[e]);
-            }
+        for (int e = 0; e < G::VEC; ++e) {
+            double u = V::get(yv, e);
+            if (!first) u = fma(-a0[e], V::get(pv, e), u);
+            u = fma(-a1[e], V::get(cv, e), u);
+            op[e] = u;
+            nn[e] = fma(u, u, nn[e]);
+            yu[e] = fma(V::get(yv, e), u, yu[e]);
+            cu[e] = fma(V::get(cv, e), u, cu[e]);
         }
         V::store(uprev + off, o);
     }
 #pragma unroll
     for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
-        for (int e = 0; e < G::VEC; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
-    __shared__ double red[WAVES][P];
+        for (int e = 0; e < G::VEC; ++e) {
+            nn[e] += __shfl_xor(nn[e], o, 64);
+            yu[e] += __shfl_xor(yu[e], o, 64);
+            cu[e] += __shfl_xor(cu[e], o, 64);
+        }
+    __shared__ double red[WAVES][3][P];
     if (grp == 0) {
 #pragma unroll
-        for (int e = 0; e < G::VEC; ++e) red[wave][p0 + e] = acc[e];
+        for (int e = 0; e < G::VEC; ++e) {
+            red[wave][0][p0 + e] = nn[e];
+            red[wave][1][p0 + e] = yu[e];
+            red[wave][2][p0 + e] = cu[e];
+        }
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < P; t += BLOCK) {
+    for (int t = threadIdx.x; t < KQ * P; t += BLOCK) {
+        const int p = t / KQ, q = t % KQ;
         double v = 0.0;
+        if (q < 3) {
 #pragma unroll
-        for (int w = 0; w < WAVES; ++w) v += red[w][t];
-        partial[(int64_t)blockIdx.x * P + t] = v;
+            for (int w = 0; w < WAVES; ++w) v += red[w][q][p];
+        }
+        partial[(int64_t)blockIdx.x * KQ * P + t] = v;
     }
 }
 
 // norm: beta = ||u_next||; s_next = 1/beta (0 after a lucky breakdown,
-// lanczos_krylov.m:91-93 with lucky_tol = 1e-8); T-record row `low` = beta.
+// lanczos_krylov.m:91-93, lucky_tol = 1e-8); T-record row `low` = beta;
+// refresh k2s for the next coef step.
 template <int P>
 __global__ __launch_bounds__(1024) void k_norm(const double* __restrict__ partial, int nblk,
+                                                double* __restrict__ k2s,
                                                 double* __restrict__ scale_next,
                                                 double* __restrict__ t_low) {
-    const int slot = blockIdx.x * 64 + (threadIdx.x & 63);
-    const double r = reduce_cols(partial, nblk, P, slot);
-    if (threadIdx.x < 64 && slot < P) {
-        const double beta = sqrt(r);
-        t_low[slot] = beta;
-        scale_next[slot] = (beta < 1e-8) ? 0.0 : 1.0 / beta;
+    const int lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 64 + lane;
+    const double r = reduce_cols(partial, nblk, KQ * P, slot);
+    if (threadIdx.x < 64 && slot < KQ * P) {
+        const int p = slot / KQ, q = slot % KQ;
+        if (q == 0) {
+            const double beta = sqrt(r);
+            t_low[p] = beta;
+            scale_next[p] = (beta < 1e-8) ? 0.0 : 1.0 / beta;
+            k2s[3 * P + p] = k2s[0 * P + p];
+            k2s[0 * P + p] = r;
+        } else if (q < 3) {
+            k2s[q * P + p] = r;
+        }
     }
 }
 
-// initial scale of a Rademacher block: ||z|| = sqrt(n)
 __global__ void k_fill(double* __restrict__ x, int count, double v) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < count) x[t] = v;
@@ -416,7 +430,7 @@ __global__ void k_fill(double* __restrict__ x, int count, double v) {
 }  // namespace kt
 
 // ---------------------------------------------------------------------------
-// host-side launchers (C++ linkage, used by kt_runtime.cpp)
+// host-side launchers (C++ linkage, used by the runtime)
 // ---------------------------------------------------------------------------
 #include "kt_launch.h"
 
@@ -466,41 +480,45 @@ hipError_t launch_rademacher(int P, int n, uint64_t seed, int64_t probe_base, co
     });
 }
 
-hipError_t launch_spmm_gram(int P, int grid, const int* rp, const int* ci, const double* va,
-                            int n, const double* ucur, const double* uprev, const double* sc,
-                            const double* sp, int first, double* y, double* partial,
-                            const int* long_rows, int n_long, int long_thresh, int long_blocks,
-                            hipStream_t st) {
-    return dispatch_p(P, [&](auto c) {
-        k_spmm_gram<decltype(c)::value, kBlock><<<grid, kBlock, 0, st>>>(
-            rp, ci, va, n, ucur, uprev, sc, sp, first, y, partial, long_rows, n_long,
-            long_thresh, long_blocks);
-    });
-}
-
-hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, double* coef,
-                            double* t_alpha, double* t_up, hipStream_t st) {
+hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int* ci,
+                           const double* va, int n, const double* ucur, const double* sc,
+                           double* y, double* partial, const int* long_rows, int n_long,
+                           int long_thresh, int long_blocks, hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
-        k_coef_cgs2<PP><<<(GQ * PP + 63) / 64, 1024, 0, st>>>(partial, nblk, first, coef,
-                                                             t_alpha, t_up);
+        if (flags & KF_NT)
+            k_spmm_dot<PP, kBlock, KF_NT><<<grid, kBlock, 0, st>>>(
+                rp, ci, va, n, ucur, sc, y, partial, long_rows, n_long, long_thresh, long_blocks);
+        else
+            k_spmm_dot<PP, kBlock, 0><<<grid, kBlock, 0, st>>>(
+                rp, ci, va, n, ucur, sc, y, partial, long_rows, n_long, long_thresh, long_blocks);
     });
 }
 
-hipError_t launch_update_norm(int P, int grid, int n, const double* y, double* uprev,
-                              const double* ucur, const double* sc, const double* sp,
-                              const double* coef, int first, double* partial, hipStream_t st) {
-    return dispatch_p(P, [&](auto c) {
-        k_update_norm<decltype(c)::value, kBlock><<<grid, kBlock, 0, st>>>(
-            n, y, uprev, ucur, sc, sp, coef, first, partial);
-    });
-}
-
-hipError_t launch_norm(int P, const double* partial, int nblk, double* scale_next, double* t_low,
-                       hipStream_t st) {
+hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, const double* k2s,
+                            const double* sc, const double* sp, double* coef, double* t_alpha,
+                            double* t_up, hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
-        k_norm<PP><<<(PP + 63) / 64, 1024, 0, st>>>(partial, nblk, scale_next, t_low);
+        k_coef_cgs2<PP><<<(PP + 63) / 64, 1024, 0, st>>>(partial, nblk, first, k2s, sc, sp, coef,
+                                                         t_alpha, t_up);
+    });
+}
+
+hipError_t launch_update(int P, int grid, int n, const double* y, double* uprev,
+                         const double* ucur, const double* sc, const double* sp,
+                         const double* coef, int first, double* partial, hipStream_t st) {
+    return dispatch_p(P, [&](auto c) {
+        k_update<decltype(c)::value, kBlock><<<grid, kBlock, 0, st>>>(n, y, uprev, ucur, sc, sp,
+                                                                      coef, first, partial);
+    });
+}
+
+hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, double* scale_next,
+                       double* t_low, hipStream_t st) {
+    return dispatch_p(P, [&](auto c) {
+        constexpr int PP = decltype(c)::value;
+        k_norm<PP><<<(KQ * PP + 63) / 64, 1024, 0, st>>>(partial, nblk, k2s, scale_next, t_low);
     });
 }
 

@@ -10,18 +10,18 @@ int long_blocks_for(int n_long, int max_blocks);
 
 hipError_t launch_rademacher(int P, int n, uint64_t seed, int64_t probe_base, const int* perm,
                              double* X, hipStream_t st);
-hipError_t launch_spmm_gram(int P, int grid, const int* rp, const int* ci, const double* va,
-                            int n, const double* ucur, const double* uprev, const double* sc,
-                            const double* sp, int first, double* y, double* partial,
-                            const int* long_rows, int n_long, int long_thresh, int long_blocks,
-                            hipStream_t st);
-hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, double* coef,
-                            double* t_alpha, double* t_up, hipStream_t st);
-hipError_t launch_update_norm(int P, int grid, int n, const double* y, double* uprev,
-                              const double* ucur, const double* sc, const double* sp,
-                              const double* coef, int first, double* partial, hipStream_t st);
-hipError_t launch_norm(int P, const double* partial, int nblk, double* scale_next, double* t_low,
-                       hipStream_t st);
+hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int* ci,
+                           const double* va, int n, const double* ucur, const double* sc,
+                           double* y, double* partial, const int* long_rows, int n_long,
+                           int long_thresh, int long_blocks, hipStream_t st);
+hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, const double* k2s,
+                            const double* sc, const double* sp, double* coef, double* t_alpha,
+                            double* t_up, hipStream_t st);
+hipError_t launch_update(int P, int grid, int n, const double* y, double* uprev,
+                         const double* ucur, const double* sc, const double* sp,
+                         const double* coef, int first, double* partial, hipStream_t st);
+hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, double* scale_next,
+                       double* t_low, hipStream_t st);
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st);
 
 }  // namespace kt

@@ -97,6 +97,7 @@ int kt_context_create(int device, kt_context_t* out) {
     hipDeviceProp_t prop;
     KT_HIP(hipGetDeviceProperties(&prop, device));
     ctx->num_cu = prop.multiProcessorCount;
+    if (const char* f = getenv("KT_K1_FLAGS")) ctx->k1_flags = atoi(f);
     KT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     *out = ctx;
     KT_GUARD_END
@@ -111,7 +112,7 @@ int kt_context_destroy(kt_context_t ctx) {
         for (auto e : s.ev) (void)hipEventDestroy(e);
     Workspace& w = ctx->ws;
     w.X0.release(); w.X1.release(); w.Y.release(); w.partial.release();
-    w.coef.release(); w.scales.release(); w.trec.release(); w.host_trec.release();
+    w.coef.release(); w.scales.release(); w.k2s.release(); w.trec.release(); w.host_trec.release();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     KT_GUARD_END

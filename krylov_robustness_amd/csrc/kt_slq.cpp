@@ -1,7 +1,7 @@
 // kt_slq.cpp -- driver of the probe-Lanczos quadrature hot path.
 //
 // For each sweep of P probes (one n x P probe block), m Lanczos steps run as
-// four launches each (K1 spmm_gram, coef, K2 update_norm, norm; see
+// four launches each (K1 spmm_dot, coef, K2 update, norm; see
 // kt_kernels.hip).  The per-probe recurrence coefficients (alpha, up, low)
 // go to a pinned host record; once all sweeps are queued the host solves
 // the m x m tridiagonal eigenproblems (kt_dense.cpp) and forms
@@ -57,7 +57,8 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         w.X0.ensure(blk_bytes);
         w.X1.ensure(blk_bytes);
         w.Y.ensure(blk_bytes);
-        w.partial.ensure(sizeof(double) * (size_t)(grid1 * 8 + grid) * P);
+        w.partial.ensure(sizeof(double) * (size_t)(grid1 + grid * 4) * P);
+        w.k2s.ensure(sizeof(double) * 4 * P);
         w.coef.ensure(sizeof(double) * 2 * P);
         w.scales.ensure(sizeof(double) * 3 * P);
         const size_t rec = (size_t)3 * m * P;  // [alpha | up | low][m][P]
@@ -65,7 +66,8 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         w.host_trec.ensure(sizeof(double) * rec * nsweeps);
 
         double* part1 = w.partial.as<double>();
-        double* part2 = part1 + (size_t)grid1 * 8 * P;
+        double* part2 = part1 + (size_t)grid1 * P;
+        double* k2s = w.k2s.as<double>();
         double* coef = w.coef.as<double>();
         double* trec = w.trec.as<double>();
         double* htrec = w.host_trec.as<double>();
@@ -78,20 +80,22 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
             double* sn = sc + 2 * P;
             KT_HIP(launch_rademacher(P, n, seed, probe_offset + s * P, A->d_perm, ucur, st));
             KT_HIP(launch_fill(sc, P, 1.0 / std::sqrt((double)n), st));
+            KT_HIP(launch_fill(k2s, P, (double)n, st));  // ||z||^2 = n
             for (int j = 0; j < m; ++j) {
                 const int first = (j == 0);
                 prof_begin(ctx, PROF_SPMM);
-                KT_HIP(launch_spmm_gram(P, grid1, A->d_rowptr, A->d_col, A->d_val, n, ucur, uprev,
-                                        sc, sp, first, w.Y.as<double>(), part1, A->d_long_rows,
-                                        A->n_long, A->long_thresh, lblocks, st));
+                KT_HIP(launch_spmm_dot(P, ctx->k1_flags, grid1, A->d_rowptr, A->d_col, A->d_val, n,
+                                       ucur, sc, w.Y.as<double>(), part1, A->d_long_rows,
+                                       A->n_long, A->long_thresh, lblocks, st));
                 prof_end(ctx, PROF_SPMM);
-                KT_HIP(launch_coef_cgs2(P, part1, grid1, first, coef, trec + (size_t)(0 * m + j) * P,
+                KT_HIP(launch_coef_cgs2(P, part1, grid1, first, k2s, sc, sp, coef,
+                                        trec + (size_t)(0 * m + j) * P,
                                         trec + (size_t)(1 * m + j) * P, st));
                 prof_begin(ctx, PROF_UPDATE);
-                KT_HIP(launch_update_norm(P, grid, n, w.Y.as<double>(), uprev, ucur, sc, sp, coef,
-                                          first, part2, st));
+                KT_HIP(launch_update(P, grid, n, w.Y.as<double>(), uprev, ucur, sc, sp, coef, first,
+                                     part2, st));
                 prof_end(ctx, PROF_UPDATE);
-                KT_HIP(launch_norm(P, part2, grid, sn, trec + (size_t)(2 * m + j) * P, st));
+                KT_HIP(launch_norm(P, part2, grid, k2s, sn, trec + (size_t)(2 * m + j) * P, st));
                 std::swap(ucur, uprev);  // uprev now holds u_{j+1}
                 double* t = sp;
                 sp = sc;

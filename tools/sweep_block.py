@@ -24,10 +24,11 @@ def main():
     else:
         A = graphs.erdos_renyi(100_000, 500_000, seed=0)
     print(f"graph {a.config} n={A.shape[0]} nnz={A.nnz} gen {time.time()-t:.1f}s", flush=True)
-    ctx = kra.Context(0)
     n, nnz = A.shape[0], A.nnz
     for var in a.variants.split(","):
       os.environ["KT_RELABEL"] = "0" if var == "natural" else "1"
+      os.environ["KT_K1_FLAGS"] = "1" if var == "nt" else "0"
+      ctx = kra.Context(0)
       D = kra.DeviceMatrix(A, ctx)
       print(f"--- variant {var}", flush=True)
       for P in [int(x) for x in a.blocks.split(",")]:
@@ -40,7 +41,7 @@ def main():
           l1, ms1 = ctx.profile_read(0)
           l2, ms2 = ctx.profile_read(1)
           k1 = ms1 / max(l1, 1); k2 = ms2 / max(l2, 1)
-          k1_bytes = 12 * nnz + 4 * (n + 1) + 24 * n * P
+          k1_bytes = 12 * nnz + 4 * (n + 1) + 16 * n * P
           k2_bytes = 32 * n * P
           per_eval_1024 = el / a.nprobes * 1024
           print(f"P={P:4d} total {el*1e3:9.1f} ms  ({1/per_eval_1024:7.3f} evals/s @1024 probes) "
