@@ -107,6 +107,7 @@ struct kt_matrix_s {
     // row r holds original row new2old[r].  Probes stay keyed by ORIGINAL
     // index (d_perm = new2old), so results do not depend on the relabelling.
     bool relabeled = false;
+    bool unit_values = false;  // every stored value == 1.0 (unweighted adjacency)
     int* d_perm = nullptr;
     std::vector<int32_t> new2old, old2new;
     // host copy (CSR, int64 pointers) for host-side algorithms and checks

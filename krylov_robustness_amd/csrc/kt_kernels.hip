@@ -52,7 +52,10 @@ template <int P> struct Geo {
 // FLAGS bit 0: non-temporal hints on the streamed (read-once) traffic of K1
 // (CSR arrays, own-row vector read, y store) so it does not evict the
 // gathered probe block from L2.
-enum : int { KF_NT = 1 };
+// FLAGS bit 1: unit-weight adjacency (every stored value is 1.0, detected at
+// matrix creation): the values array is never read (4 B per nonzero instead
+// of 12).
+enum : int { KF_NT = 1, KF_UNIT = 2 };
 
 template <int VEC> struct VecT;
 template <> struct VecT<1> {
@@ -131,9 +134,13 @@ __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
         const int c0 = ld_stream<FLAGS>(col + k), c1 = ld_stream<FLAGS>(col + k + stride);
         const int c2 = ld_stream<FLAGS>(col + k + 2 * stride);
         const int c3 = ld_stream<FLAGS>(col + k + 3 * stride);
-        const double a0 = ld_stream<FLAGS>(val + k), a1 = ld_stream<FLAGS>(val + k + stride);
-        const double a2 = ld_stream<FLAGS>(val + k + 2 * stride);
-        const double a3 = ld_stream<FLAGS>(val + k + 3 * stride);
+        double a0 = 1.0, a1 = 1.0, a2 = 1.0, a3 = 1.0;
+        if constexpr (!(FLAGS & KF_UNIT)) {
+            a0 = ld_stream<FLAGS>(val + k);
+            a1 = ld_stream<FLAGS>(val + k + stride);
+            a2 = ld_stream<FLAGS>(val + k + 2 * stride);
+            a3 = ld_stream<FLAGS>(val + k + 3 * stride);
+        }
         const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
         const typename V::T x1 = V::load(ucur + (int64_t)c1 * P + p0);
         const typename V::T x2 = V::load(ucur + (int64_t)c2 * P + p0);
@@ -148,7 +155,8 @@ __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
     }
     for (; k < end; k += stride) {
         const int c0 = ld_stream<FLAGS>(col + k);
-        const double a0 = ld_stream<FLAGS>(val + k);
+        double a0 = 1.0;
+        if constexpr (!(FLAGS & KF_UNIT)) a0 = ld_stream<FLAGS>(val + k);
         const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
 #pragma unroll
         for (int e = 0; e < G::VEC; ++e) s[e] = fma(a0, V::get(x0, e), s[e]);
@@ -248,7 +256,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
         double v = 0.0;
 #pragma unroll
         for (int w = 0; w < WAVES; ++w) v += red[w][t];
-        partial[(int64_t)blockIdx.x * P + t] = v;
+        partial[(int64_t)t * gridDim.x + blockIdx.x] = v;  // slot-major [P][grid]
     }
 }
 
@@ -257,30 +265,23 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
 // per workgroup (one per lane), 16 waves striding over the slabs in a fixed
 // order, LDS combine in wave order.  The sum lands in every lane of wave 0.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double reduce_cols(const double* __restrict__ partial, int nblk,
-                                              int slots, int slot) {
-    __shared__ double tmp[16][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// Slot-major slabs: partial[slot * nblk + b].  One WAVE per slot reads the
+// slot's nblk partials with coalesced loads (all in flight at once), sums
+// lane-wise in block order, then a fixed xor-tree -- deterministic.
+__device__ __forceinline__ double wave_reduce_slot(const double* __restrict__ partial, int nblk,
+                                                   int slot) {
+    const int lane = threadIdx.x & 63;
+    const double* base = partial + (int64_t)slot * nblk;
     double v = 0.0;
-    if (slot < slots) {
-        int b = wave;
-        for (; b + 48 < nblk; b += 64) {  // 4 loads in flight
-            const double x0 = partial[(int64_t)b * slots + slot];
-            const double x1 = partial[(int64_t)(b + 16) * slots + slot];
-            const double x2 = partial[(int64_t)(b + 32) * slots + slot];
-            const double x3 = partial[(int64_t)(b + 48) * slots + slot];
-            v += x0; v += x1; v += x2; v += x3;
-        }
-        for (; b < nblk; b += 16) v += partial[(int64_t)b * slots + slot];
+    int b = lane;
+    for (; b + 192 < nblk; b += 256) {
+        const double x0 = base[b], x1 = base[b + 64], x2 = base[b + 128], x3 = base[b + 192];
+        v += x0; v += x1; v += x2; v += x3;
     }
-    tmp[wave][lane] = v;
-    __syncthreads();
-    double r = 0.0;
-    if (wave == 0) {
+    for (; b < nblk; b += 64) v += base[b];
 #pragma unroll
-        for (int w = 0; w < 16; ++w) r += tmp[w][lane];
-    }
-    return r;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
 // k2s[4][P] carries the previous K2's sums: [0] ||u_cur||^2, [1] y_prev . u_cur,
@@ -290,16 +291,17 @@ __device__ __forceinline__ double reduce_cols(const double* __restrict__ partial
 //   G00 = s_prev^2 k2s[3], G01 = s_prev s_cur k2s[2], G11 = s_cur^2 k2s[0]
 // CGS2: h = (g0, g1), h' = h - G h, c = h + h' -> H(j-1,j) = c0, H(j,j) = c1.
 template <int P>
-__global__ __launch_bounds__(1024) void k_coef_cgs2(const double* __restrict__ partial, int nblk,
-                                                     int first, const double* __restrict__ k2s,
-                                                     const double* __restrict__ scale_cur,
-                                                     const double* __restrict__ scale_prev,
-                                                     double* __restrict__ coef,
-                                                     double* __restrict__ t_alpha,
-                                                     double* __restrict__ t_up) {
-    const int p = blockIdx.x * 64 + (threadIdx.x & 63);
-    const double g1 = reduce_cols(partial, nblk, P, p);
-    if (threadIdx.x < 64 && p < P) {
+__global__ __launch_bounds__(256) void k_coef_cgs2(const double* __restrict__ partial, int nblk,
+                                                    int first, const double* __restrict__ k2s,
+                                                    const double* __restrict__ scale_cur,
+                                                    const double* __restrict__ scale_prev,
+                                                    double* __restrict__ coef,
+                                                    double* __restrict__ t_alpha,
+                                                    double* __restrict__ t_up) {
+    const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p >= P) return;
+    const double g1 = wave_reduce_slot(partial, nblk, p);
+    if ((threadIdx.x & 63) == 0) {
         const double sc = scale_cur[p];
         const double G11 = sc * sc * k2s[0 * P + p];
         double g0 = 0.0, G00 = 0.0, G01 = 0.0;
@@ -321,7 +323,7 @@ __global__ __launch_bounds__(1024) void k_coef_cgs2(const double* __restrict__ p
 
 // ---------------------------------------------------------------------------
 // K2: u_next = y - c0 s_prev u_prev - c1 s_cur u_cur (in place over u_prev);
-// partial slab [grid][P][4]: ||u_next||^2, y.u_next, u_cur.u_next, 0.
+// partial slabs [3][P][grid]: ||u_next||^2, y.u_next, u_cur.u_next.
 // Pure streaming: rows are contiguous, so lanes cover 16 B each.
 // ---------------------------------------------------------------------------
 constexpr int KQ = 4;
@@ -386,14 +388,12 @@ __global__ __launch_bounds__(BLOCK) void k_update(
         }
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < KQ * P; t += BLOCK) {
-        const int p = t / KQ, q = t % KQ;
+    for (int t = threadIdx.x; t < 3 * P; t += BLOCK) {  // slot t = q * P + p
+        const int q = t / P, p = t % P;
         double v = 0.0;
-        if (q < 3) {
 #pragma unroll
-            for (int w = 0; w < WAVES; ++w) v += red[w][q][p];
-        }
-        partial[(int64_t)blockIdx.x * KQ * P + t] = v;
+        for (int w = 0; w < WAVES; ++w) v += red[w][q][p];
+        partial[(int64_t)t * gridDim.x + blockIdx.x] = v;
     }
 }
 
@@ -401,22 +401,22 @@ __global__ __launch_bounds__(BLOCK) void k_update(
 // lanczos_krylov.m:91-93, lucky_tol = 1e-8); T-record row `low` = beta;
 // refresh k2s for the next coef step.
 template <int P>
-__global__ __launch_bounds__(1024) void k_norm(const double* __restrict__ partial, int nblk,
-                                                double* __restrict__ k2s,
-                                                double* __restrict__ scale_next,
-                                                double* __restrict__ t_low) {
-    const int lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * 64 + lane;
-    const double r = reduce_cols(partial, nblk, KQ * P, slot);
-    if (threadIdx.x < 64 && slot < KQ * P) {
-        const int p = slot / KQ, q = slot % KQ;
+__global__ __launch_bounds__(256) void k_norm(const double* __restrict__ partial, int nblk,
+                                               double* __restrict__ k2s,
+                                               double* __restrict__ scale_next,
+                                               double* __restrict__ t_low) {
+    const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);  // slot = q * P + p
+    if (slot >= 3 * P) return;
+    const double r = wave_reduce_slot(partial, nblk, slot);
+    if ((threadIdx.x & 63) == 0) {
+        const int q = slot / P, p = slot % P;
         if (q == 0) {
             const double beta = sqrt(r);
             t_low[p] = beta;
             scale_next[p] = (beta < 1e-8) ? 0.0 : 1.0 / beta;
             k2s[3 * P + p] = k2s[0 * P + p];
             k2s[0 * P + p] = r;
-        } else if (q < 3) {
+        } else {
             k2s[q * P + p] = r;
         }
     }
@@ -486,12 +486,16 @@ hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int*
                            int long_thresh, int long_blocks, hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
-        if (flags & KF_NT)
-            k_spmm_dot<PP, kBlock, KF_NT><<<grid, kBlock, 0, st>>>(
-                rp, ci, va, n, ucur, sc, y, partial, long_rows, n_long, long_thresh, long_blocks);
-        else
-            k_spmm_dot<PP, kBlock, 0><<<grid, kBlock, 0, st>>>(
-                rp, ci, va, n, ucur, sc, y, partial, long_rows, n_long, long_thresh, long_blocks);
+#define KT_K1(F)                                                                              \
+    k_spmm_dot<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, ucur, sc, y, partial,      \
+                                                       long_rows, n_long, long_thresh, long_blocks)
+        switch (flags & 3) {
+        case 0: KT_K1(0); break;
+        case KF_NT: KT_K1(KF_NT); break;
+        case KF_UNIT: KT_K1(KF_UNIT); break;
+        default: KT_K1(KF_NT | KF_UNIT); break;
+        }
+#undef KT_K1
     });
 }
 
@@ -500,8 +504,8 @@ hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, c
                             double* t_up, hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
-        k_coef_cgs2<PP><<<(PP + 63) / 64, 1024, 0, st>>>(partial, nblk, first, k2s, sc, sp, coef,
-                                                         t_alpha, t_up);
+        k_coef_cgs2<PP><<<(PP + 3) / 4, 256, 0, st>>>(partial, nblk, first, k2s, sc, sp, coef,
+                                                      t_alpha, t_up);
     });
 }
 
@@ -518,7 +522,7 @@ hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, doub
                        double* t_low, hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
-        k_norm<PP><<<(KQ * PP + 63) / 64, 1024, 0, st>>>(partial, nblk, k2s, scale_next, t_low);
+        k_norm<PP><<<(3 * PP + 3) / 4, 256, 0, st>>>(partial, nblk, k2s, scale_next, t_low);
     });
 }
 

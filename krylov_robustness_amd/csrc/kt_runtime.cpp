@@ -222,6 +222,9 @@ int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr, con
             KT_HIP(hipMemcpy(A->d_col, c32.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
             KT_HIP(hipMemcpy(A->d_val, v64.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
         }
+        const char* un = getenv("KT_UNIT");
+        A->unit_values = !(un && un[0] == '0') &&
+                         std::all_of(v64.begin(), v64.end(), [](double v) { return v == 1.0; });
         // long-row list (device numbering) for K1's wave-per-row mode, heaviest first
         std::vector<int32_t> lr;
         for (int64_t r = 0; r < n; ++r)

@@ -57,7 +57,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         w.X0.ensure(blk_bytes);
         w.X1.ensure(blk_bytes);
         w.Y.ensure(blk_bytes);
-        w.partial.ensure(sizeof(double) * (size_t)(grid1 + grid * 4) * P);
+        w.partial.ensure(sizeof(double) * (size_t)(grid1 + grid * 3) * P);
         w.k2s.ensure(sizeof(double) * 4 * P);
         w.coef.ensure(sizeof(double) * 2 * P);
         w.scales.ensure(sizeof(double) * 3 * P);
@@ -84,7 +84,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
             for (int j = 0; j < m; ++j) {
                 const int first = (j == 0);
                 prof_begin(ctx, PROF_SPMM);
-                KT_HIP(launch_spmm_dot(P, ctx->k1_flags, grid1, A->d_rowptr, A->d_col, A->d_val, n,
+                KT_HIP(launch_spmm_dot(P, ctx->k1_flags | (A->unit_values ? 2 : 0), grid1, A->d_rowptr, A->d_col, A->d_val, n,
                                        ucur, sc, w.Y.as<double>(), part1, A->d_long_rows,
                                        A->n_long, A->long_thresh, lblocks, st));
                 prof_end(ctx, PROF_SPMM);

@@ -28,6 +28,7 @@ def main():
     for var in a.variants.split(","):
       os.environ["KT_RELABEL"] = "0" if var == "natural" else "1"
       os.environ["KT_K1_FLAGS"] = "1" if var == "nt" else "0"
+      os.environ["KT_UNIT"] = "0" if var == "valued" else "1"
       ctx = kra.Context(0)
       D = kra.DeviceMatrix(A, ctx)
       print(f"--- variant {var}", flush=True)
