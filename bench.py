@@ -73,6 +73,22 @@ def cpu_baseline(A, m, budget_s, nprobes_eval):
                       f"{el:.1f} s with {threads} OpenMP threads, extrapolated"}
 
 
+def _pmc_traffic(kernel_prefix):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    counter summary (profiles/traffic.json, produced by tools/gpu_prof.sh +
+    tools/pmc_traffic.py on this same bench command), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for k, v in t.items():
+        if k.startswith(kernel_prefix) and isinstance(v, dict):
+            return v.get("hbm_bytes_per_launch")
+    return None
+
+
 def main():
     args = parse()
     import torch  # noqa: F401  -- load torch's HIP runtime first (one runtime per process)
@@ -95,7 +111,7 @@ def main():
     ctx = kra.Context(local_rank)
     D = kra.DeviceMatrix(A, ctx)
     off, cnt = kdist.probe_shard(N, rank, world)
-    P = args.block or _auto_block(n, cnt)
+    P = args.block or kra.slq_plan(D, cnt, ctx=ctx)
 
     def step(seed):
         s1, s2, _ = kra.slq_quadforms(D, cnt, m, seed=seed, probe_offset=off, block=P, ctx=ctx)
@@ -138,9 +154,10 @@ def main():
         if l1:
             k1_ms = ms1 / l1
             achieved = k1_bytes / (k1_ms * 1e-3) / 1e9
+            traffic = _pmc_traffic(f"k_spmm_dot<{P}")
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": f"k_spmm_gram<P={P}>", "avg_launch_us": round(k1_ms * 1e3, 2),
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": f"k_spmm_dot<{P}>", "avg_launch_us": round(k1_ms * 1e3, 2),
                     "algorithmic_bytes_per_launch": k1_bytes}
             extra["k2_update_avg_us"] = round(ms2 / max(l2, 1) * 1e3, 2)
     eval_gbs = b_eval_rank / (ms_per_step * 1e-3) / 1e9
@@ -164,15 +181,6 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def _auto_block(n, cnt):
-    P = 128
-    while P > 8 and n * 8.0 * P > 96.0 * 1024 * 1024:
-        P //= 2
-    while P > 1 and P // 2 >= cnt:
-        P //= 2
-    return P
 
 
 if __name__ == "__main__":

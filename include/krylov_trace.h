@@ -86,6 +86,9 @@ int kt_matrix_info(kt_matrix_t A, int64_t* n, int64_t* nnz);
 int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_t probe_offset,
                  int64_t nprobes, int block, double* sum_q, double* sum_q2, double* q);
 
+/* The probes-per-sweep width kt_slq_trace picks when block == 0. */
+int kt_slq_plan(kt_matrix_t A, int64_t nprobes, int* block);
+
 /* Per-kernel timing (HIP events recorded on the library's stream around each
  * launch of the named kernel while enabled).  kernel: 0 = spmm_gram (K1),
  * 1 = update_norm (K2).  Returns launch count and summed milliseconds. */

@@ -48,6 +48,7 @@ SIGNATURES = [
     ("kt_matrix_info", C.c_int, [_mat_p, _i64p, _i64p]),
     ("kt_slq_trace", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int,
                                _dp, _dp, _dp]),
+    ("kt_slq_plan", C.c_int, [_mat_p, C.c_int64, _ip]),
     ("kt_profile_enable", C.c_int, [_ctx_p, C.c_int]),
     ("kt_profile_read", C.c_int, [_ctx_p, C.c_int, _i64p, _dp]),
     ("kt_profile_reset", C.c_int, [_ctx_p]),

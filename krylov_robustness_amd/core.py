@@ -148,6 +148,14 @@ def slq_quadforms(A, nprobes: int, m: int, seed: int = 0, fun="exp", probe_offse
     return float(s1.value), float(s2.value), q[:nprobes]
 
 
+def slq_plan(A, nprobes: int, ctx: Optional[Context] = None) -> int:
+    """Probes per SpMM sweep that slq_quadforms uses with block=0."""
+    D = _dev(A, ctx)
+    b = C.c_int()
+    _lib.check(_lib.load().kt_slq_plan(D.handle, int(nprobes), C.byref(b)))
+    return int(b.value)
+
+
 def slq_trace(A, nprobes: int, m: int, seed: int = 0, fun="exp", block: int = 0,
               ctx: Optional[Context] = None):
     """Plain-Hutchinson trace(f(A)) estimate with Lanczos quadrature."""

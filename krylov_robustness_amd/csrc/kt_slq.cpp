@@ -16,10 +16,12 @@
 namespace kt {
 
 static int auto_block(int64_t n, int64_t nprobes) {
-    // Keep one n x P block of the gathered vector (8nP bytes) well inside the
-    // 256 MiB Infinity Cache so that the A-driven gathers hit on-die.
+    // Largest power-of-two P whose gathered n x P block (8nP bytes) stays
+    // within ~160 MB, i.e. inside the 256 MiB Infinity Cache next to the CSR
+    // stream; measured best on MI355X for n = 1M (P = 16) and n = 100k
+    // (P = 128) -- profiles/r01_sweep.txt.
     int P = 128;
-    while (P > 8 && (double)n * 8.0 * P > 96.0 * 1024 * 1024) P >>= 1;
+    while (P > 8 && (double)n * 8.0 * P > 160.0e6) P >>= 1;
     while (P > 1 && P / 2 >= nprobes) P >>= 1;
     return P;
 }
@@ -29,6 +31,15 @@ static bool pow2_le128(int b) { return b >= 1 && b <= 128 && (b & (b - 1)) == 0;
 }  // namespace kt
 
 using namespace kt;
+
+extern "C" int kt_slq_plan(kt_matrix_t A, int64_t nprobes, int* block) {
+    if (!A || !block || nprobes < 0) {
+        kt::set_error("kt_slq_plan: bad argument");
+        return KT_ERR_ARG;
+    }
+    *block = auto_block(A->n, nprobes);
+    return KT_OK;
+}
 
 extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_t probe_offset,
                             int64_t nprobes, int block, double* sum_q, double* sum_q2, double* q) {
