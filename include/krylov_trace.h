@@ -89,6 +89,42 @@ int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_t probe_off
 /* The probes-per-sweep width kt_slq_trace picks when block == 0. */
 int kt_slq_plan(kt_matrix_t A, int64_t nprobes, int* block);
 
+/* ---- block-Krylov entry points (bs = number of columns of U, <= 128) ------
+ * U: n x rk column-major in ORIGINAL row numbering; B: rk x rk column-major.
+ * it <= 0 selects the reference default min(100, n). */
+
+/* MATLAB normest(A, tol): power estimate of ||A||_2 (called with tol 1e-2 at
+ * fun_and_grad_krylov_exp.m:26 / fun_and_grad_krylov_fun.m:27). */
+int kt_normest(kt_matrix_t A, double tol, double* nrm);
+
+/* [Xm, iter, lucky] = trace_fun_update(A, U, B, tol, it, debug, fun)
+ * (trace_fun_update.m:1): tr f(A + U B U') - tr f(A) by block Lanczos seeded
+ * with U (lanczos_krylov.m), lag-2 stopping, dense path when n <= 130. */
+int kt_trace_fun_update(kt_matrix_t A, int64_t rk, const double* U, const double* B, double tol,
+                        int it, int fun, double* Xm, int* iter, int* lucky);
+
+/* [Xm, iter, lucky, Um] = fun_update(A, U, B, fun, tol, it, debug) with four
+ * outputs (fun_update.m:1, Arnoldi branch :77-91): f(A+UBU') - f(A) ~= Um Xm Um'.
+ * Xm is ncols x ncols (column-major, buffer of max_cols^2 doubles); Um (may be
+ * NULL) is n x ncols.  When the basis reaches n/2 columns the reference's
+ * dense fallback applies (:85-90): Um = eye(n), ncols = n. */
+int kt_fun_update(kt_matrix_t A, int64_t rk, const double* U, const double* B, int fun, double tol,
+                  int it, int64_t max_cols, double* Xm, int64_t* ncols, int* iter, int* lucky,
+                  double* Um);
+
+/* [f, gr] = fun_and_grad_krylov_exp(X, A, Omega, eA, tol, it, debug)
+ * (fun_and_grad_krylov_exp.m:1).  Omega: nomega x 2 column-major, 1-based
+ * (MATLAB doubles); X, eA, gr: nomega.  KT_ERR_NOT_HERMITIAN if A is not
+ * symmetric ("FUN_AND_GRAD_KRYLOV:: matrix A is not Hermitian"). */
+int kt_fun_and_grad_krylov_exp(kt_matrix_t A, int64_t nomega, const double* X, const double* Omega,
+                               const double* eA, double tol, int it, double* f, double* gr);
+
+/* [f, gr] = fun_and_grad_krylov_fun(X, A, Omega, fun, dfun, dfA, tol, it, debug, fun_M)
+ * (fun_and_grad_krylov_fun.m:1); fun / dfun are kt_fun codes. */
+int kt_fun_and_grad_krylov_fun(kt_matrix_t A, int64_t nomega, const double* X, const double* Omega,
+                               int fun, int dfun, const double* dfA, double tol, int it, double* f,
+                               double* gr);
+
 /* Per-kernel timing (HIP events recorded on the library's stream around each
  * launch of the named kernel while enabled).  kernel: 0 = spmm_gram (K1),
  * 1 = update_norm (K2).  Returns launch count and summed milliseconds. */

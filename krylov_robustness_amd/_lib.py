@@ -2,6 +2,10 @@
 
 There is no fallback: if the in-tree shared library is missing or cannot be
 loaded, every entry point raises ``KrylovLibraryError``.
+
+If the process also uses torch, import torch FIRST: the library's ROCm
+dependencies (libamdhip64.so.7, librocblas.so.5, librocsolver.so.0) then bind
+to the copies torch already loaded (same SONAMEs) instead of a second runtime.
 """
 from __future__ import annotations
 
@@ -49,6 +53,15 @@ SIGNATURES = [
     ("kt_slq_trace", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int,
                                _dp, _dp, _dp]),
     ("kt_slq_plan", C.c_int, [_mat_p, C.c_int64, _ip]),
+    ("kt_normest", C.c_int, [_mat_p, C.c_double, _dp]),
+    ("kt_trace_fun_update", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_double, C.c_int, C.c_int,
+                                      _dp, _ip, _ip]),
+    ("kt_fun_update", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_int, C.c_double, C.c_int,
+                                C.c_int64, _dp, _i64p, _ip, _ip, _dp]),
+    ("kt_fun_and_grad_krylov_exp", C.c_int, [_mat_p, C.c_int64, _dp, _dp, _dp, C.c_double, C.c_int,
+                                             _dp, _dp]),
+    ("kt_fun_and_grad_krylov_fun", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_int, C.c_int, _dp,
+                                             C.c_double, C.c_int, _dp, _dp]),
     ("kt_profile_enable", C.c_int, [_ctx_p, C.c_int]),
     ("kt_profile_read", C.c_int, [_ctx_p, C.c_int, _i64p, _dp]),
     ("kt_profile_reset", C.c_int, [_ctx_p]),
@@ -69,7 +82,7 @@ def load():
                 f"{LIB_PATH} not found: build it with `make -C krylov_robustness_amd/csrc` "
                 "or __graft_entry__.build() (no CPU fallback exists)")
         try:
-            lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+            lib = C.CDLL(LIB_PATH)
         except OSError as e:  # pragma: no cover - depends on the box
             raise KrylovLibraryError(f"cannot load {LIB_PATH}: {e}") from e
         for name, res, args in SIGNATURES:

@@ -161,3 +161,103 @@ def slq_trace(A, nprobes: int, m: int, seed: int = 0, fun="exp", block: int = 0,
     """Plain-Hutchinson trace(f(A)) estimate with Lanczos quadrature."""
     s1, _, q = slq_quadforms(A, nprobes, m, seed, fun, 0, block, ctx)
     return s1 / max(nprobes, 1), q
+
+
+# ---------------------------------------------------------------------------
+# block-Krylov entry points (reference names and argument order)
+# ---------------------------------------------------------------------------
+def _dptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _colmajor(a, rows=None):
+    a = np.asarray(a, dtype=np.float64)
+    if a.ndim == 1:
+        a = a[:, None]
+    return np.asfortranarray(a)
+
+
+def normest(A, tol=1e-6, ctx: Optional[Context] = None) -> float:
+    """MATLAB normest(A, tol) (2-norm power estimate), as called at
+    fun_and_grad_krylov_exp.m:26."""
+    D = _dev(A, ctx)
+    out = C.c_double()
+    _lib.check(_lib.load().kt_normest(D.handle, float(tol), C.byref(out)))
+    return float(out.value)
+
+
+def trace_fun_update(A, U, B, tol=1e-12, it=None, debug=0, fun="exp", ctx: Optional[Context] = None):
+    """[Xm, iter, lucky] = trace_fun_update(A, U, B, tol, it, debug, fun)
+    (trace_fun_update.m:1)."""
+    D = _dev(A, ctx)
+    U = _colmajor(U)
+    B = _colmajor(np.atleast_2d(B))
+    xm = C.c_double()
+    itr = C.c_int()
+    lk = C.c_int()
+    _lib.check(_lib.load().kt_trace_fun_update(
+        D.handle, U.shape[1], _dptr(U), _dptr(B), float(tol), int(it or 0), _fun_code(fun),
+        C.byref(xm), C.byref(itr), C.byref(lk)))
+    return float(xm.value), int(itr.value), int(lk.value)
+
+
+def fun_update(A, U, B, fun="exp", tol=1e-12, it=None, debug=0, want_um=True,
+               ctx: Optional[Context] = None):
+    """[Xm, iter, lucky, Um] = fun_update(A, U, B, fun, tol, it, debug)
+    (fun_update.m:1, the four-output Arnoldi branch)."""
+    D = _dev(A, ctx)
+    U = _colmajor(U)
+    B = _colmajor(np.atleast_2d(B))
+    rk = U.shape[1]
+    its = int(it or min(100, D.n))
+    maxc = int(min(D.n, (its + 1) * rk))
+    Xm = np.zeros(maxc * maxc)
+    Um = np.zeros(D.n * maxc) if want_um else None
+    nc = C.c_int64()
+    itr = C.c_int()
+    lk = C.c_int()
+    _lib.check(_lib.load().kt_fun_update(
+        D.handle, rk, _dptr(U), _dptr(B), _fun_code(fun), float(tol), int(it or 0), maxc,
+        _dptr(Xm), C.byref(nc), C.byref(itr), C.byref(lk), _dptr(Um) if want_um else None))
+    k = int(nc.value)
+    X = Xm[:k * k].reshape(k, k, order="F")
+    Umat = Um[:D.n * k].reshape(D.n, k, order="F") if want_um else None
+    return X, int(itr.value), int(lk.value), Umat
+
+
+def _omega(Omega):
+    Om = np.asfortranarray(np.asarray(Omega, dtype=np.float64))
+    if Om.ndim != 2 or Om.shape[1] != 2:
+        raise _lib.KrylovError(_lib.KT_ERR_ARG, "Omega must be |Omega| x 2")
+    return Om
+
+
+def fun_and_grad_krylov_exp(X, A, Omega, eA, tol, it, debug=False, ctx: Optional[Context] = None):
+    """[f, gr] = fun_and_grad_krylov_exp(X, A, Omega, eA, tol, it, debug)
+    (fun_and_grad_krylov_exp.m:1)."""
+    D = _dev(A, ctx)
+    Om = _omega(Omega)
+    X = np.ascontiguousarray(np.asarray(X, dtype=np.float64).ravel())
+    eA = np.ascontiguousarray(np.asarray(eA, dtype=np.float64).ravel())
+    gr = np.zeros(Om.shape[0])
+    f = C.c_double()
+    _lib.check(_lib.load().kt_fun_and_grad_krylov_exp(
+        D.handle, Om.shape[0], _dptr(X), _dptr(Om), _dptr(eA), float(tol), int(it or 0),
+        C.byref(f), _dptr(gr)))
+    return float(f.value), gr
+
+
+def fun_and_grad_krylov_fun(X, A, Omega, fun, dfun, dfA, tol, it, debug=False, fun_M=None,
+                            ctx: Optional[Context] = None):
+    """[f, gr] = fun_and_grad_krylov_fun(X, A, Omega, fun, dfun, dfA, tol, it, debug, fun_M)
+    (fun_and_grad_krylov_fun.m:1)."""
+    D = _dev(A, ctx)
+    Om = _omega(Omega)
+    X = np.ascontiguousarray(np.asarray(X, dtype=np.float64).ravel())
+    dfA = np.ascontiguousarray(np.asarray(dfA, dtype=np.float64).ravel())
+    gr = np.zeros(Om.shape[0])
+    f = C.c_double()
+    _lib.check(_lib.load().kt_fun_and_grad_krylov_fun(
+        D.handle, Om.shape[0], _dptr(X), _dptr(Om), _fun_code(fun), _fun_code(dfun), _dptr(dfA),
+        float(tol), int(it or 0), C.byref(f), _dptr(gr)))
+    return float(f.value), gr

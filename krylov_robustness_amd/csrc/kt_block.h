@@ -1,0 +1,56 @@
+// kt_block.h -- device tall-skinny block operations for the block-Krylov paths
+// (lanczos_krylov.m / arnoldi_krylov.m with bs > 1, mc_trace.m's QR and
+// deflation).  Blocks are ROW-MAJOR n x ld device arrays in the matrix's
+// device row numbering (kt_runtime.cpp relabels rows by degree); a block of
+// bs columns occupies PB = pow2 >= bs columns, the padding kept at zero so
+// the SpMM kernel (which works on PB columns) multiplies zeros.
+#pragma once
+#include <rocblas/rocblas.h>
+
+#include <vector>
+
+#include "kt_internal.h"
+
+namespace kt {
+
+int pow2_at_least(int b);
+
+rocblas_handle blas(kt_context_s* ctx);
+
+// Row-major device array n x ld (zero-initialised).
+struct DevMat {
+    DevBuf buf;
+    int64_t n = 0;
+    int ld = 0;
+    void alloc(kt_context_s* ctx, int64_t n_, int ld_);
+    double* col(int c) { return buf.as<double>() + c; }
+    const double* col(int c) const { return static_cast<const double*>(buf.ptr) + c; }
+};
+
+// G (host, px x py column-major) = X[:, 0:px]' Y[:, 0:py]   (synchronises)
+void gram(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* Y,
+          int ldy, int py, std::vector<double>& G);
+// Y[:, 0:q] = beta * Y[:, 0:q] + X[:, 0:px] * C   (C host px x q column-major)
+void combine(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px,
+             const std::vector<double>& C, int q, double beta, double* Y, int ldy);
+// Y[:, 0:P] = A X[:, 0:P], P = pow2 >= cols (columns cols..P-1 of X must be 0)
+void spmm(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols);
+// copy a column slice (n x cols) between device arrays
+void copy_cols(kt_context_s* ctx, int64_t n, const double* X, int ldx, double* Y, int ldy, int cols);
+void zero_cols(kt_context_s* ctx, int64_t n, double* X, int ldx, int cols);
+// host column-major (original numbering) -> device row-major (device numbering)
+void upload_rows(kt_matrix_s* A, const double* H, int cols, double* D, int ldd);
+// device rows (given ORIGINAL row indices) -> host nrows x cols column-major
+void download_rows(kt_matrix_s* A, const double* D, int ldd, int cols,
+                   const std::vector<int64_t>& rows, std::vector<double>& out);
+// thin QR of W (n x bs at ld) in place: W <- Q, R upper bs x bs (column-major).
+// CholQR2 (shifted CholQR3 if W is ill-conditioned).  Returns false when W
+// is numerically zero (R = 0 then, Q unspecified): a lucky breakdown.
+bool cholqr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R);
+
+// small host helpers (column-major)
+void matmul(int m, int k, int n, const double* A, const double* B, double* C);  // C = A B
+double norm_fro(const std::vector<double>& M);
+double norm2_small(int m, int n, const double* M);  // spectral norm
+
+}  // namespace kt

@@ -78,6 +78,7 @@ enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_NSLOTS = 2 };
 
 struct Workspace {
     DevBuf X0, X1, Y, partial, coef, scales, k2s, trec;
+    DevBuf small, small2, qrtmp, eigA, eigW, eigInfo;  // block-Krylov scratch
     PinnedBuf host_trec;
 };
 
@@ -89,6 +90,7 @@ struct kt_context_s {
     int num_cu = 256;
     bool profile = false;
     int k1_flags = 0;  // KT_K1_FLAGS: bit 0 = non-temporal stream hints in K1
+    void* blas = nullptr;  // rocblas_handle, created on first block-Krylov use
     kt::ProfSlot prof[kt::PROF_NSLOTS];
     kt::Workspace ws;
 };
@@ -108,6 +110,7 @@ struct kt_matrix_s {
     // index (d_perm = new2old), so results do not depend on the relabelling.
     bool relabeled = false;
     bool unit_values = false;  // every stored value == 1.0 (unweighted adjacency)
+    int symmetric = -1;        // -1 unknown, 0 no, 1 yes (checked on the host copy)
     int* d_perm = nullptr;
     std::vector<int32_t> new2old, old2new;
     // host copy (CSR, int64 pointers) for host-side algorithms and checks
@@ -127,5 +130,9 @@ void prof_collect(kt_context_s* ctx);  // after stream sync: fold events into to
 double fscalar(int fun, double x);
 // Gauss quadrature e1' f(T) e1 for symmetric tridiagonal T (m x m).
 double tridiag_quadrature(int m, const double* alpha, const double* off, int fun);
+bool chol_upper(double* G, int n);
+void tri_upper_inv(const double* R, int n, double* X);
+void sym_eig_host(int n, const double* A, double* w, double* V);
+void sym_fun_from_eig(int n, const double* w, const double* V, int fun, double* F);
 
 }  // namespace kt

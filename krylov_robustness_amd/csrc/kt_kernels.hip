@@ -126,7 +126,8 @@ template <int P, int FLAGS>
 __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
                                            const int* __restrict__ col,
                                            const double* __restrict__ val,
-                                           const double* __restrict__ ucur, double* s) {
+                                           const double* __restrict__ ucur, double* s,
+                                           int ld = P) {
     using G = Geo<P>;
     using V = VecT<G::VEC>;
     int k = k0;
@@ -141,10 +142,10 @@ __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
             a2 = ld_stream<FLAGS>(val + k + 2 * stride);
             a3 = ld_stream<FLAGS>(val + k + 3 * stride);
         }
-        const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
-        const typename V::T x1 = V::load(ucur + (int64_t)c1 * P + p0);
-        const typename V::T x2 = V::load(ucur + (int64_t)c2 * P + p0);
-        const typename V::T x3 = V::load(ucur + (int64_t)c3 * P + p0);
+        const typename V::T x0 = V::load(ucur + (int64_t)c0 * ld + p0);
+        const typename V::T x1 = V::load(ucur + (int64_t)c1 * ld + p0);
+        const typename V::T x2 = V::load(ucur + (int64_t)c2 * ld + p0);
+        const typename V::T x3 = V::load(ucur + (int64_t)c3 * ld + p0);
 #pragma unroll
         for (int e = 0; e < G::VEC; ++e) {
             s[e] = fma(a0, V::get(x0, e), s[e]);
@@ -157,7 +158,7 @@ __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
         const int c0 = ld_stream<FLAGS>(col + k);
         double a0 = 1.0;
         if constexpr (!(FLAGS & KF_UNIT)) a0 = ld_stream<FLAGS>(val + k);
-        const typename V::T x0 = V::load(ucur + (int64_t)c0 * P + p0);
+        const typename V::T x0 = V::load(ucur + (int64_t)c0 * ld + p0);
 #pragma unroll
         for (int e = 0; e < G::VEC; ++e) s[e] = fma(a0, V::get(x0, e), s[e]);
     }
@@ -261,6 +262,63 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
 }
 
 // ---------------------------------------------------------------------------
+// Block SpMM for the block-Krylov paths: Y[:, 0:P] = A X[:, 0:P] with row
+// strides ldx, ldy (blocks are column slices of a wider row-major basis).
+// Same row-group / long-row mapping as K1, no reductions.
+// ---------------------------------------------------------------------------
+template <int P, int BLOCK, int FLAGS>
+__global__ __launch_bounds__(BLOCK) void k_spmm_block(
+    const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
+    int n, const double* __restrict__ X, int ldx, double* __restrict__ Y, int ldy,
+    const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks) {
+    using G = Geo<P>;
+    using V = VecT<G::VEC>;
+    constexpr int WAVES = BLOCK / 64;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int sub = lane % G::LPR;
+    const int grp = lane / G::LPR;
+    const int p0 = sub * G::VEC;
+    if ((int)blockIdx.x < long_blocks) {
+        for (int li = blockIdx.x * WAVES + wave; li < n_long; li += long_blocks * WAVES) {
+            const int row = long_rows[li];
+            double s[G::VEC];
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+            row_gather<P, FLAGS>(row_ptr[row] + grp, row_ptr[row + 1], G::GPW, p0, col, val, X, s,
+                                 ldx);
+#pragma unroll
+            for (int o = G::LPR; o < 64; o <<= 1)
+#pragma unroll
+                for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
+            if (grp == 0) {
+                typename V::T yo;
+                double* yp = reinterpret_cast<double*>(&yo);
+#pragma unroll
+                for (int e = 0; e < G::VEC; ++e) yp[e] = s[e];
+                V::store(Y + (int64_t)row * ldy + p0, yo);
+            }
+        }
+    } else {
+        const int sb = blockIdx.x - long_blocks;
+        const int groups_total = (gridDim.x - long_blocks) * WAVES * G::GPW;
+        for (int row = (sb * WAVES + wave) * G::GPW + grp; row < n; row += groups_total) {
+            const int beg = row_ptr[row], end = row_ptr[row + 1];
+            if (end - beg > long_thresh) continue;
+            double s[G::VEC];
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+            row_gather<P, FLAGS>(beg, end, 1, p0, col, val, X, s, ldx);
+            typename V::T yo;
+            double* yp = reinterpret_cast<double*>(&yo);
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) yp[e] = s[e];
+            V::store(Y + (int64_t)row * ldy + p0, yo);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Deterministic column reduction of per-block slabs [nblk][slots]: 64 slots
 // per workgroup (one per lane), 16 waves striding over the slabs in a fixed
 // order, LDS combine in wave order.  The sum lands in every lane of wave 0.
@@ -326,7 +384,6 @@ __global__ __launch_bounds__(256) void k_coef_cgs2(const double* __restrict__ pa
 // partial slabs [3][P][grid]: ||u_next||^2, y.u_next, u_cur.u_next.
 // Pure streaming: rows are contiguous, so lanes cover 16 B each.
 // ---------------------------------------------------------------------------
-constexpr int KQ = 4;
 
 template <int P, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_update(
@@ -496,6 +553,21 @@ hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int*
         default: KT_K1(KF_NT | KF_UNIT); break;
         }
 #undef KT_K1
+    });
+}
+
+hipError_t launch_spmm_block(int P, int flags, int grid, const int* rp, const int* ci,
+                             const double* va, int n, const double* X, int ldx, double* Y, int ldy,
+                             const int* long_rows, int n_long, int long_thresh, int long_blocks,
+                             hipStream_t st) {
+    return dispatch_p(P, [&](auto c) {
+        constexpr int PP = decltype(c)::value;
+        if (flags & KF_UNIT)
+            k_spmm_block<PP, kBlock, KF_UNIT><<<grid, kBlock, 0, st>>>(
+                rp, ci, va, n, X, ldx, Y, ldy, long_rows, n_long, long_thresh, long_blocks);
+        else
+            k_spmm_block<PP, kBlock, 0><<<grid, kBlock, 0, st>>>(
+                rp, ci, va, n, X, ldx, Y, ldy, long_rows, n_long, long_thresh, long_blocks);
     });
 }
 

@@ -1,0 +1,735 @@
+// kt_krylov.cpp -- block Lanczos / block Arnoldi and the low-rank-update
+// entry points on the device:
+//   lanczos_krylov.m   -> BlockLanczos   (2-block window, CGS2, thin QR)
+//   arnoldi_krylov.m   -> BlockArnoldi   (full basis, CGS2 + reorthogonalise)
+//   trace_fun_update.m -> kt_trace_fun_update
+//   fun_update.m       -> kt_fun_update (Arnoldi branch, nargout == 4)
+//   fun_and_grad_krylov_exp.m / _fun.m -> kt_fun_and_grad_krylov_exp / _fun
+//   MATLAB normest     -> kt_normest
+// Device work: SpMM (HIP kernel), Gram / combine (rocBLAS dgemm), CholQR.
+// Host work: the small projected matrices (H, Cm, eig, f(.)) -- exactly the
+// quantities the reference forms with dense MATLAB built-ins.
+#include <rocsolver/rocsolver.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+
+#include "kt_block.h"
+
+namespace kt {
+
+// ---------------------------------------------------------------------------
+// dense symmetric eig: host tred2/tql2 for small n, rocSOLVER dsyevd above.
+// ---------------------------------------------------------------------------
+static void sym_eig(kt_context_s* ctx, int n, const double* A, double* w, double* V) {
+    if (n <= 0) return;
+    if (n <= 160) {
+        sym_eig_host(n, A, w, V);
+        return;
+    }
+    Workspace& ws = ctx->ws;
+    ws.eigA.ensure(sizeof(double) * (size_t)n * n);
+    ws.eigW.ensure(sizeof(double) * 2 * (size_t)n);
+    ws.eigInfo.ensure(sizeof(rocblas_int));
+    double* dA = ws.eigA.as<double>();
+    KT_HIP(hipMemcpyAsync(dA, A, sizeof(double) * (size_t)n * n, hipMemcpyHostToDevice, ctx->stream));
+    rocblas_status s = rocsolver_dsyevd(blas(ctx), V ? rocblas_evect_original : rocblas_evect_none,
+                                        rocblas_fill_upper, n, dA, n, ws.eigW.as<double>(),
+                                        ws.eigW.as<double>() + n, ws.eigInfo.as<rocblas_int>());
+    if (s != rocblas_status_success) fail(KT_ERR_HIP, "rocsolver_dsyevd failed");
+    rocblas_int info = 0;
+    KT_HIP(hipMemcpyAsync(w, ws.eigW.ptr, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
+    if (V) KT_HIP(hipMemcpyAsync(V, dA, sizeof(double) * (size_t)n * n, hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipMemcpyAsync(&info, ws.eigInfo.ptr, sizeof(info), hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipStreamSynchronize(ctx->stream));
+    if (info != 0) fail(KT_ERR_HIP, "rocsolver_dsyevd did not converge");
+}
+
+static std::vector<double> sym_eigvals(kt_context_s* ctx, int n, const std::vector<double>& A) {
+    std::vector<double> w(n);
+    sym_eig(ctx, n, A.data(), w.data(), nullptr);
+    std::sort(w.begin(), w.end());
+    return w;
+}
+
+// f(M) for symmetric M (fun_update.m:43-59 maps exp/sinh/cosh/sin/cos/log/sqrt
+// to expm/funm/logm/sqrtm; on a symmetric matrix all equal V f(L) V').
+static std::vector<double> sym_matfun(kt_context_s* ctx, int n, const std::vector<double>& M,
+                                      int fun) {
+    std::vector<double> w(n), V((size_t)n * n), F((size_t)n * n);
+    sym_eig(ctx, n, M.data(), w.data(), V.data());
+    if (n <= 160) {
+        sym_fun_from_eig(n, w.data(), V.data(), fun, F.data());
+        return F;
+    }
+    // F = (V diag f(w)) V' as one device dgemm
+    std::vector<double> VF(V);
+    for (int k = 0; k < n; ++k) {
+        const double fk = fscalar(fun, w[k]);
+        for (int i = 0; i < n; ++i) VF[i + (size_t)k * n] *= fk;
+    }
+    DevBuf dV, dVF, dF;
+    dV.ensure(sizeof(double) * V.size());
+    dVF.ensure(sizeof(double) * V.size());
+    dF.ensure(sizeof(double) * V.size());
+    KT_HIP(hipMemcpyAsync(dV.ptr, V.data(), sizeof(double) * V.size(), hipMemcpyHostToDevice, ctx->stream));
+    KT_HIP(hipMemcpyAsync(dVF.ptr, VF.data(), sizeof(double) * V.size(), hipMemcpyHostToDevice, ctx->stream));
+    const double one = 1.0, zero = 0.0;
+    if (rocblas_dgemm(blas(ctx), rocblas_operation_none, rocblas_operation_transpose, n, n, n, &one,
+                      dVF.as<double>(), n, dV.as<double>(), n, &zero, dF.as<double>(), n) !=
+        rocblas_status_success)
+        fail(KT_ERR_HIP, "rocblas_dgemm(matfun) failed");
+    KT_HIP(hipMemcpyAsync(F.data(), dF.ptr, sizeof(double) * F.size(), hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipStreamSynchronize(ctx->stream));
+    dV.release();
+    dVF.release();
+    dF.release();
+    return F;
+}
+
+// trace_fun_update.m:43-47 / :85-89 with d1, d2 ascending
+static double trace_diff(const std::vector<double>& d1, const std::vector<double>& d2, int fun) {
+    double x = 0.0;
+    if (fun == KT_FUN_EXP) {
+        for (size_t i = 0; i < d1.size(); ++i) x += std::exp(d1[i]) * (1.0 - std::exp(d2[i] - d1[i]));
+    } else {
+        for (size_t i = 0; i < d1.size(); ++i) x += fscalar(fun, d1[i]) - fscalar(fun, d2[i]);
+    }
+    return x;
+}
+
+static bool is_symmetric_host(const kt_matrix_s* A) {
+    const int64_t n = A->n;
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t k = A->h_rowptr[i]; k < A->h_rowptr[i + 1]; ++k) {
+            const int64_t j = A->h_col[k];
+            // find (j, i)
+            const int32_t* b = A->h_col.data() + A->h_rowptr[j];
+            const int32_t* e = A->h_col.data() + A->h_rowptr[j + 1];
+            const int32_t* f = std::lower_bound(b, e, (int32_t)i);
+            if (f == e || *f != (int32_t)i) return false;
+            if (A->h_val[f - A->h_col.data()] != A->h_val[k]) return false;
+        }
+    return true;
+}
+
+static void require_symmetric(kt_matrix_s* A, const char* msg) {
+    if (A->symmetric < 0) A->symmetric = is_symmetric_host(A) ? 1 : 0;
+    if (!A->symmetric) fail(KT_ERR_NOT_HERMITIAN, msg);
+}
+
+// dense host copy of A (original numbering), column-major
+static std::vector<double> dense_A(const kt_matrix_s* A) {
+    const int64_t n = A->n;
+    std::vector<double> D((size_t)n * n, 0.0);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t k = A->h_rowptr[i]; k < A->h_rowptr[i + 1]; ++k)
+            D[(size_t)A->h_col[k] * n + i] += A->h_val[k];  // CSC==CSR for symmetric
+    return D;
+}
+
+// M + U B U' (host, column-major), U n x r, B r x r
+static void add_UBUt(std::vector<double>& M, int64_t n, int r, const double* U, const double* B) {
+    std::vector<double> UB((size_t)n * r, 0.0);
+    for (int j = 0; j < r; ++j)
+        for (int l = 0; l < r; ++l) {
+            const double b = B[l + (size_t)j * r];
+            if (b == 0.0) continue;
+            for (int64_t i = 0; i < n; ++i) UB[i + (size_t)j * n] += U[i + (size_t)l * n] * b;
+        }
+    for (int j = 0; j < r; ++j)
+        for (int64_t c = 0; c < n; ++c) {
+            const double u = U[c + (size_t)j * n];
+            if (u == 0.0) continue;
+            for (int64_t i = 0; i < n; ++i) M[i + (size_t)c * n] += UB[i + (size_t)j * n] * u;
+        }
+}
+
+// ---------------------------------------------------------------------------
+// BlockLanczos: lanczos_krylov.m (start :30-58, extend :60-67,
+// add_inf_pole :73-101, CGS2 :109-115).  Window slots 0/1 of `win`.
+// ---------------------------------------------------------------------------
+struct BlockLanczos {
+    kt_matrix_s* A;
+    kt_context_s* ctx;
+    int64_t n;
+    int bs, PB;
+    DevMat win, W;
+    int cur = 0, prev = -1;
+    int Hr = 0, Hc = 0;
+    std::vector<double> H;  // column-major Hr x Hc
+    bool lucky = false;
+
+    BlockLanczos(kt_matrix_s* A_, int bs_) : A(A_), ctx(A_->ctx), n(A_->n), bs(bs_) {
+        PB = pow2_at_least(bs);
+        if (PB > 128) fail(KT_ERR_UNSUPPORTED, "block size > 128");
+        win.alloc(ctx, n, 2 * PB);
+        W.alloc(ctx, n, PB);
+    }
+    double* slot(int s) { return win.col(s * PB); }
+
+    void grow(int add) {
+        std::vector<double> Hn((size_t)(Hr + add) * (Hc + add), 0.0);
+        for (int j = 0; j < Hc; ++j)
+            for (int i = 0; i < Hr; ++i) Hn[i + (size_t)j * (Hr + add)] = H[i + (size_t)j * Hr];
+        H.swap(Hn);
+        Hr += add;
+        Hc += add;
+    }
+
+    void start(const double* U) {  // U: host n x bs column-major (original numbering)
+        upload_rows(A, U, bs, slot(0), 2 * PB);
+        std::vector<double> R;
+        cholqr(ctx, n, slot(0), 2 * PB, bs, R);  // [V, ~] = qr(b, 0)    :48
+        cur = 0;
+        prev = -1;
+        Hr = bs;
+        Hc = 0;
+        H.clear();
+        add_inf_pole();
+    }
+    void extend() { add_inf_pole(); }
+
+    void add_inf_pole() {
+        const int ld = 2 * PB;
+        spmm(A, slot(cur), ld, W.col(0), PB, bs);  // w = A * w   :81
+        grow(bs);                                  // :85
+        // CGS2 against the window (both slots in one Gram; absent slot -> 0)
+        std::vector<double> h((size_t)2 * PB * bs, 0.0);
+        for (int pass = 0; pass < 2; ++pass) {  // :109-115
+            std::vector<double> g;
+            gram(ctx, n, win.col(0), ld, 2 * PB, W.col(0), PB, bs, g);
+            if (prev < 0)
+                for (int j = 0; j < bs; ++j)
+                    for (int i = 0; i < 2 * PB; ++i)
+                        if (i / PB != cur) g[i + (size_t)j * 2 * PB] = 0.0;
+            std::vector<double> C(g.size());
+            for (size_t t = 0; t < g.size(); ++t) {
+                C[t] = -g[t];
+                h[t] += g[t];
+            }
+            combine(ctx, n, win.col(0), ld, 2 * PB, C, bs, 1.0, W.col(0), PB);
+        }
+        // H(max(1,end-3bs+1):end-bs, end-bs+1:end) = h      :88
+        const int c0 = Hc - bs;
+        auto put = [&](int s, int row0) {
+            for (int j = 0; j < bs; ++j)
+                for (int i = 0; i < bs; ++i)
+                    H[(row0 + i) + (size_t)(c0 + j) * Hr] = h[(s * PB + i) + (size_t)j * 2 * PB];
+        };
+        if (prev >= 0) {
+            put(prev, Hr - 3 * bs);
+            put(cur, Hr - 2 * bs);
+        } else {
+            put(cur, Hr - 2 * bs);
+        }
+        std::vector<double> R;
+        const bool ok = cholqr(ctx, n, W.col(0), PB, bs, R);  // [w, R] = qr(w, 0)   :90
+        for (int j = 0; j < bs; ++j)
+            for (int i = 0; i < bs; ++i) H[(Hr - bs + i) + (size_t)(c0 + j) * Hr] = R[i + (size_t)j * bs];
+        lucky = !ok || norm_fro(R) < 1e-8;  // :91-93
+        // window rotation :94-99
+        const int dst = (prev < 0) ? 1 - cur : prev;
+        copy_cols(ctx, n, W.col(0), PB, slot(dst), ld, PB);
+        prev = cur;
+        cur = dst;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// BlockArnoldi: arnoldi_krylov.m (start :32-62, extend :64-72,
+// add_inf_pole :78-111).  Full basis in `V` (block b at columns b*PB).
+// ---------------------------------------------------------------------------
+struct BlockArnoldi {
+    kt_matrix_s* A;
+    kt_context_s* ctx;
+    int64_t n;
+    int bs, PB, maxblk;
+    int nblk = 0;  // blocks in V
+    DevMat V, W;
+    int Hr = 0, Hc = 0;
+    std::vector<double> H;
+    bool lucky = false;
+
+    BlockArnoldi(kt_matrix_s* A_, int bs_, int maxblk_) : A(A_), ctx(A_->ctx), n(A_->n), bs(bs_),
+                                                           maxblk(maxblk_) {
+        PB = pow2_at_least(bs);
+        if (PB > 128) fail(KT_ERR_UNSUPPORTED, "block size > 128");
+        V.alloc(ctx, n, maxblk * PB);
+        W.alloc(ctx, n, PB);
+    }
+    int ld() const { return maxblk * PB; }
+    double* blk(int b) { return V.col(b * PB); }
+
+    void grow(int add) {
+        std::vector<double> Hn((size_t)(Hr + add) * (Hc + add), 0.0);
+        for (int j = 0; j < Hc; ++j)
+            for (int i = 0; i < Hr; ++i) Hn[i + (size_t)j * (Hr + add)] = H[i + (size_t)j * Hr];
+        H.swap(Hn);
+        Hr += add;
+        Hc += add;
+    }
+
+    void start(const double* U) {
+        upload_rows(A, U, bs, blk(0), ld());
+        std::vector<double> R;
+        cholqr(ctx, n, blk(0), ld(), bs, R);  // [V, ~] = qr(b, 0)   :50
+        nblk = 1;
+        Hr = bs;
+        Hc = 0;
+        H.clear();
+        add_inf_pole(0);
+    }
+    void extend() { add_inf_pole(nblk - 1); }
+
+    void add_inf_pole(int last) {
+        if (nblk >= maxblk) fail(KT_ERR_UNSUPPORTED, "Arnoldi basis capacity exceeded");
+        const int L = ld();
+        const int pv = nblk * PB;
+        spmm(A, blk(last), L, W.col(0), PB, bs);  // w = A * w   :86
+        std::vector<double> h((size_t)pv * bs, 0.0);
+        for (int pass = 0; pass < 2; ++pass) {  // CGS2 :119-125
+            std::vector<double> g;
+            gram(ctx, n, V.col(0), L, pv, W.col(0), PB, bs, g);
+            std::vector<double> C(g.size());
+            for (size_t t = 0; t < g.size(); ++t) {
+                C[t] = -g[t];
+                h[t] += g[t];
+            }
+            combine(ctx, n, V.col(0), L, pv, C, bs, 1.0, W.col(0), PB);
+        }
+        grow(bs);  // :93-94
+        const int c0 = Hc - bs;
+        auto hrow = [&](int padded_row) { return (padded_row / PB) * bs + padded_row % PB; };
+        for (int j = 0; j < bs; ++j)
+            for (int i = 0; i < pv; ++i)
+                if (i % PB < bs) H[hrow(i) + (size_t)(c0 + j) * Hr] = h[i + (size_t)j * pv];  // :96
+        std::vector<double> r;
+        const bool ok = cholqr(ctx, n, W.col(0), PB, bs, r);  // [w, r] = qr(w, 0)   :99
+        lucky = !ok || norm2_small(bs, bs, r.data()) < 1e-12;  // :100-102
+        // reorthogonalise :104-106
+        std::vector<double> hh;
+        gram(ctx, n, V.col(0), L, pv, W.col(0), PB, bs, hh);
+        std::vector<double> C(hh.size());
+        for (size_t t = 0; t < hh.size(); ++t) C[t] = -hh[t];
+        combine(ctx, n, V.col(0), L, pv, C, bs, 1.0, W.col(0), PB);
+        std::vector<double> hr((size_t)pv * bs);
+        matmul(pv, bs, bs, hh.data(), r.data(), hr.data());
+        for (int j = 0; j < bs; ++j)
+            for (int i = 0; i < pv; ++i)
+                if (i % PB < bs) H[hrow(i) + (size_t)(c0 + j) * Hr] += hr[i + (size_t)j * pv];
+        for (int j = 0; j < bs; ++j)  // :108
+            for (int i = 0; i < bs; ++i) H[(Hr - bs + i) + (size_t)(c0 + j) * Hr] = r[i + (size_t)j * bs];
+        copy_cols(ctx, n, W.col(0), PB, blk(nblk), L, PB);  // V = [V, w]   :110
+        nblk += 1;
+    }
+};
+
+// Cm = (V1' U) B (V1' U)'   (trace_fun_update.m:65-66, fun_update.m:80-81)
+static std::vector<double> make_Cm(kt_context_s* ctx, kt_matrix_s* A, const double* V1, int ldv,
+                                   int bs, const double* U, int rk, const double* B) {
+    DevMat Ud;
+    const int PU = pow2_at_least(rk);
+    Ud.alloc(ctx, A->n, PU);
+    upload_rows(A, U, rk, Ud.col(0), PU);
+    std::vector<double> G;  // bs x rk
+    gram(ctx, A->n, V1, ldv, bs, Ud.col(0), PU, rk, G);
+    std::vector<double> GB((size_t)bs * rk), Cm((size_t)bs * bs);
+    matmul(bs, rk, rk, G.data(), B, GB.data());
+    for (int j = 0; j < bs; ++j)
+        for (int i = 0; i < bs; ++i) {
+            double s = 0.0;
+            for (int l = 0; l < rk; ++l) s += GB[i + (size_t)l * bs] * G[j + (size_t)l * bs];
+            Cm[i + (size_t)j * bs] = s;
+        }
+    return Cm;
+}
+
+static bool b_hermitian(int rk, const double* B) {
+    for (int j = 0; j < rk; ++j)
+        for (int i = 0; i < rk; ++i)
+            if (B[i + (size_t)j * rk] != B[j + (size_t)i * rk]) return false;
+    return true;
+}
+
+// top-left nn x nn of column-major M (Mr rows)
+static std::vector<double> top_left(const std::vector<double>& M, int Mr, int nn) {
+    std::vector<double> T((size_t)nn * nn);
+    for (int j = 0; j < nn; ++j)
+        for (int i = 0; i < nn; ++i) T[i + (size_t)j * nn] = M[i + (size_t)j * Mr];
+    return T;
+}
+
+// ---------------------------------------------------------------------------
+// trace_fun_update.m
+// ---------------------------------------------------------------------------
+double trace_fun_update_impl(kt_matrix_s* A, int rk, const double* U, const double* B, double tol,
+                             int it, int fun, int* iter_out, int* lucky_out) {
+    kt_context_s* ctx = A->ctx;
+    const int64_t n = A->n;
+    if (it <= 0) it = (int)std::min<int64_t>(100, n);  // :25-27
+    if (n <= 130) {                                    // :37-51 dense shortcut
+        std::vector<double> fA = dense_A(A), fAt = fA;
+        add_UBUt(fAt, n, rk, U, B);
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t i = 0; i < j; ++i) {
+                const double s = 0.5 * (fAt[i + j * n] + fAt[j + i * n]);
+                fAt[i + j * n] = fAt[j + i * n] = s;
+            }
+        const double x = trace_diff(sym_eigvals(ctx, (int)n, fAt), sym_eigvals(ctx, (int)n, fA), fun);
+        if (iter_out) *iter_out = 0;
+        if (lucky_out) *lucky_out = 0;
+        return x;
+    }
+    const bool herm = b_hermitian(rk, B);  // :55
+    if (!herm) fail(KT_ERR_UNSUPPORTED, "trace_fun_update: non-Hermitian B (needs a general eig)");
+    BlockLanczos L(A, rk);
+    const int d = 2;  // :58
+    double Xstop[2] = {0.0, 0.0};
+    std::vector<double> Cm;
+    double Xm = 0.0;
+    int j = 0;
+    for (j = 1; j <= it; ++j) {
+        if (j == 1) {
+            L.start(U);                                                        // :64
+            const double* V1 = L.win.col(L.prev * L.PB);                       // Um(:, 1:end-rk)
+            Cm = make_Cm(ctx, A, V1, 2 * L.PB, rk, U, rk, B);                  // :65-66
+        } else {
+            L.extend();                                                        // :68
+        }
+        const int nn = L.Hr - rk;                                              // :72-73
+        std::vector<double> Gm = top_left(L.H, L.Hr, nn), tGm = Gm;
+        for (int jj = 0; jj < rk; ++jj)
+            for (int ii = 0; ii < rk; ++ii) tGm[ii + (size_t)jj * nn] += Cm[ii + (size_t)jj * rk];  // :74-77
+        for (int b = 0; b < nn; ++b)                                           // :78-81
+            for (int a = 0; a < b; ++a) {
+                double s = 0.5 * (Gm[a + (size_t)b * nn] + Gm[b + (size_t)a * nn]);
+                Gm[a + (size_t)b * nn] = Gm[b + (size_t)a * nn] = s;
+                s = 0.5 * (tGm[a + (size_t)b * nn] + tGm[b + (size_t)a * nn]);
+                tGm[a + (size_t)b * nn] = tGm[b + (size_t)a * nn] = s;
+            }
+        Xm = trace_diff(sym_eigvals(ctx, nn, tGm), sym_eigvals(ctx, nn, Gm), fun);  // :83-89
+        if (j <= d) {                                                          // :104-118
+            Xstop[j - 1] = Xm;
+        } else {
+            if (std::fabs(Xm - Xstop[0]) < tol) break;
+            Xstop[0] = Xstop[1];
+            Xstop[1] = Xm;
+        }
+        if (L.lucky) break;                                                    // :119-124
+    }
+    if (j > it) j = it;
+    if (iter_out) *iter_out = j;
+    if (lucky_out) *lucky_out = L.lucky ? 1 : 0;
+    return Xm;
+}
+
+// ---------------------------------------------------------------------------
+// fun_update.m (Arnoldi branch).  Returns Xm (nx x nx) and either the device
+// basis (dense == false) or the dense fallback marker (Um = eye(n)).
+// ---------------------------------------------------------------------------
+struct FunUpdateResult {
+    std::vector<double> Xm;
+    int nx = 0;
+    int iter = 0;
+    bool lucky = false;
+    bool dense = false;
+    std::unique_ptr<BlockArnoldi> basis;
+};
+
+FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const double* B, int fun,
+                                double tol, int it) {
+    kt_context_s* ctx = A->ctx;
+    const int64_t n = A->n;
+    if (it <= 0) it = (int)std::min<int64_t>(100, n);  // :24-26
+    const bool herm = b_hermitian(rk, B);              // :41
+    FunUpdateResult res;
+    // basis never needs more than ~n/2 columns before the dense fallback (:85)
+    const int maxblk = (int)std::min<int64_t>(it + 1, n / (2 * (int64_t)rk) + 2);
+    res.basis.reset(new BlockArnoldi(A, rk, std::max(maxblk, 2)));
+    BlockArnoldi& Ar = *res.basis;
+    const int d = 2;
+    std::vector<std::vector<double>> Xstop;
+    std::vector<double> Cm;
+    int j = 0;
+    for (j = 1; j <= it; ++j) {
+        if (j == 1) {
+            Ar.start(U);                                                     // :79
+            Cm = make_Cm(ctx, A, Ar.blk(0), Ar.ld(), rk, U, rk, B);         // :80-81
+        } else {
+            Ar.extend();                                                     // :83
+        }
+        if (2 * (int64_t)Ar.nblk * rk >= n) {  // size(Um,2) >= size(Um,1)/2   :85-90
+            std::vector<double> fA = dense_A(A), fAt = fA;
+            add_UBUt(fAt, n, rk, U, B);
+            std::vector<double> F1 = sym_matfun(ctx, (int)n, fAt, fun), F2 = sym_matfun(ctx, (int)n, fA, fun);
+            for (size_t t = 0; t < F1.size(); ++t) F1[t] -= F2[t];
+            res.Xm.swap(F1);
+            res.nx = (int)n;
+            res.iter = j;
+            res.lucky = Ar.lucky;
+            res.dense = true;
+            return res;
+        }
+        const int nn = Ar.Hr - rk;                                           // :93
+        std::vector<double> Gm = top_left(Ar.H, Ar.Hr, nn);
+        for (int b = 0; b < nn; ++b)                                         // :94
+            for (int a = 0; a < b; ++a) {
+                const double s = 0.5 * (Gm[a + (size_t)b * nn] + Gm[b + (size_t)a * nn]);
+                Gm[a + (size_t)b * nn] = Gm[b + (size_t)a * nn] = s;
+            }
+        std::vector<double> tGm = Gm;
+        for (int jj = 0; jj < rk; ++jj)                                      // :97-104
+            for (int ii = 0; ii < rk; ++ii)
+                tGm[ii + (size_t)jj * nn] += herm ? 0.5 * (Cm[ii + (size_t)jj * rk] + Cm[jj + (size_t)ii * rk])
+                                                  : Cm[ii + (size_t)jj * rk];
+        if (!herm) fail(KT_ERR_UNSUPPORTED, "fun_update: non-Hermitian B");
+        std::vector<double> F1 = sym_matfun(ctx, nn, tGm, fun), F2 = sym_matfun(ctx, nn, Gm, fun);
+        for (size_t t = 0; t < F1.size(); ++t) F1[t] -= F2[t];               // :106
+        res.Xm = F1;
+        res.nx = nn;
+        if (j <= d) {                                                        // :109-126
+            Xstop.push_back(F1);
+        } else {
+            const int n0 = (int)std::lround(std::sqrt((double)Xstop[0].size()));
+            std::vector<double> D = F1;
+            for (int b = 0; b < n0; ++b)
+                for (int a = 0; a < n0; ++a) D[a + (size_t)b * nn] -= Xstop[0][a + (size_t)b * n0];
+            // 2-norm of the symmetric difference = max |eig|
+            const std::vector<double> ev = sym_eigvals(ctx, nn, D);
+            const double err = std::max(std::fabs(ev.front()), std::fabs(ev.back()));
+            if (err < tol) break;
+            Xstop.erase(Xstop.begin());
+            Xstop.push_back(F1);
+        }
+        if (Ar.lucky) break;                                                 // :127-130
+    }
+    if (j > it) j = it;
+    res.iter = j;
+    res.lucky = Ar.lucky;
+    return res;
+}
+
+// MATLAB normest (2-norm power estimate) on the device: x = sum(abs(A))',
+// repeat x = A'(A x)/||.|| until |e - e0| <= tol e.
+double normest_impl(kt_matrix_s* A, double tol) {
+    kt_context_s* ctx = A->ctx;
+    const int64_t n = A->n;
+    if (n == 0) return 0.0;
+    std::vector<double> x(n, 0.0);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t k = A->h_rowptr[i]; k < A->h_rowptr[i + 1]; ++k) x[A->h_col[k]] += std::fabs(A->h_val[k]);
+    DevMat X, Y;
+    X.alloc(ctx, n, 1);
+    Y.alloc(ctx, n, 1);
+    upload_rows(A, x.data(), 1, X.col(0), 1);
+    std::vector<double> g;
+    gram(ctx, n, X.col(0), 1, 1, X.col(0), 1, 1, g);
+    double e = std::sqrt(g[0]);
+    if (e == 0.0) return 0.0;
+    combine(ctx, n, X.col(0), 1, 1, std::vector<double>{1.0 / e}, 1, 0.0, Y.col(0), 1);
+    copy_cols(ctx, n, Y.col(0), 1, X.col(0), 1, 1);
+    double e0 = 0.0;
+    for (int cnt = 0; std::fabs(e - e0) > tol * e && cnt < 100; ++cnt) {
+        e0 = e;
+        spmm(A, X.col(0), 1, Y.col(0), 1, 1);  // Ax
+        gram(ctx, n, Y.col(0), 1, 1, Y.col(0), 1, 1, g);
+        const double nAx = std::sqrt(g[0]);
+        spmm(A, Y.col(0), 1, X.col(0), 1, 1);  // A'Ax (A symmetric)
+        gram(ctx, n, X.col(0), 1, 1, X.col(0), 1, 1, g);
+        const double nx = std::sqrt(g[0]);
+        if (nAx == 0.0 || nx == 0.0) return 0.0;
+        e = nx / nAx;
+        combine(ctx, n, X.col(0), 1, 1, std::vector<double>{1.0 / nx}, 1, 0.0, Y.col(0), 1);
+        copy_cols(ctx, n, Y.col(0), 1, X.col(0), 1, 1);
+    }
+    return e;
+}
+
+// Low-rank factor from edge weights (fun_and_grad_krylov_exp.m:56-73).
+static void lowrank_from_edges(int64_t n, int64_t nom, const double* X, const double* Omega,
+                               std::vector<int64_t>& aux, std::vector<double>& U,
+                               std::vector<double>& B) {
+    aux.clear();
+    for (int64_t t = 0; t < 2 * nom; ++t) aux.push_back((int64_t)std::llround(Omega[t]));
+    std::sort(aux.begin(), aux.end());
+    aux.erase(std::unique(aux.begin(), aux.end()), aux.end());  // :57 unique(Omega(:))
+    for (int64_t a : aux)
+        if (a < 1 || a > n) fail(KT_ERR_ARG, "Omega index out of range");
+    const int k = (int)aux.size();
+    U.assign((size_t)n * k, 0.0);
+    B.assign((size_t)k * k, 0.0);
+    for (int j = 0; j < k; ++j) U[(aux[j] - 1) + (size_t)j * n] = 1.0;  // :65-67
+    auto idx = [&](double v) {
+        return (int)(std::lower_bound(aux.begin(), aux.end(), (int64_t)std::llround(v)) - aux.begin());
+    };
+    for (int64_t t = 0; t < nom; ++t) {  // :68-73
+        const int i1 = idx(Omega[t]), i2 = idx(Omega[t + nom]);
+        B[i1 + (size_t)i2 * k] = X[t];
+        B[i2 + (size_t)i1 * k] = X[t];
+    }
+}
+
+// gr_k = -2 (base_k + Um(O1_k,:) Xm Um(O2_k,:)')   (fun_and_grad_krylov_exp.m:85-88)
+static void gradient(kt_matrix_s* A, FunUpdateResult& fu, int64_t nom, const double* Omega,
+                     const double* base, double* gr) {
+    const int nx = fu.nx;
+    if (fu.dense) {  // Um = eye(n)
+        for (int64_t t = 0; t < nom; ++t) {
+            const int64_t i = std::llround(Omega[t]) - 1, j = std::llround(Omega[t + nom]) - 1;
+            gr[t] = -2.0 * (base[t] + fu.Xm[i + (size_t)j * nx]);
+        }
+        return;
+    }
+    BlockArnoldi& Ar = *fu.basis;
+    std::vector<int64_t> rows;
+    for (int64_t t = 0; t < 2 * nom; ++t) rows.push_back(std::llround(Omega[t]) - 1);
+    std::vector<double> R;  // (2 nom) x (nblk PB), padded columns
+    download_rows(A, Ar.V.col(0), Ar.ld(), Ar.nblk * Ar.PB, rows, R);
+    const int nr = (int)rows.size();
+    auto um = [&](int r, int col) {  // Um(row r, unpadded column col)
+        const int b = col / Ar.bs, c = col % Ar.bs;
+        return R[r + (size_t)(b * Ar.PB + c) * nr];
+    };
+    for (int64_t t = 0; t < nom; ++t) {
+        double s = 0.0;
+        for (int b = 0; b < nx; ++b) {
+            double xb = 0.0;
+            for (int a = 0; a < nx; ++a) xb += um((int)t, a) * fu.Xm[a + (size_t)b * nx];
+            s += xb * um((int)(t + nom), b);
+        }
+        gr[t] = -2.0 * (base[t] + s);
+    }
+}
+
+}  // namespace kt
+
+using namespace kt;
+
+#define KT_TRY try {
+#define KT_CATCH                                  \
+    }                                             \
+    catch (const kt::Status& s) {                 \
+        kt::set_error(s.msg);                     \
+        return s.code;                            \
+    }                                             \
+    catch (const std::exception& e) {             \
+        kt::set_error(e.what());                  \
+        return KT_ERR_ARG;                        \
+    }                                             \
+    return KT_OK;
+
+extern "C" {
+
+int kt_normest(kt_matrix_t A, double tol, double* nrm) {
+    KT_TRY
+    if (!A || !nrm) fail(KT_ERR_ARG, "NULL argument");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    *nrm = normest_impl(A, tol);
+    KT_CATCH
+}
+
+int kt_trace_fun_update(kt_matrix_t A, int64_t rk, const double* U, const double* B, double tol,
+                        int it, int fun, double* Xm, int* iter, int* lucky) {
+    KT_TRY
+    if (!A || !U || !B || !Xm || rk < 1) fail(KT_ERR_ARG, "NULL argument or empty U");
+    if (rk > 128) fail(KT_ERR_UNSUPPORTED, "rank > 128");
+    if (fun < KT_FUN_EXP || fun > KT_FUN_SQRT) fail(KT_ERR_ARG, "unknown fun code");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    *Xm = trace_fun_update_impl(A, (int)rk, U, B, tol, it, fun, iter, lucky);
+    KT_CATCH
+}
+
+int kt_fun_update(kt_matrix_t A, int64_t rk, const double* U, const double* B, int fun, double tol,
+                  int it, int64_t max_cols, double* Xm, int64_t* ncols, int* iter, int* lucky,
+                  double* Um) {
+    KT_TRY
+    if (!A || !U || !B || !ncols || rk < 1) fail(KT_ERR_ARG, "NULL argument or empty U");
+    if (fun < KT_FUN_EXP || fun > KT_FUN_SQRT) fail(KT_ERR_ARG, "unknown fun code");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    FunUpdateResult fu = fun_update_impl(A, (int)rk, U, B, fun, tol, it);
+    *ncols = fu.nx;
+    if (iter) *iter = fu.iter;
+    if (lucky) *lucky = fu.lucky ? 1 : 0;
+    if (fu.nx > max_cols) fail(KT_ERR_ARG, "max_cols smaller than the result (query *ncols)");
+    if (Xm)
+        for (int j = 0; j < fu.nx; ++j)
+            for (int i = 0; i < fu.nx; ++i) Xm[i + (size_t)j * fu.nx] = fu.Xm[i + (size_t)j * fu.nx];
+    if (Um) {  // n x nx column-major, original numbering (fun_update.m:137)
+        const int64_t n = A->n;
+        if (fu.dense) {
+            std::memset(Um, 0, sizeof(double) * (size_t)n * fu.nx);
+            for (int64_t i = 0; i < n; ++i) Um[i + (size_t)i * n] = 1.0;
+        } else {
+            BlockArnoldi& Ar = *fu.basis;
+            const int ldv = Ar.ld();
+            std::vector<double> host((size_t)n * ldv);
+            KT_HIP(hipMemcpyAsync(host.data(), Ar.V.col(0), sizeof(double) * host.size(),
+                                  hipMemcpyDeviceToHost, A->ctx->stream));
+            KT_HIP(hipStreamSynchronize(A->ctx->stream));
+            for (int c = 0; c < fu.nx; ++c) {
+                const int pc = (c / Ar.bs) * Ar.PB + c % Ar.bs;
+                for (int64_t i = 0; i < n; ++i) Um[i + (size_t)c * n] = host[(size_t)A->old2new[i] * ldv + pc];
+            }
+        }
+    }
+    KT_CATCH
+}
+
+int kt_fun_and_grad_krylov_exp(kt_matrix_t A, int64_t nom, const double* X, const double* Omega,
+                               const double* eA, double tol, int it, double* f, double* gr) {
+    KT_TRY
+    if (!A || !f || !gr || (nom > 0 && (!X || !Omega || !eA))) fail(KT_ERR_ARG, "NULL argument");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    require_symmetric(A, "FUN_AND_GRAD_KRYLOV:: matrix A is not Hermitian");  // :21-23
+    const double nrmA = normest_impl(A, 1e-2);                                // :26
+    double sabs = 0.0;
+    for (int64_t t = 0; t < nom; ++t) sabs += std::fabs(X[t]);
+    if (sabs == 0.0) {                                                        // :30-54
+        *f = 0.0;
+        for (int64_t t = 0; t < nom; ++t) gr[t] = -2.0 * eA[t];
+        return KT_OK;
+    }
+    std::vector<int64_t> aux;
+    std::vector<double> U, B;
+    lowrank_from_edges(A->n, nom, X, Omega, aux, U, B);
+    const int k = (int)aux.size();
+    FunUpdateResult fu = fun_update_impl(A, k, U.data(), B.data(), KT_FUN_EXP, tol * std::exp(nrmA), it);  // :83
+    double tr = 0.0;
+    for (int i = 0; i < fu.nx; ++i) tr += fu.Xm[i + (size_t)i * fu.nx];
+    *f = -tr;                                                                 // :84
+    gradient(A, fu, nom, Omega, eA, gr);                                      // :85-88
+    KT_CATCH
+}
+
+int kt_fun_and_grad_krylov_fun(kt_matrix_t A, int64_t nom, const double* X, const double* Omega,
+                               int fun, int dfun, const double* dfA, double tol, int it, double* f,
+                               double* gr) {
+    KT_TRY
+    if (!A || !f || !gr || (nom > 0 && (!X || !Omega || !dfA))) fail(KT_ERR_ARG, "NULL argument");
+    if (fun < KT_FUN_EXP || fun > KT_FUN_SQRT || dfun < KT_FUN_EXP || dfun > KT_FUN_SQRT)
+        fail(KT_ERR_ARG, "unknown fun code");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    require_symmetric(A, "FUN_AND_GRAD_KRYLOV_FCONNECTIVITY:: matrix A is not Hermitian");  // :22-24
+    const double nrmA = normest_impl(A, 1e-2);                                             // :27
+    double sabs = 0.0;
+    for (int64_t t = 0; t < nom; ++t) sabs += std::fabs(X[t]);
+    if (sabs == 0.0) {                                                                     // :31-35
+        *f = 0.0;
+        for (int64_t t = 0; t < nom; ++t) gr[t] = -2.0 * dfA[t];
+        return KT_OK;
+    }
+    std::vector<int64_t> aux;
+    std::vector<double> U, B;
+    lowrank_from_edges(A->n, nom, X, Omega, aux, U, B);
+    const int k = (int)aux.size();
+    FunUpdateResult fu = fun_update_impl(A, k, U.data(), B.data(), dfun, tol * fscalar(dfun, nrmA), it);  // :64
+    *f = -trace_fun_update_impl(A, k, U.data(), B.data(), tol * fscalar(fun, nrmA), it, fun, nullptr,
+                                nullptr);                                                   // :65
+    gradient(A, fu, nom, Omega, dfA, gr);                                                   // :67-70
+    KT_CATCH
+}
+
+}  // extern "C"

@@ -14,6 +14,10 @@ hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int*
                            const double* va, int n, const double* ucur, const double* sc,
                            double* y, double* partial, const int* long_rows, int n_long,
                            int long_thresh, int long_blocks, hipStream_t st);
+hipError_t launch_spmm_block(int P, int flags, int grid, const int* rp, const int* ci,
+                             const double* va, int n, const double* X, int ldx, double* Y, int ldy,
+                             const int* long_rows, int n_long, int long_thresh, int long_blocks,
+                             hipStream_t st);
 hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, const double* k2s,
                             const double* sc, const double* sp, double* coef, double* t_alpha,
                             double* t_up, hipStream_t st);

@@ -7,6 +7,8 @@
 #include <string>
 #include <thread>
 
+#include <rocblas/rocblas.h>
+
 #include "kt_internal.h"
 
 namespace kt {
@@ -112,7 +114,10 @@ int kt_context_destroy(kt_context_t ctx) {
         for (auto e : s.ev) (void)hipEventDestroy(e);
     Workspace& w = ctx->ws;
     w.X0.release(); w.X1.release(); w.Y.release(); w.partial.release();
-    w.coef.release(); w.scales.release(); w.k2s.release(); w.trec.release(); w.host_trec.release();
+    w.coef.release(); w.scales.release(); w.k2s.release();
+    w.small.release(); w.small2.release(); w.qrtmp.release();
+    w.eigA.release(); w.eigW.release(); w.eigInfo.release();
+    if (ctx->blas) rocblas_destroy_handle(static_cast<rocblas_handle>(ctx->blas)); w.trec.release(); w.host_trec.release();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     KT_GUARD_END
@@ -178,6 +183,7 @@ int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr, con
             delete A;
             fail(KT_ERR_NOT_HERMITIAN, "FUN_AND_GRAD_KRYLOV:: matrix A is not Hermitian");
         }
+        A->symmetric = 1;
     }
     try {
         KT_HIP(hipSetDevice(ctx->device));

@@ -2,6 +2,15 @@ import json
 import os
 import sys
 
+# Load torch (and its bundled ROCm runtime / rocBLAS / rocSOLVER) BEFORE
+# libkrylov_hip.so: the library's NEEDED entries (libamdhip64.so.7,
+# librocblas.so.5, librocsolver.so.0) then bind to the copies torch already
+# mapped, so one process never holds two ROCm runtimes.  bench.py does the same.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    torch = None
+
 import numpy as np
 import pytest
 import scipy.sparse as sp

@@ -1,0 +1,146 @@
+"""GPU parity for the block-Krylov rows: device block
+Lanczos / Arnoldi entry points vs the oracle (oracle/krylov_oracle.py) and the
+reference's exact dense identities.  Tolerances: fp64 results agree to 1e-8
+relative (CholQR vs Householder QR and different summation orders change the
+basis only by signs/rounding; every compared quantity is basis-invariant)."""
+import numpy as np
+import pytest
+import scipy.linalg as sla
+import scipy.sparse as sp
+
+from conftest import load_graph
+from oracle import krylov_oracle as ko
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-8
+
+
+@pytest.fixture(scope="module")
+def kra():
+    import krylov_robustness_amd as kra
+    return kra
+
+
+def edges(A, k, offset=0):
+    I, J = sp.triu(A, 1).nonzero()
+    return np.stack([I[offset:offset + k] + 1, J[offset:offset + k] + 1], axis=1)
+
+
+@pytest.mark.parametrize("name", ["anaheim", "austria", "india", "denmark"])
+def test_normest_matches_oracle(kra, gpu_ctx, name):
+    A = load_graph(name)
+    got = kra.normest(kra.DeviceMatrix(A, gpu_ctx), 1e-2)
+    assert got == pytest.approx(ko.normest(A, 1e-2), rel=1e-9)
+
+
+@pytest.mark.parametrize("name", ["anaheim", "rome", "austria", "india"])
+def test_trace_fun_update_matches_golden(kra, gpu_ctx, values, name):
+    """krylov_miobi.m:77-99 candidates (U = [e_i e_j], B = -[0 1;1 0]) through
+    the block-Lanczos path (n > 130)."""
+    A = load_graph(name)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    n = A.shape[0]
+    for c in values[name]["trace_fun_update_break"]:
+        i, j = c["edge"]
+        U = np.zeros((n, 2)); U[i - 1, 0] = 1; U[j - 1, 1] = 1
+        B = -np.array([[0.0, 1.0], [1.0, 0.0]])
+        xm, it, lucky = kra.trace_fun_update(D, U, B, 1e-12, min(100, n), ctx=gpu_ctx)
+        assert xm == pytest.approx(c["oracle"], rel=1e-9, abs=1e-10)
+        assert xm == pytest.approx(c["exact"], rel=1e-8, abs=1e-9)
+        assert abs(it - c["iter"]) <= 1
+
+
+def test_trace_fun_update_dense_shortcut(kra, gpu_ctx):
+    A = load_graph("denmark")      # n = 96 <= 130: trace_fun_update.m:37-51
+    n = A.shape[0]
+    U = np.zeros((n, 2)); U[3, 0] = 1; U[7, 1] = 1
+    B = -np.array([[0.0, 1.0], [1.0, 0.0]])
+    for fun in ["exp", "sinh", "cosh"]:
+        xm, it, lucky = kra.trace_fun_update(kra.DeviceMatrix(A, gpu_ctx), U, B, fun=fun, ctx=gpu_ctx)
+        assert it == 0 and lucky == 0
+        assert xm == pytest.approx(ko.exact_trace_update(A, U, B, fun), rel=1e-11)
+
+
+def test_trace_fun_update_rank6_sinh(kra, gpu_ctx):
+    A = load_graph("india")
+    n = A.shape[0]
+    Om = edges(A, 3, offset=10)
+    X = np.array([0.3, -0.2, 0.1])
+    U, B = ko.lowrank_from_edges(X, Om, n)
+    xm, it, _ = kra.trace_fun_update(kra.DeviceMatrix(A, gpu_ctx), U, B, 1e-10, 100, fun="sinh",
+                                     ctx=gpu_ctx)
+    ref, it_ref, _ = ko.trace_fun_update(A, U, B, 1e-10, 100, 0, "sinh")
+    assert xm == pytest.approx(ref, rel=1e-9, abs=1e-11)
+    assert xm == pytest.approx(ko.exact_trace_update(A, U, B, "sinh"), rel=1e-8, abs=1e-10)
+
+
+def test_fun_update_arnoldi_vs_dense(kra, gpu_ctx):
+    """fun_and_grad_krylov_exp.m:90-93: Um Xm Um' ~ expm(A+UBU') - expm(A)."""
+    A = load_graph("austria")
+    n = A.shape[0]
+    U = np.zeros((n, 3)); U[0, 0] = 1; U[10, 1] = 1; U[40, 2] = 1
+    B = np.array([[0.0, 0.3, 0.0], [0.3, 0.0, -0.2], [0.0, -0.2, 0.0]])
+    Xm, it, lucky, Um = kra.fun_update(kra.DeviceMatrix(A, gpu_ctx), U, B, "exp", 1e-12, 100, ctx=gpu_ctx)
+    XX = sla.expm(A.toarray() + U @ B @ U.T) - sla.expm(A.toarray())
+    assert np.linalg.norm(XX - Um @ Xm @ Um.T) / np.linalg.norm(XX) < 1e-9
+    Xo, ito, _, Uo = ko.fun_update(A, U, B, "exp", 1e-12, 100)
+    assert Xm.shape == Xo.shape and abs(it - ito) <= 1
+    np.testing.assert_allclose(Um @ Xm @ Um.T, Uo @ Xo @ Uo.T, atol=1e-10 * np.abs(XX).max())
+
+
+def test_fun_update_dense_fallback(kra, gpu_ctx):
+    """Basis reaching n/2 columns switches to dense f(A+UBU') - f(A) (fun_update.m:85-90)."""
+    A = load_graph("denmark")
+    n = A.shape[0]
+    U = np.zeros((n, 8))
+    for c in range(8):
+        U[c * 11, c] = 1
+    B = 0.1 * (np.ones((8, 8)) - np.eye(8))
+    Xm, it, lucky, Um = kra.fun_update(kra.DeviceMatrix(A, gpu_ctx), U, B, "cosh", 1e-30, 100, ctx=gpu_ctx)
+    Xo, ito, _, Uo = ko.fun_update(A, U, B, "cosh", 1e-30, 100)
+    assert Xm.shape == (n, n) and Xo.shape == (n, n) and it == ito
+    np.testing.assert_allclose(Xm, Xo, atol=1e-12 * np.abs(Xo).max())
+    assert np.array_equal(Um, np.eye(n))
+
+
+@pytest.mark.parametrize("name", ["denmark", "austria"])
+def test_fun_and_grad_exp_matches_oracle(kra, gpu_ctx, name):
+    A = load_graph(name)
+    Om = edges(A, 6)
+    rng = np.random.default_rng(3)
+    X = rng.uniform(-0.5, 1.0, 6)
+    eA = sla.expm(A.toarray())[Om[:, 0] - 1, Om[:, 1] - 1]
+    tol = 1e-6 * np.exp(ko.normest(A, 1e-2))     # test_weighted_exp_lbfgs.m:46-47
+    f, gr = kra.fun_and_grad_krylov_exp(X, kra.DeviceMatrix(A, gpu_ctx), Om, eA, tol, 100, ctx=gpu_ctx)
+    fo, gro = ko.fun_and_grad_krylov_exp(X, A, Om, eA, tol, 100)
+    assert f == pytest.approx(fo, rel=RTOL)
+    np.testing.assert_allclose(gr, gro, rtol=RTOL, atol=1e-12)
+
+
+def test_fun_and_grad_exp_zero_and_errors(kra, gpu_ctx):
+    A = load_graph("austria")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    Om = edges(A, 2)
+    f, gr = kra.fun_and_grad_krylov_exp(np.zeros(2), D, Om, np.array([0.5, 0.25]), 1e-6, 100, ctx=gpu_ctx)
+    assert f == 0 and np.array_equal(gr, [-1.0, -0.5])          # :30-54
+    N = sp.csr_matrix(np.array([[0.0, 1.0], [0.0, 0.0]]))
+    with pytest.raises(kra.KrylovError, match="not Hermitian"):  # :21-23
+        kra.fun_and_grad_krylov_exp(np.ones(1), kra.DeviceMatrix(N, gpu_ctx), np.array([[1, 2]]),
+                                    np.zeros(1), 1e-6, 10, ctx=gpu_ctx)
+
+
+@pytest.mark.parametrize("fun,dfun", [("sinh", "cosh"), ("cosh", "sinh")])
+def test_fun_and_grad_fun_matches_oracle(kra, gpu_ctx, fun, dfun):
+    """test_weighted_sinh_lbfgs.m / _cosh_ setting on the India voltage graph."""
+    A = load_graph("india")
+    Om = edges(A, 5, offset=3)
+    rng = np.random.default_rng(5)
+    X = rng.uniform(-0.5, 1.0, 5)
+    dfA = rng.normal(size=5)
+    nrm = ko.normest(A, 1e-2)
+    tol = 1e-6 * ko.scalar_fun(fun)(nrm)
+    f, gr = kra.fun_and_grad_krylov_fun(X, kra.DeviceMatrix(A, gpu_ctx), Om, fun, dfun, dfA, tol, 100,
+                                        ctx=gpu_ctx)
+    fo, gro = ko.fun_and_grad_krylov_fun(X, A, Om, fun, dfun, dfA, tol, 100)
+    assert f == pytest.approx(fo, rel=1e-7)
+    np.testing.assert_allclose(gr, gro, rtol=1e-7, atol=1e-10)
