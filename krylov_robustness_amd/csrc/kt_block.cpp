@@ -2,6 +2,8 @@
 // plain GEMM shapes, the HIP SpMM kernel for A*X) and CholQR.
 #include "kt_block.h"
 
+#include <rocsolver/rocsolver.h>
+
 #include <cfloat>
 #include <cmath>
 
@@ -192,6 +194,33 @@ bool cholqr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector
     if (!cholqr_pass(ctx, n, W, ld, bs, 0.0, R3)) return false;
     matmul(bs, bs, bs, R3.data(), R1.data(), R.data());
     return true;
+}
+
+}  // namespace kt
+
+namespace kt {
+
+// Householder thin QR (the factorisation MATLAB's qr(w, 0) uses).  The
+// row-major n x ld block W is the column-major (ld x n) matrix M = W', so an
+// LQ factorisation of M's first bs rows (rocsolver_dgelqf) is a Householder QR
+// of W: M(0:bs,:) = L Q'  =>  W = Q' ' L'.  R = L' (upper); rocsolver_dorglq
+// then overwrites M(0:bs,:) with Q', i.e. W with Q.  Rank-deficient W is
+// handled like LAPACK: R gets ~0 diagonal entries and Q stays orthonormal.
+void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R) {
+    R.assign((size_t)bs * bs, 0.0);
+    if (n == 0 || bs == 0) return;
+    if (n < bs) fail(KT_ERR_UNSUPPORTED, "thin QR needs n >= block size");
+    DevBuf& tau = ctx->ws.small2;
+    tau.ensure(sizeof(double) * (size_t)bs);
+    rb(rocsolver_dgelqf(blas(ctx), bs, (rocblas_int)n, W, ld, tau.as<double>()), "rocsolver_dgelqf");
+    std::vector<double> top((size_t)bs * bs);  // rows 0..bs-1 of W, first bs columns
+    KT_HIP(hipMemcpy2DAsync(top.data(), sizeof(double) * bs, W, sizeof(double) * ld,
+                            sizeof(double) * bs, (size_t)bs, hipMemcpyDeviceToHost, ctx->stream));
+    rb(rocsolver_dorglq(blas(ctx), bs, (rocblas_int)n, bs, W, ld, tau.as<double>()), "rocsolver_dorglq");
+    KT_HIP(hipStreamSynchronize(ctx->stream));
+    // M(i, j) = top[j * bs + i]; L(i, j) = M(i, j), j <= i;  R(j, i) = L(i, j)
+    for (int i = 0; i < bs; ++i)
+        for (int j = 0; j <= i; ++j) R[j + (size_t)i * bs] = top[(size_t)j * bs + i];
 }
 
 }  // namespace kt

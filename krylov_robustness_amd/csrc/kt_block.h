@@ -47,6 +47,8 @@ void download_rows(kt_matrix_s* A, const double* D, int ldd, int cols,
 // CholQR2 (shifted CholQR3 if W is ill-conditioned).  Returns false when W
 // is numerically zero (R = 0 then, Q unspecified): a lucky breakdown.
 bool cholqr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R);
+// Householder thin QR of W in place (rocSOLVER LQ of W'); R upper, signs as LAPACK.
+void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R);
 
 // small host helpers (column-major)
 void matmul(int m, int k, int n, const double* A, const double* B, double* C);  // C = A B

@@ -182,7 +182,7 @@ struct BlockLanczos {
     void start(const double* U) {  // U: host n x bs column-major (original numbering)
         upload_rows(A, U, bs, slot(0), 2 * PB);
         std::vector<double> R;
-        cholqr(ctx, n, slot(0), 2 * PB, bs, R);  // [V, ~] = qr(b, 0)    :48
+        householder_qr(ctx, n, slot(0), 2 * PB, bs, R);  // [V, ~] = qr(b, 0)    :48
         cur = 0;
         prev = -1;
         Hr = bs;
@@ -226,10 +226,10 @@ struct BlockLanczos {
             put(cur, Hr - 2 * bs);
         }
         std::vector<double> R;
-        const bool ok = cholqr(ctx, n, W.col(0), PB, bs, R);  // [w, R] = qr(w, 0)   :90
+        householder_qr(ctx, n, W.col(0), PB, bs, R);  // [w, R] = qr(w, 0)   :90
         for (int j = 0; j < bs; ++j)
             for (int i = 0; i < bs; ++i) H[(Hr - bs + i) + (size_t)(c0 + j) * Hr] = R[i + (size_t)j * bs];
-        lucky = !ok || norm_fro(R) < 1e-8;  // :91-93
+        lucky = norm_fro(R) < 1e-8;  // :91-93
         // window rotation :94-99
         const int dst = (prev < 0) ? 1 - cur : prev;
         copy_cols(ctx, n, W.col(0), PB, slot(dst), ld, PB);
@@ -275,7 +275,7 @@ struct BlockArnoldi {
     void start(const double* U) {
         upload_rows(A, U, bs, blk(0), ld());
         std::vector<double> R;
-        cholqr(ctx, n, blk(0), ld(), bs, R);  // [V, ~] = qr(b, 0)   :50
+        householder_qr(ctx, n, blk(0), ld(), bs, R);  // [V, ~] = qr(b, 0)   :50
         nblk = 1;
         Hr = bs;
         Hc = 0;
@@ -307,8 +307,8 @@ struct BlockArnoldi {
             for (int i = 0; i < pv; ++i)
                 if (i % PB < bs) H[hrow(i) + (size_t)(c0 + j) * Hr] = h[i + (size_t)j * pv];  // :96
         std::vector<double> r;
-        const bool ok = cholqr(ctx, n, W.col(0), PB, bs, r);  // [w, r] = qr(w, 0)   :99
-        lucky = !ok || norm2_small(bs, bs, r.data()) < 1e-12;  // :100-102
+        householder_qr(ctx, n, W.col(0), PB, bs, r);  // [w, r] = qr(w, 0)   :99
+        lucky = norm2_small(bs, bs, r.data()) < 1e-12;  // :100-102
         // reorthogonalise :104-106
         std::vector<double> hh;
         gram(ctx, n, V.col(0), L, pv, W.col(0), PB, bs, hh);
