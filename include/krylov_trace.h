@@ -125,6 +125,33 @@ int kt_fun_and_grad_krylov_fun(kt_matrix_t A, int64_t nomega, const double* X, c
                                int fun, int dfun, const double* dfA, double tol, int it, double* f,
                                double* gr);
 
+/* ---- mc_trace / trace_exp / expmv --------------------------------------- */
+enum kt_afun { /* the Afun argument of mc_trace.m:1 */
+    KT_AFUN_MATRIX = 0,  /* Afun is the matrix itself (mc_trace.m:32-34)              */
+    KT_AFUN_LANCZOS = 1, /* f(A) x by m-step Lanczos (north star)   */
+    KT_AFUN_EXPMV = 2    /* @(x) expmv(1, A, x, [], 'double') (trace_exp.m:5)          */
+};
+
+/* [tr, res, it] = mc_trace(Afun, n, tol, maxit, isAreal, debug) (mc_trace.m:1):
+ * block Hutchinson, m = 10 columns per round, K = ceil(maxit/30) rounds with
+ * nested deflation (mc_trace.m:41-58).  Probes of round it are Rademacher
+ * columns (it-1)*20 + [0,10) (S) and + [10,20) (G) of the counter RNG. */
+int kt_mc_trace(kt_matrix_t A, int afun, int fun, int m, double tol, int maxit, int isAreal,
+                uint64_t seed, double* tr, double* res, int* it);
+
+/* tr = trace_exp(A) (trace_exp.m:1-7) = mc_trace(Afun, n, 1e-4, 1000, 1) with
+ * Afun = KT_AFUN_EXPMV (the reference composition) or KT_AFUN_LANCZOS (m steps). */
+int kt_trace_exp(kt_matrix_t A, int afun, int m, uint64_t seed, double* tr);
+
+/* [F, s, m, mv] = expmv(t, A, B, [], 'double') (expmv.m:1-94; degree selection
+ * select_taylor_degree.m, normAm.m for A >= 0).  B, F: n x ncols column-major. */
+int kt_expmv(kt_matrix_t A, double t, int64_t ncols, const double* B, double* F, int* s, int* mdeg,
+             int* mv);
+
+/* Y = f(A) X by per-column m-step Lanczos: y = ||x|| V f(T) e1 (the Lanczos-f
+ * Afun handle).  X, Y: n x ncols column-major, ncols <= 128. */
+int kt_lanczos_fmv(kt_matrix_t A, int fun, int m, int64_t ncols, const double* X, double* Y);
+
 /* Per-kernel timing (HIP events recorded on the library's stream around each
  * launch of the named kernel while enabled).  kernel: 0 = spmm_gram (K1),
  * 1 = update_norm (K2).  Returns launch count and summed milliseconds. */

@@ -8,12 +8,14 @@ include/krylov_trace.h); this package is the Python mirror of the reference
 interface used by tests and bench.py.
 """
 from ._lib import KrylovError, KrylovLibraryError, FUN_CODES, LIB_PATH
-from .core import (Context, DeviceMatrix, default_context, device_count, fun_and_grad_krylov_exp,
-                   fun_and_grad_krylov_fun, fun_update, normest, slq_plan, slq_quadforms,
-                   slq_trace, trace_fun_update)
+from .core import (Context, DeviceMatrix, default_context, device_count, expmv,
+                   fun_and_grad_krylov_exp, fun_and_grad_krylov_fun, fun_update, lanczos_fmv,
+                   mc_trace, normest, slq_plan, slq_quadforms, slq_trace, trace_exp,
+                   trace_fun_update)
 
 __all__ = [
     "KrylovError", "KrylovLibraryError", "FUN_CODES", "LIB_PATH", "Context", "DeviceMatrix",
     "default_context", "device_count", "slq_plan", "slq_quadforms", "slq_trace", "normest",
     "trace_fun_update", "fun_update", "fun_and_grad_krylov_exp", "fun_and_grad_krylov_fun",
+    "mc_trace", "trace_exp", "expmv", "lanczos_fmv",
 ]

@@ -31,6 +31,8 @@ class KrylovError(RuntimeError):
 
 # kt_status
 KT_OK, KT_ERR_ARG, KT_ERR_HIP, KT_ERR_NOT_HERMITIAN, KT_ERR_NOT_SQUARE, KT_ERR_ALLOC, KT_ERR_UNSUPPORTED = range(7)
+# kt_afun (mc_trace.m's Afun kinds)
+AFUN_CODES = {"matrix": 0, "lanczos": 1, "expmv": 2}
 # kt_fun (fun_update.m:43-59)
 FUN_CODES = {"exp": 0, "sinh": 1, "cosh": 2, "sin": 3, "cos": 4, "log": 5, "sqrt": 6}
 
@@ -62,6 +64,11 @@ SIGNATURES = [
                                              _dp, _dp]),
     ("kt_fun_and_grad_krylov_fun", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_int, C.c_int, _dp,
                                              C.c_double, C.c_int, _dp, _dp]),
+    ("kt_mc_trace", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int,
+                              C.c_uint64, _dp, _dp, _ip]),
+    ("kt_trace_exp", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_uint64, _dp]),
+    ("kt_expmv", C.c_int, [_mat_p, C.c_double, C.c_int64, _dp, _dp, _ip, _ip, _ip]),
+    ("kt_lanczos_fmv", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_int64, _dp, _dp]),
     ("kt_profile_enable", C.c_int, [_ctx_p, C.c_int]),
     ("kt_profile_read", C.c_int, [_ctx_p, C.c_int, _i64p, _dp]),
     ("kt_profile_reset", C.c_int, [_ctx_p]),

@@ -261,3 +261,62 @@ def fun_and_grad_krylov_fun(X, A, Omega, fun, dfun, dfA, tol, it, debug=False, f
         D.handle, Om.shape[0], _dptr(X), _dptr(Om), _fun_code(fun), _fun_code(dfun), _dptr(dfA),
         float(tol), int(it or 0), C.byref(f), _dptr(gr)))
     return float(f.value), gr
+
+
+# ---------------------------------------------------------------------------
+# mc_trace / trace_exp / expmv
+# ---------------------------------------------------------------------------
+def mc_trace(Afun, n=None, tol=1e-3, maxit=10, isAreal=0, debug=0, seed=0, fun="exp", m=30,
+             A=None, ctx: Optional[Context] = None):
+    """[tr, res, it] = mc_trace(Afun, n, tol, maxit, isAreal, debug) (mc_trace.m:1).
+    Afun: a matrix / DeviceMatrix (mc_trace.m:32-34), or one of the strings
+    "lanczos" (f(A) by m-step Lanczos) / "expmv" (expmv(1, A, .)) with A given."""
+    if isinstance(Afun, str):
+        kind = _lib.AFUN_CODES[Afun]
+        D = _dev(A, ctx)
+    else:
+        kind = _lib.AFUN_CODES["matrix"]
+        D = _dev(Afun, ctx)
+    if n is not None and int(n) != D.n:
+        raise _lib.KrylovError(_lib.KT_ERR_ARG, "n does not match the matrix")
+    tr = C.c_double()
+    res = C.c_double()
+    it = C.c_int()
+    _lib.check(_lib.load().kt_mc_trace(D.handle, kind, _fun_code(fun), int(m), float(tol), int(maxit),
+                                       int(isAreal), int(seed) & 0xFFFFFFFFFFFFFFFF, C.byref(tr),
+                                       C.byref(res), C.byref(it)))
+    return float(tr.value), float(res.value), int(it.value)
+
+
+def trace_exp(A, method="lanczos", m=30, seed=0, ctx: Optional[Context] = None) -> float:
+    """tr = trace_exp(A) (trace_exp.m:1-7): mc_trace(Afun, n, 1e-4, 1000, 1),
+    Afun = Lanczos-exp (default, the north-star evaluator) or expmv (the
+    reference's own composition)."""
+    D = _dev(A, ctx)
+    tr = C.c_double()
+    _lib.check(_lib.load().kt_trace_exp(D.handle, _lib.AFUN_CODES[method], int(m),
+                                        int(seed) & 0xFFFFFFFFFFFFFFFF, C.byref(tr)))
+    return float(tr.value)
+
+
+def expmv(t, A, b, ctx: Optional[Context] = None):
+    """[f, s, m, mv] = expmv(t, A, b, [], 'double') (expmv.m:1)."""
+    D = _dev(A, ctx)
+    B = _colmajor(b)
+    F = np.zeros_like(B, order="F")
+    s = C.c_int()
+    mm = C.c_int()
+    mv = C.c_int()
+    _lib.check(_lib.load().kt_expmv(D.handle, float(t), B.shape[1], _dptr(B), _dptr(F), C.byref(s),
+                                    C.byref(mm), C.byref(mv)))
+    return F, int(s.value), int(mm.value), int(mv.value)
+
+
+def lanczos_fmv(A, X, m=30, fun="exp", ctx: Optional[Context] = None):
+    """f(A) X by per-column m-step Lanczos (the Lanczos-f Afun handle)."""
+    D = _dev(A, ctx)
+    X = _colmajor(X)
+    Y = np.zeros_like(X, order="F")
+    _lib.check(_lib.load().kt_lanczos_fmv(D.handle, _fun_code(fun), int(m), X.shape[1], _dptr(X),
+                                          _dptr(Y)))
+    return Y

@@ -129,6 +129,17 @@ void download_rows(kt_matrix_s* A, const double* D, int ldd, int cols,
     }
 }
 
+void download_block(kt_matrix_s* A, const double* D, int ldd, int cols, double* out) {
+    const int64_t n = A->n;
+    if (n == 0 || cols == 0) return;
+    std::vector<double> tmp((size_t)n * cols);
+    KT_HIP(hipMemcpy2DAsync(tmp.data(), sizeof(double) * cols, D, sizeof(double) * ldd,
+                            sizeof(double) * cols, (size_t)n, hipMemcpyDeviceToHost, A->ctx->stream));
+    KT_HIP(hipStreamSynchronize(A->ctx->stream));
+    for (int c = 0; c < cols; ++c)
+        for (int64_t i = 0; i < n; ++i) out[i + (size_t)c * n] = tmp[(size_t)A->old2new[i] * cols + c];
+}
+
 void matmul(int m, int k, int n, const double* A, const double* B, double* C) {
     for (int j = 0; j < n; ++j)
         for (int i = 0; i < m; ++i) {

@@ -43,6 +43,9 @@ void upload_rows(kt_matrix_s* A, const double* H, int cols, double* D, int ldd);
 // device rows (given ORIGINAL row indices) -> host nrows x cols column-major
 void download_rows(kt_matrix_s* A, const double* D, int ldd, int cols,
                    const std::vector<int64_t>& rows, std::vector<double>& out);
+// whole device block (n x cols at ldd, device numbering) -> host column-major
+// n x cols in ORIGINAL numbering
+void download_block(kt_matrix_s* A, const double* D, int ldd, int cols, double* out);
 // thin QR of W (n x bs at ld) in place: W <- Q, R upper bs x bs (column-major).
 // CholQR2 (shifted CholQR3 if W is ill-conditioned).  Returns false when W
 // is numerically zero (R = 0 then, Q unspecified): a lucky breakdown.

@@ -26,10 +26,19 @@ struct Status {  // exception carrying a kt_status; caught at the ABI edge
             ::kt::fail(KT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));      \
     } while (0)
 
-// Growable device buffer (bytes).
+// Growable device buffer (bytes); owns its allocation (move-only).
 struct DevBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : ptr(o.ptr), bytes(o.bytes) { o.ptr = nullptr; o.bytes = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) { release(); ptr = o.ptr; bytes = o.bytes; o.ptr = nullptr; o.bytes = 0; }
+        return *this;
+    }
+    ~DevBuf() { release(); }
     void ensure(size_t want) {
         if (want <= bytes) return;
         if (ptr) (void)hipFree(ptr);
@@ -50,6 +59,10 @@ struct DevBuf {
 struct PinnedBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() { release(); }
     void ensure(size_t want) {
         if (want <= bytes) return;
         if (ptr) (void)hipHostFree(ptr);
@@ -79,6 +92,7 @@ enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_NSLOTS = 2 };
 struct Workspace {
     DevBuf X0, X1, Y, partial, coef, scales, k2s, trec;
     DevBuf small, small2, qrtmp, eigA, eigW, eigInfo;  // block-Krylov scratch
+    DevBuf hist, norm_part;                             // sweep scale history, inf-norm partials
     PinnedBuf host_trec;
 };
 

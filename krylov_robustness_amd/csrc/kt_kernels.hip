@@ -479,6 +479,54 @@ __global__ __launch_bounds__(256) void k_norm(const double* __restrict__ partial
     }
 }
 
+// ---------------------------------------------------------------------------
+// Small streaming kernels for the Afun paths (mc_trace.m / expmv.m).
+// ---------------------------------------------------------------------------
+// Y[r, c] = sum_j U[r, j*P + c] * W[j*P + c]   (f(A)x = ||x|| V f(T) e1)
+__global__ __launch_bounds__(256) void k_weighted_sum(int n, int m, int P, int nc,
+                                                      const double* __restrict__ U, int ldu,
+                                                      const double* __restrict__ W,
+                                                      double* __restrict__ Y, int ldy) {
+    const int64_t total = (int64_t)n * nc;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = t / nc;
+        const int c = (int)(t % nc);
+        double s = 0.0;
+        for (int j = 0; j < m; ++j) s = fma(U[r * ldu + (int64_t)j * P + c], W[j * P + c], s);
+        Y[r * ldy + c] = s;
+    }
+}
+
+// Y[:, 0:nc] = a X + b Y
+__global__ __launch_bounds__(256) void k_axpby(int n, int nc, double a, const double* __restrict__ X,
+                                               int ldx, double b, double* __restrict__ Y, int ldy) {
+    const int64_t total = (int64_t)n * nc;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = t / nc;
+        const int c = (int)(t % nc);
+        const double y = (b == 0.0) ? 0.0 : b * Y[r * ldy + c];
+        Y[r * ldy + c] = fma(a, X[r * ldx + c], y);
+    }
+}
+
+// per-block partial of the matrix infinity norm max_r sum_c |X[r, c]|
+__global__ __launch_bounds__(256) void k_inf_norm(int n, int nc, const double* __restrict__ X,
+                                                  int ldx, double* __restrict__ partial) {
+    double mx = 0.0;
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+        double s = 0.0;
+        for (int c = 0; c < nc; ++c) s += fabs(X[(int64_t)r * ldx + c]);
+        mx = fmax(mx, s);
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    __shared__ double red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[blockIdx.x] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+}
+
 __global__ void k_fill(double* __restrict__ x, int count, double v) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < count) x[t] = v;
@@ -596,6 +644,32 @@ hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, doub
         constexpr int PP = decltype(c)::value;
         k_norm<PP><<<(3 * PP + 3) / 4, 256, 0, st>>>(partial, nblk, k2s, scale_next, t_low);
     });
+}
+
+static int stream_grid(int64_t total) {
+    int64_t g = (total + 255) / 256;
+    if (g > 4096) g = 4096;
+    return g < 1 ? 1 : (int)g;
+}
+
+hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int ldu,
+                               const double* W, double* Y, int ldy, hipStream_t st) {
+    k_weighted_sum<<<stream_grid((int64_t)n * nc), 256, 0, st>>>(n, m, P, nc, U, ldu, W, Y, ldy);
+    return hipGetLastError();
+}
+
+hipError_t launch_axpby(int n, int nc, double a, const double* X, int ldx, double b, double* Y,
+                        int ldy, hipStream_t st) {
+    k_axpby<<<stream_grid((int64_t)n * nc), 256, 0, st>>>(n, nc, a, X, ldx, b, Y, ldy);
+    return hipGetLastError();
+}
+
+int inf_norm_blocks() { return 1024; }
+
+hipError_t launch_inf_norm(int n, int nc, const double* X, int ldx, double* partial,
+                           hipStream_t st) {
+    k_inf_norm<<<inf_norm_blocks(), 256, 0, st>>>(n, nc, X, ldx, partial);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st) {

@@ -27,5 +27,12 @@ hipError_t launch_update(int P, int grid, int n, const double* y, double* uprev,
 hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, double* scale_next,
                        double* t_low, hipStream_t st);
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st);
+hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int ldu,
+                               const double* W, double* Y, int ldy, hipStream_t st);
+hipError_t launch_axpby(int n, int nc, double a, const double* X, int ldx, double b, double* Y,
+                        int ldy, hipStream_t st);
+int inf_norm_blocks();
+hipError_t launch_inf_norm(int n, int nc, const double* X, int ldx, double* partial,
+                           hipStream_t st);
 
 }  // namespace kt

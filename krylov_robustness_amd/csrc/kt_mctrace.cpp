@@ -1,0 +1,339 @@
+// kt_mctrace.cpp -- mc_trace.m / trace_exp.m / expmv.m on the device.
+//
+//   mc_trace.m  -> kt_mc_trace: block Hutchinson with Hutch++-style nested
+//                  deflation (m = 10 columns per round, K = ceil(maxit/30)).
+//                  Afun is one of: the matrix itself (mc_trace.m:32-34), the
+//                  Lanczos-f action, or expmv (trace_exp.m:5).
+//   trace_exp.m -> kt_trace_exp: mc_trace(Afun, n, 1e-4, 1000, 1).
+//   expmv.m     -> kt_expmv (+ select_taylor_degree.m, normAm.m).
+// Probes S, G of round it are Rademacher columns (it-1)*20 + [0,10) and
+// [10,20) of the build's counter RNG (oracle/krylov_oracle.py:mc_trace).
+#include <algorithm>
+#include <cmath>
+
+#include "kt_launch.h"
+#include "kt_slq.h"
+
+namespace kt {
+
+// theta_m for m = 1..100, prec = 'double' (functions/theta_taylor.mat,
+// Al-Mohy & Higham 2011, Table; loaded by select_taylor_degree.m:31).
+static const double kTheta[100] = {
+2.2204460492503131e-16, 2.5809568029946243e-08, 1.3863478661191185e-05, 0.00033971688399768305,
+0.0024008763578872742, 0.0090656564075951018, 0.023844555325002736, 0.049912288711153226,
+0.08957760203223343, 0.1441829761614378, 0.21423580684517107, 0.29961589138115802,
+0.3997775336316795, 0.51391469361242936, 0.64108352330411988, 0.78028742566265763,
+0.93053284607865683, 1.0908637192900361, 1.2603810606426387, 1.4382525968043369,
+1.6237159502358214, 1.8160778162150852, 2.0147107809446161, 2.2190488693650896,
+2.4285825244428265, 2.6428534574594353, 2.8614496339342641, 3.0840005449891619,
+3.3101728398902708, 3.5396663487436895, 3.772210495681751, 4.0075610861180397,
+4.2454974425796959, 4.4858198594473686, 4.728347345793539, 4.9729156261919814,
+5.219375371084058, 5.4675906305245441, 5.7174374475720127, 5.9688026300418491,
+6.221582661689891, 6.4756827360799845, 6.731015898381024, 6.9875022821306301,
+7.2450684295979526, 7.5036466857888637, 7.763174657377987, 8.0235947289399796,
+8.2848536298039175, 8.5469020456849325, 8.8096942699713221, 9.0731878901761451,
+9.3373435056120133, 9.6021244728265565, 9.8674966757534008, 10.133428317897478,
+10.399889734191031, 10.666853220434106, 10.934292878475777, 11.202184475504579,
+11.470505316002537, 11.739234125080184, 12.008350942053168, 12.277837023246892,
+12.547674753126438, 12.817847562946627, 13.088339856203294, 13.359136940242903,
+13.630224963455026, 13.901590857531859, 14.173222284331819, 14.445107586931254,
+14.717235744490083, 14.989596330594328, 15.262179474771679, 15.534975826905702,
+15.807976524300871, 16.081173161174046, 16.354557760369328, 16.628122747112073,
+16.901860924634942, 17.175765451524093, 17.449829820647437, 17.724047839539214,
+17.998413612126303, 18.27292152169181, 18.54756621498051, 18.822342587358953,
+19.09724576895055, 19.372271111672617, 19.647414177108576, 19.922670725154251,
+20.198036703383082, 20.473508237083141, 20.749081619935929, 21.024753305356054,
+21.300519898663481, 21.576378150721375, 21.85232495499011, 22.128357353464594
+};
+
+enum { AFUN_MATRIX = 0, AFUN_LANCZOS = 1, AFUN_EXPMV = 2 };
+
+static double inf_norm(kt_matrix_s* A, const double* X, int ld, int nc) {
+    kt_context_s* ctx = A->ctx;
+    const int nb = inf_norm_blocks();
+    ctx->ws.norm_part.ensure(sizeof(double) * nb);
+    KT_HIP(launch_inf_norm((int)A->n, nc, X, ld, ctx->ws.norm_part.as<double>(), ctx->stream));
+    std::vector<double> h(nb);
+    KT_HIP(hipMemcpyAsync(h.data(), ctx->ws.norm_part.ptr, sizeof(double) * nb, hipMemcpyDeviceToHost,
+                          ctx->stream));
+    KT_HIP(hipStreamSynchronize(ctx->stream));
+    return *std::max_element(h.begin(), h.end());
+}
+
+// normAm.m: ||A^m||_1 for A >= 0 (exact: e = A'^m ones, c = ||e||_inf).
+static double normAm(kt_matrix_s* A, int m) {
+    kt_context_s* ctx = A->ctx;
+    const int64_t n = A->n;
+    DevMat e, t;
+    e.alloc(ctx, n, 1);
+    t.alloc(ctx, n, 1);
+    KT_HIP(launch_fill(e.col(0), (int)n, 1.0, ctx->stream));
+    for (int j = 0; j < m; ++j) {  // A symmetric: A' = A
+        spmm(A, e.col(0), 1, t.col(0), 1, 1);
+        copy_cols(ctx, n, t.col(0), 1, e.col(0), 1, 1);
+    }
+    return inf_norm(A, e.col(0), 1, 1);
+}
+
+struct Expmv {
+    int s = 1, m = 0, mv = 0;
+};
+
+// expmv.m:1-94 with prec = 'double', shift = true, bal = false, M = [] ;
+// F = exp(t A) B on nc columns of the device block B (ld), written to F.
+static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, int nc, double* F) {
+    kt_context_s* ctx = A->ctx;
+    const int64_t n = A->n;
+    hipStream_t st = ctx->stream;
+    Expmv r;
+    // shift: mu = trace(A)/n   (:31-36)
+    double trA = 0.0, minv = 0.0;
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t k = A->h_rowptr[i]; k < A->h_rowptr[i + 1]; ++k) {
+            if (A->h_col[k] == i) trA += A->h_val[k];
+            minv = std::min(minv, A->h_val[k]);
+        }
+    const double mu = n ? trA / (double)n : 0.0;
+    // select_taylor_degree(t*(A - mu I), b)   (:41; select_taylor_degree.m:16-68)
+    const int m_max = 55, p_max = 8;
+    std::vector<double> colsum(n, 0.0);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t k = A->h_rowptr[i]; k < A->h_rowptr[i + 1]; ++k)
+            colsum[A->h_col[k]] += std::fabs(t * (A->h_val[k] - (A->h_col[k] == i ? mu : 0.0)));
+    for (int64_t i = 0; i < n; ++i) {  // diagonal entries absent from the CSR still get -mu
+        bool has = false;
+        for (int64_t k = A->h_rowptr[i]; k < A->h_rowptr[i + 1]; ++k) has |= (A->h_col[k] == i);
+        if (!has) colsum[i] += std::fabs(t * mu);
+    }
+    const double normA = n ? *std::max_element(colsum.begin(), colsum.end()) : 0.0;
+    std::vector<double> alpha(p_max - 1);
+    if (normA <= 4.0 * kTheta[m_max - 1] * p_max * (p_max + 3) / ((double)m_max * nc)) {
+        std::fill(alpha.begin(), alpha.end(), normA);  // unA = 1
+    } else {
+        if (mu != 0.0 || minv < 0.0)
+            fail(KT_ERR_UNSUPPORTED, "expmv: normest1 branch of normAm.m (A - mu I not >= 0) is not built");
+        std::vector<double> eta(p_max);
+        for (int p = 1; p <= p_max; ++p) {
+            const double c = normAm(A, p + 1) * std::pow(std::fabs(t), p + 1);
+            r.mv += p + 1;
+            eta[p - 1] = std::pow(c, 1.0 / (p + 1));
+        }
+        for (int p = 1; p < p_max; ++p) alpha[p - 1] = std::max(eta[p - 1], eta[p]);
+    }
+    // M(m, p-1) = alpha(p-1) / theta(m); cost = min over (m, p) of m * ceil(M)   (expmv.m:57-67)
+    double cost = INFINITY;
+    int m_best = 0;
+    for (int mm = 1; mm <= m_max; ++mm) {
+        double cm = INFINITY;
+        for (int p = 2; p <= p_max; ++p) {
+            if (mm < p * (p - 1) - 1) continue;
+            const double Mv = alpha[p - 2] / kTheta[mm - 1];
+            double c = std::ceil(Mv) * mm;
+            if (c == 0.0) c = INFINITY;
+            cm = std::min(cm, c);
+        }
+        if (cm < cost) {
+            cost = cm;
+            m_best = mm;
+        }
+    }
+    if (t == 0.0) m_best = 0;
+    if (cost == INFINITY) cost = 0.0;
+    r.m = m_best;
+    r.s = (int)std::max(cost / std::max(m_best, 1), 1.0);
+    const double tol = std::ldexp(1.0, -53);
+    const double eta = std::exp(t * mu / r.s);  // :70
+    // f = b; b = (t/(s k)) (A - mu I) b ...   (:71-92)
+    DevMat b, Ab;
+    b.alloc(ctx, n, ld);
+    Ab.alloc(ctx, n, ld);
+    copy_cols(ctx, n, Bsrc, ld, b.col(0), ld, nc);
+    copy_cols(ctx, n, Bsrc, ld, F, ld, nc);
+    for (int i = 0; i < r.s; ++i) {
+        double c1 = inf_norm(A, b.col(0), ld, nc);
+        for (int k = 1; k <= r.m; ++k) {
+            spmm(A, b.col(0), ld, Ab.col(0), ld, nc);
+            if (mu != 0.0) KT_HIP(launch_axpby((int)n, nc, -mu, b.col(0), ld, 1.0, Ab.col(0), ld, st));
+            KT_HIP(launch_axpby((int)n, nc, t / ((double)r.s * k), Ab.col(0), ld, 0.0, b.col(0), ld, st));
+            r.mv += 1;
+            KT_HIP(launch_axpby((int)n, nc, 1.0, b.col(0), ld, 1.0, F, ld, st));
+            const double c2 = inf_norm(A, b.col(0), ld, nc);
+            if (c1 + c2 <= tol * inf_norm(A, F, ld, nc)) break;
+            c1 = c2;
+        }
+        KT_HIP(launch_axpby((int)n, nc, eta, F, ld, 0.0, F, ld, st));  // f = eta f
+        copy_cols(ctx, n, F, ld, b.col(0), ld, nc);                    // b = f
+    }
+    KT_HIP(hipStreamSynchronize(st));
+    return r;
+}
+
+// The Afun handle of mc_trace on device blocks (n x ld, nc <= ld columns).
+struct AfunDev {
+    kt_matrix_s* A;
+    int kind, fun, m;
+    void apply(const double* X, int ld, int nc, double* Y) {
+        switch (kind) {
+        case AFUN_MATRIX: spmm(A, X, ld, Y, ld, nc); break;
+        case AFUN_LANCZOS: lanczos_columns(A, X, ld, nc, m, fun, nullptr, Y, ld); break;
+        default: expmv_device(A, 1.0, X, ld, nc, Y); break;
+        }
+    }
+    // sum_c x_c' F(x_c)
+    double trace_quad(const double* X, int ld, int nc) {
+        if (kind == AFUN_LANCZOS) {
+            std::vector<double> q(nc);
+            lanczos_columns(A, X, ld, nc, m, fun, q.data(), nullptr, 0);
+            double s = 0.0;
+            for (double v : q) s += v;
+            return s;
+        }
+        DevMat Y;
+        Y.alloc(A->ctx, A->n, ld);
+        apply(X, ld, nc, Y.col(0));
+        std::vector<double> G;
+        gram(A->ctx, A->n, X, ld, nc, Y.col(0), ld, nc, G);
+        double s = 0.0;
+        for (int c = 0; c < nc; ++c) s += G[c + (size_t)c * nc];
+        return s;
+    }
+};
+
+// X <- X - Q (Q' X)  on nc columns (the deflation aux of mc_trace.m:47)
+static void project(kt_context_s* ctx, int64_t n, const double* Q, int ld, int nq, double* X, int nc) {
+    std::vector<double> G;
+    gram(ctx, n, Q, ld, nq, X, ld, nc, G);
+    for (double& g : G) g = -g;
+    combine(ctx, n, Q, ld, nq, G, nc, 1.0, X, ld);
+}
+
+// mc_trace.m:1-63
+void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isAreal, uint64_t seed,
+                   double* tr_out, double* res_out, int* it_out) {
+    kt_context_s* ctx = A->ctx;
+    const int64_t n = A->n;
+    const int mb = 10, ld = 16;                    // :36
+    const int K = (maxit + 3 * mb - 1) / (3 * mb);  // :41 ceil(maxit/30)
+    double tr = 0.0, tr_old = 0.0, tr_new = 0.0, res = 1.0;
+    std::vector<DevMat> Qs;
+    DevMat S, G, Z, Y;
+    int it = 0;
+    for (it = 1; it <= K; ++it) {
+        const int64_t base = (int64_t)(it - 1) * 2 * mb;
+        S.alloc(ctx, n, ld);
+        G.alloc(ctx, n, ld);
+        KT_HIP(launch_rademacher(ld, (int)n, seed, base, A->d_perm, S.col(0), ctx->stream));       // :43
+        KT_HIP(launch_rademacher(ld, (int)n, seed, base + mb, A->d_perm, G.col(0), ctx->stream));  // :44
+        zero_cols(ctx, n, S.col(mb), ld, ld - mb);
+        zero_cols(ctx, n, G.col(mb), ld, ld - mb);
+        // Y = Afun_it(S) = P_{it-1}..P_1 F(P_1..P_{it-1} S)                       :45
+        Z.alloc(ctx, n, ld);
+        Y.alloc(ctx, n, ld);
+        copy_cols(ctx, n, S.col(0), ld, Z.col(0), ld, mb);
+        for (int q = (int)Qs.size() - 1; q >= 0; --q) project(ctx, n, Qs[q].col(0), ld, mb, Z.col(0), mb);
+        F.apply(Z.col(0), ld, mb, Y.col(0));
+        for (size_t q = 0; q < Qs.size(); ++q) project(ctx, n, Qs[q].col(0), ld, mb, Y.col(0), mb);
+        std::vector<double> R;
+        householder_qr(ctx, n, Y.col(0), ld, mb, R);                               // [Q, ~] = qr(.,0)
+        // tr += trace(Q' Afun_it(Q)) = sum quadforms of P_1..P_{it-1} Q          :46
+        copy_cols(ctx, n, Y.col(0), ld, Z.col(0), ld, mb);
+        for (int q = (int)Qs.size() - 1; q >= 0; --q) project(ctx, n, Qs[q].col(0), ld, mb, Z.col(0), mb);
+        tr += F.trace_quad(Z.col(0), ld, mb);
+        Qs.emplace_back();                                                         // :47-48
+        Qs.back().alloc(ctx, n, ld);
+        copy_cols(ctx, n, Y.col(0), ld, Qs.back().col(0), ld, mb);
+        // tr_new = tr + trace(G' Afun_{it+1}(G)) / m                              :49
+        copy_cols(ctx, n, G.col(0), ld, Z.col(0), ld, mb);
+        for (int q = (int)Qs.size() - 1; q >= 0; --q) project(ctx, n, Qs[q].col(0), ld, mb, Z.col(0), mb);
+        tr_new = tr + F.trace_quad(Z.col(0), ld, mb) / mb;
+        res = std::fabs(tr_new - tr_old) / std::max(std::fabs(tr_new), std::fabs(tr_old));  // :50
+        if (res < tol) break;                                                      // :54-56
+        tr_old = tr_new;
+    }
+    if (it > K) it = K;
+    (void)isAreal;  // :60-62 real part: the device estimator is real
+    *tr_out = tr_new;
+    if (res_out) *res_out = res;
+    if (it_out) *it_out = it;
+}
+
+}  // namespace kt
+
+using namespace kt;
+
+#define KT_TRY try {
+#define KT_CATCH                                  \
+    }                                             \
+    catch (const kt::Status& s) {                 \
+        kt::set_error(s.msg);                     \
+        return s.code;                            \
+    }                                             \
+    catch (const std::exception& e) {             \
+        kt::set_error(e.what());                  \
+        return KT_ERR_ARG;                        \
+    }                                             \
+    return KT_OK;
+
+extern "C" {
+
+int kt_mc_trace(kt_matrix_t A, int afun, int fun, int m, double tol, int maxit, int isAreal,
+                uint64_t seed, double* tr, double* res, int* it) {
+    KT_TRY
+    if (!A || !tr) fail(KT_ERR_ARG, "NULL argument");
+    if (afun < AFUN_MATRIX || afun > AFUN_EXPMV) fail(KT_ERR_ARG, "unknown Afun kind");
+    if (fun < KT_FUN_EXP || fun > KT_FUN_SQRT) fail(KT_ERR_ARG, "unknown fun code");
+    if (afun == AFUN_LANCZOS && (m < 1 || m > 256)) fail(KT_ERR_ARG, "m must be in [1, 256]");
+    if (maxit < 1) fail(KT_ERR_ARG, "maxit must be >= 1");
+    if (A->n < 10) fail(KT_ERR_UNSUPPORTED, "mc_trace needs n >= 10 (qr of an n x 10 block)");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    AfunDev F{A, afun, fun, m};
+    mc_trace_impl(A, F, tol, maxit, isAreal, seed, tr, res, it);
+    KT_CATCH
+}
+
+int kt_trace_exp(kt_matrix_t A, int afun, int m, uint64_t seed, double* tr) {
+    KT_TRY
+    if (!A || !tr) fail(KT_ERR_ARG, "NULL argument");
+    if (afun != AFUN_LANCZOS && afun != AFUN_EXPMV) fail(KT_ERR_ARG, "trace_exp: Afun must be Lanczos or expmv");
+    if (A->n < 10) fail(KT_ERR_UNSUPPORTED, "trace_exp needs n >= 10");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    AfunDev F{A, afun, KT_FUN_EXP, m};
+    mc_trace_impl(A, F, 1e-4, 1000, 1, seed, tr, nullptr, nullptr);  // trace_exp.m:5-6
+    KT_CATCH
+}
+
+int kt_expmv(kt_matrix_t A, double t, int64_t ncols, const double* B, double* F, int* s, int* mdeg,
+             int* mv) {
+    KT_TRY
+    if (!A || !B || !F || ncols < 1 || ncols > 128) fail(KT_ERR_ARG, "bad argument (1 <= ncols <= 128)");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    const int ld = pow2_at_least((int)ncols);
+    DevMat Bd, Fd;
+    Bd.alloc(A->ctx, A->n, ld);
+    Fd.alloc(A->ctx, A->n, ld);
+    upload_rows(A, B, (int)ncols, Bd.col(0), ld);
+    Expmv r = expmv_device(A, t, Bd.col(0), ld, (int)ncols, Fd.col(0));
+    download_block(A, Fd.col(0), ld, (int)ncols, F);
+    if (s) *s = r.s;
+    if (mdeg) *mdeg = r.m;
+    if (mv) *mv = r.mv;
+    KT_CATCH
+}
+
+int kt_lanczos_fmv(kt_matrix_t A, int fun, int m, int64_t ncols, const double* X, double* Y) {
+    KT_TRY
+    if (!A || !X || !Y || ncols < 1 || ncols > 128) fail(KT_ERR_ARG, "bad argument (1 <= ncols <= 128)");
+    if (fun < KT_FUN_EXP || fun > KT_FUN_SQRT) fail(KT_ERR_ARG, "unknown fun code");
+    if (m < 1 || m > 256) fail(KT_ERR_ARG, "m must be in [1, 256]");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    const int ld = pow2_at_least((int)ncols);
+    DevMat Xd, Yd;
+    Xd.alloc(A->ctx, A->n, ld);
+    Yd.alloc(A->ctx, A->n, ld);
+    upload_rows(A, X, (int)ncols, Xd.col(0), ld);
+    lanczos_columns(A, Xd.col(0), ld, (int)ncols, m, fun, nullptr, Yd.col(0), ld);
+    download_block(A, Yd.col(0), ld, (int)ncols, Y);
+    KT_CATCH
+}
+
+}  // extern "C"

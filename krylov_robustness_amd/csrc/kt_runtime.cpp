@@ -117,6 +117,7 @@ int kt_context_destroy(kt_context_t ctx) {
     w.coef.release(); w.scales.release(); w.k2s.release();
     w.small.release(); w.small2.release(); w.qrtmp.release();
     w.eigA.release(); w.eigW.release(); w.eigInfo.release();
+    w.hist.release(); w.norm_part.release();
     if (ctx->blas) rocblas_destroy_handle(static_cast<rocblas_handle>(ctx->blas)); w.trec.release(); w.host_trec.release();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;

@@ -1,21 +1,26 @@
-// kt_slq.cpp -- driver of the probe-Lanczos quadrature hot path.
+// kt_slq.cpp -- the probe-Lanczos sweep engine and the hot-path entry point.
 //
-// For each sweep of P probes (one n x P probe block), m Lanczos steps run as
-// four launches each (K1 spmm_dot, coef, K2 update, norm; see
-// kt_kernels.hip).  The per-probe recurrence coefficients (alpha, up, low)
-// go to a pinned host record; once all sweeps are queued the host solves
-// the m x m tridiagonal eigenproblems (kt_dense.cpp) and forms
-//   q_p = ||z_p||^2 e1' f(T_p) e1,   T_p = (H + H')/2   (trace_fun_update.m:78-81).
+// One sweep = P independent single-vector Lanczos runs (one n x P block),
+// m steps of four launches each (K1 spmm_dot, coef, K2 update, norm; see
+// kt_kernels.hip).  The per-column recurrence coefficients (alpha, up, low)
+// land in a host record; the host then solves the m x m tridiagonal
+// eigenproblems (kt_dense.cpp, as the north star prescribes) and forms
+//   q_c = ||x_c||^2 e1' f(T_c) e1,   T_c = (H + H')/2   (trace_fun_update.m:78-81)
+// and, when the basis is recorded, f(A) x_c ~= ||x_c|| V_c f(T_c) e1.
+// Sweeps are seeded either by the device Rademacher generator (kt_slq_trace,
+// the Hutchinson hot path) or by a given device block (the Lanczos-f Afun
+// of mc_trace, kt_mctrace.cpp).
+#include "kt_slq.h"
+
 #include <algorithm>
 #include <cmath>
 #include <thread>
 
-#include "kt_internal.h"
 #include "kt_launch.h"
 
 namespace kt {
 
-static int auto_block(int64_t n, int64_t nprobes) {
+int slq_auto_block(int64_t n, int64_t nprobes) {
     // Largest power-of-two P whose gathered n x P block (8nP bytes) stays
     // within ~160 MB, i.e. inside the 256 MiB Infinity Cache next to the CSR
     // stream; measured best on MI355X for n = 1M (P = 16) and n = 100k
@@ -24,6 +29,181 @@ static int auto_block(int64_t n, int64_t nprobes) {
     while (P > 8 && (double)n * 8.0 * P > 160.0e6) P >>= 1;
     while (P > 1 && P / 2 >= nprobes) P >>= 1;
     return P;
+}
+
+// Run one sweep.  rec_host receives [alpha | up | low][m][P].
+// init: if seeded by RNG, `x` == nullptr; else x (device, n x ldx, ncols
+// columns, original-column norms^2 in norms2) is copied into the sweep block.
+void lanczos_sweep(kt_matrix_s* A, int P, int m, uint64_t seed, int64_t probe_base,
+                   const double* x, int ldx, int ncols, const double* norms2, double* rec_host,
+                   DevMat* basis, std::vector<double>* scale_hist) {
+    kt_context_s* ctx = A->ctx;
+    const int n = (int)A->n;
+    hipStream_t st = ctx->stream;
+    const int grid = spmm_grid(n, P, ctx->num_cu * 4);  // K2 / short rows
+    const int lblocks = long_blocks_for(A->n_long, ctx->num_cu * 2);
+    const int grid1 = grid + lblocks;                    // K1 total
+    Workspace& w = ctx->ws;
+    const size_t blk_bytes = sizeof(double) * (size_t)n * P;
+    w.X0.ensure(blk_bytes);
+    w.X1.ensure(blk_bytes);
+    w.Y.ensure(blk_bytes);
+    w.partial.ensure(sizeof(double) * (size_t)(grid1 + grid * 3) * P);
+    w.k2s.ensure(sizeof(double) * 4 * P);
+    w.coef.ensure(sizeof(double) * 2 * P);
+    w.scales.ensure(sizeof(double) * 3 * P);
+    const size_t rec = (size_t)3 * m * P;
+    w.trec.ensure(sizeof(double) * rec);
+    double* part1 = w.partial.as<double>();
+    double* part2 = part1 + (size_t)grid1 * P;
+    double* k2s = w.k2s.as<double>();
+    double* coef = w.coef.as<double>();
+    double* trec = w.trec.as<double>();
+
+    double* ucur = w.X1.as<double>();
+    double* uprev = w.X0.as<double>();
+    double* sc = w.scales.as<double>();
+    double* sp = sc + P;
+    double* sn = sc + 2 * P;
+    if (!x) {
+        KT_HIP(launch_rademacher(P, n, seed, probe_base, A->d_perm, ucur, st));
+        KT_HIP(launch_fill(sc, P, 1.0 / std::sqrt((double)n), st));
+        KT_HIP(launch_fill(k2s, P, (double)n, st));  // ||z||^2 = n
+    } else {
+        KT_HIP(hipMemsetAsync(ucur, 0, blk_bytes, st));
+        KT_HIP(hipMemcpy2DAsync(ucur, sizeof(double) * P, x, sizeof(double) * ldx,
+                                sizeof(double) * ncols, (size_t)n, hipMemcpyDeviceToDevice, st));
+        std::vector<double> s0(P, 0.0), q0(P, 0.0);
+        for (int c = 0; c < ncols; ++c)
+            if (norms2[c] > 0.0) {
+                s0[c] = 1.0 / std::sqrt(norms2[c]);
+                q0[c] = norms2[c];
+            }
+        KT_HIP(hipMemcpyAsync(sc, s0.data(), sizeof(double) * P, hipMemcpyHostToDevice, st));
+        KT_HIP(hipMemcpyAsync(k2s, q0.data(), sizeof(double) * P, hipMemcpyHostToDevice, st));
+        KT_HIP(hipStreamSynchronize(st));  // s0/q0 are stack temporaries
+    }
+    if (scale_hist) scale_hist->assign((size_t)m * P, 0.0);
+    DevBuf* hist_dev = nullptr;
+    if (scale_hist) {
+        hist_dev = &w.hist;
+        hist_dev->ensure(sizeof(double) * (size_t)m * P);
+    }
+    for (int j = 0; j < m; ++j) {
+        const int first = (j == 0);
+        if (basis) {  // record u_j and s_j (v_j = s_j u_j)
+            KT_HIP(hipMemcpy2DAsync(basis->col(j * P), sizeof(double) * basis->ld, ucur,
+                                    sizeof(double) * P, sizeof(double) * P, (size_t)n,
+                                    hipMemcpyDeviceToDevice, st));
+            KT_HIP(hipMemcpyAsync(hist_dev->as<double>() + (size_t)j * P, sc, sizeof(double) * P,
+                                  hipMemcpyDeviceToDevice, st));
+        }
+        prof_begin(ctx, PROF_SPMM);
+        KT_HIP(launch_spmm_dot(P, ctx->k1_flags | (A->unit_values ? 2 : 0), grid1, A->d_rowptr,
+                               A->d_col, A->d_val, n, ucur, sc, w.Y.as<double>(), part1,
+                               A->d_long_rows, A->n_long, A->long_thresh, lblocks, st));
+        prof_end(ctx, PROF_SPMM);
+        KT_HIP(launch_coef_cgs2(P, part1, grid1, first, k2s, sc, sp, coef,
+                                trec + (size_t)(0 * m + j) * P, trec + (size_t)(1 * m + j) * P, st));
+        prof_begin(ctx, PROF_UPDATE);
+        KT_HIP(launch_update(P, grid, n, w.Y.as<double>(), uprev, ucur, sc, sp, coef, first, part2,
+                             st));
+        prof_end(ctx, PROF_UPDATE);
+        KT_HIP(launch_norm(P, part2, grid, k2s, sn, trec + (size_t)(2 * m + j) * P, st));
+        std::swap(ucur, uprev);  // uprev now holds u_{j+1}
+        double* t = sp;
+        sp = sc;
+        sc = sn;
+        sn = t;
+    }
+    KT_HIP(hipMemcpyAsync(rec_host, trec, sizeof(double) * rec, hipMemcpyDeviceToHost, st));
+    if (scale_hist)
+        KT_HIP(hipMemcpyAsync(scale_hist->data(), hist_dev->ptr, sizeof(double) * (size_t)m * P,
+                              hipMemcpyDeviceToHost, st));
+}
+
+// Column c of a sweep record -> symmetric tridiagonal (alpha, off); returns
+// the number of steps before a lucky breakdown (lanczos_krylov.m:91-93).
+int record_tridiag(const double* R, int m, int P, int c, double* al, double* off) {
+    int steps = m;
+    for (int j = 0; j < m; ++j)
+        if (R[(size_t)(2 * m + j) * P + c] < 1e-8) {
+            steps = j + 1;
+            break;
+        }
+    for (int j = 0; j < steps; ++j) al[j] = R[(size_t)(0 * m + j) * P + c];
+    for (int j = 0; j + 1 < steps; ++j)
+        off[j] = 0.5 * (R[(size_t)(2 * m + j) * P + c] + R[(size_t)(1 * m + j + 1) * P + c]);
+    return steps;
+}
+
+template <class F>
+static void parallel_for(int64_t count, int64_t serial_below, F&& f) {
+    unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (count < serial_below) nth = 1;
+    if (nth == 1) {
+        f((int64_t)0, count);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nth; ++t) th.emplace_back(f, count * t / nth, count * (t + 1) / nth);
+    for (auto& t : th) t.join();
+}
+
+void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m, int fun,
+                     double* quad, double* Y, int ldy) {
+    kt_context_s* ctx = A->ctx;
+    const int64_t n = A->n;
+    std::vector<double> nrm2;
+    gram(ctx, n, X, ldx, ncols, X, ldx, ncols, nrm2);
+    std::vector<double> norms2(ncols);
+    for (int c = 0; c < ncols; ++c) norms2[c] = nrm2[c + (size_t)c * ncols];
+    int P = 1;
+    while (P < ncols && P < 16) P <<= 1;
+    for (int c0 = 0; c0 < ncols; c0 += P) {
+        const int nc = std::min(P, ncols - c0);
+        std::vector<double> rec((size_t)3 * m * P);
+        DevMat basis;
+        std::vector<double> hist;
+        if (Y) basis.alloc(ctx, n, m * P);
+        lanczos_sweep(A, P, m, 0, 0, X + c0, ldx, nc, norms2.data() + c0, rec.data(),
+                      Y ? &basis : nullptr, Y ? &hist : nullptr);
+        KT_HIP(hipStreamSynchronize(ctx->stream));
+        std::vector<double> W((size_t)m * P, 0.0);  // weights for Y = sum_j u_j w_j
+        for (int c = 0; c < nc; ++c) {
+            std::vector<double> al(m), off(m);
+            const int steps = record_tridiag(rec.data(), m, P, c, al.data(), off.data());
+            if (norms2[c0 + c] == 0.0) {
+                if (quad) quad[c0 + c] = 0.0;
+                continue;
+            }
+            if (quad) quad[c0 + c] = norms2[c0 + c] * tridiag_quadrature(steps, al.data(), off.data(), fun);
+            if (Y) {
+                // f(T) e1 = Z f(theta) Z(0,:)'
+                std::vector<double> T((size_t)steps * steps, 0.0), th(steps), Z((size_t)steps * steps);
+                for (int j = 0; j < steps; ++j) T[j + (size_t)j * steps] = al[j];
+                for (int j = 0; j + 1 < steps; ++j)
+                    T[j + 1 + (size_t)j * steps] = T[j + (size_t)(j + 1) * steps] = off[j];
+                sym_eig_host(steps, T.data(), th.data(), Z.data());
+                const double nx = std::sqrt(norms2[c0 + c]);
+                for (int j = 0; j < steps; ++j) {
+                    double cj = 0.0;
+                    for (int k = 0; k < steps; ++k)
+                        cj += Z[j + (size_t)k * steps] * fscalar(fun, th[k]) * Z[(size_t)k * steps];
+                    W[(size_t)j * P + c] = nx * hist[(size_t)j * P + c] * cj;  // v_j = s_j u_j
+                }
+            }
+        }
+        if (Y) {
+            DevBuf& dw = ctx->ws.small2;
+            dw.ensure(sizeof(double) * W.size());
+            KT_HIP(hipMemcpyAsync(dw.ptr, W.data(), sizeof(double) * W.size(), hipMemcpyHostToDevice,
+                                  ctx->stream));
+            KT_HIP(launch_weighted_sum((int)n, m, P, nc, basis.col(0), basis.ld, dw.as<double>(),
+                                       Y + c0, ldy, ctx->stream));
+            KT_HIP(hipStreamSynchronize(ctx->stream));
+        }
+    }
 }
 
 static bool pow2_le128(int b) { return b >= 1 && b <= 128 && (b & (b - 1)) == 0; }
@@ -37,7 +217,7 @@ extern "C" int kt_slq_plan(kt_matrix_t A, int64_t nprobes, int* block) {
         kt::set_error("kt_slq_plan: bad argument");
         return KT_ERR_ARG;
     }
-    *block = auto_block(A->n, nprobes);
+    *block = slq_auto_block(A->n, nprobes);
     return KT_OK;
 }
 
@@ -50,103 +230,32 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         if (nprobes < 0 || probe_offset < 0) fail(KT_ERR_ARG, "negative probe range");
         if (block != 0 && !pow2_le128(block)) fail(KT_ERR_ARG, "block must be 0 or a power of two <= 128");
         kt_context_s* ctx = A->ctx;
-        const int64_t n64 = A->n;
+        const int64_t n = A->n;
         if (sum_q) *sum_q = 0.0;
         if (sum_q2) *sum_q2 = 0.0;
-        if (nprobes == 0 || n64 == 0) return KT_OK;
-        const int n = (int)n64;
-        const int P = block ? block : auto_block(n64, nprobes);
+        if (nprobes == 0 || n == 0) return KT_OK;
+        const int P = block ? block : slq_auto_block(n, nprobes);
         const int64_t nsweeps = (nprobes + P - 1) / P;
-        const int grid = spmm_grid(n, P, ctx->num_cu * 4);           // K2 / short rows
-        const int lblocks = long_blocks_for(A->n_long, ctx->num_cu * 2);
-        const int grid1 = grid + lblocks;                             // K1 total
         KT_HIP(hipSetDevice(ctx->device));
-        hipStream_t st = ctx->stream;
-
+        const size_t rec = (size_t)3 * m * P;
         Workspace& w = ctx->ws;
-        const size_t blk_bytes = sizeof(double) * (size_t)n * P;
-        w.X0.ensure(blk_bytes);
-        w.X1.ensure(blk_bytes);
-        w.Y.ensure(blk_bytes);
-        w.partial.ensure(sizeof(double) * (size_t)(grid1 + grid * 3) * P);
-        w.k2s.ensure(sizeof(double) * 4 * P);
-        w.coef.ensure(sizeof(double) * 2 * P);
-        w.scales.ensure(sizeof(double) * 3 * P);
-        const size_t rec = (size_t)3 * m * P;  // [alpha | up | low][m][P]
-        w.trec.ensure(sizeof(double) * rec);
         w.host_trec.ensure(sizeof(double) * rec * nsweeps);
-
-        double* part1 = w.partial.as<double>();
-        double* part2 = part1 + (size_t)grid1 * P;
-        double* k2s = w.k2s.as<double>();
-        double* coef = w.coef.as<double>();
-        double* trec = w.trec.as<double>();
         double* htrec = w.host_trec.as<double>();
-
-        for (int64_t s = 0; s < nsweeps; ++s) {
-            double* ucur = w.X1.as<double>();
-            double* uprev = w.X0.as<double>();
-            double* sc = w.scales.as<double>();
-            double* sp = sc + P;
-            double* sn = sc + 2 * P;
-            KT_HIP(launch_rademacher(P, n, seed, probe_offset + s * P, A->d_perm, ucur, st));
-            KT_HIP(launch_fill(sc, P, 1.0 / std::sqrt((double)n), st));
-            KT_HIP(launch_fill(k2s, P, (double)n, st));  // ||z||^2 = n
-            for (int j = 0; j < m; ++j) {
-                const int first = (j == 0);
-                prof_begin(ctx, PROF_SPMM);
-                KT_HIP(launch_spmm_dot(P, ctx->k1_flags | (A->unit_values ? 2 : 0), grid1, A->d_rowptr, A->d_col, A->d_val, n,
-                                       ucur, sc, w.Y.as<double>(), part1, A->d_long_rows,
-                                       A->n_long, A->long_thresh, lblocks, st));
-                prof_end(ctx, PROF_SPMM);
-                KT_HIP(launch_coef_cgs2(P, part1, grid1, first, k2s, sc, sp, coef,
-                                        trec + (size_t)(0 * m + j) * P,
-                                        trec + (size_t)(1 * m + j) * P, st));
-                prof_begin(ctx, PROF_UPDATE);
-                KT_HIP(launch_update(P, grid, n, w.Y.as<double>(), uprev, ucur, sc, sp, coef, first,
-                                     part2, st));
-                prof_end(ctx, PROF_UPDATE);
-                KT_HIP(launch_norm(P, part2, grid, k2s, sn, trec + (size_t)(2 * m + j) * P, st));
-                std::swap(ucur, uprev);  // uprev now holds u_{j+1}
-                double* t = sp;
-                sp = sc;
-                sc = sn;
-                sn = t;
-            }
-            KT_HIP(hipMemcpyAsync(htrec + rec * s, trec, sizeof(double) * rec,
-                                  hipMemcpyDeviceToHost, st));
-        }
-        KT_HIP(hipStreamSynchronize(st));
+        for (int64_t s = 0; s < nsweeps; ++s)
+            lanczos_sweep(A, P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr, htrec + rec * s,
+                          nullptr, nullptr);
+        KT_HIP(hipStreamSynchronize(ctx->stream));
         prof_collect(ctx);
 
-        // host quadrature, parallel over probes
         std::vector<double> qv((size_t)nprobes);
-        unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-        if (nprobes < 64) nth = 1;
-        auto work = [&](int64_t p_begin, int64_t p_end) {
+        parallel_for(nprobes, 64, [&](int64_t pb, int64_t pe) {
             std::vector<double> al(m), off(m);
-            for (int64_t p = p_begin; p < p_end; ++p) {
-                const int64_t s = p / P;
-                const int c = (int)(p % P);
-                const double* R = htrec + rec * s;
-                int steps = m;
-                for (int j = 0; j < m; ++j) {
-                    if (R[(size_t)(2 * m + j) * P + c] < 1e-8) { steps = j + 1; break; }
-                }
-                for (int j = 0; j < steps; ++j) al[j] = R[(size_t)(0 * m + j) * P + c];
-                for (int j = 0; j + 1 < steps; ++j)
-                    off[j] = 0.5 * (R[(size_t)(2 * m + j) * P + c] + R[(size_t)(1 * m + j + 1) * P + c]);
+            for (int64_t p = pb; p < pe; ++p) {
+                const int steps = record_tridiag(htrec + rec * (p / P), m, P, (int)(p % P),
+                                                 al.data(), off.data());
                 qv[p] = (double)n * tridiag_quadrature(steps, al.data(), off.data(), fun);
             }
-        };
-        if (nth == 1) {
-            work(0, nprobes);
-        } else {
-            std::vector<std::thread> th;
-            for (unsigned t = 0; t < nth; ++t)
-                th.emplace_back(work, nprobes * t / nth, nprobes * (t + 1) / nth);
-            for (auto& t : th) t.join();
-        }
+        });
         double s1 = 0.0, s2 = 0.0;
         for (int64_t p = 0; p < nprobes; ++p) {
             s1 += qv[p];

@@ -1,0 +1,72 @@
+"""GPU parity for mc_trace / trace_exp / expmv / the Lanczos-f Afun (SURVEY.md
+§8a rows a1, a2, a3, a10) against the oracle on the same counter-RNG probes.
+Tolerances: 1e-9 relative where the device runs the reference algorithm
+(expmv Taylor loop, matrix Afun); 1e-6 for the Lanczos Afun inside mc_trace,
+where the device evaluates trace(Q' f(A) Q) as Gauss quadratures while the
+oracle forms the literal vectors f(A)Q ~= ||q|| V f(T) e1 (equal up to the
+loss of Lanczos orthogonality)."""
+import numpy as np
+import pytest
+
+from conftest import load_graph
+from oracle import krylov_oracle as ko
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def kra():
+    import krylov_robustness_amd as kra
+    return kra
+
+
+@pytest.mark.parametrize("name", ["anaheim", "oregon_A0", "austria"])
+def test_expmv_matches_oracle(kra, gpu_ctx, name):
+    A = load_graph(name)
+    b = np.random.default_rng(1).normal(size=(A.shape[0], 3))
+    F, s, m, mv = kra.expmv(1.0, kra.DeviceMatrix(A, gpu_ctx), b, ctx=gpu_ctx)
+    Fo, so, mo, mvo = ko.expmv(1.0, A, b)
+    assert (s, m) == (so, mo)
+    np.testing.assert_allclose(F, Fo, rtol=1e-11, atol=1e-13 * np.abs(Fo).max())
+
+
+def test_lanczos_fmv_matches_oracle(kra, gpu_ctx):
+    A = load_graph("rome")
+    X = np.random.default_rng(2).normal(size=(A.shape[0], 4))
+    Y = kra.lanczos_fmv(kra.DeviceMatrix(A, gpu_ctx), X, m=20, fun="exp", ctx=gpu_ctx)
+    Yo = ko.lanczos_fmv(A, X, 20, "exp")
+    np.testing.assert_allclose(Y, Yo, rtol=1e-8, atol=1e-10 * np.abs(Yo).max())
+
+
+@pytest.mark.parametrize("name", ["denmark", "anaheim"])
+def test_mc_trace_matrix_afun(kra, gpu_ctx, name):
+    """mc_trace.m:32-34 (Afun is a matrix), 3 rounds of nested deflation."""
+    A = load_graph(name)
+    tr, res, it = kra.mc_trace(kra.DeviceMatrix(A, gpu_ctx), A.shape[0], 1e-12, 90, 0, seed=4, ctx=gpu_ctx)
+    tro, reso, ito = ko.mc_trace(A, A.shape[0], 1e-12, 90, 0, seed=4)
+    assert it == ito == 3
+    assert tr == pytest.approx(tro, rel=1e-9, abs=1e-9)
+    assert res == pytest.approx(reso, rel=1e-6, abs=1e-9)
+
+
+def test_trace_exp_reference_composition(kra, gpu_ctx, values):
+    """trace_exp.m with Afun = expmv (the reference composition)."""
+    A = load_graph("oregon_A0")
+    tr = kra.trace_exp(kra.DeviceMatrix(A, gpu_ctx), method="expmv", seed=1, ctx=gpu_ctx)
+    tro = ko.trace_exp(A, seed=1)
+    assert tr == pytest.approx(tro, rel=1e-9)
+    assert tr == pytest.approx(values["oregon_A0"]["exact_tr_exp"], rel=1e-4)
+
+
+def test_trace_exp_lanczos_config1(kra, gpu_ctx, values):
+    """BASELINE.json configs[0]: dt_oregon A6 (n = 10,860), mc_trace + Lanczos
+    (m = 20); one round = 30 probes; vs the oracle and the exact trace."""
+    A = load_graph("oregon_A6")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    tr, res, it = kra.mc_trace("lanczos", A.shape[0], 1e-4, 30, 1, seed=0, m=20, A=D, ctx=gpu_ctx)
+    tro, reso, ito = ko.trace_exp_lanczos(A, m=20, tol=1e-4, maxit=30, seed=0)
+    assert it == ito == 1
+    assert tr == pytest.approx(tro, rel=1e-6)
+    assert tr == pytest.approx(values["oregon_A6"]["exact_tr_exp"], rel=1e-3)
+    full = kra.trace_exp(D, method="lanczos", m=20, seed=0, ctx=gpu_ctx)   # tol 1e-4, maxit 1000
+    assert full == pytest.approx(values["oregon_A6"]["exact_tr_exp"], rel=1e-4)
