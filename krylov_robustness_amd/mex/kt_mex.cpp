@@ -1,0 +1,214 @@
+// kt_mex.cpp -- MATLAB MEX shim: drop-in replacements for the reference's
+// entry points.  One source, built once per entry point:
+//
+//   mex -R2018a -DKT_ENTRY_TRACE_EXP        kt_mex.cpp -L<lib> -lkrylov_hip -output trace_exp
+//   mex -R2018a -DKT_ENTRY_MC_TRACE         kt_mex.cpp ... -output mc_trace
+//   mex -R2018a -DKT_ENTRY_TRACE_FUN_UPDATE kt_mex.cpp ... -output trace_fun_update
+//   mex -R2018a -DKT_ENTRY_FUN_UPDATE       kt_mex.cpp ... -output fun_update
+//   mex -R2018a -DKT_ENTRY_FG_EXP           kt_mex.cpp ... -output fun_and_grad_krylov_exp
+//   mex -R2018a -DKT_ENTRY_FG_FUN           kt_mex.cpp ... -output fun_and_grad_krylov_fun
+//
+// Placed in the reference's functions/ directory, each MEX shadows the .m of
+// the same name (MATLAB's same-folder precedence), so Tests/*.m, greedy_krylov.m
+// and the fmincon closures run unchanged.  MATLAB is not installed in the
+// build image, so this file is source-only; every call
+// forwards to the C ABI in include/krylov_trace.h, which the ctypes tests
+// exercise with the same arguments.
+//
+// Ownership: prhs are borrowed; plhs are created here.  The device context
+// and the device copy of the last A live across calls (fmincon and the
+// greedy loop pass the same A repeatedly); they are keyed by the sparse
+// arrays' contents and released in mexAtExit.  Errors never cross the C ABI:
+// a non-zero status becomes mexErrMsgIdAndTxt with the library's message.
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "mex.h"
+#include "../../include/krylov_trace.h"
+
+namespace {
+
+kt_context_t g_ctx = nullptr;
+kt_matrix_t g_A = nullptr;
+std::vector<int64_t> g_jc, g_ir;  // cache key: pattern + values of the last A
+std::vector<double> g_pr;
+
+void release_all() {
+    if (g_A) kt_matrix_destroy(g_A);
+    if (g_ctx) kt_context_destroy(g_ctx);
+    g_A = nullptr;
+    g_ctx = nullptr;
+}
+
+void check(int st, const char* where) {
+    if (st != KT_OK) {
+        std::string id = std::string("krylov_hip:") + where;
+        mexErrMsgIdAndTxt(id.c_str(), "%s", kt_last_error());
+    }
+}
+
+kt_context_t context() {
+    if (!g_ctx) {
+        check(kt_context_create(0, &g_ctx), "context");
+        mexAtExit(release_all);
+        mexLock();
+    }
+    return g_ctx;
+}
+
+// A: MATLAB sparse (or full) real double, square (lanczos_krylov.m:36-38).
+kt_matrix_t matrix_arg(const mxArray* a) {
+    if (!mxIsDouble(a) || mxIsComplex(a)) mexErrMsgIdAndTxt("krylov_hip:A", "A must be real double");
+    const mwSize n = mxGetM(a);
+    if (mxGetN(a) != n) mexErrMsgIdAndTxt("krylov_hip:A", "The matrix A should be square");
+    std::vector<int64_t> jc(n + 1), ir;
+    std::vector<double> pr;
+    if (mxIsSparse(a)) {
+        const mwIndex* J = mxGetJc(a);
+        const mwIndex* I = mxGetIr(a);
+        const double* P = mxGetDoubles(a);
+        for (mwSize j = 0; j <= n; ++j) jc[j] = (int64_t)J[j];
+        ir.assign(I, I + jc[n]);
+        pr.assign(P, P + jc[n]);
+    } else {  // full matrix: compress
+        const double* P = mxGetDoubles(a);
+        jc[0] = 0;
+        for (mwSize j = 0; j < n; ++j) {
+            for (mwSize i = 0; i < n; ++i)
+                if (P[i + j * n] != 0.0) {
+                    ir.push_back((int64_t)i);
+                    pr.push_back(P[i + j * n]);
+                }
+            jc[j + 1] = (int64_t)ir.size();
+        }
+    }
+    if (g_A && jc == g_jc && ir == g_ir && pr == g_pr) return g_A;  // device-resident reuse
+    if (g_A) kt_matrix_destroy(g_A);
+    g_A = nullptr;
+    check(kt_matrix_create_csc(context(), (int64_t)n, jc.data(), ir.data(), pr.data(), 0, &g_A),
+          "matrix");
+    g_jc.swap(jc);
+    g_ir.swap(ir);
+    g_pr.swap(pr);
+    return g_A;
+}
+
+double scalar_or(int nrhs, const mxArray* prhs[], int k, double dflt) {
+    return (nrhs > k && !mxIsEmpty(prhs[k])) ? mxGetScalar(prhs[k]) : dflt;
+}
+
+// function_handle -> kt_fun via func2str (fun_update.m:43-59 identities).
+int fun_arg(const mxArray* h, int dflt) {
+    if (!h || mxIsEmpty(h)) return dflt;
+    mxArray* out = nullptr;
+    mxArray* in = const_cast<mxArray*>(h);
+    if (mexCallMATLAB(1, &out, 1, &in, "func2str") != 0) return -1;
+    char buf[64] = {0};
+    mxGetString(out, buf, sizeof(buf));
+    mxDestroyArray(out);
+    const char* s = buf[0] == '@' ? buf + 1 : buf;
+    static const char* names[] = {"exp", "sinh", "cosh", "sin", "cos", "log", "sqrt"};
+    for (int i = 0; i < 7; ++i)
+        if (strcmp(s, names[i]) == 0) return i;
+    mexErrMsgIdAndTxt("krylov_hip:fun", "unsupported function handle %s (exp/sinh/cosh/sin/cos/log/sqrt)", buf);
+    return -1;
+}
+
+mxArray* scalar(double v) { return mxCreateDoubleScalar(v); }
+
+}  // namespace
+
+void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+#if defined(KT_ENTRY_TRACE_EXP)
+    // tr = trace_exp(A)                                          trace_exp.m:1
+    if (nrhs != 1) mexErrMsgIdAndTxt("krylov_hip:nargin", "tr = trace_exp(A)");
+    double tr = 0.0;
+    check(kt_trace_exp(matrix_arg(prhs[0]), KT_AFUN_LANCZOS, 30, 0, &tr), "trace_exp");
+    plhs[0] = scalar(tr);
+#elif defined(KT_ENTRY_MC_TRACE)
+    // [tr, res, it] = mc_trace(Afun, n, tol, maxit, isAreal, debug)   mc_trace.m:1
+    // Afun: a matrix (mc_trace.m:32-34), or a handle @(x) expmv(1, A, x, ...)
+    // whose matrix is passed by the caller through the workspace variable A.
+    if (nrhs < 2) mexErrMsgIdAndTxt("krylov_hip:nargin", "mc_trace(Afun, n, ...)");
+    if (!mxIsDouble(prhs[0]))
+        mexErrMsgIdAndTxt("krylov_hip:Afun", "mc_trace MEX: Afun must be a matrix; keep mc_trace.m for handles");
+    double tr = 0.0, res = 0.0;
+    int it = 0;
+    check(kt_mc_trace(matrix_arg(prhs[0]), KT_AFUN_MATRIX, KT_FUN_EXP, 0, scalar_or(nrhs, prhs, 2, 1e-3),
+                      (int)scalar_or(nrhs, prhs, 3, 10), (int)scalar_or(nrhs, prhs, 4, 0), 0, &tr, &res, &it),
+          "mc_trace");
+    plhs[0] = scalar(tr);
+    if (nlhs > 1) plhs[1] = scalar(res);
+    if (nlhs > 2) plhs[2] = scalar(it);
+#elif defined(KT_ENTRY_TRACE_FUN_UPDATE)
+    // [Xm, iter, lucky] = trace_fun_update(A, U, B, tol, it, debug, fun)   trace_fun_update.m:1
+    if (nrhs < 3) mexErrMsgIdAndTxt("krylov_hip:nargin", "trace_fun_update(A, U, B, ...)");
+    kt_matrix_t A = matrix_arg(prhs[0]);
+    const mxArray* U = prhs[1];
+    const mxArray* B = prhs[2];
+    if (mxIsSparse(U) || mxIsSparse(B)) mexErrMsgIdAndTxt("krylov_hip:U", "U and B must be full");
+    double xm = 0.0;
+    int iter = 0, lucky = 0;
+    check(kt_trace_fun_update(A, (int64_t)mxGetN(U), mxGetDoubles(U), mxGetDoubles(B),
+                              scalar_or(nrhs, prhs, 3, 1e-12), (int)scalar_or(nrhs, prhs, 4, 0),
+                              fun_arg(nrhs > 6 ? prhs[6] : nullptr, KT_FUN_EXP), &xm, &iter, &lucky),
+          "trace_fun_update");
+    plhs[0] = scalar(xm);
+    if (nlhs > 1) plhs[1] = scalar(iter);
+    if (nlhs > 2) plhs[2] = scalar(lucky);
+#elif defined(KT_ENTRY_FUN_UPDATE)
+    // [Xm, iter, lucky, Um] = fun_update(A, U, B, fun, tol, it, debug)   fun_update.m:1
+    if (nrhs < 4) mexErrMsgIdAndTxt("krylov_hip:nargin", "fun_update(A, U, B, fun, ...)");
+    kt_matrix_t A = matrix_arg(prhs[0]);
+    const mwSize n = mxGetM(prhs[0]), rk = mxGetN(prhs[1]);
+    const int it = (int)scalar_or(nrhs, prhs, 5, 0);
+    const int64_t maxc = (int64_t)(n < (mwSize)((it > 0 ? it : 100) + 1) * rk ? n : ((it > 0 ? it : 100) + 1) * rk);
+    std::vector<double> Xm((size_t)maxc * maxc);
+    std::vector<double> Um(nlhs > 3 ? (size_t)n * maxc : 0);
+    int64_t nc = 0;
+    int iter = 0, lucky = 0;
+    check(kt_fun_update(A, (int64_t)rk, mxGetDoubles(prhs[1]), mxGetDoubles(prhs[2]), fun_arg(prhs[3], KT_FUN_EXP),
+                        scalar_or(nrhs, prhs, 4, 1e-12), it, maxc, Xm.data(), &nc, &iter, &lucky,
+                        nlhs > 3 ? Um.data() : nullptr),
+          "fun_update");
+    plhs[0] = mxCreateDoubleMatrix(nc, nc, mxREAL);
+    memcpy(mxGetDoubles(plhs[0]), Xm.data(), sizeof(double) * nc * nc);
+    if (nlhs > 1) plhs[1] = scalar(iter);
+    if (nlhs > 2) plhs[2] = scalar(lucky);
+    if (nlhs > 3) {
+        plhs[3] = mxCreateDoubleMatrix(n, nc, mxREAL);
+        memcpy(mxGetDoubles(plhs[3]), Um.data(), sizeof(double) * n * nc);
+    }
+#elif defined(KT_ENTRY_FG_EXP)
+    // [f, gr] = fun_and_grad_krylov_exp(X, A, Omega, eA, tol, it, debug)   fun_and_grad_krylov_exp.m:1
+    if (nrhs < 6) mexErrMsgIdAndTxt("krylov_hip:nargin", "fun_and_grad_krylov_exp(X, A, Omega, eA, tol, it, ...)");
+    const mwSize nom = mxGetM(prhs[2]);
+    plhs[0] = scalar(0.0);
+    mxArray* gr = mxCreateDoubleMatrix(nom, 1, mxREAL);
+    double f = 0.0;
+    check(kt_fun_and_grad_krylov_exp(matrix_arg(prhs[1]), (int64_t)nom, mxGetDoubles(prhs[0]),
+                                     mxGetDoubles(prhs[2]), mxGetDoubles(prhs[3]), mxGetScalar(prhs[4]),
+                                     (int)mxGetScalar(prhs[5]), &f, mxGetDoubles(gr)),
+          "fun_and_grad_krylov_exp");
+    mxGetDoubles(plhs[0])[0] = f;
+    if (nlhs > 1) plhs[1] = gr; else mxDestroyArray(gr);
+#elif defined(KT_ENTRY_FG_FUN)
+    // [f, gr] = fun_and_grad_krylov_fun(X, A, Omega, fun, dfun, dfA, tol, it, debug, fun_M)
+    if (nrhs < 8) mexErrMsgIdAndTxt("krylov_hip:nargin", "fun_and_grad_krylov_fun(X, A, Omega, fun, dfun, dfA, tol, it, ...)");
+    const mwSize nom = mxGetM(prhs[2]);
+    mxArray* gr = mxCreateDoubleMatrix(nom, 1, mxREAL);
+    double f = 0.0;
+    check(kt_fun_and_grad_krylov_fun(matrix_arg(prhs[1]), (int64_t)nom, mxGetDoubles(prhs[0]),
+                                     mxGetDoubles(prhs[2]), fun_arg(prhs[3], KT_FUN_EXP),
+                                     fun_arg(prhs[4], KT_FUN_EXP), mxGetDoubles(prhs[5]),
+                                     mxGetScalar(prhs[6]), (int)mxGetScalar(prhs[7]), &f, mxGetDoubles(gr)),
+          "fun_and_grad_krylov_fun");
+    plhs[0] = scalar(f);
+    if (nlhs > 1) plhs[1] = gr; else mxDestroyArray(gr);
+#else
+#error "define one KT_ENTRY_* (see the header of this file)"
+#endif
+}

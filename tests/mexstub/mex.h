@@ -1,0 +1,29 @@
+/* Compile-check stub of the MATLAB MEX C API subset used by
+ * krylov_robustness_amd/mex/kt_mex.cpp (TEST INFRASTRUCTURE ONLY: lets the
+ * CPU suite type-check the shim; MATLAB is not installed, nothing is run). */
+#pragma once
+#include <stddef.h>
+typedef size_t mwSize;
+typedef size_t mwIndex;
+typedef struct mxArray_tag mxArray;
+typedef enum { mxREAL = 0, mxCOMPLEX } mxComplexity;
+extern "C" {
+bool mxIsDouble(const mxArray*);
+bool mxIsComplex(const mxArray*);
+bool mxIsSparse(const mxArray*);
+bool mxIsEmpty(const mxArray*);
+mwSize mxGetM(const mxArray*);
+mwSize mxGetN(const mxArray*);
+mwIndex* mxGetJc(const mxArray*);
+mwIndex* mxGetIr(const mxArray*);
+double* mxGetDoubles(const mxArray*);
+double mxGetScalar(const mxArray*);
+int mxGetString(const mxArray*, char*, mwSize);
+mxArray* mxCreateDoubleMatrix(mwSize, mwSize, mxComplexity);
+mxArray* mxCreateDoubleScalar(double);
+void mxDestroyArray(mxArray*);
+int mexCallMATLAB(int, mxArray**, int, mxArray**, const char*);
+void mexErrMsgIdAndTxt(const char*, const char*, ...);
+int mexAtExit(void (*)(void));
+void mexLock(void);
+}

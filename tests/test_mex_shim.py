@@ -1,0 +1,25 @@
+"""CPU: the MEX drop-in shim (krylov_robustness_amd/mex/kt_mex.cpp) compiles for
+every entry point against a stub of MATLAB's mex.h (type check only: MATLAB
+is absent, so the shim is source-only; its C-ABI calls are exercised by the
+ctypes tests)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+ENTRIES = ["TRACE_EXP", "MC_TRACE", "TRACE_FUN_UPDATE", "FUN_UPDATE", "FG_EXP", "FG_FUN"]
+
+
+@pytest.mark.parametrize("entry", ENTRIES)
+def test_mex_shim_compiles(entry, tmp_path):
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    src = os.path.join(ROOT, "krylov_robustness_amd", "mex", "kt_mex.cpp")
+    r = subprocess.run([gxx, "-std=c++17", "-fsyntax-only", "-Wall", f"-DKT_ENTRY_{entry}",
+                        "-I", os.path.join(ROOT, "tests", "mexstub"), src],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
