@@ -84,10 +84,11 @@ void spmm(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols
     if (P > 128) fail(KT_ERR_UNSUPPORTED, "block width > 128");
     const int n = (int)A->n;
     const int grid = spmm_grid(n, P, ctx->num_cu * 4);
-    const int lblocks = long_blocks_for(A->n_long, ctx->num_cu * 2);
-    KT_HIP(launch_spmm_block(P, A->unit_values ? 2 : 0, grid + lblocks, A->d_rowptr, A->d_col,
-                             A->d_val, n, X, ldx, Y, ldy, A->d_long_rows, A->n_long,
-                             A->long_thresh, lblocks, ctx->stream));
+    const DevCSR& M = natural_csr(A);  // block paths run in the reference's row order
+    const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
+    KT_HIP(launch_spmm_block(P, A->unit_values ? 2 : 0, grid + lblocks, M.rowptr, M.col, M.val, n,
+                             X, ldx, Y, ldy, M.long_rows, M.n_long, A->long_thresh, lblocks,
+                             ctx->stream));
 }
 
 void copy_cols(kt_context_s* ctx, int64_t n, const double* X, int ldx, double* Y, int ldy,
@@ -109,7 +110,7 @@ void upload_rows(kt_matrix_s* A, const double* H, int cols, double* D, int ldd) 
     if (n == 0 || cols == 0) return;
     std::vector<double> tmp((size_t)n * cols, 0.0);  // compact row-major, device numbering
     for (int c = 0; c < cols; ++c)
-        for (int64_t i = 0; i < n; ++i) tmp[(size_t)A->old2new[i] * cols + c] = H[(size_t)c * n + i];
+        for (int64_t i = 0; i < n; ++i) tmp[(size_t)i * cols + c] = H[(size_t)c * n + i];
     KT_HIP(hipMemcpy2DAsync(D, sizeof(double) * ldd, tmp.data(), sizeof(double) * cols,
                             sizeof(double) * cols, (size_t)n, hipMemcpyHostToDevice, A->ctx->stream));
     KT_HIP(hipStreamSynchronize(A->ctx->stream));
@@ -121,7 +122,7 @@ void download_rows(kt_matrix_s* A, const double* D, int ldd, int cols,
     out.assign((size_t)nr * cols, 0.0);
     std::vector<double> row(cols);
     for (int r = 0; r < nr; ++r) {
-        const int64_t dr = A->old2new[rows[r]];
+        const int64_t dr = rows[r];
         KT_HIP(hipMemcpyAsync(row.data(), D + (size_t)dr * ldd, sizeof(double) * cols,
                               hipMemcpyDeviceToHost, A->ctx->stream));
         KT_HIP(hipStreamSynchronize(A->ctx->stream));
@@ -137,7 +138,7 @@ void download_block(kt_matrix_s* A, const double* D, int ldd, int cols, double* 
                             sizeof(double) * cols, (size_t)n, hipMemcpyDeviceToHost, A->ctx->stream));
     KT_HIP(hipStreamSynchronize(A->ctx->stream));
     for (int c = 0; c < cols; ++c)
-        for (int64_t i = 0; i < n; ++i) out[i + (size_t)c * n] = tmp[(size_t)A->old2new[i] * cols + c];
+        for (int64_t i = 0; i < n; ++i) out[i + (size_t)c * n] = tmp[(size_t)i * cols + c];
 }
 
 void matmul(int m, int k, int n, const double* A, const double* B, double* C) {

@@ -38,13 +38,12 @@ void spmm(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols
 // copy a column slice (n x cols) between device arrays
 void copy_cols(kt_context_s* ctx, int64_t n, const double* X, int ldx, double* Y, int ldy, int cols);
 void zero_cols(kt_context_s* ctx, int64_t n, double* X, int ldx, int cols);
-// host column-major (original numbering) -> device row-major (device numbering)
+// host column-major -> device row-major
 void upload_rows(kt_matrix_s* A, const double* H, int cols, double* D, int ldd);
-// device rows (given ORIGINAL row indices) -> host nrows x cols column-major
+// device rows (row indices) -> host nrows x cols column-major
 void download_rows(kt_matrix_s* A, const double* D, int ldd, int cols,
                    const std::vector<int64_t>& rows, std::vector<double>& out);
-// whole device block (n x cols at ldd, device numbering) -> host column-major
-// n x cols in ORIGINAL numbering
+// whole device block (n x cols at ldd) -> host column-major n x cols
 void download_block(kt_matrix_s* A, const double* D, int ldd, int cols, double* out);
 // thin QR of W (n x bs at ld) in place: W <- Q, R upper bs x bs (column-major).
 // CholQR2 (shifted CholQR3 if W is ill-conditioned).  Returns false when W

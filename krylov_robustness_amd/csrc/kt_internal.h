@@ -109,31 +109,46 @@ struct kt_context_s {
     kt::Workspace ws;
 };
 
+namespace kt {
+// One device copy of A as CSR (int32 indices), rows in some order.
+struct DevCSR {
+    int* rowptr = nullptr;
+    int* col = nullptr;
+    double* val = nullptr;
+    int* long_rows = nullptr;  // rows with degree > long_thresh, heaviest first
+    int n_long = 0;
+    int* perm = nullptr;       // device row -> original row (nullptr: identity)
+    bool built = false;
+    void release();
+};
+}  // namespace kt
+
 struct kt_matrix_s {
     kt_context_s* ctx = nullptr;
     int64_t n = 0, nnz = 0;
-    int* d_rowptr = nullptr;
-    int* d_col = nullptr;
-    double* d_val = nullptr;
-    // rows with degree > long_thresh, hubs first (one wave per such row in K1)
-    int* d_long_rows = nullptr;
-    int n_long = 0;
     int long_thresh = 64;
-    // Device rows are relabelled by descending degree (hubs first): device
-    // row r holds original row new2old[r].  Probes stay keyed by ORIGINAL
-    // index (d_perm = new2old), so results do not depend on the relabelling.
-    bool relabeled = false;
     bool unit_values = false;  // every stored value == 1.0 (unweighted adjacency)
     int symmetric = -1;        // -1 unknown, 0 no, 1 yes (checked on the host copy)
-    int* d_perm = nullptr;
+    // hub: rows relabelled by descending degree (hubs first) for the probe
+    // hot path; probes stay keyed by ORIGINAL index via hub.perm, so results
+    // do not depend on the relabelling.
+    kt::DevCSR hub;
     std::vector<int32_t> new2old, old2new;
-    // host copy (CSR, int64 pointers) for host-side algorithms and checks
+    // nat: natural row order, built on first use by the block-Krylov and
+    // mc_trace paths so that Householder QR sees the reference's row order
+    // (rank-deficient completions qr(w,0) picks depend on it).
+    kt::DevCSR nat;
+    // host copy (CSR, int64 pointers, original order)
     std::vector<int64_t> h_rowptr;
     std::vector<int32_t> h_col;
     std::vector<double> h_val;
 };
 
 namespace kt {
+
+// build one device CSR of A with rows in the order new2old (identity if empty)
+void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out);
+const DevCSR& natural_csr(kt_matrix_s* A);
 
 // profiling helpers (no-ops unless ctx->profile)
 void prof_begin(kt_context_s* ctx, int slot);

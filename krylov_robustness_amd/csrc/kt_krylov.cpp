@@ -671,7 +671,7 @@ int kt_fun_update(kt_matrix_t A, int64_t rk, const double* U, const double* B, i
             KT_HIP(hipStreamSynchronize(A->ctx->stream));
             for (int c = 0; c < fu.nx; ++c) {
                 const int pc = (c / Ar.bs) * Ar.PB + c % Ar.bs;
-                for (int64_t i = 0; i < n; ++i) Um[i + (size_t)c * n] = host[(size_t)A->old2new[i] * ldv + pc];
+                for (int64_t i = 0; i < n; ++i) Um[i + (size_t)c * n] = host[(size_t)i * ldv + pc];
             }
         }
     }

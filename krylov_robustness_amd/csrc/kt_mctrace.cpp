@@ -222,8 +222,8 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
         const int64_t base = (int64_t)(it - 1) * 2 * mb;
         S.alloc(ctx, n, ld);
         G.alloc(ctx, n, ld);
-        KT_HIP(launch_rademacher(ld, (int)n, seed, base, A->d_perm, S.col(0), ctx->stream));       // :43
-        KT_HIP(launch_rademacher(ld, (int)n, seed, base + mb, A->d_perm, G.col(0), ctx->stream));  // :44
+        KT_HIP(launch_rademacher(ld, (int)n, seed, base, nullptr, S.col(0), ctx->stream));       // :43
+        KT_HIP(launch_rademacher(ld, (int)n, seed, base + mb, nullptr, G.col(0), ctx->stream));  // :44
         zero_cols(ctx, n, S.col(mb), ld, ld - mb);
         zero_cols(ctx, n, G.col(mb), ld, ld - mb);
         // Y = Afun_it(S) = P_{it-1}..P_1 F(P_1..P_{it-1} S)                       :45

@@ -50,6 +50,74 @@ void prof_collect(kt_context_s* ctx) {
     }
 }
 
+void DevCSR::release() {
+    if (rowptr) (void)hipFree(rowptr);
+    if (col) (void)hipFree(col);
+    if (val) (void)hipFree(val);
+    if (long_rows) (void)hipFree(long_rows);
+    if (perm) (void)hipFree(perm);
+    rowptr = col = long_rows = perm = nullptr;
+    val = nullptr;
+    n_long = 0;
+    built = false;
+}
+
+void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out) {
+    const int64_t n = A->n, nnz = A->nnz;
+    const bool ident = new2old.empty();
+    auto orig = [&](int64_t r) -> int64_t { return ident ? r : new2old[r]; };
+    std::vector<int32_t> rp32(n + 1), c32(std::max<int64_t>(nnz, 1));
+    std::vector<double> v64(std::max<int64_t>(nnz, 1));
+    rp32[0] = 0;
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t o = orig(r);
+        rp32[r + 1] = rp32[r] + (int32_t)(A->h_rowptr[o + 1] - A->h_rowptr[o]);
+    }
+    std::vector<std::pair<int32_t, double>> tmp;
+    for (int64_t r = 0; r < n; ++r) {
+        const int64_t o = orig(r);
+        tmp.clear();
+        for (int64_t k = A->h_rowptr[o]; k < A->h_rowptr[o + 1]; ++k)
+            tmp.push_back({ident ? A->h_col[k] : A->old2new[A->h_col[k]], A->h_val[k]});
+        std::sort(tmp.begin(), tmp.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        for (size_t t = 0; t < tmp.size(); ++t) {
+            c32[rp32[r] + t] = tmp[t].first;
+            v64[rp32[r] + t] = tmp[t].second;
+        }
+    }
+    std::vector<int32_t> lr;
+    for (int64_t r = 0; r < n; ++r)
+        if (rp32[r + 1] - rp32[r] > A->long_thresh) lr.push_back((int32_t)r);
+    std::stable_sort(lr.begin(), lr.end(), [&](int32_t a, int32_t b) {
+        return rp32[a + 1] - rp32[a] > rp32[b + 1] - rp32[b];
+    });
+    try {
+        KT_HIP(hipMalloc(&out.rowptr, sizeof(int) * (n + 1)));
+        KT_HIP(hipMalloc(&out.col, sizeof(int) * c32.size()));
+        KT_HIP(hipMalloc(&out.val, sizeof(double) * v64.size()));
+        KT_HIP(hipMalloc(&out.long_rows, sizeof(int) * std::max<size_t>(lr.size(), 1)));
+        KT_HIP(hipMemcpy(out.rowptr, rp32.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice));
+        KT_HIP(hipMemcpy(out.col, c32.data(), sizeof(int) * c32.size(), hipMemcpyHostToDevice));
+        KT_HIP(hipMemcpy(out.val, v64.data(), sizeof(double) * v64.size(), hipMemcpyHostToDevice));
+        if (!lr.empty())
+            KT_HIP(hipMemcpy(out.long_rows, lr.data(), sizeof(int) * lr.size(), hipMemcpyHostToDevice));
+        out.n_long = (int)lr.size();
+        if (!ident) {
+            KT_HIP(hipMalloc(&out.perm, sizeof(int) * std::max<int64_t>(n, 1)));
+            if (n) KT_HIP(hipMemcpy(out.perm, new2old.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+        }
+    } catch (...) {
+        out.release();
+        throw;
+    }
+    out.built = true;
+}
+
+const DevCSR& natural_csr(kt_matrix_s* A) {
+    if (!A->nat.built) build_csr(A, std::vector<int32_t>(), A->nat);
+    return A->nat;
+}
+
 }  // namespace kt
 
 using namespace kt;
@@ -188,67 +256,23 @@ int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr, con
     }
     try {
         KT_HIP(hipSetDevice(ctx->device));
+        A->unit_values = std::all_of(A->h_val.begin(), A->h_val.end(), [](double v) { return v == 1.0; });
+        const char* un = getenv("KT_UNIT");
+        if (un && un[0] == '0') A->unit_values = false;
         // degree-descending relabelling (stable, so ties keep original order)
         const char* rl = getenv("KT_RELABEL");
-        A->relabeled = !(rl && rl[0] == '0');
+        const bool relabel = !(rl && rl[0] == '0');
         A->new2old.resize(n);
         A->old2new.resize(n);
         for (int64_t i = 0; i < n; ++i) A->new2old[i] = (int32_t)i;
-        if (A->relabeled)
+        if (relabel)
             std::stable_sort(A->new2old.begin(), A->new2old.end(), [&](int32_t a, int32_t b) {
                 return A->h_rowptr[a + 1] - A->h_rowptr[a] > A->h_rowptr[b + 1] - A->h_rowptr[b];
             });
         for (int64_t r = 0; r < n; ++r) A->old2new[A->new2old[r]] = (int32_t)r;
-        std::vector<int32_t> rp32(n + 1), c32(nnz);
-        std::vector<double> v64(nnz);
-        rp32[0] = 0;
-        for (int64_t r = 0; r < n; ++r) {
-            const int64_t o = A->new2old[r];
-            rp32[r + 1] = rp32[r] + (int32_t)(A->h_rowptr[o + 1] - A->h_rowptr[o]);
-        }
-        std::vector<std::pair<int32_t, double>> tmp;
-        for (int64_t r = 0; r < n; ++r) {
-            const int64_t o = A->new2old[r];
-            tmp.clear();
-            for (int64_t k = A->h_rowptr[o]; k < A->h_rowptr[o + 1]; ++k)
-                tmp.push_back({A->old2new[A->h_col[k]], A->h_val[k]});
-            std::sort(tmp.begin(), tmp.end(),
-                      [](const auto& x, const auto& y) { return x.first < y.first; });
-            for (size_t t = 0; t < tmp.size(); ++t) {
-                c32[rp32[r] + t] = tmp[t].first;
-                v64[rp32[r] + t] = tmp[t].second;
-            }
-        }
-        KT_HIP(hipMalloc(&A->d_rowptr, sizeof(int) * (n + 1)));
-        KT_HIP(hipMalloc(&A->d_col, sizeof(int) * std::max<int64_t>(nnz, 1)));
-        KT_HIP(hipMalloc(&A->d_val, sizeof(double) * std::max<int64_t>(nnz, 1)));
-        KT_HIP(hipMalloc(&A->d_perm, sizeof(int) * std::max<int64_t>(n, 1)));
-        KT_HIP(hipMemcpy(A->d_rowptr, rp32.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice));
-        if (n) KT_HIP(hipMemcpy(A->d_perm, A->new2old.data(), sizeof(int) * n, hipMemcpyHostToDevice));
-        if (nnz) {
-            KT_HIP(hipMemcpy(A->d_col, c32.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
-            KT_HIP(hipMemcpy(A->d_val, v64.data(), sizeof(double) * nnz, hipMemcpyHostToDevice));
-        }
-        const char* un = getenv("KT_UNIT");
-        A->unit_values = !(un && un[0] == '0') &&
-                         std::all_of(v64.begin(), v64.end(), [](double v) { return v == 1.0; });
-        // long-row list (device numbering) for K1's wave-per-row mode, heaviest first
-        std::vector<int32_t> lr;
-        for (int64_t r = 0; r < n; ++r)
-            if (rp32[r + 1] - rp32[r] > A->long_thresh) lr.push_back((int32_t)r);
-        std::stable_sort(lr.begin(), lr.end(), [&](int32_t a, int32_t b) {
-            return rp32[a + 1] - rp32[a] > rp32[b + 1] - rp32[b];
-        });
-        A->n_long = (int)lr.size();
-        KT_HIP(hipMalloc(&A->d_long_rows, sizeof(int) * std::max<size_t>(lr.size(), 1)));
-        if (!lr.empty())
-            KT_HIP(hipMemcpy(A->d_long_rows, lr.data(), sizeof(int) * lr.size(), hipMemcpyHostToDevice));
+        build_csr(A, A->new2old, A->hub);
     } catch (...) {
-        if (A->d_rowptr) (void)hipFree(A->d_rowptr);
-        if (A->d_col) (void)hipFree(A->d_col);
-        if (A->d_val) (void)hipFree(A->d_val);
-        if (A->d_long_rows) (void)hipFree(A->d_long_rows);
-        if (A->d_perm) (void)hipFree(A->d_perm);
+        A->hub.release();
         delete A;
         throw;
     }
@@ -261,11 +285,8 @@ int kt_matrix_destroy(kt_matrix_t A) {
     if (!A) return KT_OK;
     (void)hipSetDevice(A->ctx->device);
     (void)hipStreamSynchronize(A->ctx->stream);
-    if (A->d_rowptr) (void)hipFree(A->d_rowptr);
-    if (A->d_col) (void)hipFree(A->d_col);
-    if (A->d_val) (void)hipFree(A->d_val);
-    if (A->d_long_rows) (void)hipFree(A->d_long_rows);
-    if (A->d_perm) (void)hipFree(A->d_perm);
+    A->hub.release();
+    A->nat.release();
     delete A;
     KT_GUARD_END
 }

@@ -34,14 +34,14 @@ int slq_auto_block(int64_t n, int64_t nprobes) {
 // Run one sweep.  rec_host receives [alpha | up | low][m][P].
 // init: if seeded by RNG, `x` == nullptr; else x (device, n x ldx, ncols
 // columns, original-column norms^2 in norms2) is copied into the sweep block.
-void lanczos_sweep(kt_matrix_s* A, int P, int m, uint64_t seed, int64_t probe_base,
+void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base,
                    const double* x, int ldx, int ncols, const double* norms2, double* rec_host,
                    DevMat* basis, std::vector<double>* scale_hist) {
     kt_context_s* ctx = A->ctx;
     const int n = (int)A->n;
     hipStream_t st = ctx->stream;
     const int grid = spmm_grid(n, P, ctx->num_cu * 4);  // K2 / short rows
-    const int lblocks = long_blocks_for(A->n_long, ctx->num_cu * 2);
+    const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
     const int grid1 = grid + lblocks;                    // K1 total
     Workspace& w = ctx->ws;
     const size_t blk_bytes = sizeof(double) * (size_t)n * P;
@@ -66,7 +66,7 @@ void lanczos_sweep(kt_matrix_s* A, int P, int m, uint64_t seed, int64_t probe_ba
     double* sp = sc + P;
     double* sn = sc + 2 * P;
     if (!x) {
-        KT_HIP(launch_rademacher(P, n, seed, probe_base, A->d_perm, ucur, st));
+        KT_HIP(launch_rademacher(P, n, seed, probe_base, M.perm, ucur, st));
         KT_HIP(launch_fill(sc, P, 1.0 / std::sqrt((double)n), st));
         KT_HIP(launch_fill(k2s, P, (double)n, st));  // ||z||^2 = n
     } else {
@@ -99,9 +99,9 @@ void lanczos_sweep(kt_matrix_s* A, int P, int m, uint64_t seed, int64_t probe_ba
                                   hipMemcpyDeviceToDevice, st));
         }
         prof_begin(ctx, PROF_SPMM);
-        KT_HIP(launch_spmm_dot(P, ctx->k1_flags | (A->unit_values ? 2 : 0), grid1, A->d_rowptr,
-                               A->d_col, A->d_val, n, ucur, sc, w.Y.as<double>(), part1,
-                               A->d_long_rows, A->n_long, A->long_thresh, lblocks, st));
+        KT_HIP(launch_spmm_dot(P, ctx->k1_flags | (A->unit_values ? 2 : 0), grid1, M.rowptr, M.col,
+                               M.val, n, ucur, sc, w.Y.as<double>(), part1, M.long_rows, M.n_long,
+                               A->long_thresh, lblocks, st));
         prof_end(ctx, PROF_SPMM);
         KT_HIP(launch_coef_cgs2(P, part1, grid1, first, k2s, sc, sp, coef,
                                 trec + (size_t)(0 * m + j) * P, trec + (size_t)(1 * m + j) * P, st));
@@ -166,7 +166,7 @@ void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m,
         DevMat basis;
         std::vector<double> hist;
         if (Y) basis.alloc(ctx, n, m * P);
-        lanczos_sweep(A, P, m, 0, 0, X + c0, ldx, nc, norms2.data() + c0, rec.data(),
+        lanczos_sweep(A, natural_csr(A), P, m, 0, 0, X + c0, ldx, nc, norms2.data() + c0, rec.data(),
                       Y ? &basis : nullptr, Y ? &hist : nullptr);
         KT_HIP(hipStreamSynchronize(ctx->stream));
         std::vector<double> W((size_t)m * P, 0.0);  // weights for Y = sum_j u_j w_j
@@ -242,7 +242,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         w.host_trec.ensure(sizeof(double) * rec * nsweeps);
         double* htrec = w.host_trec.as<double>();
         for (int64_t s = 0; s < nsweeps; ++s)
-            lanczos_sweep(A, P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr, htrec + rec * s,
+            lanczos_sweep(A, A->hub, P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr, htrec + rec * s,
                           nullptr, nullptr);
         KT_HIP(hipStreamSynchronize(ctx->stream));
         prof_collect(ctx);

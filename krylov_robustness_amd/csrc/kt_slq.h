@@ -8,13 +8,13 @@ namespace kt {
 int slq_auto_block(int64_t n, int64_t nprobes);
 
 // One sweep of P independent single-vector Lanczos runs (see kt_slq.cpp).
-void lanczos_sweep(kt_matrix_s* A, int P, int m, uint64_t seed, int64_t probe_base,
+void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base,
                    const double* x, int ldx, int ncols, const double* norms2, double* rec_host,
                    DevMat* basis, std::vector<double>* scale_hist);
 
 int record_tridiag(const double* R, int m, int P, int c, double* al, double* off);
 
-// For the ncols columns of the device block X (n x ldx, device numbering):
+// For the ncols columns of the device block X (n x ldx, natural row order):
 // quad[c] = x_c' f(A) x_c by m-step Lanczos quadrature (may be NULL) and, if
 // Y != NULL, Y[:, c] = ||x_c|| V_c f(T_c) e1 ~= f(A) x_c.
 void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m, int fun,

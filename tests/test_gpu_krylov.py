@@ -151,3 +151,22 @@ def test_fun_and_grad_fun_matches_oracle(kra, gpu_ctx, fun, dfun):
     fo, gro = ko.fun_and_grad_krylov_fun(X, A, Om, fun, dfun, dfA, tol, 100)
     assert f == pytest.approx(fo, rel=1e-7)
     np.testing.assert_allclose(gr, gro, rtol=1e-7, atol=1e-10)
+
+
+def test_trace_fun_update_leaf_candidates(kra, gpu_ctx):
+    """Break candidates at leaf nodes of the India grid (krylov_miobi.m:77-99):
+    A*U has an exactly dependent column after CGS2, so qr(w, 0) completes the
+    basis (Householder, LAPACK semantics, in the reference's row order)."""
+    A = load_graph("india")
+    n = A.shape[0]
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    deg = np.diff(A.indptr)
+    for leaf in np.flatnonzero(deg == 1)[:6]:
+        i = A.indices[A.indptr[leaf]]
+        U = np.zeros((n, 2)); U[min(i, leaf), 0] = 1; U[max(i, leaf), 1] = 1
+        B = -np.array([[0.0, 1.0], [1.0, 0.0]])
+        xm, it, _ = kra.trace_fun_update(D, U, B, 1e-12, 100, ctx=gpu_ctx)
+        ref, it_ref, _ = ko.trace_fun_update(A, U, B, 1e-12, 100, 0, "exp")
+        assert xm == pytest.approx(ref, rel=1e-9, abs=1e-11)
+        assert xm == pytest.approx(ko.exact_trace_update(A, U, B), rel=1e-8, abs=1e-10)
+        assert abs(it - it_ref) <= 1
