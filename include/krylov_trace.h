@@ -152,6 +152,39 @@ int kt_expmv(kt_matrix_t A, double t, int64_t ncols, const double* B, double* F,
  * Afun handle).  X, Y: n x ncols column-major, ncols <= 128. */
 int kt_lanczos_fmv(kt_matrix_t A, int fun, int m, int64_t ncols, const double* X, double* Y);
 
+/* ---- greedy edge selection (krylov_miobi.m / greedy_krylov.m) ---------- */
+
+/* Batched trace_fun_update over candidate edges, the inner loop of
+ * krylov_miobi.m:76-99.  Candidate c (0-based node indices ei[c], ej[c]):
+ *   ei != ej : U = [e_ei, e_ej], B (2 x 2 column-major, Hermitian)
+ *   ei == ej : U = e_ei,         B = b_self
+ * Xm[c] = tr f(A + U B U') - tr f(A) estimated exactly as trace_fun_update.m
+ * does (tol, it, lag-2 stop, lucky breakdown, dense shortcut n <= 130);
+ * iter, lucky (nullable) as trace_fun_update's outputs.  Replaces ncand
+ * calls of trace_fun_update.m:1 from krylov_miobi.m:99. */
+int kt_trace_fun_update_pairs(kt_matrix_t A, int64_t ncand, const int64_t* ei, const int64_t* ej,
+                              const double* B, double b_self, double tol, int it, int fun,
+                              double* Xm, int* iter, int* lucky);
+
+/* krylov_miobi.m:1 with E given as 0-based pairs (E(j,1) >= E(j,2) in the
+ * reference's 1-based form).  make = 0 ('break') or 1 ('make'); rescale as
+ * krylov_miobi.m:78-84 (B = -+[0 1;1 0]/rescale).  A is edited IN PLACE
+ * (A(i,j) = A(j,i) = 0 or 1, krylov_miobi.m:129-135), the returned A_new.
+ * sel_i/sel_j (capacity min(k, nE), nullable) receive the chosen edges in
+ * order, rob the summed variation, nsel their count.  Errors: the
+ * reference's KRYLOV_MIOBI:: messages. */
+int kt_krylov_miobi(kt_matrix_t A, int k, int64_t nE, const int64_t* ei, const int64_t* ej,
+                    double tol, int it, int make, double rescale, int64_t* sel_i, int64_t* sel_j,
+                    double* rob, int64_t* nsel);
+
+/* A(i,j) = A(j,i) = value for each pair (value 0 removes the entry, as MATLAB
+ * sparse assignment does); device copies are refreshed. */
+int kt_matrix_set_pairs(kt_matrix_t A, int64_t count, const int64_t* ei, const int64_t* ej,
+                        double value);
+/* Copy A back out as CSC (colptr n+1, rowind/vals nnz; sizes from
+ * kt_matrix_info).  rowind / vals may be NULL. */
+int kt_matrix_export_csc(kt_matrix_t A, int64_t* colptr, int64_t* rowind, double* vals);
+
 /* Per-kernel timing (HIP events recorded on the library's stream around each
  * launch of the named kernel while enabled).  kernel: 0 = spmm_gram (K1),
  * 1 = update_norm (K2).  Returns launch count and summed milliseconds. */

@@ -108,6 +108,35 @@ class DeviceMatrix:
     def handle(self):
         return self._h
 
+    def info(self):
+        """(n, nnz) of the current device matrix (nnz changes with edge edits)."""
+        n = C.c_int64()
+        nnz = C.c_int64()
+        _lib.check(_lib.load().kt_matrix_info(self._h, C.byref(n), C.byref(nnz)))
+        return int(n.value), int(nnz.value)
+
+    def to_scipy(self):
+        """The matrix as scipy CSC (reflects set_pairs / krylov_miobi edits)."""
+        import scipy.sparse as sp
+        n, nnz = self.info()
+        colptr = np.zeros(n + 1, dtype=np.int64)
+        rowind = np.zeros(max(nnz, 1), dtype=np.int64)
+        vals = np.zeros(max(nnz, 1))
+        _lib.check(_lib.load().kt_matrix_export_csc(
+            self._h, colptr.ctypes.data_as(C.POINTER(C.c_int64)),
+            rowind.ctypes.data_as(C.POINTER(C.c_int64)), vals.ctypes.data_as(C.POINTER(C.c_double))))
+        return sp.csc_matrix((vals[:nnz], rowind[:nnz], colptr), shape=(n, n))
+
+    def set_pairs(self, E, value):
+        """A(i,j) = A(j,i) = value for the 1-based pairs E (value 0 deletes)."""
+        E = np.asarray(E, dtype=np.int64).reshape(-1, 2)
+        ei = np.ascontiguousarray(E[:, 0] - 1)
+        ej = np.ascontiguousarray(E[:, 1] - 1)
+        _lib.check(_lib.load().kt_matrix_set_pairs(
+            self._h, E.shape[0], ei.ctypes.data_as(C.POINTER(C.c_int64)),
+            ej.ctypes.data_as(C.POINTER(C.c_int64)), float(value)))
+        self.n, self.nnz = self.info()
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             _lib.load().kt_matrix_destroy(self._h)

@@ -1,0 +1,365 @@
+// kt_greedy.cpp -- the candidate loop of krylov_miobi.m, batched on the device.
+//
+// krylov_miobi.m:76-125 scores every candidate edge h with
+//   trace_fun_update(A, U_h, B, tol, it)      U_h = [e_i, e_j],  B = -+[0 1;1 0]/rescale
+// one call after another.  Here all candidates of a greedy step advance
+// together: ONE SpMM over the 2C columns of the pair block per Lanczos step,
+// one fused CGS2 + Householder-QR launch (kt_pairs.hip), one small copy of the
+// per-candidate coefficients to the host, and per-candidate host work on the
+// 2j x 2j projected matrices with per-candidate stopping masks.  Candidate
+// h's numbers follow trace_fun_update.m exactly as the single-call path
+// (kt_krylov.cpp) does; only the order of independent work changes.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+#include "kt_krylov.h"
+#include "kt_launch.h"
+
+namespace kt {
+
+namespace {
+
+constexpr int kMaxPairs = 256;  // candidates per device batch (512 columns)
+
+// Per-candidate Lanczos state: the 2x2 blocks lanczos_krylov.m:88,90 writes
+// into H at step b (column-major): D = h(cur), P = h(prev), R = qr's R.
+struct PairRun {
+    std::vector<double> D, P, R;
+    double Cm[4] = {0, 0, 0, 0};
+    double Xstop[2] = {0, 0};
+    double Xm = 0.0;
+    int iter = 0;
+    bool lucky = false;
+    bool done = false;
+};
+
+// trace_fun_update.m:71-89 for one candidate after j Lanczos steps
+double pair_xm(const PairRun& s, int j, int fun, std::vector<double>& G, std::vector<double>& T,
+               std::vector<double>& w1, std::vector<double>& w2) {
+    const int nn = 2 * j;
+    G.assign((size_t)nn * nn, 0.0);
+    auto put = [&](const std::vector<double>& blk, int b, int row0, int col0) {
+        for (int jj = 0; jj < 2; ++jj)
+            for (int ii = 0; ii < 2; ++ii)
+                G[(row0 + ii) + (size_t)(col0 + jj) * nn] = blk[4 * b + ii + 2 * jj];
+    };
+    for (int b = 0; b < j; ++b) {
+        put(s.D, b, 2 * b, 2 * b);
+        if (b >= 1) put(s.P, b, 2 * (b - 1), 2 * b);
+        if (b + 1 < j) put(s.R, b, 2 * (b + 1), 2 * b);
+    }
+    T = G;
+    for (int jj = 0; jj < 2; ++jj)
+        for (int ii = 0; ii < 2; ++ii) T[ii + (size_t)jj * nn] += s.Cm[ii + 2 * jj];
+    for (int b = 0; b < nn; ++b)  // herm: (X + X')/2   :78-81
+        for (int a = 0; a < b; ++a) {
+            double x = 0.5 * (G[a + (size_t)b * nn] + G[b + (size_t)a * nn]);
+            G[a + (size_t)b * nn] = G[b + (size_t)a * nn] = x;
+            x = 0.5 * (T[a + (size_t)b * nn] + T[b + (size_t)a * nn]);
+            T[a + (size_t)b * nn] = T[b + (size_t)a * nn] = x;
+        }
+    w1.resize(nn);
+    w2.resize(nn);
+    sym_eig_host(nn, T.data(), w1.data(), nullptr);
+    sym_eig_host(nn, G.data(), w2.data(), nullptr);
+    std::sort(w1.begin(), w1.end());
+    std::sort(w2.begin(), w2.end());
+    return trace_diff(w1, w2, fun);
+}
+
+// Run f(i) for i in [0, count) on up to 16 host threads (small eig problems).
+template <class F>
+void parallel_for(int count, int64_t work_per_item, F f) {
+    int nt = (int)std::min<int64_t>(16, std::max<int64_t>(1, (int64_t)count * work_per_item / 200000));
+    nt = std::min<int>(nt, (int)std::max(1u, std::thread::hardware_concurrency()));
+    nt = std::min(nt, count);
+    if (nt <= 1) {
+        for (int i = 0; i < count; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t]() {
+            for (int i = t; i < count; i += nt) f(i);
+        });
+    for (auto& x : th) x.join();
+}
+
+// One device batch of C <= kMaxPairs two-column candidates.
+void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej, const double* B,
+                    double tol, int it, int fun, double* Xm, int* iter, int* lucky) {
+    kt_context_s* ctx = A->ctx;
+    const int64_t n = A->n;
+    const int cols = 2 * C;
+    const int CP = cols <= 64 ? pow2_at_least(cols) : (cols + 127) / 128 * 128;
+    DevMat S[3];
+    for (auto& s : S) s.alloc(ctx, n, CP);
+    DevBuf didx, dhr;
+    didx.ensure(sizeof(int) * 2 * (size_t)C);
+    dhr.ensure(sizeof(double) * 11 * (size_t)C);
+    PinnedBuf hhr;
+    hhr.ensure(sizeof(double) * 11 * (size_t)C);
+    std::vector<int> idx(2 * (size_t)C);
+    for (int c = 0; c < C; ++c) {
+        idx[c] = (int)ei[c];
+        idx[C + c] = (int)ej[c];
+    }
+    KT_HIP(hipMemcpyAsync(didx.ptr, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice,
+                          ctx->stream));
+    double* hr = hhr.as<double>();
+    auto fetch = [&]() {
+        KT_HIP(hipMemcpyAsync(hr, dhr.ptr, sizeof(double) * 11 * (size_t)C, hipMemcpyDeviceToHost,
+                              ctx->stream));
+        KT_HIP(hipStreamSynchronize(ctx->stream));
+    };
+    // [V, ~] = qr(U, 0)  (lanczos_krylov.m:48); V1' U = R exactly for unit
+    // selectors, so Cm = R B R'  (trace_fun_update.m:65-66)
+    KT_HIP(launch_pair_select(C, didx.as<int>(), didx.as<int>() + C, S[0].col(0), CP, ctx->stream));
+    KT_HIP(launch_pair_orth(C, (int)n, nullptr, nullptr, S[0].col(0), CP, dhr.as<double>(), ctx->stream));
+    fetch();
+    std::vector<PairRun> run(C);
+    for (int c = 0; c < C; ++c) {
+        const double R[4] = {hr[11 * c + 8], 0.0, hr[11 * c + 9], hr[11 * c + 10]};
+        double RB[4], Rt[4] = {R[0], R[2], R[1], R[3]};
+        matmul(2, 2, 2, R, B, RB);
+        matmul(2, 2, 2, RB, Rt, run[c].Cm);
+    }
+    int cur = 0, prev = -1, w = 1;
+    int active = C;
+    const int d = 2;  // lag (trace_fun_update.m:58)
+    for (int j = 1; j <= it && active > 0; ++j) {
+        // w = A * w over every candidate (lanczos_krylov.m:81)
+        for (int c0 = 0; c0 < CP; c0 += 128)
+            spmm(A, S[cur].col(c0), CP, S[w].col(c0), CP, std::min(128, cols - c0));
+        KT_HIP(launch_pair_orth(C, (int)n, prev >= 0 ? S[prev].col(0) : nullptr, S[cur].col(0),
+                                S[w].col(0), CP, dhr.as<double>(), ctx->stream));
+        fetch();
+        const int freed = prev >= 0 ? prev : 3 - cur - w;
+        prev = cur;
+        cur = w;
+        w = freed;
+        std::vector<int> todo;
+        for (int c = 0; c < C; ++c) {
+            if (run[c].done) continue;
+            PairRun& s = run[c];
+            const double* h = hr + 11 * c;
+            // h rows (prev0, prev1, cur0, cur1) x cols (w0, w1)
+            s.P.insert(s.P.end(), {h[0], h[1], h[4], h[5]});
+            s.D.insert(s.D.end(), {h[2], h[3], h[6], h[7]});
+            s.R.insert(s.R.end(), {h[8], 0.0, h[9], h[10]});
+            s.lucky = std::sqrt(h[8] * h[8] + h[9] * h[9] + h[10] * h[10]) < 1e-8;  // :91-93
+            todo.push_back(c);
+        }
+        parallel_for((int)todo.size(), 16 * (int64_t)j * j * j, [&](int t) {
+            std::vector<double> G, T, w1, w2;
+            PairRun& s = run[todo[t]];
+            s.Xm = pair_xm(s, j, fun, G, T, w1, w2);
+        });
+        for (int c : todo) {
+            PairRun& s = run[c];
+            bool stop = false;
+            if (j <= d) {  // :104-118
+                s.Xstop[j - 1] = s.Xm;
+            } else if (std::fabs(s.Xm - s.Xstop[0]) < tol) {
+                stop = true;
+            } else {
+                s.Xstop[0] = s.Xstop[1];
+                s.Xstop[1] = s.Xm;
+            }
+            if (!stop && s.lucky) stop = true;  // :119-124
+            if (stop || j == it) {
+                s.done = true;
+                s.iter = j;
+                --active;
+            }
+        }
+    }
+    for (int c = 0; c < C; ++c) {
+        Xm[c] = run[c].Xm;
+        if (iter) iter[c] = run[c].iter;
+        if (lucky) lucky[c] = run[c].lucky ? 1 : 0;
+    }
+}
+
+// host CSR edit of one entry (row r, column col); value 0 deletes
+void set_entry(kt_matrix_s* A, int64_t r, int32_t col, double value) {
+    auto b = A->h_col.begin() + A->h_rowptr[r], e = A->h_col.begin() + A->h_rowptr[r + 1];
+    auto f = std::lower_bound(b, e, col);
+    const int64_t k = f - A->h_col.begin();
+    const bool found = f != e && *f == col;
+    if (found && value != 0.0) {
+        A->h_val[k] = value;
+        return;
+    }
+    if (!found && value == 0.0) return;
+    const int64_t delta = found ? -1 : 1;
+    if (found) {
+        A->h_col.erase(A->h_col.begin() + k);
+        A->h_val.erase(A->h_val.begin() + k);
+    } else {
+        A->h_col.insert(A->h_col.begin() + k, col);
+        A->h_val.insert(A->h_val.begin() + k, value);
+    }
+    for (int64_t i = r + 1; i <= A->n; ++i) A->h_rowptr[i] += delta;
+    A->nnz += delta;
+}
+
+}  // namespace
+
+void trace_fun_update_pairs(kt_matrix_s* A, int64_t nC, const int64_t* ei, const int64_t* ej,
+                            const double* B, double B1, double tol, int it, int fun, double* Xm,
+                            int* iter, int* lucky) {
+    const int64_t n = A->n;
+    if (it <= 0) it = (int)std::min<int64_t>(100, n);  // trace_fun_update.m:25-27
+    for (int64_t c = 0; c < nC; ++c)
+        if (ei[c] < 0 || ei[c] >= n || ej[c] < 0 || ej[c] >= n)
+            fail(KT_ERR_ARG, "candidate edge index out of range");
+    std::vector<int64_t> pairs, singles;
+    for (int64_t c = 0; c < nC; ++c) (ei[c] != ej[c] && n > 130 ? pairs : singles).push_back(c);
+    // self-loop candidates (krylov_miobi.m:88-98) and the dense shortcut of
+    // trace_fun_update.m:37-51 (n <= 130) go through the single-call path
+    std::vector<double> U;
+    for (int64_t c : singles) {
+        const bool two = ei[c] != ej[c];
+        U.assign((size_t)n * (two ? 2 : 1), 0.0);
+        U[ei[c]] = 1.0;
+        if (two) U[n + ej[c]] = 1.0;
+        int itc = 0, lc = 0;
+        Xm[c] = trace_fun_update_impl(A, two ? 2 : 1, U.data(), two ? B : &B1, tol, it, fun, &itc, &lc);
+        if (iter) iter[c] = itc;
+        if (lucky) lucky[c] = lc;
+    }
+    if (pairs.empty()) return;
+    if (B[1] != B[2]) fail(KT_ERR_UNSUPPORTED, "trace_fun_update: non-Hermitian B (needs a general eig)");
+    (void)natural_csr(A);
+    for (size_t b0 = 0; b0 < pairs.size(); b0 += kMaxPairs) {
+        const int C = (int)std::min<size_t>(kMaxPairs, pairs.size() - b0);
+        std::vector<int64_t> bi(C), bj(C);
+        std::vector<double> xm(C);
+        std::vector<int> itv(C), lv(C);
+        for (int c = 0; c < C; ++c) {
+            bi[c] = ei[pairs[b0 + c]];
+            bj[c] = ej[pairs[b0 + c]];
+        }
+        run_pair_batch(A, C, bi.data(), bj.data(), B, tol, it, fun, xm.data(), itv.data(), lv.data());
+        for (int c = 0; c < C; ++c) {
+            const int64_t o = pairs[b0 + c];
+            Xm[o] = xm[c];
+            if (iter) iter[o] = itv[c];
+            if (lucky) lucky[o] = lv[c];
+        }
+    }
+}
+
+void set_pairs(kt_matrix_s* A, int64_t count, const int64_t* ei, const int64_t* ej, double value) {
+    for (int64_t t = 0; t < count; ++t)
+        if (ei[t] < 0 || ei[t] >= A->n || ej[t] < 0 || ej[t] >= A->n)
+            fail(KT_ERR_ARG, "edge index out of range");
+    KT_HIP(hipStreamSynchronize(A->ctx->stream));
+    for (int64_t t = 0; t < count; ++t) {
+        set_entry(A, ei[t], (int32_t)ej[t], value);
+        if (ei[t] != ej[t]) set_entry(A, ej[t], (int32_t)ei[t], value);
+    }
+    refresh_device(A);
+}
+
+}  // namespace kt
+
+using namespace kt;
+
+#define KT_GUARD_BEGIN try {
+#define KT_GUARD_END                                   \
+    }                                                  \
+    catch (const kt::Status& s) {                      \
+        kt::set_error(s.msg);                          \
+        return s.code;                                 \
+    }                                                  \
+    catch (const std::bad_alloc&) {                    \
+        kt::set_error("host allocation failed");       \
+        return KT_ERR_ALLOC;                           \
+    }                                                  \
+    catch (const std::exception& e) {                  \
+        kt::set_error(e.what());                       \
+        return KT_ERR_ARG;                             \
+    }                                                  \
+    return KT_OK;
+
+extern "C" {
+
+int kt_trace_fun_update_pairs(kt_matrix_t A, int64_t ncand, const int64_t* ei, const int64_t* ej,
+                              const double* B, double b_self, double tol, int it, int fun,
+                              double* Xm, int* iter, int* lucky) {
+    KT_GUARD_BEGIN
+    if (!A || !B || !Xm || (ncand > 0 && (!ei || !ej))) fail(KT_ERR_ARG, "NULL argument");
+    if (ncand < 0) fail(KT_ERR_ARG, "negative candidate count");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    trace_fun_update_pairs(A, ncand, ei, ej, B, b_self, tol, it, fun, Xm, iter, lucky);
+    KT_GUARD_END
+}
+
+int kt_matrix_set_pairs(kt_matrix_t A, int64_t count, const int64_t* ei, const int64_t* ej,
+                        double value) {
+    KT_GUARD_BEGIN
+    if (!A || (count > 0 && (!ei || !ej))) fail(KT_ERR_ARG, "NULL argument");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    set_pairs(A, count, ei, ej, value);
+    KT_GUARD_END
+}
+
+int kt_matrix_export_csc(kt_matrix_t A, int64_t* colptr, int64_t* rowind, double* vals) {
+    KT_GUARD_BEGIN
+    if (!A || !colptr) fail(KT_ERR_ARG, "NULL argument");
+    std::copy(A->h_rowptr.begin(), A->h_rowptr.end(), colptr);  // CSR == CSC (symmetric A)
+    if (rowind) for (int64_t k = 0; k < A->nnz; ++k) rowind[k] = A->h_col[k];
+    if (vals) std::copy(A->h_val.begin(), A->h_val.end(), vals);
+    KT_GUARD_END
+}
+
+int kt_krylov_miobi(kt_matrix_t A, int k, int64_t nE, const int64_t* ei, const int64_t* ej,
+                    double tol, int it, int make, double rescale, int64_t* sel_i, int64_t* sel_j,
+                    double* rob, int64_t* nsel) {
+    KT_GUARD_BEGIN
+    if (!A || !rob || !nsel || (nE > 0 && (!ei || !ej))) fail(KT_ERR_ARG, "NULL argument");
+    if (k < 0 || nE < 0) fail(KT_ERR_ARG, "negative k or candidate count");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    require_symmetric(A, "KRYLOV_MIOBI:: Adjacency matrix should be symmetric");  // :26-28
+    if (it <= 0) it = (int)std::min<int64_t>(100, A->n);                        // :32-34
+    if (!make && A->nnz < 2 * (int64_t)k)                                       // :63-65
+        fail(KT_ERR_ARG, "KRYLOV_MIOBI:: edges to be removed are more than edges in the network");
+    const double sg = make ? 1.0 : -1.0;
+    const double B[4] = {0.0, sg / rescale, sg / rescale, 0.0};  // :78-84
+    std::vector<int64_t> Ei(ei, ei + nE), Ej(ej, ej + nE);
+    std::vector<double> xm;
+    double total = 0.0;
+    int64_t done = 0;
+    const int64_t steps = std::min<int64_t>(k, nE);
+    for (int64_t s = 0; s < steps; ++s) {  // :70
+        const int64_t m = (int64_t)Ei.size();
+        xm.assign(m, 0.0);
+        trace_fun_update_pairs(A, m, Ei.data(), Ej.data(), B, sg, tol, it, KT_FUN_EXP, xm.data(),
+                               nullptr, nullptr);  // :76-99
+        int64_t best = -1;  // :112-124 (strict comparison: first extreme wins)
+        double bv = make ? -INFINITY : INFINITY;
+        for (int64_t h = 0; h < m; ++h)
+            if (make ? xm[h] > bv : xm[h] < bv) {
+                bv = xm[h];
+                best = h;
+            }
+        if (best < 0) fail(KT_ERR_ARG, "KRYLOV_MIOBI:: no finite candidate score");
+        const int64_t ci = Ei[best], cj = Ej[best];
+        Ei.erase(Ei.begin() + best);  // :127
+        Ej.erase(Ej.begin() + best);
+        set_pairs(A, 1, &ci, &cj, make ? 1.0 : 0.0);  // :129-135
+        if (sel_i) sel_i[done] = ci;
+        if (sel_j) sel_j[done] = cj;
+        total += bv;
+        ++done;
+    }
+    *rob = total;
+    *nsel = done;
+    KT_GUARD_END
+}
+
+}  // extern "C"

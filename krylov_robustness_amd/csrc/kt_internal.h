@@ -149,6 +149,7 @@ namespace kt {
 // build one device CSR of A with rows in the order new2old (identity if empty)
 void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out);
 const DevCSR& natural_csr(kt_matrix_s* A);
+void refresh_device(kt_matrix_s* A);
 
 // profiling helpers (no-ops unless ctx->profile)
 void prof_begin(kt_context_s* ctx, int slot);

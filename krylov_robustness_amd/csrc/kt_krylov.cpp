@@ -16,7 +16,7 @@
 #include <cstring>
 #include <memory>
 
-#include "kt_block.h"
+#include "kt_krylov.h"
 
 namespace kt {
 
@@ -90,7 +90,7 @@ static std::vector<double> sym_matfun(kt_context_s* ctx, int n, const std::vecto
 }
 
 // trace_fun_update.m:43-47 / :85-89 with d1, d2 ascending
-static double trace_diff(const std::vector<double>& d1, const std::vector<double>& d2, int fun) {
+double trace_diff(const std::vector<double>& d1, const std::vector<double>& d2, int fun) {
     double x = 0.0;
     if (fun == KT_FUN_EXP) {
         for (size_t i = 0; i < d1.size(); ++i) x += std::exp(d1[i]) * (1.0 - std::exp(d2[i] - d1[i]));
@@ -115,7 +115,7 @@ static bool is_symmetric_host(const kt_matrix_s* A) {
     return true;
 }
 
-static void require_symmetric(kt_matrix_s* A, const char* msg) {
+void require_symmetric(kt_matrix_s* A, const char* msg) {
     if (A->symmetric < 0) A->symmetric = is_symmetric_host(A) ? 1 : 0;
     if (!A->symmetric) fail(KT_ERR_NOT_HERMITIAN, msg);
 }

@@ -32,6 +32,11 @@ hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int
 hipError_t launch_axpby(int n, int nc, double a, const double* X, int ldx, double b, double* Y,
                         int ldy, hipStream_t st);
 int inf_norm_blocks();
+// batched greedy candidates (kt_pairs.hip)
+hipError_t launch_pair_select(int C, const int* ii, const int* jj, double* X, int ld,
+                              hipStream_t st);
+hipError_t launch_pair_orth(int C, int n, const double* prev, const double* cur, double* W,
+                            int ld, double* hr, hipStream_t st);
 hipError_t launch_inf_norm(int n, int nc, const double* X, int ldx, double* partial,
                            hipStream_t st);
 

@@ -113,6 +113,29 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
     out.built = true;
 }
 
+// (Re)build the device copies after the host CSR changed: the degree-
+// relabelled hub CSR now, the natural-order CSR lazily (natural_csr).
+void refresh_device(kt_matrix_s* A) {
+    const int64_t n = A->n;
+    A->hub.release();
+    A->nat.release();
+    A->unit_values = std::all_of(A->h_val.begin(), A->h_val.end(), [](double v) { return v == 1.0; });
+    const char* un = getenv("KT_UNIT");
+    if (un && un[0] == '0') A->unit_values = false;
+    // degree-descending relabelling (stable, so ties keep original order)
+    const char* rl = getenv("KT_RELABEL");
+    const bool relabel = !(rl && rl[0] == '0');
+    A->new2old.resize(n);
+    A->old2new.resize(n);
+    for (int64_t i = 0; i < n; ++i) A->new2old[i] = (int32_t)i;
+    if (relabel)
+        std::stable_sort(A->new2old.begin(), A->new2old.end(), [&](int32_t a, int32_t b) {
+            return A->h_rowptr[a + 1] - A->h_rowptr[a] > A->h_rowptr[b + 1] - A->h_rowptr[b];
+        });
+    for (int64_t r = 0; r < n; ++r) A->old2new[A->new2old[r]] = (int32_t)r;
+    build_csr(A, A->new2old, A->hub);
+}
+
 const DevCSR& natural_csr(kt_matrix_s* A) {
     if (!A->nat.built) build_csr(A, std::vector<int32_t>(), A->nat);
     return A->nat;
@@ -256,21 +279,7 @@ int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr, con
     }
     try {
         KT_HIP(hipSetDevice(ctx->device));
-        A->unit_values = std::all_of(A->h_val.begin(), A->h_val.end(), [](double v) { return v == 1.0; });
-        const char* un = getenv("KT_UNIT");
-        if (un && un[0] == '0') A->unit_values = false;
-        // degree-descending relabelling (stable, so ties keep original order)
-        const char* rl = getenv("KT_RELABEL");
-        const bool relabel = !(rl && rl[0] == '0');
-        A->new2old.resize(n);
-        A->old2new.resize(n);
-        for (int64_t i = 0; i < n; ++i) A->new2old[i] = (int32_t)i;
-        if (relabel)
-            std::stable_sort(A->new2old.begin(), A->new2old.end(), [&](int32_t a, int32_t b) {
-                return A->h_rowptr[a + 1] - A->h_rowptr[a] > A->h_rowptr[b + 1] - A->h_rowptr[b];
-            });
-        for (int64_t r = 0; r < n; ++r) A->old2new[A->new2old[r]] = (int32_t)r;
-        build_csr(A, A->new2old, A->hub);
+        refresh_device(A);
     } catch (...) {
         A->hub.release();
         delete A;

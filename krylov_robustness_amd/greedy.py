@@ -1,0 +1,205 @@
+"""Greedy edge selection over the device path: krylov_miobi.m / greedy_krylov.m.
+
+``krylov_miobi`` scores every candidate edge of a greedy step with the batched
+device evaluation (kt_trace_fun_update_pairs: one block-2 Lanczos run per
+candidate, all candidates advanced by one SpMM per step) and edits A on the
+device (kt_matrix_set_pairs).  ``greedy_krylov`` is the reference's outer loop
+(greedy_krylov.m:64-93) with the search-space heuristics find_top_edges.m /
+find_top_missing_edges.m restated on the host: they are ordering/combinatorics
+on node centralities, not bandwidth work.
+
+Indices follow the reference: edges are 1-based (i, j) rows with
+E(:, 1) >= E(:, 2) for krylov_miobi's candidate lists.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from .core import Context, DeviceMatrix, _dev, _dptr, _fun_code, normest
+
+
+def _i64(a):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.int64))
+    return a, a.ctypes.data_as(C.POINTER(C.c_int64))
+
+
+def trace_fun_update_pairs(A, E, B, tol=1e-12, it=None, fun="exp", b_self=None,
+                           ctx: Optional[Context] = None):
+    """Xm[h] = trace_fun_update(A, U_h, B, tol, it, 0, fun) for every candidate
+    edge h of E (q x 2, 1-based), U_h = [e_E(h,1), e_E(h,2)] as built in
+    krylov_miobi.m:76-98 (a self-loop candidate uses U = e_i and B = b_self).
+    Returns (Xm, iter, lucky) arrays."""
+    D = _dev(A, ctx)
+    E = np.asarray(E, dtype=np.int64).reshape(-1, 2)
+    q = E.shape[0]
+    ei, pi = _i64(E[:, 0] - 1)
+    ej, pj = _i64(E[:, 1] - 1)
+    Bm = np.asfortranarray(np.asarray(B, dtype=np.float64).reshape(2, 2))
+    if b_self is None:
+        b_self = float(Bm[0, 1])
+    xm = np.zeros(q)
+    itr = np.zeros(q, dtype=np.int32)
+    lk = np.zeros(q, dtype=np.int32)
+    _lib.check(_lib.load().kt_trace_fun_update_pairs(
+        D.handle, q, pi, pj, _dptr(Bm), float(b_self), float(tol), int(it or 0), _fun_code(fun),
+        _dptr(xm), itr.ctypes.data_as(C.POINTER(C.c_int)), lk.ctypes.data_as(C.POINTER(C.c_int))))
+    return xm, itr, lk
+
+
+def krylov_miobi(A, k, E=None, tol=1e-12, it=None, poles=np.inf, debug=0, miobi="break",
+                 rescale=1.0, ctx: Optional[Context] = None):
+    """[edges, rob, A_new] = krylov_miobi(A, k, E, tol, it, poles, debug, miobi, rescale)
+    (krylov_miobi.m:1).  A may be a DeviceMatrix (edited in place and returned)
+    or a matrix (uploaded; the returned DeviceMatrix holds A_new)."""
+    if miobi not in ("break", "make"):
+        raise _lib.KrylovError(_lib.KT_ERR_ARG, "KRYLOV_MIOBI:: not supported option for miobi")
+    D = _dev(A, ctx)
+    if E is None or len(E) == 0:  # :42-46  all edges with E(:,1) >= E(:,2)
+        S = D.to_scipy().tocoo()
+        keep = S.row >= S.col
+        E = np.stack([S.row[keep], S.col[keep]], axis=1) + 1
+        E = E[np.lexsort((E[:, 0], E[:, 1]))]  # MATLAB find(): column-major order
+    E = np.asarray(E, dtype=np.int64).reshape(-1, 2)
+    nE = E.shape[0]
+    ei, pi = _i64(E[:, 0] - 1)
+    ej, pj = _i64(E[:, 1] - 1)
+    cap = max(min(int(k), nE), 1)
+    si = np.zeros(cap, dtype=np.int64)
+    sj = np.zeros(cap, dtype=np.int64)
+    rob = C.c_double()
+    ns = C.c_int64()
+    _lib.check(_lib.load().kt_krylov_miobi(
+        D.handle, int(k), nE, pi, pj, float(tol), int(it or 0), 1 if miobi == "make" else 0,
+        float(rescale), si.ctypes.data_as(C.POINTER(C.c_int64)),
+        sj.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(rob), C.byref(ns)))
+    m = int(ns.value)
+    edges = np.stack([si[:m] + 1, sj[:m] + 1], axis=1)
+    return edges, float(rob.value), D
+
+
+def find_top_edges(A, centrality, num, order="mult"):
+    """find_top_edges.m:1-40: the top `num` existing edges (1-based, i > j)."""
+    import scipy.sparse as sp
+    L = sp.tril(sp.csc_matrix(A), -1).tocsc()
+    L.eliminate_zeros()
+    L.sort_indices()
+    J = np.repeat(np.arange(L.shape[1]), np.diff(L.indptr))  # find(): column-major
+    I = L.indices.astype(np.int64)
+    c = np.asarray(centrality, dtype=np.float64).ravel()
+    if order == "mult":  # :22-25
+        score = c[I] * c[J]
+        ind = np.argsort(-score, kind="stable")
+    elif order == "min":  # :26-37
+        sc = np.sort(c)[::-1]
+        first = {}
+        for pos, v in enumerate(sc):
+            first.setdefault(v, pos + 1)
+        c1 = np.array([first[v] for v in c[I]], dtype=np.float64)
+        c2 = np.array([first[v] for v in c[J]], dtype=np.float64)
+        mn, mx = np.minimum(c1, c2), np.maximum(c1, c2)
+        ind = np.argsort(mx * (mx - 1) / 2 + mn, kind="stable")
+    else:
+        return np.stack([I + 1, J + 1], axis=1)
+    if len(I) < num:
+        raise IndexError("FIND_TOP_EDGES:: there are not enough edges in the graph")
+    ind = ind[:num]
+    return np.stack([I[ind] + 1, J[ind] + 1], axis=1)
+
+
+def find_top_missing_edges(A, centrality, num, order="min"):
+    """find_top_missing_edges.m:1-67: the top `num` missing edges (1-based)."""
+    import scipy.sparse as sp
+    A = sp.csr_matrix(A)
+    n = A.shape[0]
+    c = np.asarray(centrality, dtype=np.float64).ravel()
+    indC = np.argsort(-c, kind="stable")  # [sc, indC] = sort(centrality, 'descend')
+    sc = c[indC]
+    if order == "min":  # :52-64
+        E = []
+        j = 1
+        while len(E) < num:
+            if j >= n:
+                raise IndexError("FIND_TOP_MISSING_EDGES:: not enough missing edges")
+            col = A[indC[:j], :][:, [indC[j]]].toarray().ravel()
+            for t in np.flatnonzero(col == 0):
+                E.append((indC[t] + 1, indC[j] + 1))
+            j += 1
+        return np.array(E[:num], dtype=np.int64)
+    if order == "mult":  # :22-51
+        if (n * n - A.nnz - n) / 2 <= num:
+            raise RuntimeError("FIND_TOP_MISSING_EDGES:: output E is not assigned on this branch "
+                               "(find_top_missing_edges.m:23-30 returns before setting E)")
+        min_N, ln = 2, 0
+        while ln < num:
+            ln += int(np.sum(A[indC[:min_N - 1], :][:, [indC[min_N - 1]]].toarray() == 0))
+            min_N += 1
+        min_N -= 1
+        N = int(np.sum(sc[0] * sc > sc[min_N - 1] ** 2))
+        S = np.triu(np.outer(c[indC[:N]], c[indC[:N]]))
+        lin = np.argsort(-S.ravel(order="F"), kind="stable")
+        I, J = lin % N, lin // N
+        I, J = indC[I], indC[J]
+        E = []
+        for a, b in zip(I, J):
+            if len(E) >= num:
+                break
+            if a != b and A[a, b] == 0:
+                E.append((a + 1, b + 1))
+        return np.array(E, dtype=np.int64).reshape(-1, 2)
+    raise ValueError(f"unknown order {order!r}")
+
+
+def compute_centrality(A, kind="eig"):
+    """compute_centrality.m (host helper; 'eig' = |leading eigenvector|, 'deg')."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as sla
+    A = sp.csr_matrix(A, dtype=np.float64)
+    if kind == "deg":
+        return np.asarray(A.sum(axis=0)).ravel()
+    _, u = sla.eigsh(A, k=1, which="LM")  # eigs(A, 1): largest magnitude
+    return np.abs(u[:, 0])
+
+
+def greedy_krylov(A, k, Q=0, centrality=None, order="mult", tol=1e-12, it=None, poles=np.inf,
+                  debug=0, miobi="break", rescale=1.0, ctx: Optional[Context] = None):
+    """[edges, rob_variation, A_new] = greedy_krylov(A, k, Q, centrality, order, tol, it,
+    poles, debug, miobi, rescale)  (greedy_krylov.m:1-100).  Returns A_new as
+    the DeviceMatrix the edits were applied to (``.to_scipy()`` for the host copy)."""
+    D = _dev(A, ctx)
+    S = D.to_scipy()
+    if (S != S.T).nnz:  # :27-29
+        raise _lib.KrylovError(_lib.KT_ERR_NOT_HERMITIAN, "GREEDY_KRYLOV:: Adjacency matrix should be symmetric")
+    if not Q:
+        Q = int(np.asarray(S.sum(axis=0)).max())  # :42-44
+    if miobi == "break" and S.nnz < 2 * k:  # :54-56
+        raise _lib.KrylovError(_lib.KT_ERR_ARG, "GREEDY_KRYLOV:: edges to be removed are more than edges in the network")
+    if centrality is None:
+        centrality = compute_centrality(S, "eig")
+    edges = np.zeros((0, 2), dtype=np.int64)
+    rob = 0.0
+    top = None
+    last = None
+    for j in range(int(k)):  # :64-93
+        if j == 0:
+            top = (find_top_missing_edges(S, centrality, Q + k, order) if miobi == "make"
+                   else find_top_edges(S, centrality, Q + k, order))
+        else:  # drop the previously selected edge from the search space
+            hit = np.flatnonzero(np.all(top == last, axis=1))
+            if len(hit):
+                top = np.delete(top, hit[0], axis=0)
+        E = top[:Q]
+        tmp_edges, tmp_rob, D = krylov_miobi(D, 1, E, tol, it, poles, debug, miobi, rescale)
+        edges = np.vstack([edges, tmp_edges])
+        rob += tmp_rob
+        last = tmp_edges[0] if len(tmp_edges) else None
+    return edges, rob, D
+
+
+def default_greedy_tol(A, rel=1e-6, ctx: Optional[Context] = None):
+    """tol = 1e-6 * exp(normest(A)) as the greedy test drivers set it
+    (Tests/test_unweighted_break.m:56,74: nrm = exp(normest(A, 1e-2)))."""
+    return rel * float(np.exp(normest(A, 1e-2, ctx=ctx)))

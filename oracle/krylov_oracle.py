@@ -765,8 +765,8 @@ def exact_trace_update(A, U, B, fun="exp"):
 # ---------------------------------------------------------------------------
 # greedy edge selection: krylov_miobi.m / greedy_krylov.m (host loop logic)
 # ---------------------------------------------------------------------------
-def krylov_miobi(A, k, E, tol=1e-12, it=None, debug=0, miobi="break", rescale=1.0):
-    """krylov_miobi.m:1-142 (E 1-based, E(j,1) >= E(j,2))."""
+def krylov_miobi(A, k, E, tol=1e-12, it=None, poles=np.inf, debug=0, miobi="break", rescale=1.0):
+    """krylov_miobi.m:1-142 (E 1-based, E(j,1) >= E(j,2); poles unused there too)."""
     A = sp.csr_matrix(A, dtype=np.float64).copy()
     E = np.asarray(E, dtype=np.int64).copy()
     n = A.shape[0]
@@ -800,4 +800,71 @@ def krylov_miobi(A, k, E, tol=1e-12, it=None, debug=0, miobi="break", rescale=1.
         A = A.tocsr(); A.eliminate_zeros()
         edges = np.vstack([edges, chosen])
         rob += mx[1]
+    return edges, rob, A
+
+
+def find_top_edges(A, centrality, num, order="mult"):
+    """find_top_edges.m:14-39, written as the reference's loops."""
+    A = sp.csc_matrix(A)
+    n = A.shape[0]
+    I, J = [], []
+    for j in range(n):                                    # find(tril(A,-1)): column-major
+        for t in range(A.indptr[j], A.indptr[j + 1]):
+            i = A.indices[t]
+            if i > j and A.data[t] != 0:
+                I.append(i)
+                J.append(j)
+    order_idx = list(range(len(I)))
+    cen = [float(x) for x in np.ravel(centrality)]
+    if order == "mult":                                   # :22-25
+        c = [cen[I[h]] * cen[J[h]] for h in range(len(I))]
+        order_idx = sorted(range(len(I)), key=lambda h: -c[h])        # stable, descending
+    elif order == "min":                                  # :26-37
+        sc = sorted(cen, reverse=True)
+        scores = []
+        for h in range(len(I)):
+            c1 = sc.index(cen[I[h]]) + 1
+            c2 = sc.index(cen[J[h]]) + 1
+            mn, mx = min(c1, c2), max(c1, c2)
+            scores.append(mx * (mx - 1) / 2 + mn)
+        order_idx = sorted(range(len(I)), key=lambda h: scores[h])    # stable, ascending
+    if len(I) < num:
+        raise IndexError("FIND_TOP_EDGES:: there are not enough edges in the graph")
+    return np.array([[I[h] + 1, J[h] + 1] for h in order_idx[:num]], dtype=np.int64)
+
+
+def find_top_missing_edges_min(A, centrality, num):
+    """find_top_missing_edges.m:52-64 ('min' order), as the reference's loop."""
+    A = sp.csr_matrix(A)
+    cen = np.ravel(centrality)
+    indC = sorted(range(len(cen)), key=lambda i: -cen[i])        # sort(.., 'descend'), stable
+    E = []
+    j = 1
+    while len(E) < num:
+        for t in range(j):
+            if A[indC[t], indC[j]] == 0:
+                E.append([indC[t] + 1, indC[j] + 1])
+        j += 1
+    return np.array(E[:num], dtype=np.int64)
+
+
+def greedy_krylov(A, k, Q, centrality, order="mult", tol=1e-12, it=None, poles=np.inf, debug=0,
+                  miobi="break", rescale=1.0):
+    """greedy_krylov.m:64-93 over krylov_miobi (break: find_top_edges; make:
+    find_top_missing_edges with the 'min' order)."""
+    edges = np.zeros((0, 2), dtype=np.int64)
+    rob = 0.0
+    top = None
+    tmp_edges = None
+    for j in range(k):
+        if j == 0:
+            top = (find_top_edges(A, centrality, Q + k, order) if miobi == "break"
+                   else find_top_missing_edges_min(A, centrality, Q + k))
+        else:
+            hit = [h for h in range(len(top)) if tuple(top[h]) == tuple(tmp_edges[0])]
+            top = np.delete(top, hit[0], axis=0)
+        E = top[:Q]
+        tmp_edges, tmp_rob, A = krylov_miobi(A, 1, E, tol, it, poles, debug, miobi, rescale)
+        edges = np.vstack([edges, tmp_edges])
+        rob += tmp_rob
     return edges, rob, A

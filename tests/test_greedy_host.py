@@ -1,0 +1,55 @@
+"""Host-side search-space heuristics of the greedy path (find_top_edges.m,
+find_top_missing_edges.m) against the oracle's loop restatements, and the
+greedy argument checks that run before any device work.  CPU only."""
+import numpy as np
+import pytest
+
+from conftest import load_graph
+from oracle import krylov_oracle as ko
+
+import krylov_robustness_amd as kra
+
+
+@pytest.mark.parametrize("name", ["india", "rome", "austria", "anaheim"])
+@pytest.mark.parametrize("order", ["mult", "min"])
+def test_find_top_edges_matches_oracle(name, order):
+    A = load_graph(name)
+    c = kra.compute_centrality(A)
+    num = min(120, A.nnz // 2)
+    np.testing.assert_array_equal(kra.find_top_edges(A, c, num, order),
+                                  ko.find_top_edges(A, c, num, order))
+
+
+def test_find_top_edges_ties_keep_find_order():
+    """Equal centralities: MATLAB's stable sort keeps find()'s column-major order."""
+    A = load_graph("denmark")
+    c = np.ones(A.shape[0])
+    E = kra.find_top_edges(A, c, 20, "mult")
+    np.testing.assert_array_equal(E, ko.find_top_edges(A, c, 20, "mult"))
+    assert np.all(np.diff(E[:, 1]) >= 0)          # columns ascending
+    assert np.all(E[:, 0] > E[:, 1])               # tril(A, -1)
+
+
+def test_find_top_edges_too_few():
+    A = load_graph("denmark")
+    with pytest.raises(IndexError):
+        kra.find_top_edges(A, np.ones(A.shape[0]), A.nnz, "min")
+
+
+@pytest.mark.parametrize("name", ["india", "rome", "austria"])
+def test_find_top_missing_edges_min(name):
+    A = load_graph(name)
+    c = kra.compute_centrality(A)
+    E = kra.find_top_missing_edges(A, c, 80, "min")
+    np.testing.assert_array_equal(E, ko.find_top_missing_edges_min(A, c, 80))
+    assert all(A[i - 1, j - 1] == 0 and i != j for i, j in E)
+
+
+def test_find_top_missing_edges_mult_are_missing():
+    A = load_graph("austria")
+    c = kra.compute_centrality(A)
+    E = kra.find_top_missing_edges(A, c, 40, "mult")
+    assert len(E) == 40
+    assert all(A[i - 1, j - 1] == 0 and i != j for i, j in E)
+    s = c[E[:, 0] - 1] * c[E[:, 1] - 1]
+    assert np.all(np.diff(s) <= 1e-15)            # descending products
