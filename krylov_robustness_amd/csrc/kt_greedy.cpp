@@ -10,8 +10,15 @@
 // h's numbers follow trace_fun_update.m exactly as the single-call path
 // (kt_krylov.cpp) does; only the order of independent work changes.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 
 #include "kt_krylov.h"
@@ -69,23 +76,81 @@ double pair_xm(const PairRun& s, int j, int fun, std::vector<double>& G, std::ve
     return trace_diff(w1, w2, fun);
 }
 
-// Run f(i) for i in [0, count) on up to 16 host threads (small eig problems).
-template <class F>
-void parallel_for(int count, int64_t work_per_item, F f) {
-    int nt = (int)std::min<int64_t>(16, std::max<int64_t>(1, (int64_t)count * work_per_item / 200000));
-    nt = std::min<int>(nt, (int)std::max(1u, std::thread::hardware_concurrency()));
-    nt = std::min(nt, count);
-    if (nt <= 1) {
-        for (int i = 0; i < count; ++i) f(i);
-        return;
+// Persistent host worker pool for the per-candidate eig work (spawning
+// threads every Lanczos step costs more than the work itself).
+class HostPool {
+   public:
+    static HostPool& get() {
+        static HostPool pool;
+        return pool;
     }
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t)
-        th.emplace_back([&, t]() {
-            for (int i = t; i < count; i += nt) f(i);
-        });
-    for (auto& x : th) x.join();
-}
+    // f(i) for i in [0, count); the caller thread participates
+    void run(int count, const std::function<void(int)>& f) {
+        if (count <= 0) return;
+        if (workers_.empty() || count < 8) {
+            for (int i = 0; i < count; ++i) f(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &f;
+            count_ = count;
+            next_.store(0);
+            pending_ = (int)workers_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain(f, count);
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+   private:
+    HostPool() {
+        int nt = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) - 1;
+        if (const char* e = getenv("KT_HOST_THREADS")) nt = std::max(0, atoi(e) - 1);
+        for (int t = 0; t < nt; ++t) workers_.emplace_back([this] { loop(); });
+    }
+    void drain(const std::function<void(int)>& f, int count) {
+        for (int i = next_.fetch_add(1); i < count; i = next_.fetch_add(1)) f(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* f;
+            int count;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                f = job_;
+                count = count_;
+            }
+            if (f) drain(*f, count);
+            std::lock_guard<std::mutex> lk(m_);
+            if (--pending_ == 0) done_cv_.notify_one();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)>* job_ = nullptr;
+    int count_ = 0, pending_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
 
 // One device batch of C <= kMaxPairs two-column candidates.
 void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej, const double* B,
@@ -93,32 +158,65 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
     kt_context_s* ctx = A->ctx;
     const int64_t n = A->n;
     const int cols = 2 * C;
+    using clk = std::chrono::steady_clock;
+    static const bool timing = getenv("KT_PAIRS_TIMING") != nullptr;
+    double t_setup = 0, t_gpu = 0, t_host = 0;
+    auto t0 = clk::now();
+    auto lap = [&](double& acc) {
+        auto t = clk::now();
+        acc += std::chrono::duration<double, std::milli>(t - t0).count();
+        t0 = t;
+    };
     const int CP = cols <= 64 ? pow2_at_least(cols) : (cols + 127) / 128 * 128;
-    DevMat S[3];
-    for (auto& s : S) s.alloc(ctx, n, CP);
-    DevBuf didx, dhr;
-    didx.ensure(sizeof(int) * 2 * (size_t)C);
-    dhr.ensure(sizeof(double) * 11 * (size_t)C);
-    PinnedBuf hhr;
-    hhr.ensure(sizeof(double) * 11 * (size_t)C);
+    Workspace& ws = ctx->ws;
+    const size_t blk_bytes = sizeof(double) * (size_t)std::max<int64_t>(n, 1) * CP;
+    double* S[3];
+    for (int t = 0; t < 3; ++t) {
+        ws.pair_blk[t].ensure(blk_bytes);
+        S[t] = ws.pair_blk[t].as<double>();
+    }
+    ws.pair_idx.ensure(sizeof(int) * 2 * (size_t)C);
+    ws.pair_hr.ensure(sizeof(double) * 11 * (size_t)C);
+    ws.pair_coef.ensure(sizeof(double) * pairs_coef_doubles(C));
+    ws.pair_part.ensure(sizeof(double) * pairs_part_doubles((int)n, C, ctx->num_cu));
+    for (auto& b : ws.pair_host) b.ensure(sizeof(double) * 11 * (size_t)C);
+    double* dhr = ws.pair_hr.as<double>();
+    auto orth = [&](const double* p, const double* u, double* W) {
+        KT_HIP(launch_pairs_orth(C, (int)n, ctx->num_cu, p, u, W, CP, ws.pair_coef.as<double>(),
+                                 ws.pair_part.as<double>(), dhr, ctx->stream));
+    };
     std::vector<int> idx(2 * (size_t)C);
     for (int c = 0; c < C; ++c) {
         idx[c] = (int)ei[c];
         idx[C + c] = (int)ej[c];
     }
-    KT_HIP(hipMemcpyAsync(didx.ptr, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice,
+    // S[0] = 0 (the SpMM then keeps the padding columns of S[1], S[2] at 0)
+    KT_HIP(hipMemsetAsync(S[0], 0, blk_bytes, ctx->stream));
+    KT_HIP(hipMemcpyAsync(ws.pair_idx.ptr, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice,
                           ctx->stream));
-    double* hr = hhr.as<double>();
+    double* hr = ws.pair_host[0].as<double>();
+    struct Events {
+        hipEvent_t e[2] = {nullptr, nullptr};
+        Events() {
+            for (auto& x : e) KT_HIP(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+        }
+        ~Events() {
+            for (auto& x : e)
+                if (x) (void)hipEventDestroy(x);
+        }
+    } evs;
+    hipEvent_t* ev = evs.e;
     auto fetch = [&]() {
-        KT_HIP(hipMemcpyAsync(hr, dhr.ptr, sizeof(double) * 11 * (size_t)C, hipMemcpyDeviceToHost,
+        KT_HIP(hipMemcpyAsync(hr, dhr, sizeof(double) * 11 * (size_t)C, hipMemcpyDeviceToHost,
                               ctx->stream));
         KT_HIP(hipStreamSynchronize(ctx->stream));
     };
     // [V, ~] = qr(U, 0)  (lanczos_krylov.m:48); V1' U = R exactly for unit
     // selectors, so Cm = R B R'  (trace_fun_update.m:65-66)
-    KT_HIP(launch_pair_select(C, didx.as<int>(), didx.as<int>() + C, S[0].col(0), CP, ctx->stream));
-    KT_HIP(launch_pair_orth(C, (int)n, nullptr, nullptr, S[0].col(0), CP, dhr.as<double>(), ctx->stream));
+    KT_HIP(launch_pair_select(C, ws.pair_idx.as<int>(), ws.pair_idx.as<int>() + C, S[0], CP, ctx->stream));
+    orth(nullptr, nullptr, S[0]);
     fetch();
+    lap(t_setup);
     std::vector<PairRun> run(C);
     for (int c = 0; c < C; ++c) {
         const double R[4] = {hr[11 * c + 8], 0.0, hr[11 * c + 9], hr[11 * c + 10]};
@@ -126,25 +224,39 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
         matmul(2, 2, 2, R, B, RB);
         matmul(2, 2, 2, RB, Rt, run[c].Cm);
     }
+    // Step j's device work (SpMM + CGS2/QR + copy of its coefficients) is
+    // queued before the host processes step j-1, so the host eig work of
+    // one step overlaps the device work of the next.  A step launched after
+    // every candidate stopped is simply discarded.
     int cur = 0, prev = -1, w = 1;
-    int active = C;
-    const int d = 2;  // lag (trace_fun_update.m:58)
-    for (int j = 1; j <= it && active > 0; ++j) {
+    PinnedBuf* hbuf = ws.pair_host;
+    auto launch_step = [&](int slot) {
         // w = A * w over every candidate (lanczos_krylov.m:81)
         for (int c0 = 0; c0 < CP; c0 += 128)
-            spmm(A, S[cur].col(c0), CP, S[w].col(c0), CP, std::min(128, cols - c0));
-        KT_HIP(launch_pair_orth(C, (int)n, prev >= 0 ? S[prev].col(0) : nullptr, S[cur].col(0),
-                                S[w].col(0), CP, dhr.as<double>(), ctx->stream));
-        fetch();
+            spmm(A, S[cur] + c0, CP, S[w] + c0, CP, std::min(128, cols - c0));
+        orth(prev >= 0 ? S[prev] : nullptr, S[cur], S[w]);
+        KT_HIP(hipMemcpyAsync(hbuf[slot].ptr, dhr, sizeof(double) * 11 * (size_t)C,
+                              hipMemcpyDeviceToHost, ctx->stream));
+        KT_HIP(hipEventRecord(ev[slot], ctx->stream));
         const int freed = prev >= 0 ? prev : 3 - cur - w;
         prev = cur;
         cur = w;
         w = freed;
-        std::vector<int> todo;
+    };
+    int active = C;
+    const int d = 2;  // lag (trace_fun_update.m:58)
+    std::vector<int> todo;
+    launch_step(0);
+    for (int j = 1; j <= it && active > 0; ++j) {
+        KT_HIP(hipEventSynchronize(ev[(j - 1) & 1]));
+        lap(t_gpu);
+        if (j < it) launch_step(j & 1);
+        const double* hr_j = hbuf[(j - 1) & 1].as<double>();
+        todo.clear();
         for (int c = 0; c < C; ++c) {
             if (run[c].done) continue;
             PairRun& s = run[c];
-            const double* h = hr + 11 * c;
+            const double* h = hr_j + 11 * c;
             // h rows (prev0, prev1, cur0, cur1) x cols (w0, w1)
             s.P.insert(s.P.end(), {h[0], h[1], h[4], h[5]});
             s.D.insert(s.D.end(), {h[2], h[3], h[6], h[7]});
@@ -152,8 +264,8 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
             s.lucky = std::sqrt(h[8] * h[8] + h[9] * h[9] + h[10] * h[10]) < 1e-8;  // :91-93
             todo.push_back(c);
         }
-        parallel_for((int)todo.size(), 16 * (int64_t)j * j * j, [&](int t) {
-            std::vector<double> G, T, w1, w2;
+        HostPool::get().run((int)todo.size(), [&](int t) {
+            thread_local std::vector<double> G, T, w1, w2;
             PairRun& s = run[todo[t]];
             s.Xm = pair_xm(s, j, fun, G, T, w1, w2);
         });
@@ -175,7 +287,12 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
                 --active;
             }
         }
+        lap(t_host);
     }
+    KT_HIP(hipStreamSynchronize(ctx->stream));
+    if (timing)
+        fprintf(stderr, "[kt pairs] C=%d n=%lld setup %.3f ms  gpu %.3f ms  host %.3f ms\n", C,
+                (long long)n, t_setup, t_gpu, t_host);
     for (int c = 0; c < C; ++c) {
         Xm[c] = run[c].Xm;
         if (iter) iter[c] = run[c].iter;

@@ -94,6 +94,10 @@ struct Workspace {
     DevBuf small, small2, qrtmp, eigA, eigW, eigInfo;  // block-Krylov scratch
     DevBuf hist, norm_part;                             // sweep scale history, inf-norm partials
     PinnedBuf host_trec;
+    // batched greedy candidates (kt_greedy.cpp): 3 pair blocks, indices,
+    // per-candidate coefficients / partials / host records
+    DevBuf pair_blk[3], pair_idx, pair_coef, pair_part, pair_hr;
+    PinnedBuf pair_host[2];
 };
 
 }  // namespace kt
@@ -150,6 +154,7 @@ namespace kt {
 void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out);
 const DevCSR& natural_csr(kt_matrix_s* A);
 void refresh_device(kt_matrix_s* A);
+const DevCSR& hub_csr(kt_matrix_s* A);
 
 // profiling helpers (no-ops unless ctx->profile)
 void prof_begin(kt_context_s* ctx, int slot);

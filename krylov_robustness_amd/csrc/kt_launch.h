@@ -35,8 +35,13 @@ int inf_norm_blocks();
 // batched greedy candidates (kt_pairs.hip)
 hipError_t launch_pair_select(int C, const int* ii, const int* jj, double* X, int ld,
                               hipStream_t st);
-hipError_t launch_pair_orth(int C, int n, const double* prev, const double* cur, double* W,
-                            int ld, double* hr, hipStream_t st);
+// CGS2 of W against [prev cur] (cur == nullptr: none) + Householder thin QR,
+// per candidate; hr[c*11 + 0..10] = (h [8], R11, R12, R22)
+hipError_t launch_pairs_orth(int C, int n, int num_cu, const double* prev, const double* cur,
+                             double* W, int ld, double* coef, double* part, double* hr,
+                             hipStream_t st);
+size_t pairs_part_doubles(int n, int C, int num_cu);
+size_t pairs_coef_doubles(int C);
 hipError_t launch_inf_norm(int n, int nc, const double* X, int ldx, double* partial,
                            hipStream_t st);
 

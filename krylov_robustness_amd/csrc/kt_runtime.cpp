@@ -113,15 +113,20 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
     out.built = true;
 }
 
-// (Re)build the device copies after the host CSR changed: the degree-
-// relabelled hub CSR now, the natural-order CSR lazily (natural_csr).
+// Drop the device copies after the host CSR changed; hub_csr / natural_csr
+// rebuild them on next use.
 void refresh_device(kt_matrix_s* A) {
-    const int64_t n = A->n;
     A->hub.release();
     A->nat.release();
     A->unit_values = std::all_of(A->h_val.begin(), A->h_val.end(), [](double v) { return v == 1.0; });
     const char* un = getenv("KT_UNIT");
     if (un && un[0] == '0') A->unit_values = false;
+}
+
+// degree-relabelled CSR of the probe hot path, built on first use
+const DevCSR& hub_csr(kt_matrix_s* A) {
+    if (A->hub.built) return A->hub;
+    const int64_t n = A->n;
     // degree-descending relabelling (stable, so ties keep original order)
     const char* rl = getenv("KT_RELABEL");
     const bool relabel = !(rl && rl[0] == '0');
@@ -134,6 +139,7 @@ void refresh_device(kt_matrix_s* A) {
         });
     for (int64_t r = 0; r < n; ++r) A->old2new[A->new2old[r]] = (int32_t)r;
     build_csr(A, A->new2old, A->hub);
+    return A->hub;
 }
 
 const DevCSR& natural_csr(kt_matrix_s* A) {
@@ -280,6 +286,7 @@ int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr, con
     try {
         KT_HIP(hipSetDevice(ctx->device));
         refresh_device(A);
+        (void)hub_csr(A);
     } catch (...) {
         A->hub.release();
         delete A;

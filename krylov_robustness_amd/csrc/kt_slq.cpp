@@ -242,7 +242,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         w.host_trec.ensure(sizeof(double) * rec * nsweeps);
         double* htrec = w.host_trec.as<double>();
         for (int64_t s = 0; s < nsweeps; ++s)
-            lanczos_sweep(A, A->hub, P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr, htrec + rec * s,
+            lanczos_sweep(A, hub_csr(A), P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr, htrec + rec * s,
                           nullptr, nullptr);
         KT_HIP(hipStreamSynchronize(ctx->stream));
         prof_collect(ctx);
