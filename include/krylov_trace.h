@@ -185,6 +185,16 @@ int kt_matrix_set_pairs(kt_matrix_t A, int64_t count, const int64_t* ei, const i
  * kt_matrix_info).  rowind / vals may be NULL. */
 int kt_matrix_export_csc(kt_matrix_t A, int64_t* colptr, int64_t* rowind, double* vals);
 
+/* ---- entries of f(A) (function_multiple_entries.m) -------------------- */
+
+/* X[h] ~= f(A)(oi[h], oj[h]) for h < k (0-based indices) by one Arnoldi run
+ * per distinct row index (function_multiple_entries.m:1 with poles = inf);
+ * tol / it as the reference (lag-3 stop on f(Gm) e1, it <= 0: min(100, n));
+ * iter (nullable) = Krylov steps taken.  Replaces
+ * function_multiple_entries.m:1 (Tests/test_weighted_*.m:52-77). */
+int kt_function_multiple_entries(kt_matrix_t A, int64_t k, const int64_t* oi, const int64_t* oj,
+                                 int fun, double tol, int it, double* X, int* iter);
+
 /* Per-kernel timing (HIP events recorded on the library's stream around each
  * launch of the named kernel while enabled).  kernel: 0 = spmm_gram (K1),
  * 1 = update_norm (K2).  Returns launch count and summed milliseconds. */

@@ -75,6 +75,8 @@ SIGNATURES = [
                                   C.c_int, C.c_double, _i64p, _i64p, _dp, _i64p]),
     ("kt_matrix_set_pairs", C.c_int, [_mat_p, C.c_int64, _i64p, _i64p, C.c_double]),
     ("kt_matrix_export_csc", C.c_int, [_mat_p, _i64p, _i64p, _dp]),
+    ("kt_function_multiple_entries", C.c_int, [_mat_p, C.c_int64, _i64p, _i64p, C.c_int, C.c_double,
+                                               C.c_int, _dp, _ip]),
     ("kt_profile_enable", C.c_int, [_ctx_p, C.c_int]),
     ("kt_profile_read", C.c_int, [_ctx_p, C.c_int, _i64p, _dp]),
     ("kt_profile_reset", C.c_int, [_ctx_p]),

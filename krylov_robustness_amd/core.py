@@ -349,3 +349,23 @@ def lanczos_fmv(A, X, m=30, fun="exp", ctx: Optional[Context] = None):
     _lib.check(_lib.load().kt_lanczos_fmv(D.handle, _fun_code(fun), int(m), X.shape[1], _dptr(X),
                                           _dptr(Y)))
     return Y
+
+
+def function_multiple_entries(A, omega, f="exp", tol=1e-12, it=None, poles=np.inf, debug=0,
+                              ctx: Optional[Context] = None):
+    """[X, iter] = function_multiple_entries(A, omega, f, tol, it, poles, debug)
+    (function_multiple_entries.m:1); omega is (k x 2), 1-based as in MATLAB."""
+    if not (np.isscalar(poles) and np.isinf(poles)):
+        raise _lib.KrylovError(_lib.KT_ERR_UNSUPPORTED,
+                               "FUNCTION_MULTIPLE_ENTRIES::Unsupported rational Krylov yet")
+    D = _dev(A, ctx)
+    om = np.asarray(omega, dtype=np.int64).reshape(-1, 2)
+    oi = np.ascontiguousarray(om[:, 0] - 1)
+    oj = np.ascontiguousarray(om[:, 1] - 1)
+    X = np.zeros(om.shape[0])
+    itr = C.c_int()
+    _lib.check(_lib.load().kt_function_multiple_entries(
+        D.handle, om.shape[0], oi.ctypes.data_as(C.POINTER(C.c_int64)),
+        oj.ctypes.data_as(C.POINTER(C.c_int64)), _fun_code(f), float(tol), int(it or 0),
+        _dptr(X), C.byref(itr)))
+    return X, int(itr.value)

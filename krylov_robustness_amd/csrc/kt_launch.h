@@ -41,6 +41,15 @@ hipError_t launch_pairs_orth(int C, int n, int num_cu, const double* prev, const
                              double* W, int ld, double* coef, double* part, double* hr,
                              hipStream_t st);
 size_t pairs_part_doubles(int n, int C, int num_cu);
+// column-batched single-vector Arnoldi (kt_colbatch.hip); V blocks at stride vstride
+int col_nrb(int n, int num_cu);
+hipError_t launch_col_dots(int n, int P, int nb, int64_t vstride, const double* V, const double* W,
+                           int r_lo, int num_cu, double* part, double* out, hipStream_t st);
+hipError_t launch_col_update(int n, int P, int nb, int64_t vstride, const double* V,
+                             const double* h, double* W, hipStream_t st);
+hipError_t launch_col_householder(int n, int P, const double* s, double* W, double* Q, double* r,
+                                  hipStream_t st);
+hipError_t launch_col_select(int C, int P, const int* idx, double* X, hipStream_t st);
 size_t pairs_coef_doubles(int C);
 hipError_t launch_inf_norm(int n, int nc, const double* X, int ldx, double* partial,
                            hipStream_t st);

@@ -868,3 +868,82 @@ def greedy_krylov(A, k, Q, centrality, order="mult", tol=1e-12, it=None, poles=n
         edges = np.vstack([edges, tmp_edges])
         rob += tmp_rob
     return edges, rob, A
+
+
+# ---------------------------------------------------------------------------
+# function_multiple_entries.m (poles = inf)
+# ---------------------------------------------------------------------------
+def fme_matrix_fun(name: str):
+    """function_multiple_entries.m:47-60: exp->expm, sin/cos->funm, log->logm,
+    sqrt->sqrtm, anything else funm(M, f) (sinh/cosh here)."""
+    if name == "exp":
+        return sla.expm
+    if name in ("sin", "cos"):
+        return lambda M: np.real_if_close(sla.funm(M, scalar_fun(name)))
+    if name == "sinh":
+        return sla.sinhm
+    if name == "cosh":
+        return sla.coshm
+    if name == "log":
+        return sla.logm
+    if name == "sqrt":
+        return sla.sqrtm
+    raise ValueError(name)
+
+
+def function_multiple_entries(A, omega, f="exp", tol=1e-12, it=None, poles=np.inf, debug=0):
+    """[X, iter] = function_multiple_entries(A, omega, f, tol, it, poles, debug)
+    (function_multiple_entries.m:1-181); omega is 1-based (k x 2)."""
+    omega = np.asarray(omega, dtype=np.int64).reshape(-1, 2)
+    n = A.shape[0]
+    if it is None:
+        it = min(100, n)                                  # :24-26
+    k = omega.shape[0]
+    I0 = list(dict.fromkeys(omega[:, 0].tolist()))        # unique(.., 'stable')   :42
+    row = {t: i for i, t in enumerate(I0)}                # the handle keeps the first I  :44
+    fM = fme_matrix_fun(f)
+    d = 3                                                 # :63
+    Xstop = [[] for _ in range(k)]
+    notconverged = list(range(k))
+    St = [None] * len(I0)
+    Uaux = np.zeros(len(I0))
+    Gm = [None] * len(I0)
+    Xm = [None] * k
+    I = list(I0)
+    j = 0
+    for j in range(1, it + 1):                            # :84
+        for h in I:                                       # :86
+            r_ = row[h]
+            if j == 1:
+                U = np.zeros((n, 1)); U[h - 1, 0] = 1.0
+                St[r_] = arnoldi_krylov_start(A, U)
+                Uaux[r_] = (St[r_].V.T @ U)[0, 0]         # :94-95
+            else:
+                St[r_] = arnoldi_krylov_extend(St[r_])
+            Gm[r_] = St[r_].H[:-1, :]                     # :106
+        stop = True
+        for h in list(notconverged):                      # :113
+            Xm[h] = fM(Gm[row[omega[h, 0]]])
+            if j <= d:
+                Xstop[h].append(Xm[h])
+                stop = False
+            else:
+                nn = Xm[h].shape[0]
+                old = np.zeros((nn, nn))
+                o = Xstop[h][0]
+                old[:o.shape[0], :o.shape[1]] = o
+                err = np.linalg.norm((Xm[h] - old)[:, 0])
+                if err > tol:
+                    stop = False
+                else:
+                    notconverged = [x for x in notconverged if x != h]
+                    I = list(dict.fromkeys(omega[notconverged, 0].tolist()))
+                Xstop[h] = Xstop[h][1:d] + [Xm[h]]
+        if stop:
+            break
+    X = np.zeros(k)
+    for h in range(k):                                    # :163-165
+        r_ = row[omega[h, 0]]
+        nn = Xm[h].shape[0]
+        X[h] = St[r_].V[omega[h, 1] - 1, :nn] @ Xm[h][:, 0] * Uaux[r_]
+    return X, j
