@@ -45,14 +45,37 @@ void DevMat::alloc(kt_context_s* ctx, int64_t n_, int ld_) {
 void gram(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* Y,
           int ldy, int py, std::vector<double>& G) {
     G.assign((size_t)px * py, 0.0);
-    if (px == 0 || py == 0) return;
+    if (px == 0 || py == 0 || n == 0) return;
     DevBuf& d = ctx->ws.small;
-    d.ensure(sizeof(double) * (size_t)px * py);
     const double one = 1.0, zero = 0.0;
-    // column-major views: X is (ldx x n), Y is (ldy x n);  G = X(0:px,:) Y(0:py,:)'
-    rb(rocblas_dgemm(blas(ctx), rocblas_operation_none, rocblas_operation_transpose, px, py,
-                     (rocblas_int)n, &one, X, ldx, Y, ldy, &zero, d.as<double>(), px),
-       "rocblas_dgemm(gram)");
+    const int64_t count = (int64_t)px * py;
+    // column-major views: X is (ldx x n), Y is (ldy x n);  G = X(0:px,:) Y(0:py,:)'.
+    // The reduction dimension n is long and the output tiny, so split it over
+    // S row chunks (one strided-batched GEMM) and add the S slabs in a fixed
+    // order: enough workgroups to fill the chip.
+    int S = (int)std::min<int64_t>(64, std::max<int64_t>(1, n / 1024));
+    while (S > 1 && count * S > (int64_t)1 << 24) S /= 2;
+    const int64_t chunk = n / S;
+    const int64_t rem = n - chunk * S;
+    const int slabs = S + (rem > 0 ? 1 : 0);
+    d.ensure(sizeof(double) * (size_t)count * (slabs + 1));
+    double* part = d.as<double>() + count;
+    if (S == 1 && rem == 0) {
+        rb(rocblas_dgemm(blas(ctx), rocblas_operation_none, rocblas_operation_transpose, px, py,
+                         (rocblas_int)n, &one, X, ldx, Y, ldy, &zero, d.as<double>(), px),
+           "rocblas_dgemm(gram)");
+    } else {
+        rb(rocblas_dgemm_strided_batched(blas(ctx), rocblas_operation_none, rocblas_operation_transpose,
+                                         px, py, (rocblas_int)chunk, &one, X, ldx, chunk * ldx, Y, ldy,
+                                         chunk * ldy, &zero, part, px, count, S),
+           "rocblas_dgemm_strided_batched(gram)");
+        if (rem > 0)
+            rb(rocblas_dgemm(blas(ctx), rocblas_operation_none, rocblas_operation_transpose, px, py,
+                             (rocblas_int)rem, &one, X + chunk * S * ldx, ldx, Y + chunk * S * ldy, ldy,
+                             &zero, part + count * S, px),
+               "rocblas_dgemm(gram tail)");
+        KT_HIP(launch_sum_slabs((int)count, slabs, part, d.as<double>(), ctx->stream));
+    }
     KT_HIP(hipMemcpyAsync(G.data(), d.ptr, sizeof(double) * G.size(), hipMemcpyDeviceToHost,
                           ctx->stream));
     KT_HIP(hipStreamSynchronize(ctx->stream));
@@ -212,27 +235,63 @@ bool cholqr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector
 
 namespace kt {
 
-// Householder thin QR (the factorisation MATLAB's qr(w, 0) uses).  The
-// row-major n x ld block W is the column-major (ld x n) matrix M = W', so an
-// LQ factorisation of M's first bs rows (rocsolver_dgelqf) is a Householder QR
-// of W: M(0:bs,:) = L Q'  =>  W = Q' ' L'.  R = L' (upper); rocsolver_dorglq
-// then overwrites M(0:bs,:) with Q', i.e. W with Q.  Rank-deficient W is
-// handled like LAPACK: R gets ~0 diagonal entries and Q stays orthonormal.
+// Householder thin QR (the factorisation MATLAB's qr(w, 0) uses: LAPACK
+// reflectors, R with dlarfg's signs, Q = H_1 ... H_bs E), on the tall-skinny
+// kernels of kt_tsqr.hip.  Exactly rank-deficient W takes dlarfg's tau = 0
+// branch, so its completion matches LAPACK's.
 void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R) {
     R.assign((size_t)bs * bs, 0.0);
     if (n == 0 || bs == 0) return;
     if (n < bs) fail(KT_ERR_UNSUPPORTED, "thin QR needs n >= block size");
-    DevBuf& tau = ctx->ws.small2;
-    tau.ensure(sizeof(double) * (size_t)bs);
-    rb(rocsolver_dgelqf(blas(ctx), bs, (rocblas_int)n, W, ld, tau.as<double>()), "rocsolver_dgelqf");
-    std::vector<double> top((size_t)bs * bs);  // rows 0..bs-1 of W, first bs columns
+    if (bs > 128) fail(KT_ERR_UNSUPPORTED, "thin QR block size > 128");
+    const int BP = pow2_at_least(bs);
+    Workspace& ws = ctx->ws;
+    const int nrb = ts_nrb((int)n, ctx->num_cu);
+    ws.ts_V.ensure(sizeof(double) * (size_t)n * BP);
+    ws.ts_part.ensure(sizeof(double) * (size_t)BP * nrb);
+    ws.ts_small.ensure(sizeof(double) * ((size_t)3 * BP + (size_t)bs * bs));
+    double* V = ws.ts_V.as<double>();
+    double* pivot = ws.ts_small.as<double>();
+    double* sums = pivot + BP;
+    double* taus = sums + BP;
+    double* Md = taus + BP;
+    KT_HIP(hipMemsetAsync(V, 0, sizeof(double) * (size_t)n * BP, ctx->stream));
+    KT_HIP(launch_ts_reflectors((int)n, bs, BP, W, ld, V, pivot, sums, ws.ts_part.as<double>(), taus,
+                                ctx->num_cu, ctx->stream));
+    std::vector<double> top((size_t)bs * bs), V1((size_t)bs * BP), tau(bs);
     KT_HIP(hipMemcpy2DAsync(top.data(), sizeof(double) * bs, W, sizeof(double) * ld,
                             sizeof(double) * bs, (size_t)bs, hipMemcpyDeviceToHost, ctx->stream));
-    rb(rocsolver_dorglq(blas(ctx), bs, (rocblas_int)n, bs, W, ld, tau.as<double>()), "rocsolver_dorglq");
-    KT_HIP(hipStreamSynchronize(ctx->stream));
-    // M(i, j) = top[j * bs + i]; L(i, j) = M(i, j), j <= i;  R(j, i) = L(i, j)
+    KT_HIP(hipMemcpyAsync(V1.data(), V, sizeof(double) * (size_t)bs * BP, hipMemcpyDeviceToHost,
+                          ctx->stream));
+    KT_HIP(hipMemcpyAsync(tau.data(), taus, sizeof(double) * bs, hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<double> G;  // V' V (bs x bs), gram synchronises the stream
+    gram(ctx, n, V, BP, bs, V, BP, bs, G);
     for (int i = 0; i < bs; ++i)
-        for (int j = 0; j <= i; ++j) R[j + (size_t)i * bs] = top[(size_t)j * bs + i];
+        for (int j = i; j < bs; ++j) R[i + (size_t)j * bs] = top[(size_t)i * bs + j];
+    // dlarft (forward, columnwise): T upper bs x bs, column-major
+    std::vector<double> T((size_t)bs * bs, 0.0), tmp(bs);
+    for (int i = 0; i < bs; ++i) {
+        if (tau[i] != 0.0) {
+            for (int l = 0; l < i; ++l) tmp[l] = -tau[i] * G[l + (size_t)i * bs];
+            for (int l = 0; l < i; ++l) {
+                double s = 0.0;
+                for (int q = l; q < i; ++q) s += T[l + (size_t)q * bs] * tmp[q];
+                T[l + (size_t)i * bs] = s;
+            }
+        }
+        T[i + (size_t)i * bs] = tau[i];
+    }
+    // M = T V1'  (row-major for the kernel: M[k * bs + j])
+    std::vector<double> M((size_t)bs * bs, 0.0);
+    for (int k = 0; k < bs; ++k)
+        for (int j = 0; j < bs; ++j) {
+            double s = 0.0;
+            for (int l = k; l < bs; ++l) s += T[k + (size_t)l * bs] * V1[(size_t)j * BP + l];
+            M[(size_t)k * bs + j] = s;
+        }
+    KT_HIP(hipMemcpyAsync(Md, M.data(), sizeof(double) * M.size(), hipMemcpyHostToDevice, ctx->stream));
+    KT_HIP(launch_ts_formq((int)n, bs, BP, V, Md, W, ld, ctx->stream));
+    KT_HIP(hipStreamSynchronize(ctx->stream));  // M lives on this frame
 }
 
 }  // namespace kt

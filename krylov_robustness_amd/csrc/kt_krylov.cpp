@@ -12,7 +12,10 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 
@@ -23,7 +26,36 @@ namespace kt {
 // ---------------------------------------------------------------------------
 // dense symmetric eig: host tred2/tql2 for small n, rocSOLVER dsyevd above.
 // ---------------------------------------------------------------------------
+struct EigStats {
+    int64_t calls = 0, dev_calls = 0;
+    double ms = 0.0;
+    int maxn = 0;
+    ~EigStats() {
+        if (getenv("KT_EIG_STATS"))
+            fprintf(stderr, "[kt eig] calls %lld (device %lld) max n %d total %.1f ms\n",
+                    (long long)calls, (long long)dev_calls, maxn, ms);
+    }
+};
+static EigStats g_eig;
+
+struct EigTimer {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~EigTimer() {
+        g_eig.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+};
+
+static void sym_eig_dispatch(kt_context_s* ctx, int n, const double* A, double* w, double* V);
+
 static void sym_eig(kt_context_s* ctx, int n, const double* A, double* w, double* V) {
+    EigTimer tm;
+    g_eig.calls++;
+    g_eig.maxn = std::max(g_eig.maxn, n);
+    if (n > 160) g_eig.dev_calls++;
+    sym_eig_dispatch(ctx, n, A, w, V);
+}
+
+static void sym_eig_dispatch(kt_context_s* ctx, int n, const double* A, double* w, double* V) {
     if (n <= 0) return;
     if (n <= 160) {
         sym_eig_host(n, A, w, V);

@@ -41,6 +41,14 @@ hipError_t launch_pairs_orth(int C, int n, int num_cu, const double* prev, const
                              double* W, int ld, double* coef, double* part, double* hr,
                              hipStream_t st);
 size_t pairs_part_doubles(int n, int C, int num_cu);
+// tall-skinny Householder QR (kt_tsqr.hip)
+int ts_nrb(int n, int num_cu);
+hipError_t launch_ts_reflectors(int n, int bs, int BP, double* W, int ld, double* V, double* pivot,
+                                double* sums, double* part, double* taus, int num_cu,
+                                hipStream_t st);
+hipError_t launch_ts_formq(int n, int bs, int BP, const double* V, const double* M, double* W,
+                           int ld, hipStream_t st);
+hipError_t launch_sum_slabs(int count, int S, const double* part, double* G, hipStream_t st);
 // column-batched single-vector Arnoldi (kt_colbatch.hip); V blocks at stride vstride
 int col_nrb(int n, int num_cu);
 hipError_t launch_col_dots(int n, int P, int nb, int64_t vstride, const double* V, const double* W,

@@ -1,0 +1,188 @@
+// kt_tsqr.hip -- Householder thin QR of a tall-skinny row-major n x bs block
+// (bs <= 128), the factorisation MATLAB's qr(w, 0) computes (LAPACK dgeqr2
+// reflectors + dorgqr's Q), for lanczos_krylov.m:90, arnoldi_krylov.m:99 and
+// mc_trace.m's qr(., 0).
+//
+// One launch per column k applies reflector H_k to the trailing columns and,
+// in the same pass, accumulates the sums the NEXT column's reflector needs
+//   sums[j] = W(k+2:n, k+1)' W(k+2:n, j),  j >= k+1
+// (sums[k+1] = ||W(k+2:n, k+1)||^2, dlarfg's xnorm^2; sums[j > k+1] give
+// t_j = v' w_j without another pass).  A one-wave-per-column reduce launch
+// sums the per-workgroup partials in a fixed order and snapshots the next
+// pivot row, so every workgroup of the next step derives identical
+// coefficients.  Q = (I - V T V') E is then formed with the compact-WY
+// factor T (dlarft, host) in one more pass.
+#include <hip/hip_runtime.h>
+
+#include "kt_launch.h"
+
+namespace kt {
+
+constexpr int kTsBlock = 256;
+
+__device__ __forceinline__ void ts_larfg(double alpha, double xx, double& beta, double& tau,
+                                         double& scal) {
+    if (xx == 0.0) {
+        beta = alpha;
+        tau = 0.0;
+        scal = 1.0;
+        return;
+    }
+    beta = -copysign(hypot(alpha, sqrt(xx)), alpha);
+    tau = (beta - alpha) / beta;
+    scal = 1.0 / (alpha - beta);
+}
+
+// Step k (k = -1: prologue, no reflector, only the sums for column 0).
+// Thread (row slot, column c): c = tid % BP.  V (n x BP, pre-zeroed) receives
+// the reflector v_k; W row k column k receives beta_k (R's diagonal).
+__global__ __launch_bounds__(kTsBlock) void k_ts_step(int n, int bs, int BP, int k,
+                                                      double* __restrict__ W, int ld,
+                                                      double* __restrict__ V,
+                                                      const double* __restrict__ pivot,
+                                                      const double* __restrict__ sums,
+                                                      int rows_per_blk, double* __restrict__ part,
+                                                      double* __restrict__ taus) {
+    __shared__ double red[kTsBlock];
+    const int c = threadIdx.x % BP;
+    const int sub = threadIdx.x / BP;
+    const int rpi = kTsBlock / BP;  // rows per block iteration
+    const int kn = k + 1;           // the column whose sums we accumulate
+    double beta = 0.0, tau = 0.0, scal = 1.0, tc = 0.0, tn = 0.0;
+    if (k >= 0) {
+        ts_larfg(pivot[k], sums[k], beta, tau, scal);
+        if (c > k && c < bs) tc = pivot[c] + scal * sums[c];
+        if (kn < bs) tn = pivot[kn] + scal * sums[kn];
+        if (blockIdx.x == 0 && threadIdx.x == 0) taus[k] = tau;
+    }
+    const int r0 = blockIdx.x * rows_per_blk;
+    const int r1 = min(n, r0 + rows_per_blk);
+    const int rstart = max(r0, k < 0 ? 0 : k);
+    double acc = 0.0;
+    // uniform trip count across the workgroup (barrier inside)
+    for (int base = rstart; base < r1; base += rpi) {
+        const int r = base + sub;
+        const bool live = r < r1 && c < bs;
+        double wk = 0.0, wn = 0.0, wc = 0.0;
+        if (live) {
+            if (k >= 0) wk = W[(int64_t)r * ld + k];
+            if (kn < bs) wn = W[(int64_t)r * ld + kn];
+            wc = W[(int64_t)r * ld + c];
+        }
+        __syncthreads();  // every read of this row block before any write
+        if (live) {
+            double v = 0.0;
+            if (k >= 0) {
+                v = (r == k) ? 1.0 : wk * scal;
+                if (c == k) {
+                    V[(int64_t)r * BP + k] = v;
+                    if (r == k) W[(int64_t)r * ld + k] = beta;
+                } else if (c > k) {
+                    wc -= tau * v * tc;
+                    W[(int64_t)r * ld + c] = wc;
+                }
+            }
+            if (kn < bs && c >= kn && r > kn) {
+                const double wn_new = k >= 0 ? wn - tau * v * tn : wn;
+                acc = fma(wn_new, wc, acc);
+            }
+        }
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x < BP && kn < bs) {
+        double s = 0.0;
+        for (int q = 0; q < rpi; ++q) s += red[q * BP + threadIdx.x];
+        part[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+// sums[j] = sum_b part[j][b] for j in [kn, bs); pivot[j] = W(kn, j) for all j
+__global__ __launch_bounds__(256) void k_ts_reduce(int bs, int kn, int nrb,
+                                                   const double* __restrict__ part,
+                                                   const double* __restrict__ W, int ld,
+                                                   double* __restrict__ sums,
+                                                   double* __restrict__ pivot) {
+    const int j = kn + blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x < 64)
+        for (int q = threadIdx.x; q < bs; q += 64) pivot[q] = W[(int64_t)kn * ld + q];
+    if (j >= bs) return;
+    const double* p = part + (int64_t)j * nrb;
+    double s = 0.0;
+    for (int i = lane; i < nrb; i += 64) s += p[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) sums[j] = s;
+}
+
+// W[r][j] = (r == j) - sum_k V[r][k] M[k][j]   (Q = E - V (T V1'))
+__global__ __launch_bounds__(kTsBlock) void k_ts_formq(int n, int bs, int BP,
+                                                       const double* __restrict__ V,
+                                                       const double* __restrict__ M,
+                                                       double* __restrict__ W, int ld) {
+    const int64_t total = (int64_t)n * BP;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int j = (int)(t % BP);
+        const int64_t r = t / BP;
+        if (j >= bs) continue;
+        const double* vr = V + r * BP;
+        const int kmax = r < bs ? (int)r + 1 : bs;  // V is unit lower trapezoidal
+        double s = 0.0;
+        for (int kk = 0; kk < kmax; ++kk) s = fma(vr[kk], M[kk * bs + j], s);
+        W[r * ld + j] = (r == j ? 1.0 : 0.0) - s;
+    }
+}
+
+static int ts_rows_per_blk(int n, int num_cu) {
+    int want = 2 * num_cu;
+    int rpb = (n + want - 1) / want;
+    return rpb < 64 ? 64 : rpb;
+}
+
+int ts_nrb(int n, int num_cu) {
+    const int rpb = ts_rows_per_blk(n, num_cu);
+    return (n + rpb - 1) / rpb;
+}
+
+// Reflector sweep: after it, W's top bs x bs upper triangle is R, V holds the
+// reflectors (unit lower trapezoidal), taus the scalars.
+hipError_t launch_ts_reflectors(int n, int bs, int BP, double* W, int ld, double* V, double* pivot,
+                                double* sums, double* part, double* taus, int num_cu,
+                                hipStream_t st) {
+    const int rpb = ts_rows_per_blk(n, num_cu);
+    const int nrb = (n + rpb - 1) / rpb;
+    for (int k = -1; k < bs; ++k) {
+        k_ts_step<<<nrb, kTsBlock, 0, st>>>(n, bs, BP, k, W, ld, V, pivot, sums, rpb, part, taus);
+        const int kn = k + 1;
+        if (kn < bs)
+            k_ts_reduce<<<(bs - kn + 3) / 4, 256, 0, st>>>(bs, kn, nrb, part, W, ld, sums, pivot);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_ts_formq(int n, int bs, int BP, const double* V, const double* M, double* W,
+                           int ld, hipStream_t st) {
+    int64_t g = ((int64_t)n * BP + kTsBlock - 1) / kTsBlock;
+    if (g > 8192) g = 8192;
+    k_ts_formq<<<(int)g, kTsBlock, 0, st>>>(n, bs, BP, V, M, W, ld);
+    return hipGetLastError();
+}
+
+// G = sum_s part[s] (px*py each), fixed order
+__global__ void k_sum_slabs(int count, int S, const double* __restrict__ part,
+                            double* __restrict__ G) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    double s = 0.0;
+    for (int q = 0; q < S; ++q) s += part[(int64_t)q * count + t];
+    G[t] = s;
+}
+
+hipError_t launch_sum_slabs(int count, int S, const double* part, double* G, hipStream_t st) {
+    k_sum_slabs<<<(count + 255) / 256, 256, 0, st>>>(count, S, part, G);
+    return hipGetLastError();
+}
+
+}  // namespace kt

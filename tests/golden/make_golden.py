@@ -61,7 +61,30 @@ def load_graphs():
     return g
 
 
+def save_csr(path, graphs):
+    arrays = {}
+    for k, A in graphs.items():
+        A = A.tocsr()
+        A.sort_indices()
+        arrays[k + "__indptr"] = A.indptr.astype(np.int64)
+        arrays[k + "__indices"] = A.indices.astype(np.int32)
+        arrays[k + "__data"] = A.data.astype(np.float64)
+        arrays[k + "__n"] = np.array([A.shape[0]], dtype=np.int64)
+    np.savez_compressed(path, **arrays)
+
+
+def main_hawaii():
+    """Config 3's graph: Transport Hawaii, unweighted LCC, in
+    its own file so graphs.npz stays byte-stable."""
+    P = sio.loadmat(os.path.join(REF, "datasets_paper", "Transport", "Hawaii.mat"))["Problem"]
+    A = unweighted(P["A"][0, 0])
+    save_csr(os.path.join(HERE, "hawaii.npz"), {"hawaii": A})
+    print("hawaii", A.shape[0], A.nnz)
+
+
 def main():
+    if "--hawaii" in sys.argv:
+        return main_hawaii()
     graphs = load_graphs()
     arrays = {}
     for k, A in graphs.items():

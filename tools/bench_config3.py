@@ -1,0 +1,106 @@
+"""Config 3 (BASELINE.json configs[2]): Transport Hawaii (largest
+connected component of spones(A + A'), n = 21,774), f = sinh, df = cosh, the
+pipeline of Tests/test_weighted_sinh_lbfgs.m:50-86 and :208 on the device:
+
+  1. tr(sinh(A)) by N = 256 Rademacher probes (SLQ, m = 30), replacing the
+     dense eig normaliser of :50; checked against the exact spectrum value
+  2. Omega: find_top_edges(A, c, 100, 'min'), then the top 30 by
+     dfA = function_multiple_entries(A, E, @cosh, tol_df, 100)      (:64-86)
+  3. [f, gr] = fun_and_grad_krylov_fun(X, A, Omega, @sinh, @cosh, dfA, tol, 100)
+     at a seeded nonzero X (uniform in [-0.5, 1] * A_ij, sum <= 10)   (:208)
+
+Every device stage is timed (best of --repeat) and compared with the numpy
+oracle on the same inputs (CPU time reported beside it).  One JSON line."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch  # noqa: F401  (torch's ROCm runtime first)
+import numpy as np
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import krylov_robustness_amd as kra  # noqa: E402
+from conftest import load_graph, GOLDEN  # noqa: E402
+
+
+def best(fn, repeat):
+    ts, out = [], None
+    for _ in range(repeat):
+        t0 = time.perf_counter()
+        out = fn()
+        ts.append(time.perf_counter() - t0)
+    return out, min(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--repeat", type=int, default=3)
+    ap.add_argument("--probes", type=int, default=256)
+    ap.add_argument("--m", type=int, default=30)
+    ap.add_argument("--no-oracle", action="store_true")
+    a = ap.parse_args()
+    A = load_graph("hawaii")
+    n = A.shape[0]
+    ctx = kra.Context(0)
+    D = kra.DeviceMatrix(A, ctx, check_symmetric=True)
+    out = {"workload": "config3 hawaii-lcc sinh/cosh", "n": n, "nnz": int(A.nnz)}
+
+    nrm, t = best(lambda: kra.normest(D, 1e-2, ctx=ctx), a.repeat)
+    out["normest"] = nrm
+    out["normest_s"] = t
+    # 1. tr(sinh(A)) by SLQ
+    kra.slq_quadforms(D, 16, a.m, seed=3, fun="sinh", ctx=ctx)
+    (tr, qdev), t = best(lambda: kra.slq_trace(D, a.probes, a.m, seed=3, fun="sinh", ctx=ctx), a.repeat)
+    out.update({"tr_sinh_slq": tr, "tr_sinh_slq_s": t, "probes": a.probes, "lanczos_m": a.m})
+    vp = os.path.join(GOLDEN, "hawaii_values.json")
+    if os.path.exists(vp):
+        ex = json.load(open(vp))["exact_tr_sinh"]
+        out["tr_sinh_exact"] = ex
+        out["tr_sinh_rel_err"] = abs(tr - ex) / abs(ex)
+    # 2. Omega from centrality + function_multiple_entries(cosh)
+    c = kra.compute_centrality(A)
+    E = kra.find_top_edges(A, c, 100, "min")
+    tol_df = 1e-6 * np.cosh(nrm)
+    (temp, fit), t = best(lambda: kra.function_multiple_entries(D, E, "cosh", tol_df, 100, ctx=ctx),
+                          a.repeat)
+    out.update({"fme_entries": len(E), "fme_iter": fit, "fme_s": t})
+    ind = np.argsort(-temp, kind="stable")[:30]
+    Om = E[ind]
+    dfA = temp[ind]
+    # 3. objective + gradient at a seeded nonzero X
+    rng = np.random.default_rng(11)
+    w = np.array([A[i - 1, j - 1] for i, j in Om])
+    X = rng.uniform(-0.5, 1.0, size=30) * w
+    if X.sum() > 10:
+        X *= 10 / X.sum()
+    tol = 1e-6 * np.sinh(nrm)
+    (f, gr), t = best(lambda: kra.fun_and_grad_krylov_fun(X, D, Om, "sinh", "cosh", dfA, tol, 100,
+                                                          ctx=ctx), a.repeat)
+    out.update({"fg_f": f, "fg_gr_norm": float(np.linalg.norm(gr)), "fg_s": t})
+    out["device_pipeline_s"] = out["normest_s"] + out["tr_sinh_slq_s"] + out["fme_s"] + out["fg_s"]
+    if not a.no_oracle:
+        from oracle import krylov_oracle as ko
+        t0 = time.perf_counter()
+        To, fo_it = ko.function_multiple_entries(A, E, "cosh", tol_df, 100)
+        out["oracle_fme_s"] = time.perf_counter() - t0
+        out["fme_max_rel_diff"] = float(np.abs(To - temp).max() / np.abs(To).max())
+        out["fme_iter_oracle"] = fo_it
+        t0 = time.perf_counter()
+        fo, gro = ko.fun_and_grad_krylov_fun(X, A, Om, "sinh", "cosh", dfA, tol, 100)
+        out["oracle_fg_s"] = time.perf_counter() - t0
+        out["fg_f_rel_diff"] = abs(fo - f) / abs(fo)
+        out["fg_gr_rel_diff"] = float(np.abs(gro - gr).max() / np.abs(gro).max())
+        t0 = time.perf_counter()
+        _, qo = ko.slq_trace(A, 32, a.m, seed=3, fun="sinh")
+        out["oracle_slq_32probes_s"] = time.perf_counter() - t0
+        out["slq_q_max_rel_diff"] = float(np.abs(qo - qdev[:32]).max() / np.abs(qo).max())
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
