@@ -152,6 +152,13 @@ int kt_expmv(kt_matrix_t A, double t, int64_t ncols, const double* B, double* F,
  * Afun handle).  X, Y: n x ncols column-major, ncols <= 128. */
 int kt_lanczos_fmv(kt_matrix_t A, int fun, int m, int64_t ncols, const double* X, double* Y);
 
+/* [Q, R] = qr(W, 0) on the device (MATLAB's economy Householder QR: LAPACK
+ * reflector signs, tau = 0 completions of exactly dependent columns), the
+ * factorisation lanczos_krylov.m:90, arnoldi_krylov.m:99 and mc_trace.m use.
+ * W, Q: n x bs column-major, R: bs x bs column-major, 1 <= bs <= 128. */
+int kt_householder_qr(kt_context_t ctx, int64_t n, int64_t bs, const double* W, double* Q,
+                      double* R);
+
 /* ---- greedy edge selection (krylov_miobi.m / greedy_krylov.m) ---------- */
 
 /* Batched trace_fun_update over candidate edges, the inner loop of

@@ -369,3 +369,14 @@ def function_multiple_entries(A, omega, f="exp", tol=1e-12, it=None, poles=np.in
         oj.ctypes.data_as(C.POINTER(C.c_int64)), _fun_code(f), float(tol), int(it or 0),
         _dptr(X), C.byref(itr)))
     return X, int(itr.value)
+
+
+def householder_qr(W, ctx: Optional[Context] = None):
+    """[Q, R] = qr(W, 0) on the device (kt_householder_qr)."""
+    ctx = ctx or default_context()
+    W = np.asfortranarray(np.asarray(W, dtype=np.float64))
+    n, bs = W.shape
+    Q = np.zeros((n, bs), order="F")
+    R = np.zeros((bs, bs), order="F")
+    _lib.check(_lib.load().kt_householder_qr(ctx.handle, n, bs, _dptr(W), _dptr(Q), _dptr(R)))
+    return Q, R

@@ -655,6 +655,28 @@ using namespace kt;
 
 extern "C" {
 
+int kt_householder_qr(kt_context_t ctx, int64_t n, int64_t bs, const double* W, double* Q,
+                      double* R) {
+    KT_TRY
+    if (!ctx || !W || !Q || !R) fail(KT_ERR_ARG, "NULL argument");
+    if (bs < 1 || bs > 128 || n < bs) fail(KT_ERR_UNSUPPORTED, "need 1 <= bs <= 128 and n >= bs");
+    KT_HIP(hipSetDevice(ctx->device));
+    DevBuf d;
+    d.ensure(sizeof(double) * (size_t)n * bs);
+    std::vector<double> rm((size_t)n * bs);
+    for (int64_t c = 0; c < bs; ++c)
+        for (int64_t i = 0; i < n; ++i) rm[(size_t)i * bs + c] = W[i + (size_t)c * n];
+    KT_HIP(hipMemcpyAsync(d.ptr, rm.data(), sizeof(double) * rm.size(), hipMemcpyHostToDevice, ctx->stream));
+    std::vector<double> Rv;
+    householder_qr(ctx, n, d.as<double>(), (int)bs, (int)bs, Rv);
+    KT_HIP(hipMemcpyAsync(rm.data(), d.ptr, sizeof(double) * rm.size(), hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipStreamSynchronize(ctx->stream));
+    for (int64_t c = 0; c < bs; ++c)
+        for (int64_t i = 0; i < n; ++i) Q[i + (size_t)c * n] = rm[(size_t)i * bs + c];
+    std::copy(Rv.begin(), Rv.end(), R);
+    KT_CATCH
+}
+
 int kt_normest(kt_matrix_t A, double tol, double* nrm) {
     KT_TRY
     if (!A || !nrm) fail(KT_ERR_ARG, "NULL argument");
