@@ -7,6 +7,8 @@
 //   mex -R2018a -DKT_ENTRY_FUN_UPDATE       kt_mex.cpp ... -output fun_update
 //   mex -R2018a -DKT_ENTRY_FG_EXP           kt_mex.cpp ... -output fun_and_grad_krylov_exp
 //   mex -R2018a -DKT_ENTRY_FG_FUN           kt_mex.cpp ... -output fun_and_grad_krylov_fun
+//   mex -R2018a -DKT_ENTRY_KRYLOV_MIOBI     kt_mex.cpp ... -output krylov_miobi
+//   mex -R2018a -DKT_ENTRY_FME              kt_mex.cpp ... -output function_multiple_entries
 //
 // Placed in the reference's functions/ directory, each MEX shadows the .m of
 // the same name (MATLAB's same-folder precedence), so Tests/*.m, greedy_krylov.m
@@ -119,6 +121,43 @@ int fun_arg(const mxArray* h, int dflt) {
 
 mxArray* scalar(double v) { return mxCreateDoubleScalar(v); }
 
+// k x 2 MATLAB index matrix (1-based doubles) -> 0-based columns
+void pairs_arg(const mxArray* E, std::vector<int64_t>& a, std::vector<int64_t>& b) {
+    const mwSize k = mxGetM(E);
+    if (k > 0 && mxGetN(E) != 2) mexErrMsgIdAndTxt("krylov_hip:E", "index list must be k x 2");
+    const double* p = mxGetDoubles(E);
+    a.resize(k);
+    b.resize(k);
+    for (mwSize h = 0; h < k; ++h) {
+        a[h] = (int64_t)p[h] - 1;
+        b[h] = (int64_t)p[h + k] - 1;
+    }
+}
+
+// the (edited) device matrix back as MATLAB sparse; refreshes the cache key
+mxArray* export_sparse(kt_matrix_t A) {
+    int64_t n = 0, nnz = 0;
+    check(kt_matrix_info(A, &n, &nnz), "export");
+    std::vector<int64_t> jc(n + 1), ir(nnz);
+    std::vector<double> pr(nnz);
+    check(kt_matrix_export_csc(A, jc.data(), ir.data(), pr.data()), "export");
+    mxArray* S = mxCreateSparse((mwSize)n, (mwSize)n, (mwSize)(nnz > 0 ? nnz : 1), mxREAL);
+    mwIndex* J = mxGetJc(S);
+    mwIndex* I = mxGetIr(S);
+    double* P = mxGetDoubles(S);
+    for (int64_t j = 0; j <= n; ++j) J[j] = (mwIndex)jc[j];
+    for (int64_t t = 0; t < nnz; ++t) {
+        I[t] = (mwIndex)ir[t];
+        P[t] = pr[t];
+    }
+    if (A == g_A) {
+        g_jc.swap(jc);
+        g_ir.swap(ir);
+        g_pr.swap(pr);
+    }
+    return S;
+}
+
 }  // namespace
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
@@ -208,6 +247,66 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
           "fun_and_grad_krylov_fun");
     plhs[0] = scalar(f);
     if (nlhs > 1) plhs[1] = gr; else mxDestroyArray(gr);
+#elif defined(KT_ENTRY_KRYLOV_MIOBI)
+    // [edges, rob, A_new] = krylov_miobi(A, k, E, tol, it, poles, debug, miobi, rescale)
+    //                                                                krylov_miobi.m:1
+    if (nrhs < 2) mexErrMsgIdAndTxt("krylov_hip:nargin", "krylov_miobi(A, k, E, ...)");
+    kt_matrix_t A = matrix_arg(prhs[0]);
+    const int k = (int)mxGetScalar(prhs[1]);
+    std::vector<int64_t> ei, ej;
+    if (nrhs > 2 && !mxIsEmpty(prhs[2])) {
+        pairs_arg(prhs[2], ei, ej);
+    } else {  // :42-46 all edges with E(:,1) >= E(:,2), in find() order
+        int64_t n = 0, nnz = 0;
+        check(kt_matrix_info(A, &n, &nnz), "krylov_miobi");
+        std::vector<int64_t> jc(n + 1), ir(nnz);
+        check(kt_matrix_export_csc(A, jc.data(), ir.data(), nullptr), "krylov_miobi");
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t t = jc[j]; t < jc[j + 1]; ++t)
+                if (ir[t] >= j) {
+                    ei.push_back(ir[t]);
+                    ej.push_back(j);
+                }
+    }
+    char mode[16] = "break";
+    if (nrhs > 7 && !mxIsEmpty(prhs[7])) mxGetString(prhs[7], mode, sizeof(mode));
+    int make = 0;
+    if (strcmp(mode, "make") == 0) make = 1;
+    else if (strcmp(mode, "break") != 0)
+        mexErrMsgIdAndTxt("krylov_hip:miobi", "KRYLOV_MIOBI:: not supported option for miobi");
+    const int64_t cap = (int64_t)ei.size() < k ? (int64_t)ei.size() : k;
+    std::vector<int64_t> si(cap > 0 ? cap : 1), sj(cap > 0 ? cap : 1);
+    double rob = 0.0;
+    int64_t ns = 0;
+    check(kt_krylov_miobi(A, k, (int64_t)ei.size(), ei.data(), ej.data(), scalar_or(nrhs, prhs, 3, 1e-12),
+                          (int)scalar_or(nrhs, prhs, 4, 0), make, scalar_or(nrhs, prhs, 8, 1.0), si.data(),
+                          sj.data(), &rob, &ns),
+          "krylov_miobi");
+    plhs[0] = mxCreateDoubleMatrix((mwSize)ns, 2, mxREAL);
+    double* e = mxGetDoubles(plhs[0]);
+    for (int64_t h = 0; h < ns; ++h) {
+        e[h] = (double)(si[h] + 1);
+        e[h + ns] = (double)(sj[h] + 1);
+    }
+    if (nlhs > 1) plhs[1] = scalar(rob);
+    if (nlhs > 2) plhs[2] = export_sparse(A);
+#elif defined(KT_ENTRY_FME)
+    // [X, iter] = function_multiple_entries(A, omega, f, tol, it, poles, debug)
+    //                                                    function_multiple_entries.m:1
+    if (nrhs < 3) mexErrMsgIdAndTxt("krylov_hip:nargin", "function_multiple_entries(A, omega, f, ...)");
+    if (nrhs > 5 && !mxIsEmpty(prhs[5]) && !(mxGetM(prhs[5]) * mxGetN(prhs[5]) == 1 &&
+                                             mxGetScalar(prhs[5]) == mxGetInf()))
+        mexErrMsgIdAndTxt("krylov_hip:poles", "FUNCTION_MULTIPLE_ENTRIES::Unsupported rational Krylov yet");
+    std::vector<int64_t> oi, oj;
+    pairs_arg(prhs[1], oi, oj);
+    mxArray* X = mxCreateDoubleMatrix((mwSize)oi.size(), 1, mxREAL);
+    int iter = 0;
+    check(kt_function_multiple_entries(matrix_arg(prhs[0]), (int64_t)oi.size(), oi.data(), oj.data(),
+                                       fun_arg(prhs[2], KT_FUN_EXP), scalar_or(nrhs, prhs, 3, 1e-12),
+                                       (int)scalar_or(nrhs, prhs, 4, 0), mxGetDoubles(X), &iter),
+          "function_multiple_entries");
+    plhs[0] = X;
+    if (nlhs > 1) plhs[1] = scalar(iter);
 #else
 #error "define one KT_ENTRY_* (see the header of this file)"
 #endif

@@ -21,6 +21,8 @@ double mxGetScalar(const mxArray*);
 int mxGetString(const mxArray*, char*, mwSize);
 mxArray* mxCreateDoubleMatrix(mwSize, mwSize, mxComplexity);
 mxArray* mxCreateDoubleScalar(double);
+mxArray* mxCreateSparse(mwSize, mwSize, mwSize, mxComplexity);
+double mxGetInf(void);
 void mxDestroyArray(mxArray*);
 int mexCallMATLAB(int, mxArray**, int, mxArray**, const char*);
 void mexErrMsgIdAndTxt(const char*, const char*, ...);

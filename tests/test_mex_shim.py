@@ -10,7 +10,8 @@ import pytest
 
 from conftest import ROOT
 
-ENTRIES = ["TRACE_EXP", "MC_TRACE", "TRACE_FUN_UPDATE", "FUN_UPDATE", "FG_EXP", "FG_FUN"]
+ENTRIES = ["TRACE_EXP", "MC_TRACE", "TRACE_FUN_UPDATE", "FUN_UPDATE", "FG_EXP", "FG_FUN",
+           "KRYLOV_MIOBI", "FME"]
 
 
 @pytest.mark.parametrize("entry", ENTRIES)
