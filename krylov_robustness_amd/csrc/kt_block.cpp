@@ -109,7 +109,7 @@ void spmm(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols
     const int grid = spmm_grid(n, P, ctx->num_cu * 4);
     const DevCSR& M = natural_csr(A);  // block paths run in the reference's row order
     const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
-    KT_HIP(launch_spmm_block(P, A->unit_values ? 2 : 0, grid + lblocks, M.rowptr, M.col, M.val, n,
+    KT_HIP(launch_spmm_block(P, (A->unit_values ? 2 : 0) | (ctx->k1_flags & 4), grid + lblocks, M.rowptr, M.col, M.val, n,
                              X, ldx, Y, ldy, M.long_rows, M.n_long, A->long_thresh, lblocks,
                              ctx->stream));
 }

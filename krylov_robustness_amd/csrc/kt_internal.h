@@ -89,8 +89,14 @@ struct ProfSlot {
 
 enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_NSLOTS = 2 };
 
-struct Workspace {
+// Buffers of one probe-sweep lane (kt_slq.cpp); two lanes let two sweeps
+// run on two streams.
+struct SweepBufs {
     DevBuf X0, X1, Y, partial, coef, scales, k2s, trec;
+};
+
+struct Workspace {
+    SweepBufs sweep[4];
     DevBuf small, small2, qrtmp, eigA, eigW, eigInfo;  // block-Krylov scratch
     DevBuf hist, norm_part;                             // sweep scale history, inf-norm partials
     PinnedBuf host_trec;
@@ -106,6 +112,7 @@ struct Workspace {
 struct kt_context_s {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};  // extra probe-sweep lanes (lazy)
     int num_cu = 256;
     bool profile = false;
     int k1_flags = 0;  // KT_K1_FLAGS: bit 0 = non-temporal stream hints in K1
@@ -158,8 +165,8 @@ void refresh_device(kt_matrix_s* A);
 const DevCSR& hub_csr(kt_matrix_s* A);
 
 // profiling helpers (no-ops unless ctx->profile)
-void prof_begin(kt_context_s* ctx, int slot);
-void prof_end(kt_context_s* ctx, int slot);
+void prof_begin(kt_context_s* ctx, int slot, hipStream_t st = nullptr);
+void prof_end(kt_context_s* ctx, int slot, hipStream_t st = nullptr);
 void prof_collect(kt_context_s* ctx);  // after stream sync: fold events into totals
 
 // dense host helpers (kt_dense.cpp)

@@ -55,7 +55,10 @@ template <int P> struct Geo {
 // FLAGS bit 1: unit-weight adjacency (every stored value is 1.0, detected at
 // matrix creation): the values array is never read (4 B per nonzero instead
 // of 12).
-enum : int { KF_NT = 1, KF_UNIT = 2 };
+// FLAGS bit 2: deep gather issue -- up to 8 column indices, then up to 8 row
+// gathers in flight per row group per round trip (predicated tails, no
+// serial remainder loop), for graphs whose rows are mostly short.
+enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4 };
 
 template <int VEC> struct VecT;
 template <> struct VecT<1> {
@@ -164,6 +167,51 @@ __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
     }
 }
 
+// Same sum as row_gather, issued 8 deep: the 8 column indices of a chunk are
+// loaded together, then the 8 row gathers (a tail entry re-reads the chunk's
+// first row with weight 0, so no lane branches), then the 8 FMAs.
+template <int P, int FLAGS>
+__device__ __forceinline__ void row_gather8(int k0, int end, int stride, int p0,
+                                            const int* __restrict__ col,
+                                            const double* __restrict__ val,
+                                            const double* __restrict__ ucur, double* s,
+                                            int ld = P) {
+    using G = Geo<P>;
+    using V = VecT<G::VEC>;
+    for (int k = k0; k < end; k += 8 * stride) {
+        int c[8];
+        double a[8];
+        const int c0 = ld_stream<FLAGS>(col + k);
+        c[0] = c0;
+        a[0] = (FLAGS & KF_UNIT) ? 1.0 : ld_stream<FLAGS>(val + k);
+#pragma unroll
+        for (int i = 1; i < 8; ++i) {
+            const int idx = k + i * stride;
+            const bool ok = idx < end;
+            c[i] = ok ? ld_stream<FLAGS>(col + idx) : c0;
+            if constexpr (FLAGS & KF_UNIT) a[i] = ok ? 1.0 : 0.0;
+            else a[i] = ok ? ld_stream<FLAGS>(val + idx) : 0.0;
+        }
+        typename V::T x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = V::load(ucur + (int64_t)c[i] * ld + p0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) s[e] = fma(a[i], V::get(x[i], e), s[e]);
+    }
+}
+
+template <int P, int FLAGS>
+__device__ __forceinline__ void gather_row(int k0, int end, int stride, int p0,
+                                           const int* __restrict__ col,
+                                           const double* __restrict__ val,
+                                           const double* __restrict__ ucur, double* s,
+                                           int ld = P) {
+    if constexpr (FLAGS & KF_MLP) row_gather8<P, FLAGS>(k0, end, stride, p0, col, val, ucur, s, ld);
+    else row_gather<P, FLAGS>(k0, end, stride, p0, col, val, ucur, s, ld);
+}
+
 // y_r = s_cur * sum; accumulate v_cur . y.
 template <int P, int FLAGS>
 __device__ __forceinline__ void row_epilogue(int row, int p0, const double* s, const double* sc,
@@ -220,7 +268,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            row_gather<P, FLAGS>(beg + grp, end, G::GPW, p0, col, val, ucur, s);
+            gather_row<P, FLAGS>(beg + grp, end, G::GPW, p0, col, val, ucur, s);
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
@@ -237,7 +285,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            row_gather<P, FLAGS>(beg, end, 1, p0, col, val, ucur, s);
+            gather_row<P, FLAGS>(beg, end, 1, p0, col, val, ucur, s);
             row_epilogue<P, FLAGS>(row, p0, s, sc, ucur, y, acc);
         }
     }
@@ -285,7 +333,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_block(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            row_gather<P, FLAGS>(row_ptr[row] + grp, row_ptr[row + 1], G::GPW, p0, col, val, X, s,
+            gather_row<P, FLAGS>(row_ptr[row] + grp, row_ptr[row + 1], G::GPW, p0, col, val, X, s,
                                  ldx);
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
@@ -308,7 +356,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_block(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            row_gather<P, FLAGS>(beg, end, 1, p0, col, val, X, s, ldx);
+            gather_row<P, FLAGS>(beg, end, 1, p0, col, val, X, s, ldx);
             typename V::T yo;
             double* yp = reinterpret_cast<double*>(&yo);
 #pragma unroll
@@ -594,11 +642,15 @@ hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int*
 #define KT_K1(F)                                                                              \
     k_spmm_dot<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, ucur, sc, y, partial,      \
                                                        long_rows, n_long, long_thresh, long_blocks)
-        switch (flags & 3) {
+        switch (flags & 7) {
         case 0: KT_K1(0); break;
         case KF_NT: KT_K1(KF_NT); break;
         case KF_UNIT: KT_K1(KF_UNIT); break;
-        default: KT_K1(KF_NT | KF_UNIT); break;
+        case KF_NT | KF_UNIT: KT_K1(KF_NT | KF_UNIT); break;
+        case KF_MLP: KT_K1(KF_MLP); break;
+        case KF_MLP | KF_NT: KT_K1(KF_MLP | KF_NT); break;
+        case KF_MLP | KF_UNIT: KT_K1(KF_MLP | KF_UNIT); break;
+        default: KT_K1(KF_MLP | KF_NT | KF_UNIT); break;
         }
 #undef KT_K1
     });
@@ -610,12 +662,16 @@ hipError_t launch_spmm_block(int P, int flags, int grid, const int* rp, const in
                              hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
-        if (flags & KF_UNIT)
-            k_spmm_block<PP, kBlock, KF_UNIT><<<grid, kBlock, 0, st>>>(
-                rp, ci, va, n, X, ldx, Y, ldy, long_rows, n_long, long_thresh, long_blocks);
-        else
-            k_spmm_block<PP, kBlock, 0><<<grid, kBlock, 0, st>>>(
-                rp, ci, va, n, X, ldx, Y, ldy, long_rows, n_long, long_thresh, long_blocks);
+#define KT_SB(F)                                                                      \
+    k_spmm_block<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, X, ldx, Y, ldy,    \
+                                                         long_rows, n_long, long_thresh, long_blocks)
+        switch (flags & (KF_UNIT | KF_MLP)) {
+        case 0: KT_SB(0); break;
+        case KF_UNIT: KT_SB(KF_UNIT); break;
+        case KF_MLP: KT_SB(KF_MLP); break;
+        default: KT_SB(KF_UNIT | KF_MLP); break;
+        }
+#undef KT_SB
     });
 }
 

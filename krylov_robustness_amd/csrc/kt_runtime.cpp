@@ -17,7 +17,7 @@ static thread_local std::string g_last_error;
 
 void set_error(const std::string& msg) { g_last_error = msg; }
 
-void prof_begin(kt_context_s* ctx, int slot) {
+void prof_begin(kt_context_s* ctx, int slot, hipStream_t st) {
     if (!ctx->profile) return;
     ProfSlot& s = ctx->prof[slot];
     if (s.used + 2 > s.ev.size()) {
@@ -27,13 +27,13 @@ void prof_begin(kt_context_s* ctx, int slot) {
             s.ev.push_back(e);
         }
     }
-    KT_HIP(hipEventRecord(s.ev[s.used], ctx->stream));
+    KT_HIP(hipEventRecord(s.ev[s.used], st ? st : ctx->stream));
 }
 
-void prof_end(kt_context_s* ctx, int slot) {
+void prof_end(kt_context_s* ctx, int slot, hipStream_t st) {
     if (!ctx->profile) return;
     ProfSlot& s = ctx->prof[slot];
-    KT_HIP(hipEventRecord(s.ev[s.used + 1], ctx->stream));
+    KT_HIP(hipEventRecord(s.ev[s.used + 1], st ? st : ctx->stream));
     s.used += 2;
 }
 
@@ -209,13 +209,20 @@ int kt_context_destroy(kt_context_t ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& s : ctx->prof)
         for (auto e : s.ev) (void)hipEventDestroy(e);
+    for (auto a : ctx->aux_stream)
+        if (a) (void)hipStreamSynchronize(a);
     Workspace& w = ctx->ws;
-    w.X0.release(); w.X1.release(); w.Y.release(); w.partial.release();
-    w.coef.release(); w.scales.release(); w.k2s.release();
+    for (auto& b : w.sweep) {
+        b.X0.release(); b.X1.release(); b.Y.release(); b.partial.release();
+        b.coef.release(); b.scales.release(); b.k2s.release(); b.trec.release();
+    }
     w.small.release(); w.small2.release(); w.qrtmp.release();
     w.eigA.release(); w.eigW.release(); w.eigInfo.release();
     w.hist.release(); w.norm_part.release();
-    if (ctx->blas) rocblas_destroy_handle(static_cast<rocblas_handle>(ctx->blas)); w.trec.release(); w.host_trec.release();
+    if (ctx->blas) rocblas_destroy_handle(static_cast<rocblas_handle>(ctx->blas));
+    w.host_trec.release();
+    for (auto a : ctx->aux_stream)
+        if (a) (void)hipStreamDestroy(a);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     KT_GUARD_END

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <thread>
 
 #include "kt_launch.h"
@@ -36,14 +37,17 @@ int slq_auto_block(int64_t n, int64_t nprobes) {
 // columns, original-column norms^2 in norms2) is copied into the sweep block.
 void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base,
                    const double* x, int ldx, int ncols, const double* norms2, double* rec_host,
-                   DevMat* basis, std::vector<double>* scale_hist) {
+                   DevMat* basis, std::vector<double>* scale_hist, int lane) {
     kt_context_s* ctx = A->ctx;
     const int n = (int)A->n;
-    hipStream_t st = ctx->stream;
+    if (lane < 0 || lane > 3) fail(KT_ERR_ARG, "sweep lane out of range");
+    if (lane && !ctx->aux_stream[lane - 1])
+        KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[lane - 1], hipStreamNonBlocking));
+    hipStream_t st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
     const int grid = spmm_grid(n, P, ctx->num_cu * 4);  // K2 / short rows
     const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
     const int grid1 = grid + lblocks;                    // K1 total
-    Workspace& w = ctx->ws;
+    SweepBufs& w = ctx->ws.sweep[lane];
     const size_t blk_bytes = sizeof(double) * (size_t)n * P;
     w.X0.ensure(blk_bytes);
     w.X1.ensure(blk_bytes);
@@ -86,7 +90,7 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
     if (scale_hist) scale_hist->assign((size_t)m * P, 0.0);
     DevBuf* hist_dev = nullptr;
     if (scale_hist) {
-        hist_dev = &w.hist;
+        hist_dev = &ctx->ws.hist;
         hist_dev->ensure(sizeof(double) * (size_t)m * P);
     }
     for (int j = 0; j < m; ++j) {
@@ -98,17 +102,17 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
             KT_HIP(hipMemcpyAsync(hist_dev->as<double>() + (size_t)j * P, sc, sizeof(double) * P,
                                   hipMemcpyDeviceToDevice, st));
         }
-        prof_begin(ctx, PROF_SPMM);
+        prof_begin(ctx, PROF_SPMM, st);
         KT_HIP(launch_spmm_dot(P, ctx->k1_flags | (A->unit_values ? 2 : 0), grid1, M.rowptr, M.col,
                                M.val, n, ucur, sc, w.Y.as<double>(), part1, M.long_rows, M.n_long,
                                A->long_thresh, lblocks, st));
-        prof_end(ctx, PROF_SPMM);
+        prof_end(ctx, PROF_SPMM, st);
         KT_HIP(launch_coef_cgs2(P, part1, grid1, first, k2s, sc, sp, coef,
                                 trec + (size_t)(0 * m + j) * P, trec + (size_t)(1 * m + j) * P, st));
-        prof_begin(ctx, PROF_UPDATE);
+        prof_begin(ctx, PROF_UPDATE, st);
         KT_HIP(launch_update(P, grid, n, w.Y.as<double>(), uprev, ucur, sc, sp, coef, first, part2,
                              st));
-        prof_end(ctx, PROF_UPDATE);
+        prof_end(ctx, PROF_UPDATE, st);
         KT_HIP(launch_norm(P, part2, grid, k2s, sn, trec + (size_t)(2 * m + j) * P, st));
         std::swap(ucur, uprev);  // uprev now holds u_{j+1}
         double* t = sp;
@@ -241,10 +245,18 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         Workspace& w = ctx->ws;
         w.host_trec.ensure(sizeof(double) * rec * nsweeps);
         double* htrec = w.host_trec.as<double>();
+        // KT_SLQ_LANES=L (<= 4): sweeps round-robin over L streams, so one
+        // sweep's streaming K2 and small launches overlap another sweep's
+        // gather-bound K1
+        const char* le = getenv("KT_SLQ_LANES");
+        const int lanes_env = le ? std::max(1, std::min(4, atoi(le))) : 3;  // measured best: 3
+        const int lanes = (int)std::min<int64_t>(nsweeps, lanes_env);
+        const DevCSR& H = hub_csr(A);
         for (int64_t s = 0; s < nsweeps; ++s)
-            lanczos_sweep(A, hub_csr(A), P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr, htrec + rec * s,
-                          nullptr, nullptr);
+            lanczos_sweep(A, H, P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr, htrec + rec * s,
+                          nullptr, nullptr, (int)(s % lanes));
         KT_HIP(hipStreamSynchronize(ctx->stream));
+        for (int l = 1; l < lanes; ++l) KT_HIP(hipStreamSynchronize(ctx->aux_stream[l - 1]));
         prof_collect(ctx);
 
         std::vector<double> qv((size_t)nprobes);

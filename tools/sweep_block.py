@@ -27,7 +27,8 @@ def main():
     n, nnz = A.shape[0], A.nnz
     for var in a.variants.split(","):
       os.environ["KT_RELABEL"] = "0" if var == "natural" else "1"
-      os.environ["KT_K1_FLAGS"] = "1" if var == "nt" else "0"
+      os.environ["KT_K1_FLAGS"] = {"nt": "1", "mlp": "4", "mlpnt": "5"}.get(var, "0")
+      os.environ["KT_SLQ_LANES"] = var[5:] if var.startswith("lanes") else "1"
       os.environ["KT_UNIT"] = "0" if var == "valued" else "1"
       ctx = kra.Context(0)
       D = kra.DeviceMatrix(A, ctx)
