@@ -159,6 +159,13 @@ int kt_lanczos_fmv(kt_matrix_t A, int fun, int m, int64_t ncols, const double* X
 int kt_householder_qr(kt_context_t ctx, int64_t n, int64_t bs, const double* W, double* Q,
                       double* R);
 
+/* Host symmetric eigensolver used for the small projected matrices (the
+ * m x m / 2j x 2j eig of trace_fun_update.m:83-84, lanczos quadrature):
+ * Householder tridiagonalisation + implicit QL.  A: n x n column-major
+ * (symmetric), w: n eigenvalues (unsorted), V: n x n eigenvectors or NULL.
+ * Pure host code (no device needed). */
+int kt_host_sym_eig(int n, const double* A, double* w, double* V);
+
 /* ---- greedy edge selection (krylov_miobi.m / greedy_krylov.m) ---------- */
 
 /* Batched trace_fun_update over candidate edges, the inner loop of

@@ -129,7 +129,7 @@ void tri_upper_inv(const double* R, int n, double* X) {
 // the accumulated orthogonal transform in Z (if want_vectors), followed by
 // implicit-shift QL.  On exit: w ascending eigenvalues, Z (col-major) the
 // eigenvectors.  Classic tred2/tql2 structure, written for column-major.
-static void tred2(int n, double* a /* in: sym, out: Q */, double* d, double* e) {
+static void tred2(int n, double* a /* in: sym, out: Q */, double* d, double* e, bool vecs) {
     for (int i = n - 1; i > 0; --i) {
         const int l = i - 1;
         double h = 0.0, scale = 0.0;
@@ -170,6 +170,10 @@ static void tred2(int n, double* a /* in: sym, out: Q */, double* d, double* e) 
     }
     d[0] = 0.0;
     e[0] = 0.0;
+    if (!vecs) {  // eigenvalues only: no accumulation of the transformations
+        for (int i = 0; i < n; ++i) d[i] = a[i + i * n];
+        return;
+    }
     for (int i = 0; i < n; ++i) {
         const int l = i - 1;
         if (d[i] != 0.0) {
@@ -250,7 +254,7 @@ static void tql2(int n, double* d, double* e, double* z /* nullable */) {
 void sym_eig_host(int n, const double* A, double* w, double* V /* nullable */) {
     if (n <= 0) return;
     std::vector<double> a(A, A + (size_t)n * n), e(n);
-    tred2(n, a.data(), w, e.data());
+    tred2(n, a.data(), w, e.data(), V != nullptr);
     tql2(n, w, e.data(), V ? a.data() : nullptr);
     if (V) std::copy(a.begin(), a.end(), V);
 }
@@ -272,3 +276,12 @@ void sym_fun_from_eig(int n, const double* w, const double* V, int fun, double* 
 }
 
 }  // namespace kt
+
+extern "C" int kt_host_sym_eig(int n, const double* A, double* w, double* V) {
+    if (n < 0 || (n > 0 && (!A || !w))) {
+        kt::set_error("kt_host_sym_eig: bad argument");
+        return KT_ERR_ARG;
+    }
+    kt::sym_eig_host(n, A, w, V);
+    return KT_OK;
+}
