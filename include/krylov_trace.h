@@ -209,6 +209,24 @@ int kt_matrix_export_csc(kt_matrix_t A, int64_t* colptr, int64_t* rowind, double
 int kt_function_multiple_entries(kt_matrix_t A, int64_t k, const int64_t* oi, const int64_t* oj,
                                  int fun, double tol, int it, double* X, int* iter);
 
+/* ---- Frechet derivatives and Hessians (multiple_frechet_eval.m,
+ *      hessianfcn_exp.m, hessianfcn_fun.m) ----------------------------- */
+
+/* out[h + t * k] = Df(A)(e_oi[h] e_oj[h]')(ti[t], tj[t]) for h < k, t < ntarget
+ * (0-based), i.e. the reference's Um{row(i)}(ti, :) * Xm{h} * Vm{col(j)}(tj, :)'
+ * from multiple_frechet_eval.m:1 (poles = inf, same tol / it / lag-3 stop).
+ * A must be symmetric (the Hessians' A + XX + XX' are).  iter nullable. */
+int kt_frechet_entries(kt_matrix_t A, int64_t k, const int64_t* oi, const int64_t* oj, int fun,
+                       double tol, int it, int64_t ntarget, const int64_t* ti, const int64_t* tj,
+                       double* out, int* iter);
+
+/* Hes = hessianfcn_exp(X, A, Omega, tol, it) (fun = KT_FUN_EXP) or
+ * hessianfcn_fun(X, A, Omega, f, tol, it): Omega nomega x 2 column-major,
+ * 1-based (MATLAB doubles), X nomega, Hes nomega x nomega column-major.
+ * Replaces hessianfcn_exp.m:1 / hessianfcn_fun.m:1 (fmincon HessianFcn). */
+int kt_hessianfcn(kt_matrix_t A, int64_t nomega, const double* X, const double* Omega, int fun,
+                  double tol, int it, double* Hes);
+
 /* Per-kernel timing (HIP events recorded on the library's stream around each
  * launch of the named kernel while enabled).  kernel: 0 = spmm_gram (K1),
  * 1 = update_norm (K2).  Returns launch count and summed milliseconds. */

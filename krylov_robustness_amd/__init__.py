@@ -9,7 +9,8 @@ interface used by tests and bench.py.
 """
 from ._lib import KrylovError, KrylovLibraryError, FUN_CODES, LIB_PATH
 from .core import (Context, DeviceMatrix, default_context, device_count, expmv,
-                   function_multiple_entries, householder_qr,
+                   frechet_entries, function_multiple_entries, hessianfcn, hessianfcn_exp,
+                   hessianfcn_fun, householder_qr,
                    fun_and_grad_krylov_exp, fun_and_grad_krylov_fun, fun_update, lanczos_fmv,
                    mc_trace, normest, slq_plan, slq_quadforms, slq_trace, trace_exp,
                    trace_fun_update)
@@ -22,5 +23,6 @@ __all__ = [
     "trace_fun_update", "fun_update", "fun_and_grad_krylov_exp", "fun_and_grad_krylov_fun",
     "mc_trace", "trace_exp", "expmv", "lanczos_fmv", "trace_fun_update_pairs", "krylov_miobi",
     "greedy_krylov", "find_top_edges", "find_top_missing_edges", "compute_centrality",
-    "default_greedy_tol", "function_multiple_entries", "householder_qr",
+    "default_greedy_tol", "function_multiple_entries", "householder_qr", "frechet_entries",
+    "hessianfcn", "hessianfcn_exp", "hessianfcn_fun",
 ]

@@ -380,3 +380,45 @@ def householder_qr(W, ctx: Optional[Context] = None):
     R = np.zeros((bs, bs), order="F")
     _lib.check(_lib.load().kt_householder_qr(ctx.handle, n, bs, _dptr(W), _dptr(Q), _dptr(R)))
     return Q, R
+
+
+def frechet_entries(A, omega, targets, f="exp", tol=1e-12, it=None, ctx: Optional[Context] = None):
+    """out[h, t] = Df(A)(e_i e_j')(p, q) for omega[h] = (i, j) and targets[t] =
+    (p, q), all 1-based -- the entries multiple_frechet_eval.m:1 exposes through
+    Um{row(i)} * Xm{h} * Vm{col(j)}'.  Returns (out, iter)."""
+    D = _dev(A, ctx)
+    om = np.asarray(omega, dtype=np.int64).reshape(-1, 2)
+    tg = np.asarray(targets, dtype=np.int64).reshape(-1, 2)
+    oi, oj = np.ascontiguousarray(om[:, 0] - 1), np.ascontiguousarray(om[:, 1] - 1)
+    ti, tj = np.ascontiguousarray(tg[:, 0] - 1), np.ascontiguousarray(tg[:, 1] - 1)
+    out = np.zeros((om.shape[0], tg.shape[0]), order="F")
+    itr = C.c_int()
+    p64 = C.POINTER(C.c_int64)
+    _lib.check(_lib.load().kt_frechet_entries(
+        D.handle, om.shape[0], oi.ctypes.data_as(p64), oj.ctypes.data_as(p64), _fun_code(f),
+        float(tol), int(it or 0), tg.shape[0], ti.ctypes.data_as(p64), tj.ctypes.data_as(p64),
+        _dptr(out), C.byref(itr)))
+    return out, int(itr.value)
+
+
+def hessianfcn(X, A, Omega, f="exp", tol=1e-12, it=None, ctx: Optional[Context] = None):
+    """Hes = hessianfcn_exp(X, A, Omega, tol, it) / hessianfcn_fun(X, A, Omega, f, tol, it)
+    (hessianfcn_exp.m:1, hessianfcn_fun.m:1)."""
+    D = _dev(A, ctx)
+    Om = _omega(Omega)
+    X = np.ascontiguousarray(np.asarray(X, dtype=np.float64).ravel())
+    k = Om.shape[0]
+    H = np.zeros((k, k), order="F")
+    _lib.check(_lib.load().kt_hessianfcn(D.handle, k, _dptr(X), _dptr(Om), _fun_code(f), float(tol),
+                                         int(it or 0), _dptr(H)))
+    return H
+
+
+def hessianfcn_exp(X, A, Omega, tol=1e-12, it=None, ctx: Optional[Context] = None):
+    """hessianfcn_exp.m:1."""
+    return hessianfcn(X, A, Omega, "exp", tol, it, ctx)
+
+
+def hessianfcn_fun(X, A, Omega, f, tol=1e-12, it=None, ctx: Optional[Context] = None):
+    """hessianfcn_fun.m:1."""
+    return hessianfcn(X, A, Omega, f, tol, it, ctx)

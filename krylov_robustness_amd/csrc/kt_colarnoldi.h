@@ -1,0 +1,43 @@
+// kt_colarnoldi.h -- a batch of independent single-vector Arnoldi runs
+// (arnoldi_krylov.m with bs = 1, poles = inf), one per start index e_t, all
+// advanced by one SpMM per step.  Shared by function_multiple_entries.m
+// (kt_fme.cpp) and multiple_frechet_eval.m / hessianfcn_*.m (kt_frechet.cpp).
+#pragma once
+#include <vector>
+
+#include "kt_krylov.h"
+
+namespace kt {
+
+class ColArnoldi {
+   public:
+    // starts: distinct 0-based row indices (<= 128); it: max steps
+    ColArnoldi(kt_matrix_s* A, const std::vector<int64_t>& starts, int it);
+    int cols() const { return C_; }
+    int steps() const { return j_; }
+    // one Arnoldi step for every column (arnoldi_krylov.m:78-111)
+    void step();
+    // Gm = H(1:j, 1:j) of column c (column-major j x j)
+    void gm(int c, std::vector<double>& G) const;
+    // (V1' e_t)(1) of column c  (function_multiple_entries.m:94-95)
+    double uaux(int c) const { return uaux_[c]; }
+    // basis entries V_c(r, k) for the given rows, k < nk (nk <= steps() + 1):
+    // out[(ri * nk + k) * cols() + c]
+    void rows(const std::vector<int64_t>& rr, int nk, std::vector<double>& out) const;
+
+   private:
+    kt_matrix_s* A_;
+    kt_context_s* ctx_;
+    int64_t n_;
+    int C_, P_, it_, j_ = 0, nrb_;
+    int64_t vs_;
+    DevBuf basis_, W_, part_, red_, idx_;
+    std::vector<std::vector<double>> H_;  // (it+1) x it column-major per column
+    std::vector<double> uaux_;
+};
+
+// symmetric eigendecomposition of (G + G')/2, j x j: w ascending, V columns
+void sym_eig_small(int j, const std::vector<double>& G, std::vector<double>& w,
+                   std::vector<double>& V);
+
+}  // namespace kt

@@ -1,4 +1,6 @@
-// kt_fme.cpp -- function_multiple_entries.m on the device.
+// kt_fme.cpp -- function_multiple_entries.m on the device, and the
+// column-batched single-vector Arnoldi engine (ColArnoldi) it shares with
+// multiple_frechet_eval.m (kt_frechet.cpp).
 //
 // f(A)(i, j) for every (i, j) of omega by one single-vector Arnoldi run per
 // distinct row index i (arnoldi_krylov.m with bs = 1, started at e_i), all
@@ -12,10 +14,117 @@
 #include <cstring>
 #include <unordered_map>
 
-#include "kt_krylov.h"
+#include "kt_colarnoldi.h"
 #include "kt_launch.h"
 
 namespace kt {
+
+ColArnoldi::ColArnoldi(kt_matrix_s* A, const std::vector<int64_t>& starts, int it)
+    : A_(A), ctx_(A->ctx), n_(A->n), C_((int)starts.size()), it_(it) {
+    if (C_ < 1 || C_ > 128) fail(KT_ERR_UNSUPPORTED, "ColArnoldi: 1..128 columns");
+    P_ = pow2_at_least(C_);
+    vs_ = n_ * (int64_t)P_;
+    basis_.ensure(sizeof(double) * (size_t)vs_ * (it_ + 1));
+    W_.ensure(sizeof(double) * (size_t)vs_);
+    nrb_ = col_nrb((int)n_, ctx_->num_cu);
+    part_.ensure(sizeof(double) * (size_t)nrb_ * P_ * (it_ + 1));
+    // red: h1 | h2 | hh (it x P each) | s (P) | r (P)
+    red_.ensure(sizeof(double) * ((size_t)3 * it_ * P_ + 2 * P_));
+    std::vector<int> ridx(starts.begin(), starts.end());
+    idx_.ensure(sizeof(int) * ridx.size());
+    double* V = basis_.as<double>();
+    double* sq = red_.as<double>() + (size_t)3 * it_ * P_;
+    double* rr = sq + P_;
+    KT_HIP(hipMemcpyAsync(idx_.ptr, ridx.data(), sizeof(int) * ridx.size(), hipMemcpyHostToDevice,
+                          ctx_->stream));
+    KT_HIP(hipMemsetAsync(V, 0, sizeof(double) * (size_t)vs_, ctx_->stream));
+    KT_HIP(launch_col_select(C_, P_, idx_.as<int>(), V, ctx_->stream));
+    // [V, ~] = qr(e_t, 0)   (arnoldi_krylov.m:50)
+    KT_HIP(launch_col_dots((int)n_, P_, 1, 0, V, V, 1, ctx_->num_cu, part_.as<double>(), sq, ctx_->stream));
+    KT_HIP(launch_col_householder((int)n_, P_, sq, V, V, rr, ctx_->stream));
+    uaux_.assign(C_, 0.0);
+    for (int c = 0; c < C_; ++c)
+        KT_HIP(hipMemcpyAsync(&uaux_[c], V + starts[c] * P_ + c, sizeof(double),
+                              hipMemcpyDeviceToHost, ctx_->stream));
+    KT_HIP(hipStreamSynchronize(ctx_->stream));
+    H_.assign(C_, std::vector<double>((size_t)(it_ + 1) * it_, 0.0));
+}
+
+void ColArnoldi::step() {
+    if (j_ >= it_) fail(KT_ERR_UNSUPPORTED, "ColArnoldi: step budget exhausted");
+    const int j = ++j_;
+    const int n = (int)n_;
+    double* V = basis_.as<double>();
+    double* W = W_.as<double>();
+    double* h1 = red_.as<double>();
+    double* h2 = h1 + (size_t)it_ * P_;
+    double* hh = h2 + (size_t)it_ * P_;
+    double* sq = hh + (size_t)it_ * P_;
+    double* rr = sq + P_;
+    double* part = part_.as<double>();
+    double* Vj1 = V + (size_t)(j - 1) * vs_;
+    double* Vj = V + (size_t)j * vs_;
+    hipStream_t st = ctx_->stream;
+    spmm(A_, Vj1, P_, W, P_, C_);  // w = A * V(:, end)   (arnoldi_krylov.m:86)
+    // CGS2 against the whole basis (arnoldi_krylov.m:119-125)
+    KT_HIP(launch_col_dots(n, P_, j, vs_, V, W, 0, ctx_->num_cu, part, h1, st));
+    KT_HIP(launch_col_update(n, P_, j, vs_, V, h1, W, st));
+    KT_HIP(launch_col_dots(n, P_, j, vs_, V, W, 0, ctx_->num_cu, part, h2, st));
+    KT_HIP(launch_col_update(n, P_, j, vs_, V, h2, W, st));
+    // [w, r] = qr(w, 0)   (:99)
+    KT_HIP(launch_col_dots(n, P_, 1, 0, W, W, 1, ctx_->num_cu, part, sq, st));
+    KT_HIP(launch_col_householder(n, P_, sq, W, Vj, rr, st));
+    // reorthogonalise: hh = V' w; w = w - V hh   (:104-106)
+    KT_HIP(launch_col_dots(n, P_, j, vs_, V, Vj, 0, ctx_->num_cu, part, hh, st));
+    KT_HIP(launch_col_update(n, P_, j, vs_, V, hh, Vj, st));
+    std::vector<double> hb1((size_t)j * P_), hb2((size_t)j * P_), hbh((size_t)j * P_), rb(P_);
+    KT_HIP(hipMemcpyAsync(hb1.data(), h1, sizeof(double) * hb1.size(), hipMemcpyDeviceToHost, st));
+    KT_HIP(hipMemcpyAsync(hb2.data(), h2, sizeof(double) * hb2.size(), hipMemcpyDeviceToHost, st));
+    KT_HIP(hipMemcpyAsync(hbh.data(), hh, sizeof(double) * hbh.size(), hipMemcpyDeviceToHost, st));
+    KT_HIP(hipMemcpyAsync(rb.data(), rr, sizeof(double) * P_, hipMemcpyDeviceToHost, st));
+    KT_HIP(hipStreamSynchronize(st));
+    const int Hld = it_ + 1;
+    for (int c = 0; c < C_; ++c) {
+        std::vector<double>& Hc = H_[c];
+        const double r = rb[c];
+        for (int k = 0; k < j; ++k)  // H(1:end-1, end) = h + hh * r   (:96, :106)
+            Hc[k + (size_t)(j - 1) * Hld] =
+                (hb1[(size_t)k * P_ + c] + hb2[(size_t)k * P_ + c]) + hbh[(size_t)k * P_ + c] * r;
+        Hc[j + (size_t)(j - 1) * Hld] = r;  // H(end, end) = r   (:108)
+    }
+}
+
+void ColArnoldi::gm(int c, std::vector<double>& G) const {
+    const int j = j_, Hld = it_ + 1;
+    G.resize((size_t)j * j);
+    for (int b = 0; b < j; ++b)
+        for (int a = 0; a < j; ++a) G[a + (size_t)b * j] = H_[c][a + (size_t)b * Hld];
+}
+
+void ColArnoldi::rows(const std::vector<int64_t>& rr, int nk, std::vector<double>& out) const {
+    out.assign(rr.size() * (size_t)nk * C_, 0.0);
+    std::vector<double> buf((size_t)nk * P_);
+    const double* V = static_cast<const double*>(basis_.ptr);
+    for (size_t ri = 0; ri < rr.size(); ++ri) {
+        KT_HIP(hipMemcpy2DAsync(buf.data(), sizeof(double) * P_, V + rr[ri] * P_,
+                                sizeof(double) * vs_, sizeof(double) * P_, (size_t)nk,
+                                hipMemcpyDeviceToHost, ctx_->stream));
+        KT_HIP(hipStreamSynchronize(ctx_->stream));
+        for (int k = 0; k < nk; ++k)
+            for (int c = 0; c < C_; ++c) out[(ri * nk + k) * C_ + c] = buf[(size_t)k * P_ + c];
+    }
+}
+
+void sym_eig_small(int j, const std::vector<double>& G, std::vector<double>& w,
+                   std::vector<double>& V) {
+    std::vector<double> S((size_t)j * j);
+    for (int b = 0; b < j; ++b)
+        for (int a = 0; a < j; ++a)
+            S[a + (size_t)b * j] = 0.5 * (G[a + (size_t)b * j] + G[b + (size_t)a * j]);
+    w.resize(j);
+    V.resize((size_t)j * j);
+    sym_eig_host(j, S.data(), w.data(), V.data());
+}
 
 namespace {
 
@@ -25,7 +134,6 @@ struct Entry {
     int64_t j2;   // omega(h, 2), 0-based
     std::vector<double> Xm;  // f(Gm) e1 at convergence / last step
     std::vector<double> stop[3];
-    int nstop = 0;
     bool conv = false;
 };
 
@@ -33,11 +141,8 @@ struct Entry {
 // up to rounding for symmetric A and is symmetrised first (the reference's
 // expm/funm of the Hessenberg G agree to that rounding).
 std::vector<double> fun_e1(int j, const std::vector<double>& G, int fun) {
-    std::vector<double> S((size_t)j * j), w(j), V((size_t)j * j);
-    for (int b = 0; b < j; ++b)
-        for (int a = 0; a < j; ++a)
-            S[a + (size_t)b * j] = 0.5 * (G[a + (size_t)b * j] + G[b + (size_t)a * j]);
-    sym_eig_host(j, S.data(), w.data(), V.data());
+    std::vector<double> w, V;
+    sym_eig_small(j, G, w, V);
     std::vector<double> out(j, 0.0);
     for (int k = 0; k < j; ++k) {
         const double coef = fscalar(fun, w[k]) * V[0 + (size_t)k * j];
@@ -48,83 +153,18 @@ std::vector<double> fun_e1(int j, const std::vector<double>& G, int fun) {
 
 int run_group(kt_matrix_s* A, const std::vector<int64_t>& rows, std::vector<Entry>& ents, int fun,
               double tol, int it) {
-    kt_context_s* ctx = A->ctx;
-    const int64_t n = A->n;
-    const int C = (int)rows.size();
-    const int P = pow2_at_least(C);
-    const int64_t vs = n * (int64_t)P;  // step-block stride
-    DevBuf basis, Wb, part, red, idx;
-    basis.ensure(sizeof(double) * (size_t)vs * (it + 1));
-    Wb.ensure(sizeof(double) * (size_t)vs);
-    const int nrb = col_nrb((int)n, ctx->num_cu);
-    part.ensure(sizeof(double) * (size_t)nrb * P * (it + 1));
-    // red: h1 | h2 | hh (it x P each) | s (P) | r (P)
-    red.ensure(sizeof(double) * ((size_t)3 * it * P + 2 * P));
-    double* V = basis.as<double>();
-    double* W = Wb.as<double>();
-    double* h1 = red.as<double>();
-    double* h2 = h1 + (size_t)it * P;
-    double* hh = h2 + (size_t)it * P;
-    double* sq = hh + (size_t)it * P;
-    double* rr = sq + P;
-    std::vector<int> ridx(rows.begin(), rows.end());
-    idx.ensure(sizeof(int) * ridx.size());
-    KT_HIP(hipMemcpyAsync(idx.ptr, ridx.data(), sizeof(int) * ridx.size(), hipMemcpyHostToDevice,
-                          ctx->stream));
-    KT_HIP(hipMemsetAsync(V, 0, sizeof(double) * (size_t)vs, ctx->stream));
-    KT_HIP(launch_col_select(C, P, idx.as<int>(), V, ctx->stream));
-    // [V, ~] = qr(e_i, 0)   (arnoldi_krylov.m:50)
-    KT_HIP(launch_col_dots((int)n, P, 1, 0, V, V, 1, ctx->num_cu, part.as<double>(), sq, ctx->stream));
-    KT_HIP(launch_col_householder((int)n, P, sq, V, V, rr, ctx->stream));
-    // Uaux(c) = (V' e_i)(1) = V(i, c)   (function_multiple_entries.m:94-95)
-    std::vector<double> uaux(C);
-    for (int c = 0; c < C; ++c)
-        KT_HIP(hipMemcpyAsync(&uaux[c], V + (int64_t)rows[c] * P + c, sizeof(double),
-                              hipMemcpyDeviceToHost, ctx->stream));
-    KT_HIP(hipStreamSynchronize(ctx->stream));
-
-    std::vector<std::vector<double>> H(C);  // column-major (it+1) x it per column
-    const int Hld = it + 1;
-    for (auto& x : H) x.assign((size_t)Hld * it, 0.0);
-    std::vector<double> hb1((size_t)it * P), hb2((size_t)it * P), hbh((size_t)it * P), rb(P);
+    ColArnoldi ca(A, rows, it);
+    const int C = ca.cols();
     std::vector<char> col_live(C, 1);
     const int d = 3;  // lag (function_multiple_entries.m:63)
     int j = 0;
+    std::vector<double> G;
     for (j = 1; j <= it; ++j) {
-        double* Vj1 = V + (size_t)(j - 1) * vs;
-        double* Vj = V + (size_t)j * vs;
-        spmm(A, Vj1, P, W, P, C);  // w = A * V(:, end)   (arnoldi_krylov.m:86)
-        // CGS2 against the whole basis (arnoldi_krylov.m:119-125)
-        KT_HIP(launch_col_dots((int)n, P, j, vs, V, W, 0, ctx->num_cu, part.as<double>(), h1, ctx->stream));
-        KT_HIP(launch_col_update((int)n, P, j, vs, V, h1, W, ctx->stream));
-        KT_HIP(launch_col_dots((int)n, P, j, vs, V, W, 0, ctx->num_cu, part.as<double>(), h2, ctx->stream));
-        KT_HIP(launch_col_update((int)n, P, j, vs, V, h2, W, ctx->stream));
-        // [w, r] = qr(w, 0)   (:99)
-        KT_HIP(launch_col_dots((int)n, P, 1, 0, W, W, 1, ctx->num_cu, part.as<double>(), sq, ctx->stream));
-        KT_HIP(launch_col_householder((int)n, P, sq, W, Vj, rr, ctx->stream));
-        // reorthogonalise: hh = V' w; w = w - V hh   (:104-106)
-        KT_HIP(launch_col_dots((int)n, P, j, vs, V, Vj, 0, ctx->num_cu, part.as<double>(), hh, ctx->stream));
-        KT_HIP(launch_col_update((int)n, P, j, vs, V, hh, Vj, ctx->stream));
-        KT_HIP(hipMemcpyAsync(hb1.data(), h1, sizeof(double) * (size_t)j * P, hipMemcpyDeviceToHost, ctx->stream));
-        KT_HIP(hipMemcpyAsync(hb2.data(), h2, sizeof(double) * (size_t)j * P, hipMemcpyDeviceToHost, ctx->stream));
-        KT_HIP(hipMemcpyAsync(hbh.data(), hh, sizeof(double) * (size_t)j * P, hipMemcpyDeviceToHost, ctx->stream));
-        KT_HIP(hipMemcpyAsync(rb.data(), rr, sizeof(double) * P, hipMemcpyDeviceToHost, ctx->stream));
-        KT_HIP(hipStreamSynchronize(ctx->stream));
-        for (int c = 0; c < C; ++c) {
-            std::vector<double>& Hc = H[c];
-            const double r = rb[c];
-            for (int k = 0; k < j; ++k)  // H(1:end-1, end) = h + hh * r   (:96, :106)
-                Hc[k + (size_t)(j - 1) * Hld] =
-                    (hb1[(size_t)k * P + c] + hb2[(size_t)k * P + c]) + hbh[(size_t)k * P + c] * r;
-            Hc[j + (size_t)(j - 1) * Hld] = r;  // H(end, end) = r   (:108)
-        }
-        // f(Gm) e1 for the columns that still have unconverged entries
+        ca.step();
         std::vector<std::vector<double>> F(C);
         for (int c = 0; c < C; ++c) {
             if (!col_live[c]) continue;
-            std::vector<double> G((size_t)j * j);
-            for (int b = 0; b < j; ++b)
-                for (int a = 0; a < j; ++a) G[a + (size_t)b * j] = H[c][a + (size_t)b * Hld];
+            ca.gm(c, G);
             F[c] = fun_e1(j, G, fun);
         }
         bool stop = true;  // :113-156
@@ -156,21 +196,20 @@ int run_group(kt_matrix_s* A, const std::vector<int64_t>& rows, std::vector<Entr
     }
     const int iter = std::min(j, it);
     // X(h) = Um(j2, 1:nn) * Xm(:, 1) * Uaux   (:163-165)
-    std::unordered_map<int64_t, std::vector<double>> urow;  // j2 -> (iter+1) x P
-    for (const Entry& e : ents) {
-        if (urow.count(e.j2)) continue;
-        std::vector<double> buf((size_t)(iter + 1) * P);
-        KT_HIP(hipMemcpy2DAsync(buf.data(), sizeof(double) * P, V + e.j2 * P, sizeof(double) * vs,
-                                sizeof(double) * P, (size_t)(iter + 1), hipMemcpyDeviceToHost,
-                                ctx->stream));
-        urow.emplace(e.j2, std::move(buf));
-    }
-    KT_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<int64_t> need;
+    std::unordered_map<int64_t, size_t> at;
+    for (const Entry& e : ents)
+        if (!at.count(e.j2)) {
+            at.emplace(e.j2, need.size());
+            need.push_back(e.j2);
+        }
+    std::vector<double> U;
+    ca.rows(need, iter + 1, U);
     for (Entry& e : ents) {
-        const std::vector<double>& u = urow[e.j2];
+        const size_t ri = at[e.j2];
         double x = 0.0;
-        for (size_t i = 0; i < e.Xm.size(); ++i) x += u[i * P + e.col] * e.Xm[i];
-        e.Xm.assign(1, x * uaux[e.col]);
+        for (size_t i = 0; i < e.Xm.size(); ++i) x += U[(ri * (iter + 1) + i) * C + e.col] * e.Xm[i];
+        e.Xm.assign(1, x * ca.uaux(e.col));
     }
     return iter;
 }

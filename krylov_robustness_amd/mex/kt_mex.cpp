@@ -9,6 +9,8 @@
 //   mex -R2018a -DKT_ENTRY_FG_FUN           kt_mex.cpp ... -output fun_and_grad_krylov_fun
 //   mex -R2018a -DKT_ENTRY_KRYLOV_MIOBI     kt_mex.cpp ... -output krylov_miobi
 //   mex -R2018a -DKT_ENTRY_FME              kt_mex.cpp ... -output function_multiple_entries
+//   mex -R2018a -DKT_ENTRY_HESS_EXP         kt_mex.cpp ... -output hessianfcn_exp
+//   mex -R2018a -DKT_ENTRY_HESS_FUN         kt_mex.cpp ... -output hessianfcn_fun
 //
 // Placed in the reference's functions/ directory, each MEX shadows the .m of
 // the same name (MATLAB's same-folder precedence), so Tests/*.m, greedy_krylov.m
@@ -307,6 +309,25 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
           "function_multiple_entries");
     plhs[0] = X;
     if (nlhs > 1) plhs[1] = scalar(iter);
+#elif defined(KT_ENTRY_HESS_EXP) || defined(KT_ENTRY_HESS_FUN)
+    // Hes = hessianfcn_exp(X, A, Omega, tol, it)          hessianfcn_exp.m:1
+    // Hes = hessianfcn_fun(X, A, Omega, f, tol, it)       hessianfcn_fun.m:1
+#if defined(KT_ENTRY_HESS_EXP)
+    const int off = 0;
+    const int fcode = KT_FUN_EXP;
+#else
+    const int off = 1;
+    if (nrhs < 4) mexErrMsgIdAndTxt("krylov_hip:nargin", "hessianfcn_fun(X, A, Omega, f, tol, it)");
+    const int fcode = fun_arg(prhs[3], KT_FUN_EXP);
+#endif
+    if (nrhs < 3) mexErrMsgIdAndTxt("krylov_hip:nargin", "hessianfcn(X, A, Omega, ...)");
+    const mwSize nom = mxGetM(prhs[2]);
+    mxArray* H = mxCreateDoubleMatrix(nom, nom, mxREAL);
+    check(kt_hessianfcn(matrix_arg(prhs[1]), (int64_t)nom, mxGetDoubles(prhs[0]), mxGetDoubles(prhs[2]),
+                        fcode, scalar_or(nrhs, prhs, 3 + off, 1e-12), (int)scalar_or(nrhs, prhs, 4 + off, 0),
+                        mxGetDoubles(H)),
+          "hessianfcn");
+    plhs[0] = H;
 #else
 #error "define one KT_ENTRY_* (see the header of this file)"
 #endif

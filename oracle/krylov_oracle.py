@@ -947,3 +947,129 @@ def function_multiple_entries(A, omega, f="exp", tol=1e-12, it=None, poles=np.in
         nn = Xm[h].shape[0]
         X[h] = St[r_].V[omega[h, 1] - 1, :nn] @ Xm[h][:, 0] * Uaux[r_]
     return X, j
+
+
+# ---------------------------------------------------------------------------
+# multiple_frechet_eval.m / hessianfcn_exp.m / hessianfcn_fun.m (poles = inf)
+# ---------------------------------------------------------------------------
+def frechet_matrix_fun(name: str):
+    """multiple_frechet_eval.m:60-77."""
+    if name == "exp":
+        return sla.expm
+    if name == "sin":
+        return sla.sinm
+    if name == "cos":
+        return sla.cosm
+    if name == "log":
+        return sla.logm
+    if name == "sqrt":
+        return sla.sqrtm
+    if name == "sinh":
+        return lambda M: (sla.expm(M) - sla.expm(-M)) / 2
+    if name == "cosh":
+        return lambda M: (sla.expm(M) + sla.expm(-M)) / 2
+    raise ValueError(name)
+
+
+def multiple_frechet_eval(A, omega, f="exp", tol=1e-12, it=None, poles=np.inf, debug=0):
+    """[Um, Xm, Vm, row, col, iter] = multiple_frechet_eval(A, omega, f, tol, it, poles, debug)
+    (multiple_frechet_eval.m:1-212); omega 1-based.  Returns Um/Vm as lists
+    (bases with the last block dropped, :207-212), Xm per entry, and the
+    row/col maps as dicts index -> position."""
+    omega = np.asarray(omega, dtype=np.int64).reshape(-1, 2)
+    n = A.shape[0]
+    if it is None:
+        it = min(100, n)
+    k = omega.shape[0]
+    AT = sp.csr_matrix(A).T.tocsr()                       # :55
+    I0 = list(dict.fromkeys(omega[:, 0].tolist()))
+    J0 = list(dict.fromkeys(omega[:, 1].tolist()))
+    row = {t: i for i, t in enumerate(I0)}
+    col = {t: i for i, t in enumerate(J0)}
+    fM = frechet_matrix_fun(f)
+    d = 3
+    Xstop = [[] for _ in range(k)]
+    notconverged = list(range(k))
+    SA = [None] * len(I0); SB = [None] * len(J0)
+    Uaux = np.zeros(len(I0)); Vaux = np.zeros(len(J0))
+    Gm = [None] * len(I0); Hm = [None] * len(J0)
+    Xm = [None] * k
+    I, J = list(I0), list(J0)
+    j = 0
+    for j in range(1, it + 1):
+        for h in I:                                       # :99-125
+            r_ = row[h]
+            if j == 1:
+                U = np.zeros((n, 1)); U[h - 1, 0] = 1.0
+                SA[r_] = arnoldi_krylov_start(A, U)
+                Uaux[r_] = (SA[r_].V.T @ U)[0, 0]
+            else:
+                SA[r_] = arnoldi_krylov_extend(SA[r_])
+            Gm[r_] = SA[r_].H[:-1, :]
+        for h in J:                                       # :127-148
+            c_ = col[h]
+            if j == 1:
+                V = np.zeros((n, 1)); V[h - 1, 0] = 1.0
+                SB[c_] = arnoldi_krylov_start(AT, V)
+                Vaux[c_] = (SB[c_].V.T @ V)[0, 0]
+            else:
+                SB[c_] = arnoldi_krylov_extend(SB[c_])
+            Hm[c_] = SB[c_].H[:-1, :] @ np.linalg.inv(SB[c_].K[:-1, :])
+        stop = True
+        for h in list(notconverged):                      # :150-196
+            G = Gm[row[omega[h, 0]]]
+            Hh = Hm[col[omega[h, 1]]]
+            Cm = np.zeros((j, j)); Cm[0, 0] = Uaux[row[omega[h, 0]]] * Vaux[col[omega[h, 1]]]
+            Fm = np.block([[G, Cm], [np.zeros((Hh.shape[1], G.shape[1])), Hh.T]])
+            Fm = fM(Fm)
+            Xm[h] = Fm[:G.shape[0], G.shape[1]:]
+            if j <= d:
+                Xstop[h].append(Xm[h])
+                stop = False
+            else:
+                nn = Xm[h].shape[0]
+                old = np.zeros((nn, nn))
+                o = Xstop[h][0]
+                old[:o.shape[0], :o.shape[1]] = o
+                err = np.linalg.norm(Xm[h] - old, 2)
+                if err > tol:
+                    stop = False
+                else:
+                    notconverged = [x for x in notconverged if x != h]
+                    I = list(dict.fromkeys(omega[notconverged, 0].tolist()))
+                    J = list(dict.fromkeys(omega[notconverged, 1].tolist()))
+                Xstop[h] = Xstop[h][1:d] + [Xm[h]]
+        if stop:
+            break
+    Um = [s.V[:, :-1] for s in SA]                        # :207-212
+    Vm = [s.V[:, :-1] for s in SB]
+    return Um, Xm, Vm, row, col, j
+
+
+def hessianfcn(X, A, Omega, f="exp", tol=1e-12, it=None):
+    """hessianfcn_exp.m:1-17 (f = exp) / hessianfcn_fun.m:1-17."""
+    Omega = np.asarray(Omega, dtype=np.int64).reshape(-1, 2)
+    n = A.shape[0]
+    k = Omega.shape[0]
+    XX = sp.csr_matrix((np.asarray(X, dtype=np.float64).ravel(), (Omega[:, 0] - 1, Omega[:, 1] - 1)),
+                       shape=(n, n))
+    XX = XX + XX.T
+    At = (sp.csr_matrix(A) + XX).tocsr()
+    Um, Xm, Vm, row, col, _ = multiple_frechet_eval(At, Omega, f, tol, it, np.inf, False)
+    Hes = np.zeros((k, k))
+    for jj in range(k):
+        h, kk = Omega[jj]
+        a, b = Xm[jj].shape
+        for l in range(jj, k):
+            Hes[jj, l] = Um[row[h]][Omega[l, 0] - 1, :a] @ Xm[jj] @ Vm[col[kk]][Omega[l, 1] - 1, :b]
+        Hes[jj + 1:, jj] = Hes[jj, jj + 1:]
+    return -2 * Hes
+
+
+def exact_frechet(A, i, j, f="exp"):
+    """Df(A)(e_i e_j') as the (1,2) block of f([A E; 0 A]) (dense; small n)."""
+    n = A.shape[0]
+    Ad = _full(A)
+    E = np.zeros((n, n)); E[i - 1, j - 1] = 1.0
+    F = frechet_matrix_fun(f)(np.block([[Ad, E], [np.zeros((n, n)), Ad]]))
+    return F[:n, n:]

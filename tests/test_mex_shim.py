@@ -11,7 +11,7 @@ import pytest
 from conftest import ROOT
 
 ENTRIES = ["TRACE_EXP", "MC_TRACE", "TRACE_FUN_UPDATE", "FUN_UPDATE", "FG_EXP", "FG_FUN",
-           "KRYLOV_MIOBI", "FME"]
+           "KRYLOV_MIOBI", "FME", "HESS_EXP", "HESS_FUN"]
 
 
 @pytest.mark.parametrize("entry", ENTRIES)
