@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import warnings
 from typing import Optional
 
 import numpy as np
@@ -227,6 +228,11 @@ def trace_fun_update(A, U, B, tol=1e-12, it=None, debug=0, fun="exp", ctx: Optio
     _lib.check(_lib.load().kt_trace_fun_update(
         D.handle, U.shape[1], _dptr(U), _dptr(B), float(tol), int(it or 0), _fun_code(fun),
         C.byref(xm), C.byref(itr), C.byref(lk)))
+    its = int(it) if it else min(100, D.n)
+    if lk.value and debug:  # trace_fun_update.m:119-124
+        warnings.warn("TRACE_FUN_UPDATE:: Detected lucky breakdown")
+    if itr.value == its:  # :128-130
+        warnings.warn("TRACE_FUN_UPDATE:: Reached maximum number of iterations")
     return float(xm.value), int(itr.value), int(lk.value)
 
 
@@ -248,6 +254,10 @@ def fun_update(A, U, B, fun="exp", tol=1e-12, it=None, debug=0, want_um=True,
     _lib.check(_lib.load().kt_fun_update(
         D.handle, rk, _dptr(U), _dptr(B), _fun_code(fun), float(tol), int(it or 0), maxc,
         _dptr(Xm), C.byref(nc), C.byref(itr), C.byref(lk), _dptr(Um) if want_um else None))
+    if lk.value:  # fun_update.m:127-130
+        warnings.warn("FUN_UPDATE:: Detected lucky breakdown")
+    if itr.value == its:  # :133-135
+        warnings.warn("FUN_UPDATE:: Reached maximum number of iterations")
     k = int(nc.value)
     X = Xm[:k * k].reshape(k, k, order="F")
     Umat = Um[:D.n * k].reshape(D.n, k, order="F") if want_um else None
@@ -368,6 +378,8 @@ def function_multiple_entries(A, omega, f="exp", tol=1e-12, it=None, poles=np.in
         D.handle, om.shape[0], oi.ctypes.data_as(C.POINTER(C.c_int64)),
         oj.ctypes.data_as(C.POINTER(C.c_int64)), _fun_code(f), float(tol), int(it or 0),
         _dptr(X), C.byref(itr)))
+    if itr.value == (int(it) if it else min(100, D.n)):  # function_multiple_entries.m:158-161
+        warnings.warn("FUNCTION_MULTIPLE_ENTRIES:: Reached maximum number of iterations")
     return X, int(itr.value)
 
 
@@ -398,6 +410,8 @@ def frechet_entries(A, omega, targets, f="exp", tol=1e-12, it=None, ctx: Optiona
         D.handle, om.shape[0], oi.ctypes.data_as(p64), oj.ctypes.data_as(p64), _fun_code(f),
         float(tol), int(it or 0), tg.shape[0], ti.ctypes.data_as(p64), tj.ctypes.data_as(p64),
         _dptr(out), C.byref(itr)))
+    if itr.value == (int(it) if it else min(100, D.n)):  # multiple_frechet_eval.m:202-204
+        warnings.warn("MULTIPLE_FRECHET_EVAL:: Reached maximum number of iterations")
     return out, int(itr.value)
 
 

@@ -25,6 +25,7 @@
 // arrays' contents and released in mexAtExit.  Errors never cross the C ABI:
 // a non-zero status becomes mexErrMsgIdAndTxt with the library's message.
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -166,8 +167,12 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
 #if defined(KT_ENTRY_TRACE_EXP)
     // tr = trace_exp(A)                                          trace_exp.m:1
     if (nrhs != 1) mexErrMsgIdAndTxt("krylov_hip:nargin", "tr = trace_exp(A)");
+    // Afun: the Lanczos-quadrature Afun (north star, default) or the
+    // reference's own expmv handle (trace_exp.m:5) with KT_TRACE_EXP_AFUN=expmv
+    const char* af = getenv("KT_TRACE_EXP_AFUN");
+    const int afun = (af && strcmp(af, "expmv") == 0) ? KT_AFUN_EXPMV : KT_AFUN_LANCZOS;
     double tr = 0.0;
-    check(kt_trace_exp(matrix_arg(prhs[0]), KT_AFUN_LANCZOS, 30, 0, &tr), "trace_exp");
+    check(kt_trace_exp(matrix_arg(prhs[0]), afun, 30, 0, &tr), "trace_exp");
     plhs[0] = scalar(tr);
 #elif defined(KT_ENTRY_MC_TRACE)
     // [tr, res, it] = mc_trace(Afun, n, tol, maxit, isAreal, debug)   mc_trace.m:1
@@ -197,6 +202,14 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
                               scalar_or(nrhs, prhs, 3, 1e-12), (int)scalar_or(nrhs, prhs, 4, 0),
                               fun_arg(nrhs > 6 ? prhs[6] : nullptr, KT_FUN_EXP), &xm, &iter, &lucky),
           "trace_fun_update");
+    {  // warnings stay warnings (trace_fun_update.m:119-130)
+        const int it_arg = (int)scalar_or(nrhs, prhs, 4, 0);
+        const int it_eff = it_arg > 0 ? it_arg : (int)(mxGetM(prhs[0]) < 100 ? mxGetM(prhs[0]) : 100);
+        if (lucky && scalar_or(nrhs, prhs, 5, 0) != 0)
+            mexWarnMsgIdAndTxt("TRACE_FUN_UPDATE:lucky", "TRACE_FUN_UPDATE:: Detected lucky breakdown");
+        if (iter == it_eff)
+            mexWarnMsgIdAndTxt("TRACE_FUN_UPDATE:maxit", "TRACE_FUN_UPDATE:: Reached maximum number of iterations");
+    }
     plhs[0] = scalar(xm);
     if (nlhs > 1) plhs[1] = scalar(iter);
     if (nlhs > 2) plhs[2] = scalar(lucky);
@@ -215,6 +228,9 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
                         scalar_or(nrhs, prhs, 4, 1e-12), it, maxc, Xm.data(), &nc, &iter, &lucky,
                         nlhs > 3 ? Um.data() : nullptr),
           "fun_update");
+    if (lucky) mexWarnMsgIdAndTxt("FUN_UPDATE:lucky", "FUN_UPDATE:: Detected lucky breakdown");  // fun_update.m:127-128
+    if (iter == (it > 0 ? it : (int)(n < 100 ? n : 100)))
+        mexWarnMsgIdAndTxt("FUN_UPDATE:maxit", "FUN_UPDATE:: Reached maximum number of iterations");  // :133-135
     plhs[0] = mxCreateDoubleMatrix(nc, nc, mxREAL);
     memcpy(mxGetDoubles(plhs[0]), Xm.data(), sizeof(double) * nc * nc);
     if (nlhs > 1) plhs[1] = scalar(iter);
@@ -307,6 +323,13 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
                                        fun_arg(prhs[2], KT_FUN_EXP), scalar_or(nrhs, prhs, 3, 1e-12),
                                        (int)scalar_or(nrhs, prhs, 4, 0), mxGetDoubles(X), &iter),
           "function_multiple_entries");
+    {
+        const int it_arg = (int)scalar_or(nrhs, prhs, 4, 0);
+        const mwSize na = mxGetM(prhs[0]);
+        if (iter == (it_arg > 0 ? it_arg : (int)(na < 100 ? na : 100)))  // :158-161
+            mexWarnMsgIdAndTxt("FUNCTION_MULTIPLE_ENTRIES:maxit",
+                               "FUNCTION_MULTIPLE_ENTRIES:: Reached maximum number of iterations");
+    }
     plhs[0] = X;
     if (nlhs > 1) plhs[1] = scalar(iter);
 #elif defined(KT_ENTRY_HESS_EXP) || defined(KT_ENTRY_HESS_FUN)

@@ -26,6 +26,7 @@ double mxGetInf(void);
 void mxDestroyArray(mxArray*);
 int mexCallMATLAB(int, mxArray**, int, mxArray**, const char*);
 void mexErrMsgIdAndTxt(const char*, const char*, ...);
+void mexWarnMsgIdAndTxt(const char*, const char*, ...);
 int mexAtExit(void (*)(void));
 void mexLock(void);
 }

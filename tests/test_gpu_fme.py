@@ -68,3 +68,17 @@ def test_fme_rejects_rational_poles(kra, gpu_ctx):
     A = load_graph("austria")
     with pytest.raises(kra.KrylovError, match="rational"):
         kra.function_multiple_entries(A, [[1, 2]], "exp", 1e-8, 10, poles=[1.0], ctx=gpu_ctx)
+
+
+def test_maxit_warnings_stay_warnings(kra, gpu_ctx):
+    """The reference's 'Reached maximum number of iterations' warnings
+    (function_multiple_entries.m:158-161, trace_fun_update.m:128-130) are
+    warnings, not errors, and the results are still returned."""
+    A = load_graph("rome")
+    with pytest.warns(UserWarning, match="FUNCTION_MULTIPLE_ENTRIES:: Reached maximum"):
+        X, it = kra.function_multiple_entries(A, [[1, 2], [5, 5]], "exp", 1e-30, 4, ctx=gpu_ctx)
+    assert it == 4 and np.all(np.isfinite(X))
+    U = np.zeros((A.shape[0], 2)); U[0, 0] = 1; U[1, 1] = 1
+    with pytest.warns(UserWarning, match="TRACE_FUN_UPDATE:: Reached maximum"):
+        xm, it, _ = kra.trace_fun_update(A, U, -np.array([[0, 1.0], [1.0, 0]]), 1e-30, 5, ctx=gpu_ctx)
+    assert it == 5 and np.isfinite(xm)
