@@ -15,7 +15,8 @@ from .core import (Context, DeviceMatrix, default_context, device_count, expmv,
                    mc_trace, normest, slq_plan, slq_quadforms, slq_trace, trace_exp,
                    trace_fun_update)
 from .greedy import (compute_centrality, default_greedy_tol, find_top_edges,
-                     find_top_missing_edges, greedy_krylov, krylov_miobi, trace_fun_update_pairs)
+                     find_top_missing_edges, greedy_krylov, krylov_miobi, krylov_miobi_sharded,
+                     miobi_loop, select_extreme, trace_fun_update_pairs)
 
 __all__ = [
     "KrylovError", "KrylovLibraryError", "FUN_CODES", "LIB_PATH", "Context", "DeviceMatrix",
@@ -23,6 +24,6 @@ __all__ = [
     "trace_fun_update", "fun_update", "fun_and_grad_krylov_exp", "fun_and_grad_krylov_fun",
     "mc_trace", "trace_exp", "expmv", "lanczos_fmv", "trace_fun_update_pairs", "krylov_miobi",
     "greedy_krylov", "find_top_edges", "find_top_missing_edges", "compute_centrality",
-    "default_greedy_tol", "function_multiple_entries", "householder_qr", "frechet_entries",
+    "default_greedy_tol", "krylov_miobi_sharded", "miobi_loop", "select_extreme", "function_multiple_entries", "householder_qr", "frechet_entries",
     "hessianfcn", "hessianfcn_exp", "hessianfcn_fun",
 ]

@@ -40,3 +40,23 @@ def allreduce_max(val: float, device=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def allgather_concat(x, counts, group=None):
+    """Concatenate per-rank 1-D float64 arrays in rank order (rank r holds
+    counts[r] values).  Pads to max(counts) so one fixed-size all_gather works
+    on gloo and RCCL alike; RCCL needs device tensors (current GPU)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    m = max(int(max(counts)), 1)
+    backend = dist.get_backend(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    t = torch.zeros(m, dtype=torch.float64, device=dev)
+    x = np.asarray(x, dtype=np.float64).ravel()
+    if x.size:
+        t[:x.size] = torch.from_numpy(x).to(dev)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    return np.concatenate([p[:int(c)].cpu().numpy() for p, c in zip(parts, counts)])

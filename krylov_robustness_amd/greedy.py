@@ -81,6 +81,66 @@ def krylov_miobi(A, k, E=None, tol=1e-12, it=None, poles=np.inf, debug=0, miobi=
     return edges, float(rob.value), D
 
 
+def select_extreme(xm, make):
+    """krylov_miobi.m:112-124: strict comparison, the first extreme wins.
+    Returns (index, value); index -1 if no candidate compares (all NaN)."""
+    best, bv = -1, (-np.inf if make else np.inf)
+    for h, v in enumerate(np.asarray(xm, dtype=np.float64)):
+        if (v > bv) if make else (v < bv):
+            best, bv = h, float(v)
+    return best, bv
+
+
+def miobi_loop(k, E, make, score, edit):
+    """Host loop of krylov_miobi.m:70-139 over injectable scoring / editing:
+    score(E) -> the trace variation of every candidate row of E (1-based),
+    edit(edge, value) applies A(i,j) = A(j,i) = value.  Returns (edges, rob)."""
+    E = np.asarray(E, dtype=np.int64).reshape(-1, 2).copy()
+    edges, rob = [], 0.0
+    for _ in range(min(int(k), E.shape[0])):
+        xm = score(E)
+        best, bv = select_extreme(xm, make)
+        if best < 0:
+            raise _lib.KrylovError(_lib.KT_ERR_ARG, "KRYLOV_MIOBI:: no finite candidate score")
+        chosen = E[best].copy()
+        E = np.delete(E, best, axis=0)               # :127
+        edit(chosen, 1.0 if make else 0.0)           # :129-135
+        edges.append(chosen)
+        rob += bv
+    return np.array(edges, dtype=np.int64).reshape(-1, 2), rob
+
+
+def krylov_miobi_sharded(A, k, E, tol=1e-12, it=None, poles=np.inf, debug=0, miobi="break",
+                         rescale=1.0, group=None, ctx: Optional[Context] = None):
+    """krylov_miobi with the candidate scoring sharded over the ranks of the
+    process group: rank r scores its contiguous slice of E on
+    its own GPU (kt_trace_fun_update_pairs), the scores are all-gathered in
+    rank order, every rank picks the same extreme candidate and edits its own
+    device copy of A.  Same result as krylov_miobi on one GPU."""
+    import torch.distributed as dist
+    from .dist import allgather_concat, probe_shard
+    if miobi not in ("break", "make"):
+        raise _lib.KrylovError(_lib.KT_ERR_ARG, "KRYLOV_MIOBI:: not supported option for miobi")
+    D = _dev(A, ctx)
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    make = miobi == "make"
+    sg = 1.0 if make else -1.0
+    B = sg * np.array([[0.0, 1.0], [1.0, 0.0]]) / rescale
+
+    def score(Ecur):
+        counts = [probe_shard(len(Ecur), r, world)[1] for r in range(world)]
+        off, cnt = probe_shard(len(Ecur), rank, world)
+        xm = (trace_fun_update_pairs(D, Ecur[off:off + cnt], B, tol, it, b_self=sg, ctx=ctx)[0]
+              if cnt else np.zeros(0))
+        return allgather_concat(xm, counts, group)
+
+    def edit(e, value):
+        D.set_pairs([e], value)
+
+    edges, rob = miobi_loop(k, E, make, score, edit)
+    return edges, rob, D
+
+
 def find_top_edges(A, centrality, num, order="mult"):
     """find_top_edges.m:1-40: the top `num` existing edges (1-based, i > j)."""
     import scipy.sparse as sp

@@ -63,3 +63,63 @@ def test_gloo_world2_matches_single():
     _, q1 = slq_ref.slq_trace(load_graph("anaheim"), 50, 20, seed=5)
     assert s[0] == pytest.approx(q1.sum(), rel=1e-12)
     assert s[1] == pytest.approx((q1 ** 2).sum(), rel=1e-12)
+
+
+def _greedy_worker(rank, world, port, out):
+    """krylov_miobi with candidates sharded over the ranks:
+    each rank scores its slice (here with the oracle's trace_fun_update, the
+    device pairs call on the GPU box), scores are all-gathered, every rank
+    edits its own copy of A."""
+    import numpy as np
+    import scipy.sparse as sp
+    import torch.distributed as dist
+    from oracle import krylov_oracle as ko
+    import krylov_robustness_amd as kra
+    from krylov_robustness_amd.dist import allgather_concat, probe_shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    A = sp.lil_matrix(load_graph("austria"))
+    E = kra.find_top_edges(A.tocsr(), kra.compute_centrality(A.tocsr()), 12, "min")
+    B = -np.array([[0.0, 1.0], [1.0, 0.0]])
+    n = A.shape[0]
+
+    def score(Ecur):
+        counts = [probe_shard(len(Ecur), r, world)[1] for r in range(world)]
+        off, cnt = probe_shard(len(Ecur), rank, world)
+        xm = []
+        for i, j in Ecur[off:off + cnt]:
+            U = np.zeros((n, 2)); U[i - 1, 0] = 1; U[j - 1, 1] = 1
+            xm.append(ko.trace_fun_update(A.tocsr(), U, B, 1e-10, 60)[0])
+        return allgather_concat(np.array(xm), counts)
+
+    def edit(e, v):
+        A[e[0] - 1, e[1] - 1] = v
+        A[e[1] - 1, e[0] - 1] = v
+
+    edges, rob = kra.miobi_loop(3, E, False, score, edit)
+    if rank == 0:
+        out.put((edges.tolist(), rob))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_greedy_matches_single():
+    import torch.multiprocessing as mp
+    from oracle import krylov_oracle as ko
+    import krylov_robustness_amd as kra
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_greedy_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    edges, rob = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    A = load_graph("austria")
+    E = kra.find_top_edges(A, kra.compute_centrality(A), 12, "min")
+    eo, ro, _ = ko.krylov_miobi(A, 3, E, 1e-10, 60, np.inf, 0, "break", 1.0)
+    assert edges == eo.tolist()
+    assert rob == pytest.approx(ro, rel=1e-12)

@@ -140,3 +140,25 @@ def test_greedy_krylov_config5_slice(kra, gpu_ctx):
     np.testing.assert_array_equal(edges, eo)
     assert rob == pytest.approx(ro, rel=1e-7)
     assert (abs(D2.to_scipy() - sp.csc_matrix(Ao)) > 0).nnz == 0
+
+
+def test_krylov_miobi_sharded_world1(kra, gpu_ctx):
+    """The sharded greedy step through a 1-rank gloo group on
+    the device gives krylov_miobi's edges, variation and A_new."""
+    import os
+    import socket
+    import torch.distributed as dist
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        A, c = _india(kra)
+        E = kra.find_top_edges(A, c, 40, "min")
+        e1, r1, D1 = kra.krylov_miobi_sharded(kra.DeviceMatrix(A, gpu_ctx), 3, E, 1e-6, 100, ctx=gpu_ctx)
+        e2, r2, D2 = kra.krylov_miobi(kra.DeviceMatrix(A, gpu_ctx), 3, E, 1e-6, 100, ctx=gpu_ctx)
+        np.testing.assert_array_equal(e1, e2)
+        assert r1 == pytest.approx(r2, rel=1e-12)
+        assert (abs(D1.to_scipy() - D2.to_scipy()) > 0).nnz == 0
+    finally:
+        dist.destroy_process_group()
