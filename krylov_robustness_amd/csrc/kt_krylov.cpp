@@ -20,6 +20,7 @@
 #include <memory>
 
 #include "kt_krylov.h"
+#include "kt_launch.h"
 
 namespace kt {
 
@@ -89,10 +90,79 @@ static std::vector<double> sym_eigvals(kt_context_s* ctx, int n, const std::vect
     return w;
 }
 
+// exp(sgn * M) for an n x n matrix M (host, column-major) on the device:
+// truncated Taylor of degree 18 evaluated by Paterson-Stockmeyer (powers X^2,
+// X^3, X^4 and four Horner steps in X^4) on X = sgn M / 2^s, then s
+// squarings; s = max(0, ceil(log2(||M||_1 / theta_18))) with theta_18 the
+// double-precision Taylor bound of Al-Mohy & Higham (expm(M) of
+// fun_update.m:43-59 is a scaling-and-squaring method too).
+static std::vector<double> expm_device(kt_context_s* ctx, int n, const std::vector<double>& M,
+                                       double sgn) {
+    const double theta18 = 1.0908637192900361;
+    double nrm1 = 0.0;
+    for (int j = 0; j < n; ++j) {
+        double c = 0.0;
+        for (int i = 0; i < n; ++i) c += std::fabs(M[i + (size_t)j * n]);
+        nrm1 = std::max(nrm1, c);
+    }
+    int s = 0;
+    if (nrm1 > theta18) s = (int)std::ceil(std::log2(nrm1 / theta18));
+    const double scale = sgn * std::ldexp(1.0, -s);
+    std::vector<double> Xh(M.size());
+    for (size_t t = 0; t < M.size(); ++t) Xh[t] = scale * M[t];
+    const size_t nn = (size_t)n * n;
+    DevBuf buf;
+    buf.ensure(sizeof(double) * nn * 6);
+    double* X1 = buf.as<double>();
+    double* X2 = X1 + nn;
+    double* X3 = X2 + nn;
+    double* X4 = X3 + nn;
+    double* T = X4 + nn;
+    double* U = T + nn;
+    hipStream_t st = ctx->stream;
+    KT_HIP(hipMemcpyAsync(X1, Xh.data(), sizeof(double) * nn, hipMemcpyHostToDevice, st));
+    const double one = 1.0, zero = 0.0;
+    auto mm = [&](const double* A, const double* B, double* C) {
+        if (rocblas_dgemm(blas(ctx), rocblas_operation_none, rocblas_operation_none, n, n, n, &one, A, n,
+                          B, n, &zero, C, n) != rocblas_status_success)
+            fail(KT_ERR_HIP, "rocblas_dgemm(expm) failed");
+    };
+    mm(X1, X1, X2);
+    mm(X2, X1, X3);
+    mm(X2, X2, X4);
+    double c[19];
+    c[0] = 1.0;
+    for (int k = 1; k <= 18; ++k) c[k] = c[k - 1] / k;
+    // T = B_4 = c16 I + c17 X + c18 X^2;  T = T X^4 + B_k, k = 3..0
+    KT_HIP(launch_poly4(n, 0.0, nullptr, c[16], c[17], X1, c[18], X2, 0.0, nullptr, T, st));
+    for (int k = 3; k >= 0; --k) {
+        mm(T, X4, U);
+        KT_HIP(launch_poly4(n, 1.0, U, c[4 * k], c[4 * k + 1], X1, c[4 * k + 2], X2, c[4 * k + 3], X3, T, st));
+    }
+    for (int q = 0; q < s; ++q) {  // squaring
+        mm(T, T, U);
+        std::swap(T, U);
+    }
+    std::vector<double> F(nn);
+    KT_HIP(hipMemcpyAsync(F.data(), T, sizeof(double) * nn, hipMemcpyDeviceToHost, st));
+    KT_HIP(hipStreamSynchronize(st));
+    return F;
+}
+
 // f(M) for symmetric M (fun_update.m:43-59 maps exp/sinh/cosh/sin/cos/log/sqrt
-// to expm/funm/logm/sqrtm; on a symmetric matrix all equal V f(L) V').
+// to expm/funm/logm/sqrtm; on a symmetric matrix all equal V f(L) V').  Above
+// the host-eig size, exp/sinh/cosh take the reference's own route, expm
+// (scaling and squaring on the device): (expm(M) -+ expm(-M)) / 2.
 static std::vector<double> sym_matfun(kt_context_s* ctx, int n, const std::vector<double>& M,
                                       int fun) {
+    if (n > 160 && (fun == KT_FUN_EXP || fun == KT_FUN_SINH || fun == KT_FUN_COSH)) {
+        std::vector<double> E = expm_device(ctx, n, M, 1.0);
+        if (fun == KT_FUN_EXP) return E;
+        const std::vector<double> Em = expm_device(ctx, n, M, -1.0);
+        const double sg = fun == KT_FUN_SINH ? -1.0 : 1.0;
+        for (size_t t = 0; t < E.size(); ++t) E[t] = 0.5 * (E[t] + sg * Em[t]);
+        return E;
+    }
     std::vector<double> w(n), V((size_t)n * n), F((size_t)n * n);
     sym_eig(ctx, n, M.data(), w.data(), V.data());
     if (n <= 160) {

@@ -170,3 +170,24 @@ def test_trace_fun_update_leaf_candidates(kra, gpu_ctx):
         assert xm == pytest.approx(ref, rel=1e-9, abs=1e-11)
         assert xm == pytest.approx(ko.exact_trace_update(A, U, B), rel=1e-8, abs=1e-10)
         assert abs(it - it_ref) <= 1
+
+
+@pytest.mark.parametrize("fun", ["exp", "sinh", "cosh"])
+def test_fun_update_wide_block_device_expm(kra, gpu_ctx, fun):
+    """A 48-column block (30 edges' worth, as config 3) makes the projection
+    exceed 160 after four steps, where f(Gm) switches to the device
+    scaling-and-squaring expm (fun_update.m:43-59 maps sinh/cosh to
+    (expm(M) -+ expm(-M))/2); vs the oracle (scipy expm) on the same block."""
+    A = load_graph("rome")
+    n = A.shape[0]
+    rng = np.random.default_rng(11)
+    rows = rng.choice(n, 48, replace=False)
+    U = np.zeros((n, 48))
+    U[rows, np.arange(48)] = 1.0
+    Bh = rng.normal(scale=0.05, size=(48, 48))
+    B = (Bh + Bh.T) / 2
+    Xm, it, _, Um = kra.fun_update(kra.DeviceMatrix(A, gpu_ctx), U, B, fun, 1e-9, 8, ctx=gpu_ctx)
+    Xo, ito, _, Uo = ko.fun_update(A, U, B, fun, 1e-9, 8)
+    assert Xm.shape[0] > 160 and it == ito
+    P, Po = Um @ Xm @ Um.T, Uo @ Xo @ Uo.T
+    np.testing.assert_allclose(P, Po, atol=1e-10 * np.abs(Po).max())
