@@ -224,6 +224,65 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
         matmul(2, 2, 2, R, B, RB);
         matmul(2, 2, 2, RB, Rt, run[c].Cm);
     }
+    static const bool host_mode = getenv("KT_PAIRS_HOST") != nullptr;
+    if (!host_mode) {
+        // Device mode: the projected eigenproblems, Xm and the stop masks of
+        // every candidate run on the device (k_pair_eig), so the Lanczos
+        // steps are queued back to back; the host only polls the active
+        // count of the previous step and stops queuing once it reaches 0 (a
+        // step queued after that is discarded: done candidates are frozen).
+        const int nnmax = 2 * it;
+        const int64_t sstride = 2 * (int64_t)nnmax * nnmax + 3 * (int64_t)nnmax;
+        ws.pair_hist.ensure(sizeof(double) * (size_t)it * C * 11);
+        ws.pair_state.ensure(sizeof(double) * (size_t)C * 8 + sizeof(double) * 4 * (size_t)C);
+        ws.pair_scratch.ensure(sizeof(double) * (size_t)C * sstride);
+        ws.pair_active.ensure(sizeof(int) * 2);
+        ws.pair_active_host.ensure(sizeof(int) * 2);
+        double* hist = ws.pair_hist.as<double>();
+        double* state = ws.pair_state.as<double>();
+        double* dcm = state + (size_t)C * 8;
+        int* act_dev = ws.pair_active.as<int>();
+        int* act_host = ws.pair_active_host.as<int>();
+        std::vector<double> cm((size_t)4 * C);
+        for (int c = 0; c < C; ++c)
+            for (int t = 0; t < 4; ++t) cm[(size_t)4 * c + t] = run[c].Cm[t];
+        KT_HIP(hipMemsetAsync(state, 0, sizeof(double) * (size_t)C * 8, ctx->stream));
+        KT_HIP(hipMemcpyAsync(dcm, cm.data(), sizeof(double) * cm.size(), hipMemcpyHostToDevice, ctx->stream));
+        int cur = 0, prev = -1, w = 1;
+        for (int j = 1; j <= it; ++j) {
+            for (int c0 = 0; c0 < CP; c0 += 128)  // w = A * w   (lanczos_krylov.m:81)
+                spmm(A, S[cur] + c0, CP, S[w] + c0, CP, std::min(128, cols - c0));
+            double* hj = hist + (size_t)(j - 1) * C * 11;
+            KT_HIP(launch_pairs_orth(C, (int)n, ctx->num_cu, prev >= 0 ? S[prev] : nullptr, S[cur], S[w], CP,
+                                     ws.pair_coef.as<double>(), ws.pair_part.as<double>(), hj, ctx->stream));
+            KT_HIP(launch_pair_eig(C, j, it, fun, tol, hist, dcm, ws.pair_scratch.as<double>(), sstride,
+                                   state, act_dev + (j & 1), ctx->stream));
+            KT_HIP(hipMemcpyAsync(act_host + (j & 1), act_dev + (j & 1), sizeof(int), hipMemcpyDeviceToHost,
+                                  ctx->stream));
+            KT_HIP(hipEventRecord(ev[j & 1], ctx->stream));
+            const int freed = prev >= 0 ? prev : 3 - cur - w;
+            prev = cur;
+            cur = w;
+            w = freed;
+            if (j >= 2) {  // poll the previous step while this one runs
+                KT_HIP(hipEventSynchronize(ev[(j - 1) & 1]));
+                if (act_host[(j - 1) & 1] == 0) break;
+            }
+        }
+        KT_HIP(hipStreamSynchronize(ctx->stream));
+        lap(t_gpu);
+        std::vector<double> sv((size_t)C * 8);
+        KT_HIP(hipMemcpy(sv.data(), state, sizeof(double) * sv.size(), hipMemcpyDeviceToHost));
+        for (int c = 0; c < C; ++c) {
+            Xm[c] = sv[(size_t)8 * c + 2];
+            if (iter) iter[c] = (int)sv[(size_t)8 * c + 3];
+            if (lucky) lucky[c] = sv[(size_t)8 * c + 4] != 0.0 ? 1 : 0;
+        }
+        if (timing)
+            fprintf(stderr, "[kt pairs] device mode C=%d n=%lld setup %.3f ms  loop %.3f ms\n", C,
+                    (long long)n, t_setup, t_gpu);
+        return;
+    }
     // Step j's device work (SpMM + CGS2/QR + copy of its coefficients) is
     // queued before the host processes step j-1, so the host eig work of
     // one step overlaps the device work of the next.  A step launched after

@@ -104,6 +104,8 @@ struct Workspace {
     // per-candidate coefficients / partials / host records
     DevBuf pair_blk[3], pair_idx, pair_coef, pair_part, pair_hr;
     PinnedBuf pair_host[2];
+    DevBuf pair_hist, pair_state, pair_scratch, pair_active;  // device-mode candidate state
+    PinnedBuf pair_active_host;
     DevBuf ts_V, ts_part, ts_small;  // tall-skinny Householder QR (kt_tsqr.hip)
 };
 

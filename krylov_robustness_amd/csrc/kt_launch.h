@@ -41,6 +41,10 @@ hipError_t launch_pairs_orth(int C, int n, int num_cu, const double* prev, const
                              double* W, int ld, double* coef, double* part, double* hr,
                              hipStream_t st);
 size_t pairs_part_doubles(int n, int C, int num_cu);
+// per-candidate projected eigenproblems + stop logic; state C x 8 doubles
+hipError_t launch_pair_eig(int C, int j, int it, int fun, double tol, const double* hist,
+                           const double* Cm, double* scratch, int64_t sstride, double* state,
+                           int* active, hipStream_t st);
 // tall-skinny Householder QR (kt_tsqr.hip)
 int ts_nrb(int n, int num_cu);
 hipError_t launch_ts_reflectors(int n, int bs, int BP, double* W, int ld, double* V, double* pivot,

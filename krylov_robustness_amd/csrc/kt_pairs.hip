@@ -245,6 +245,405 @@ __global__ __launch_bounds__(256) void k_pairs_coef(int C, int nrb, const double
     }
 }
 
+// ---------------------------------------------------------------------------
+// Per-candidate projected eigenproblems on the device (trace_fun_update.m:
+// 71-118 for every candidate of a batch, one thread per candidate): build
+// the 2j x 2j block-tridiagonal Gm from the step history, tGm = Gm + Cm,
+// symmetrise, eigenvalues by Householder tridiagonalisation + implicit QL
+// (the host kt_dense.cpp routine), Xm = sum f(d1) - f(d2), lag-2 stop and
+// lucky breakdown.  Done candidates are frozen, so the Lanczos loop can run
+// ahead of the host.
+// ---------------------------------------------------------------------------
+__device__ double dev_fscalar(int fun, double x) {
+    switch (fun) {
+    case 0: return exp(x);
+    case 1: return sinh(x);
+    case 2: return cosh(x);
+    case 3: return sin(x);
+    case 4: return cos(x);
+    case 5: return log(x);
+    case 6: return sqrt(x);
+    }
+    return 0.0;
+}
+
+// eigenvalues (ascending, in d) of the symmetric n x n column-major `a`
+// (destroyed); e: n scratch
+__device__ void dev_sym_eigvals(int n, double* a, double* d, double* e) {
+    for (int i = n - 1; i > 0; --i) {  // tred2, values only
+        const int l = i - 1;
+        double h = 0.0, scale = 0.0;
+        if (l > 0) {
+            for (int k = 0; k <= l; ++k) scale += fabs(a[i + k * n]);
+            if (scale == 0.0) {
+                e[i] = a[i + l * n];
+            } else {
+                for (int k = 0; k <= l; ++k) {
+                    a[i + k * n] /= scale;
+                    h += a[i + k * n] * a[i + k * n];
+                }
+                double f = a[i + l * n];
+                double g = (f >= 0.0 ? -sqrt(h) : sqrt(h));
+                e[i] = scale * g;
+                h -= f * g;
+                a[i + l * n] = f - g;
+                f = 0.0;
+                for (int j = 0; j <= l; ++j) {
+                    a[j + i * n] = a[i + j * n] / h;
+                    g = 0.0;
+                    for (int k = 0; k <= j; ++k) g += a[j + k * n] * a[i + k * n];
+                    for (int k = j + 1; k <= l; ++k) g += a[k + j * n] * a[i + k * n];
+                    e[j] = g / h;
+                    f += e[j] * a[i + j * n];
+                }
+                const double hh = f / (h + h);
+                for (int j = 0; j <= l; ++j) {
+                    f = a[i + j * n];
+                    e[j] = g = e[j] - hh * f;
+                    for (int k = 0; k <= j; ++k) a[j + k * n] -= (f * e[k] + g * a[i + k * n]);
+                }
+            }
+        } else {
+            e[i] = a[i + l * n];
+        }
+        d[i] = h;
+    }
+    d[0] = 0.0;
+    e[0] = 0.0;
+    for (int i = 0; i < n; ++i) d[i] = a[i + i * n];
+    // implicit QL, values only (tql2 without vectors)
+    for (int i = 1; i < n; ++i) e[i - 1] = e[i];
+    e[n - 1] = 0.0;
+    const double eps = 2.220446049250313e-16;
+    for (int l = 0; l < n; ++l) {
+        int iter = 0;
+        for (;;) {
+            int m = l;
+            for (; m < n - 1; ++m) {
+                const double dd = fabs(d[m]) + fabs(d[m + 1]);
+                if (fabs(e[m]) <= eps * dd) break;
+            }
+            if (m == l || iter++ == 200) break;
+            double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+            double r = hypot(g, 1.0);
+            g = d[m] - d[l] + e[l] / (g + copysign(r, g));
+            double sn = 1.0, cs = 1.0, p = 0.0;
+            bool deflated = false;
+            for (int i = m - 1; i >= l; --i) {
+                const double f = sn * e[i];
+                const double b = cs * e[i];
+                r = hypot(f, g);
+                e[i + 1] = r;
+                if (r == 0.0) {
+                    d[i + 1] -= p;
+                    e[m] = 0.0;
+                    deflated = true;
+                    break;
+                }
+                sn = f / r;
+                cs = g / r;
+                g = d[i + 1] - p;
+                r = (d[i] - g) * sn + 2.0 * cs * b;
+                p = sn * r;
+                d[i + 1] = g + p;
+                g = cs * r - b;
+            }
+            if (deflated) continue;
+            d[l] -= p;
+            e[l] = g;
+            e[m] = 0.0;
+        }
+    }
+    for (int i = 1; i < n; ++i) {  // insertion sort
+        const double v = d[i];
+        int k = i - 1;
+        while (k >= 0 && d[k] > v) {
+            d[k + 1] = d[k];
+            --k;
+        }
+        d[k + 1] = v;
+    }
+}
+
+// state per candidate (doubles): [0] Xstop(1) [1] Xstop(2) [2] Xm [3] iter
+// [4] lucky [5] done
+enum : int { PS_X0 = 0, PS_X1 = 1, PS_XM = 2, PS_ITER = 3, PS_LUCKY = 4, PS_DONE = 5, PS_N = 8 };
+
+__global__ void k_pair_eig(int C, int j, int it, int fun, double tol,
+                           const double* __restrict__ hist, const double* __restrict__ Cm,
+                           double* __restrict__ scratch, int64_t sstride,
+                           double* __restrict__ state) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double* st = state + (int64_t)c * PS_N;
+    if (st[PS_DONE] != 0.0) return;
+    const int nn = 2 * j;
+    double* G = scratch + (int64_t)c * sstride;
+    double* T = G + (size_t)nn * nn;
+    double* d1 = T + (size_t)nn * nn;
+    double* d2 = d1 + nn;
+    double* e = d2 + nn;
+    for (int t = 0; t < nn * nn; ++t) G[t] = 0.0;
+    for (int b = 0; b < j; ++b) {  // lanczos_krylov.m:85-90 block placement
+        const double* h = hist + ((int64_t)b * C + c) * 11;
+        // D = h(cur) at (2b, 2b);  P = h(prev) at (2b-2, 2b);  R at (2b+2, 2b)
+        G[(2 * b) + (2 * b) * nn] = h[2];
+        G[(2 * b + 1) + (2 * b) * nn] = h[3];
+        G[(2 * b) + (2 * b + 1) * nn] = h[6];
+        G[(2 * b + 1) + (2 * b + 1) * nn] = h[7];
+        if (b >= 1) {
+            G[(2 * b - 2) + (2 * b) * nn] = h[0];
+            G[(2 * b - 1) + (2 * b) * nn] = h[1];
+            G[(2 * b - 2) + (2 * b + 1) * nn] = h[4];
+            G[(2 * b - 1) + (2 * b + 1) * nn] = h[5];
+        }
+        if (b + 1 < j) {
+            G[(2 * b + 2) + (2 * b) * nn] = h[8];
+            G[(2 * b + 2) + (2 * b + 1) * nn] = h[9];
+            G[(2 * b + 3) + (2 * b + 1) * nn] = h[10];
+        }
+    }
+    for (int t = 0; t < nn * nn; ++t) T[t] = G[t];
+    const double* cm = Cm + (int64_t)c * 4;
+    T[0] += cm[0];
+    T[1] += cm[1];
+    T[nn] += cm[2];
+    T[nn + 1] += cm[3];
+    for (int b = 0; b < nn; ++b)  // (X + X') / 2   trace_fun_update.m:78-81
+        for (int a = 0; a < b; ++a) {
+            double x = 0.5 * (G[a + b * nn] + G[b + a * nn]);
+            G[a + b * nn] = G[b + a * nn] = x;
+            x = 0.5 * (T[a + b * nn] + T[b + a * nn]);
+            T[a + b * nn] = T[b + a * nn] = x;
+        }
+    dev_sym_eigvals(nn, T, d1, e);
+    dev_sym_eigvals(nn, G, d2, e);
+    double xm = 0.0;  // :85-89
+    if (fun == 0) {
+        for (int i = 0; i < nn; ++i) xm += exp(d1[i]) * (1.0 - exp(d2[i] - d1[i]));
+    } else {
+        for (int i = 0; i < nn; ++i) xm += dev_fscalar(fun, d1[i]) - dev_fscalar(fun, d2[i]);
+    }
+    const double* hj = hist + ((int64_t)(j - 1) * C + c) * 11;
+    const bool lucky = sqrt(hj[8] * hj[8] + hj[9] * hj[9] + hj[10] * hj[10]) < 1e-8;  // :91-93
+    st[PS_XM] = xm;
+    st[PS_LUCKY] = lucky ? 1.0 : 0.0;
+    bool stop = false;
+    if (j <= 2) {  // :104-118, lag d = 2
+        st[PS_X0 + j - 1] = xm;
+    } else if (fabs(xm - st[PS_X0]) < tol) {
+        stop = true;
+    } else {
+        st[PS_X0] = st[PS_X1];
+        st[PS_X1] = xm;
+    }
+    if (stop || lucky || j == it) {
+        st[PS_DONE] = 1.0;
+        st[PS_ITER] = j;
+    }
+}
+
+// ---- one WAVE per candidate (2j <= 56): the two projections live in LDS ----
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Eigenvalues of the symmetric n x n row-major LDS matrix A (n <= 64,
+// destroyed): Householder tridiagonalisation with lane i owning row i of the
+// trailing block, then Sturm-count bisection with lane k finding the k-th
+// smallest eigenvalue (so the result is already sorted).  d, e, v, w: LDS
+// vectors of length n.  Returns this lane's eigenvalue (lanes >= n: 0).
+__device__ double wave_sym_eig(int n, double* A, double* d, double* e, double* v, double* w) {
+    const int lane = threadIdx.x & 63;
+    for (int k = 0; k + 2 < n; ++k) {  // dsytd2 (lower), reflector on A(k+1:n, k)
+        const int m = n - k - 1;
+        const double xi = (lane < m) ? A[(k + 1 + lane) * n + k] : 0.0;
+        const double alpha = __shfl(xi, 0, 64);
+        const double xn2 = wave_sum64(lane >= 1 ? xi * xi : 0.0);
+        double tau = 0.0, beta = alpha, scal = 1.0;
+        if (xn2 != 0.0) {
+            beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
+            tau = (beta - alpha) / beta;
+            scal = 1.0 / (alpha - beta);
+        }
+        if (lane == 0) {
+            d[k] = A[k * n + k];
+            e[k] = beta;
+        }
+        if (lane < m) v[lane] = (lane == 0) ? 1.0 : xi * scal;
+        __syncthreads();
+        if (tau != 0.0) {
+            // p = tau * A22 v ; w = p - (tau/2)(p'v) v ; A22 -= v w' + w v'
+            double p = 0.0;
+            if (lane < m)
+                for (int j = 0; j < m; ++j) p = fma(A[(k + 1 + lane) * n + (k + 1 + j)], v[j], p);
+            p *= tau;
+            const double pv = wave_sum64(lane < m ? p * v[lane] : 0.0);
+            const double wi = p - 0.5 * tau * pv * (lane < m ? v[lane] : 0.0);
+            if (lane < m) w[lane] = wi;
+            __syncthreads();
+            if (lane < m) {
+                const double vi = v[lane];
+                for (int j = 0; j < m; ++j)
+                    A[(k + 1 + lane) * n + (k + 1 + j)] -= vi * w[j] + wi * v[j];
+            }
+        }
+        __syncthreads();
+    }
+    if (lane == 0) {
+        if (n >= 2) {
+            d[n - 2] = A[(n - 2) * n + (n - 2)];
+            e[n - 2] = A[(n - 1) * n + (n - 2)];
+        }
+        d[n - 1] = A[(n - 1) * n + (n - 1)];
+    }
+    __syncthreads();
+    // Gershgorin interval, then bisection on the Sturm count
+    double lo = 0.0, hi = 0.0, emax2 = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i + 1 < n ? fabs(e[i]) : 0.0);
+        lo = (i == 0) ? d[i] - r : fmin(lo, d[i] - r);
+        hi = (i == 0) ? d[i] + r : fmax(hi, d[i] + r);
+        if (i + 1 < n) emax2 = fmax(emax2, e[i] * e[i]);
+    }
+    const double span = fmax(hi - lo, 1e-300);
+    lo -= 2.2e-16 * span + 1e-300;
+    hi += 2.2e-16 * span + 1e-300;
+    const double pivmin = fmax(2.2250738585072014e-308 * fmax(1.0, emax2), 1e-300);
+    if (lane >= n) return 0.0;
+    double a = lo, b = hi;
+    for (int itb = 0; itb < 80; ++itb) {
+        const double x = 0.5 * (a + b);
+        if (x <= a || x >= b) break;
+        int cnt = 0;  // eigenvalues < x
+        double q = d[0] - x;
+        if (fabs(q) < pivmin) q = -pivmin;
+        cnt += q < 0.0;
+        for (int i = 1; i < n; ++i) {
+            q = d[i] - x - e[i - 1] * e[i - 1] / q;
+            if (fabs(q) < pivmin) q = -pivmin;
+            cnt += q < 0.0;
+        }
+        if (cnt > lane) b = x;  // the (lane+1)-th smallest is below x
+        else a = x;
+    }
+    return 0.5 * (a + b);
+}
+
+__global__ __launch_bounds__(64) void k_pair_eig_wave(int C, int j, int it, int fun, double tol,
+                                                      const double* __restrict__ hist,
+                                                      const double* __restrict__ Cm,
+                                                      double* __restrict__ state) {
+    extern __shared__ double sm[];
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
+    double* st = state + (int64_t)c * PS_N;
+    if (st[PS_DONE] != 0.0) return;
+    const int nn = 2 * j;
+    double* G = sm;
+    double* T = G + nn * nn;
+    double* d = T + nn * nn;
+    double* e = d + nn;
+    double* v = e + nn;
+    double* w = v + nn;
+    for (int t = lane; t < nn * nn; t += 64) G[t] = 0.0;
+    __syncthreads();
+    for (int b = lane; b < j; b += 64) {  // row-major G[r * nn + col]
+        const double* h = hist + ((int64_t)b * C + c) * 11;
+        G[(2 * b) * nn + 2 * b] = h[2];
+        G[(2 * b + 1) * nn + 2 * b] = h[3];
+        G[(2 * b) * nn + 2 * b + 1] = h[6];
+        G[(2 * b + 1) * nn + 2 * b + 1] = h[7];
+        if (b >= 1) {
+            G[(2 * b - 2) * nn + 2 * b] = h[0];
+            G[(2 * b - 1) * nn + 2 * b] = h[1];
+            G[(2 * b - 2) * nn + 2 * b + 1] = h[4];
+            G[(2 * b - 1) * nn + 2 * b + 1] = h[5];
+        }
+        if (b + 1 < j) {
+            G[(2 * b + 2) * nn + 2 * b] = h[8];
+            G[(2 * b + 2) * nn + 2 * b + 1] = h[9];
+            G[(2 * b + 3) * nn + 2 * b + 1] = h[10];
+        }
+    }
+    __syncthreads();
+    for (int t = lane; t < nn * nn; t += 64) T[t] = G[t];
+    __syncthreads();
+    if (lane == 0) {
+        const double* cm = Cm + (int64_t)c * 4;  // column-major 2x2
+        T[0] += cm[0];
+        T[nn] += cm[1];
+        T[1] += cm[2];
+        T[nn + 1] += cm[3];
+    }
+    __syncthreads();
+    for (int t = lane; t < nn * nn; t += 64) {  // (X + X') / 2   :78-81
+        const int r = t / nn, q = t % nn;
+        if (q < r) {
+            const double g = 0.5 * (G[r * nn + q] + G[q * nn + r]);
+            const double x = 0.5 * (T[r * nn + q] + T[q * nn + r]);
+            G[r * nn + q] = G[q * nn + r] = g;
+            T[r * nn + q] = T[q * nn + r] = x;
+        }
+    }
+    __syncthreads();
+    const double l1 = wave_sym_eig(nn, T, d, e, v, w);
+    __syncthreads();
+    const double l2 = wave_sym_eig(nn, G, d, e, v, w);
+    double term = 0.0;  // :85-89 (lane k holds the k-th smallest of each)
+    if (lane < nn)
+        term = (fun == 0) ? exp(l1) * (1.0 - exp(l2 - l1)) : dev_fscalar(fun, l1) - dev_fscalar(fun, l2);
+    const double xm = wave_sum64(term);
+    if (lane == 0) {
+        const double* hj = hist + ((int64_t)(j - 1) * C + c) * 11;
+        const bool lucky = sqrt(hj[8] * hj[8] + hj[9] * hj[9] + hj[10] * hj[10]) < 1e-8;
+        st[PS_XM] = xm;
+        st[PS_LUCKY] = lucky ? 1.0 : 0.0;
+        bool stop = false;
+        if (j <= 2) {
+            st[PS_X0 + j - 1] = xm;
+        } else if (fabs(xm - st[PS_X0]) < tol) {
+            stop = true;
+        } else {
+            st[PS_X0] = st[PS_X1];
+            st[PS_X1] = xm;
+        }
+        if (stop || lucky || j == it) {
+            st[PS_DONE] = 1.0;
+            st[PS_ITER] = j;
+        }
+    }
+}
+
+// active[0] = number of candidates not done
+__global__ void k_pair_active(int C, const double* __restrict__ state, int* __restrict__ active) {
+    __shared__ int red[256];
+    int cnt = 0;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) cnt += state[(int64_t)c * PS_N + PS_DONE] == 0.0;
+    red[threadIdx.x] = cnt;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) active[0] = red[0];
+}
+
+hipError_t launch_pair_eig(int C, int j, int it, int fun, double tol, const double* hist,
+                           const double* Cm, double* scratch, int64_t sstride, double* state,
+                           int* active, hipStream_t st) {
+    if (2 * j <= 56) {  // 2 nn^2 + 4 nn doubles <= 52 KB of LDS
+        const size_t lds = sizeof(double) * (2 * (size_t)(2 * j) * (2 * j) + 4 * (size_t)(2 * j));
+        k_pair_eig_wave<<<C, 64, lds, st>>>(C, j, it, fun, tol, hist, Cm, state);
+    } else {
+        k_pair_eig<<<(C + 63) / 64, 64, 0, st>>>(C, j, it, fun, tol, hist, Cm, scratch, sstride, state);
+    }
+    k_pair_active<<<1, 256, 0, st>>>(C, state, active);
+    return hipGetLastError();
+}
+
 // U_c = [e_i, e_j] (krylov_miobi.m:82-84); X pre-zeroed.
 __global__ void k_pair_select(int C, const int* __restrict__ ii, const int* __restrict__ jj,
                               double* __restrict__ X, int ld) {
