@@ -224,7 +224,7 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
         matmul(2, 2, 2, R, B, RB);
         matmul(2, 2, 2, RB, Rt, run[c].Cm);
     }
-    static const bool host_mode = getenv("KT_PAIRS_HOST") != nullptr;
+    const bool host_mode = getenv("KT_PAIRS_HOST") != nullptr;
     if (!host_mode) {
         // Device mode: the projected eigenproblems, Xm and the stop masks of
         // every candidate run on the device (k_pair_eig), so the Lanczos

@@ -162,3 +162,18 @@ def test_krylov_miobi_sharded_world1(kra, gpu_ctx):
         assert (abs(D1.to_scipy() - D2.to_scipy()) > 0).nnz == 0
     finally:
         dist.destroy_process_group()
+
+
+def test_pairs_device_and_host_eig_agree(kra, gpu_ctx, monkeypatch):
+    """The device-resident per-candidate eig (one wavefront per candidate,
+    Sturm bisection) and the host path (tred2/tql2 pool) give the same scores
+    and iteration counts."""
+    A, c = _india(kra)
+    E = kra.find_top_edges(A, c, 96, "min")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    x_dev, it_dev, l_dev = kra.trace_fun_update_pairs(D, E, BREAK, 1e-10, 100, ctx=gpu_ctx)
+    monkeypatch.setenv("KT_PAIRS_HOST", "1")
+    x_host, it_host, l_host = kra.trace_fun_update_pairs(D, E, BREAK, 1e-10, 100, ctx=gpu_ctx)
+    np.testing.assert_allclose(x_dev, x_host, rtol=1e-12, atol=1e-14)
+    np.testing.assert_array_equal(it_dev, it_host)
+    np.testing.assert_array_equal(l_dev, l_host)
