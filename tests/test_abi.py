@@ -60,3 +60,27 @@ def test_missing_library_raises(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_lib.KrylovLibraryError):
         _lib.load()
+
+
+def test_every_entry_point_rejects_null_handles():
+    """Every compute entry point reports KT_ERR_ARG (or another status) for a
+    NULL matrix / context and NULL buffers -- never a crash -- and leaves a
+    message in kt_last_error()."""
+    from krylov_robustness_amd import _lib
+    lib = _lib.load()
+    skip = {"kt_abi_version", "kt_last_error", "kt_device_count", "kt_context_create",
+            "kt_context_destroy", "kt_matrix_destroy"}
+    for name, res, args in _lib.SIGNATURES:
+        if name in skip:
+            continue
+        vals = []
+        for a in args:
+            if a in (C.c_int, C.c_int64, C.c_uint64):
+                vals.append(1)
+            elif a is C.c_double:
+                vals.append(1e-8)
+            else:
+                vals.append(None)
+        st = getattr(lib, name)(*vals)
+        assert st != _lib.KT_OK, name
+        assert lib.kt_last_error(), name
