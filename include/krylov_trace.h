@@ -227,6 +227,15 @@ int kt_frechet_entries(kt_matrix_t A, int64_t k, const int64_t* oi, const int64_
 int kt_hessianfcn(kt_matrix_t A, int64_t nomega, const double* X, const double* Omega, int fun,
                   double tol, int it, double* Hes);
 
+/* Leading eigenpair of symmetric A (compute_centrality.m:15-17: [u, lambda]
+ * = eigs(A, 1); centrality = abs(u)): full-reorthogonalisation Arnoldi on
+ * the device from the ones vector, restarted from the Ritz vector, residual
+ * |h(j+1,j) y(j)| <= tol |lambda| (tol <= 0: machine epsilon); maxit = Krylov
+ * steps per restart (<= 0: 300).  v (n, nullable): unit 2-norm, sum(v) >= 0.
+ * steps (nullable): total Arnoldi steps.  Largest algebraic eigenvalue (the
+ * Perron root of an adjacency matrix). */
+int kt_eigs_leading(kt_matrix_t A, double tol, int maxit, double* lambda, double* v, int* steps);
+
 /* Per-kernel timing (HIP events recorded on the library's stream around each
  * launch of the named kernel while enabled).  kernel: 0 = spmm_gram (K1),
  * 1 = update_norm (K2).  Returns launch count and summed milliseconds. */

@@ -9,7 +9,7 @@ interface used by tests and bench.py.
 """
 from ._lib import KrylovError, KrylovLibraryError, FUN_CODES, LIB_PATH
 from .core import (Context, DeviceMatrix, default_context, device_count, expmv,
-                   frechet_entries, function_multiple_entries, hessianfcn, hessianfcn_exp,
+                   eigs_leading, frechet_entries, function_multiple_entries, hessianfcn, hessianfcn_exp,
                    hessianfcn_fun, householder_qr,
                    fun_and_grad_krylov_exp, fun_and_grad_krylov_fun, fun_update, lanczos_fmv,
                    mc_trace, normest, slq_plan, slq_quadforms, slq_trace, trace_exp,

@@ -82,6 +82,7 @@ SIGNATURES = [
     ("kt_frechet_entries", C.c_int, [_mat_p, C.c_int64, _i64p, _i64p, C.c_int, C.c_double, C.c_int,
                                      C.c_int64, _i64p, _i64p, _dp, _ip]),
     ("kt_hessianfcn", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_int, C.c_double, C.c_int, _dp]),
+    ("kt_eigs_leading", C.c_int, [_mat_p, C.c_double, C.c_int, _dp, _dp, _ip]),
     ("kt_profile_enable", C.c_int, [_ctx_p, C.c_int]),
     ("kt_profile_read", C.c_int, [_ctx_p, C.c_int, _i64p, _dp]),
     ("kt_profile_reset", C.c_int, [_ctx_p]),

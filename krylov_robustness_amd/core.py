@@ -436,3 +436,16 @@ def hessianfcn_exp(X, A, Omega, tol=1e-12, it=None, ctx: Optional[Context] = Non
 def hessianfcn_fun(X, A, Omega, f, tol=1e-12, it=None, ctx: Optional[Context] = None):
     """hessianfcn_fun.m:1."""
     return hessianfcn(X, A, Omega, f, tol, it, ctx)
+
+
+def eigs_leading(A, tol=0.0, maxit=0, ctx: Optional[Context] = None):
+    """[u, lambda] = eigs(A, 1) for symmetric A on the device (kt_eigs_leading);
+    returns (lambda, u) with ||u|| = 1, sum(u) >= 0."""
+    D = _dev(A, ctx)
+    n, _ = D.info()
+    v = np.zeros(max(n, 1))
+    lam = C.c_double()
+    st = C.c_int()
+    _lib.check(_lib.load().kt_eigs_leading(D.handle, float(tol), int(maxit), C.byref(lam), _dptr(v),
+                                           C.byref(st)))
+    return float(lam.value), v[:n]

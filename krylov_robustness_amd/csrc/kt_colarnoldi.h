@@ -13,6 +13,8 @@ class ColArnoldi {
    public:
     // starts: distinct 0-based row indices (<= 128); it: max steps
     ColArnoldi(kt_matrix_s* A, const std::vector<int64_t>& starts, int it);
+    // general start block: X host n x C column-major (C <= 128)
+    ColArnoldi(kt_matrix_s* A, const double* X, int C, int it);
     int cols() const { return C_; }
     int steps() const { return j_; }
     // one Arnoldi step for every column (arnoldi_krylov.m:78-111)
@@ -24,8 +26,14 @@ class ColArnoldi {
     // basis entries V_c(r, k) for the given rows, k < nk (nk <= steps() + 1):
     // out[(ri * nk + k) * cols() + c]
     void rows(const std::vector<int64_t>& rr, int nk, std::vector<double>& out) const;
+    // H(i, j) of column c (0-based, i <= steps(), j < steps())
+    double h(int c, int i, int j) const { return H_[c][i + (size_t)j * (it_ + 1)]; }
+    // out (host n x C column-major) = sum_{k < nk} V_k y_k, y[k * C + c]
+    void combine(const std::vector<double>& y, int nk, double* out);
 
    private:
+    void init_buffers();
+    void start_qr();
     kt_matrix_s* A_;
     kt_context_s* ctx_;
     int64_t n_;

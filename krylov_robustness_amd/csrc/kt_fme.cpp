@@ -19,8 +19,7 @@
 
 namespace kt {
 
-ColArnoldi::ColArnoldi(kt_matrix_s* A, const std::vector<int64_t>& starts, int it)
-    : A_(A), ctx_(A->ctx), n_(A->n), C_((int)starts.size()), it_(it) {
+void ColArnoldi::init_buffers() {
     if (C_ < 1 || C_ > 128) fail(KT_ERR_UNSUPPORTED, "ColArnoldi: 1..128 columns");
     P_ = pow2_at_least(C_);
     vs_ = n_ * (int64_t)P_;
@@ -30,24 +29,64 @@ ColArnoldi::ColArnoldi(kt_matrix_s* A, const std::vector<int64_t>& starts, int i
     part_.ensure(sizeof(double) * (size_t)nrb_ * P_ * (it_ + 1));
     // red: h1 | h2 | hh (it x P each) | s (P) | r (P)
     red_.ensure(sizeof(double) * ((size_t)3 * it_ * P_ + 2 * P_));
-    std::vector<int> ridx(starts.begin(), starts.end());
-    idx_.ensure(sizeof(int) * ridx.size());
+    KT_HIP(hipMemsetAsync(basis_.ptr, 0, sizeof(double) * (size_t)vs_, ctx_->stream));
+    H_.assign(C_, std::vector<double>((size_t)(it_ + 1) * it_, 0.0));
+}
+
+// [V, ~] = qr(start block, 0)   (arnoldi_krylov.m:50)
+void ColArnoldi::start_qr() {
     double* V = basis_.as<double>();
     double* sq = red_.as<double>() + (size_t)3 * it_ * P_;
     double* rr = sq + P_;
-    KT_HIP(hipMemcpyAsync(idx_.ptr, ridx.data(), sizeof(int) * ridx.size(), hipMemcpyHostToDevice,
-                          ctx_->stream));
-    KT_HIP(hipMemsetAsync(V, 0, sizeof(double) * (size_t)vs_, ctx_->stream));
-    KT_HIP(launch_col_select(C_, P_, idx_.as<int>(), V, ctx_->stream));
-    // [V, ~] = qr(e_t, 0)   (arnoldi_krylov.m:50)
     KT_HIP(launch_col_dots((int)n_, P_, 1, 0, V, V, 1, ctx_->num_cu, part_.as<double>(), sq, ctx_->stream));
     KT_HIP(launch_col_householder((int)n_, P_, sq, V, V, rr, ctx_->stream));
+}
+
+ColArnoldi::ColArnoldi(kt_matrix_s* A, const std::vector<int64_t>& starts, int it)
+    : A_(A), ctx_(A->ctx), n_(A->n), C_((int)starts.size()), it_(it) {
+    init_buffers();
+    std::vector<int> ridx(starts.begin(), starts.end());
+    idx_.ensure(sizeof(int) * ridx.size());
+    double* V = basis_.as<double>();
+    KT_HIP(hipMemcpyAsync(idx_.ptr, ridx.data(), sizeof(int) * ridx.size(), hipMemcpyHostToDevice,
+                          ctx_->stream));
+    KT_HIP(launch_col_select(C_, P_, idx_.as<int>(), V, ctx_->stream));
+    start_qr();
     uaux_.assign(C_, 0.0);
     for (int c = 0; c < C_; ++c)
         KT_HIP(hipMemcpyAsync(&uaux_[c], V + starts[c] * P_ + c, sizeof(double),
                               hipMemcpyDeviceToHost, ctx_->stream));
     KT_HIP(hipStreamSynchronize(ctx_->stream));
-    H_.assign(C_, std::vector<double>((size_t)(it_ + 1) * it_, 0.0));
+}
+
+ColArnoldi::ColArnoldi(kt_matrix_s* A, const double* X, int C, int it)
+    : A_(A), ctx_(A->ctx), n_(A->n), C_(C), it_(it) {
+    init_buffers();
+    std::vector<double> rm((size_t)n_ * P_, 0.0);
+    for (int c = 0; c < C_; ++c)
+        for (int64_t i = 0; i < n_; ++i) rm[(size_t)i * P_ + c] = X[i + (size_t)c * n_];
+    KT_HIP(hipMemcpyAsync(basis_.ptr, rm.data(), sizeof(double) * rm.size(), hipMemcpyHostToDevice,
+                          ctx_->stream));
+    start_qr();
+    uaux_.assign(C_, 0.0);
+    KT_HIP(hipStreamSynchronize(ctx_->stream));
+}
+
+void ColArnoldi::combine(const std::vector<double>& y, int nk, double* out) {
+    // W = 0; W -= V (-y)  (the column update kernel with negated weights)
+    std::vector<double> hy((size_t)nk * P_, 0.0);
+    for (int k = 0; k < nk; ++k)
+        for (int c = 0; c < C_; ++c) hy[(size_t)k * P_ + c] = -y[(size_t)k * C_ + c];
+    double* dh = red_.as<double>();  // h1 slab, it x P >= nk x P
+    if (nk > it_) fail(KT_ERR_ARG, "ColArnoldi::combine: too many blocks");
+    KT_HIP(hipMemcpyAsync(dh, hy.data(), sizeof(double) * hy.size(), hipMemcpyHostToDevice, ctx_->stream));
+    KT_HIP(hipMemsetAsync(W_.ptr, 0, sizeof(double) * (size_t)vs_, ctx_->stream));
+    KT_HIP(launch_col_update((int)n_, P_, nk, vs_, basis_.as<double>(), dh, W_.as<double>(), ctx_->stream));
+    std::vector<double> rm((size_t)n_ * P_);
+    KT_HIP(hipMemcpyAsync(rm.data(), W_.ptr, sizeof(double) * rm.size(), hipMemcpyDeviceToHost, ctx_->stream));
+    KT_HIP(hipStreamSynchronize(ctx_->stream));
+    for (int c = 0; c < C_; ++c)
+        for (int64_t i = 0; i < n_; ++i) out[i + (size_t)c * n_] = rm[(size_t)i * P_ + c];
 }
 
 void ColArnoldi::step() {
@@ -252,9 +291,73 @@ void function_multiple_entries_impl(kt_matrix_s* A, int64_t k, const int64_t* oi
     if (iter_out) *iter_out = iter;
 }
 
+// Leading eigenpair of symmetric A (compute_centrality.m:15-17, eigs(A, 1)):
+// full-reorthogonalisation Arnoldi (ColArnoldi) from the ones vector,
+// explicitly restarted from the Ritz vector; stops when the Ritz residual
+// |h(j+1, j) y(j)| <= tol |theta|.  v: unit 2-norm, sign fixed so sum(v) >= 0.
+double eigs_leading_impl(kt_matrix_s* A, double tol, int maxit, double* v, int* steps_out) {
+    const int64_t n = A->n;
+    if (n == 0) return 0.0;
+    if (tol <= 0.0) tol = 2.220446049250313e-16;
+    const int m = (int)std::min<int64_t>(std::max(maxit > 0 ? maxit : 300, 2), std::max<int64_t>(n, 2));
+    std::vector<double> x(n, 1.0), G, w, Q;
+    double theta = 0.0;
+    int total = 0;
+    for (int restart = 0; restart < 20; ++restart) {
+        ColArnoldi ca(A, x.data(), 1, std::min<int64_t>(m, n));
+        int j = 0;
+        bool conv = false;
+        std::vector<double> y;
+        for (j = 1; j <= ca.steps() + 1 && j <= std::min<int64_t>(m, n); ++j) {
+            ca.step();
+            ca.gm(0, G);
+            sym_eig_small(j, G, w, Q);
+            theta = w[j - 1];
+            y.assign(Q.begin() + (size_t)(j - 1) * j, Q.begin() + (size_t)j * j);
+            const double res = std::fabs(ca.h(0, j, j - 1) * y[j - 1]);
+            if (res <= tol * std::fabs(theta) || j == n) {
+                conv = true;
+                break;
+            }
+        }
+        if (j > ca.steps()) j = ca.steps();
+        total += j;
+        ca.combine(y, j, x.data());
+        double nrm = 0.0, sum = 0.0;
+        for (double t : x) {
+            nrm += t * t;
+            sum += t;
+        }
+        nrm = std::sqrt(nrm);
+        const double sg = sum < 0.0 ? -1.0 : 1.0;
+        for (double& t : x) t *= sg / nrm;
+        if (conv) break;
+    }
+    if (v) std::copy(x.begin(), x.end(), v);
+    if (steps_out) *steps_out = total;
+    return theta;
+}
+
 }  // namespace kt
 
 using namespace kt;
+
+extern "C" int kt_eigs_leading(kt_matrix_t A, double tol, int maxit, double* lambda, double* v,
+                               int* steps) {
+    try {
+        if (!A || !lambda) fail(KT_ERR_ARG, "NULL argument");
+        KT_HIP(hipSetDevice(A->ctx->device));
+        require_symmetric(A, "EIGS:: symmetric A required");
+        *lambda = eigs_leading_impl(A, tol, maxit, v, steps);
+    } catch (const Status& s) {
+        set_error(s.msg);
+        return s.code;
+    } catch (const std::bad_alloc&) {
+        set_error("host allocation failed");
+        return KT_ERR_ALLOC;
+    }
+    return KT_OK;
+}
 
 extern "C" int kt_function_multiple_entries(kt_matrix_t A, int64_t k, const int64_t* oi,
                                             const int64_t* oj, int fun, double tol, int it,

@@ -213,10 +213,17 @@ def find_top_missing_edges(A, centrality, num, order="min"):
     raise ValueError(f"unknown order {order!r}")
 
 
-def compute_centrality(A, kind="eig"):
-    """compute_centrality.m (host helper; 'eig' = |leading eigenvector|, 'deg')."""
+def compute_centrality(A, kind="eig", ctx: Optional[Context] = None):
+    """compute_centrality.m: 'eig' = abs(leading eigenvector) (:15-17), on the
+    device when A is a DeviceMatrix (kt_eigs_leading), else scipy eigsh;
+    'deg' = column sums (:18-19)."""
     import scipy.sparse as sp
     import scipy.sparse.linalg as sla
+    if isinstance(A, DeviceMatrix):
+        if kind == "deg":
+            return np.asarray(A.to_scipy().sum(axis=0)).ravel()
+        from .core import eigs_leading
+        return np.abs(eigs_leading(A, ctx=ctx)[1])
     A = sp.csr_matrix(A, dtype=np.float64)
     if kind == "deg":
         return np.asarray(A.sum(axis=0)).ravel()
@@ -238,7 +245,7 @@ def greedy_krylov(A, k, Q=0, centrality=None, order="mult", tol=1e-12, it=None, 
     if miobi == "break" and S.nnz < 2 * k:  # :54-56
         raise _lib.KrylovError(_lib.KT_ERR_ARG, "GREEDY_KRYLOV:: edges to be removed are more than edges in the network")
     if centrality is None:
-        centrality = compute_centrality(S, "eig")
+        centrality = compute_centrality(D, "eig", ctx=ctx)
     edges = np.zeros((0, 2), dtype=np.int64)
     rob = 0.0
     top = None
