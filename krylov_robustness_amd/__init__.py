@@ -17,6 +17,8 @@ from .core import (Context, DeviceMatrix, default_context, device_count, expmv,
 from .greedy import (compute_centrality, default_greedy_tol, find_top_edges,
                      find_top_missing_edges, greedy_krylov, krylov_miobi, krylov_miobi_sharded,
                      miobi_loop, select_extreme, trace_fun_update_pairs)
+from . import datasets, matv73
+from .datasets import load_problem, load_unweighted, prepare_unweighted, prepare_weighted
 
 __all__ = [
     "KrylovError", "KrylovLibraryError", "FUN_CODES", "LIB_PATH", "Context", "DeviceMatrix",
@@ -25,5 +27,6 @@ __all__ = [
     "mc_trace", "trace_exp", "expmv", "lanczos_fmv", "trace_fun_update_pairs", "krylov_miobi",
     "greedy_krylov", "find_top_edges", "find_top_missing_edges", "compute_centrality",
     "default_greedy_tol", "krylov_miobi_sharded", "miobi_loop", "select_extreme", "function_multiple_entries", "householder_qr", "frechet_entries",
-    "hessianfcn", "hessianfcn_exp", "hessianfcn_fun",
+    "hessianfcn", "hessianfcn_exp", "hessianfcn_fun", "eigs_leading", "datasets", "matv73",
+    "load_problem", "load_unweighted", "prepare_unweighted", "prepare_weighted",
 ]

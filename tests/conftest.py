@@ -32,6 +32,14 @@ def load_graph(name):
                          shape=(n, n))
 
 
+def load_v73_graph(name):
+    """A prepared MAT v7.3 dataset (drugs / as_735 / collegemsg), make_golden.py --v73."""
+    z = np.load(os.path.join(GOLDEN, "v73_graphs.npz"))
+    n = int(z[name + "__n"][0])
+    return sp.csr_matrix((z[name + "__data"], z[name + "__indices"], z[name + "__indptr"]),
+                         shape=(n, n))
+
+
 def golden_values():
     with open(os.path.join(GOLDEN, "values.json")) as f:
         return json.load(f)

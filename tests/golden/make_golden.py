@@ -82,9 +82,73 @@ def main_hawaii():
     print("hawaii", A.shape[0], A.nnz)
 
 
+V73 = ["Drugs", "as_735", "CollegeMsg"]
+
+
+def _sha(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def main_v73():
+    """The three MAT v7.3 (HDF5) datasets of datasets_paper/Misc (SURVEY.md
+    §8f row 4), read with the package's own reader:
+      * v73_values.json -- digests of the raw Problem.A (shape, nnz, sum,
+        sha256 of the CSC arrays) that pin the reader, the CollegeMsg
+        temporal-edge cross-check, and exact spectra of the prepared graphs;
+        an oracle greedy_krylov 'make' selection on CollegeMsg
+      * v73_graphs.npz -- the prepared graphs (test_unweighted_make.m:41-52)
+    """
+    from krylov_robustness_amd import datasets as ds
+    graphs, vals = {}, {"_doc": "raw_* pin the MAT v7.3 reader; exact_* dense "
+                                "eigvalsh of the prepared graph; oracle_* from "
+                                "oracle/krylov_oracle.py"}
+    for name in V73:
+        path = os.path.join(REF, "datasets_paper", "Misc", name + ".mat")
+        t0 = time.time()
+        P = ds.load_variable(path, "Problem")
+        R = sp.csc_matrix(P["A"])
+        rec = {"raw_shape": list(R.shape), "raw_nnz": int(R.nnz), "raw_sum": float(R.sum()),
+               "raw_sha_indptr": _sha(R.indptr.astype(np.int64)),
+               "raw_sha_indices": _sha(R.indices.astype(np.int64)),
+               "raw_sha_data": _sha(R.data.astype(np.float64)),
+               "name": P.get("name")}
+        if name == "CollegeMsg":
+            te = np.asarray(P["aux"]["temporal_edges"])
+            rec["temporal_edges"] = [int(te.shape[0]), int(te.shape[1])]
+        A = ds.prepare_unweighted(P["A"])
+        graphs[name.lower()] = A
+        d = np.linalg.eigvalsh(A.toarray())
+        rec.update({"n": int(A.shape[0]), "nnz": int(A.nnz), "lambda_max": float(d.max()),
+                    "exact_tr_exp": float(np.sum(np.exp(d))),
+                    "exact_tr_sinh": float(np.sum(np.sinh(d))),
+                    "exact_tr_cosh": float(np.sum(np.cosh(d)))})
+        vals[name.lower()] = rec
+        print(name, rec["n"], rec["nnz"], f"{time.time() - t0:.1f}s", flush=True)
+    # greedy_krylov 'make' on CollegeMsg (test_unweighted_make.m:70-76 with a
+    # smaller budget): eigenvector centrality from a dense eigh
+    A = graphs["collegemsg"]
+    w, V = np.linalg.eigh(A.toarray())
+    cen = np.abs(V[:, -1])
+    t0 = time.time()
+    k, Q = 3, 40
+    edges, rob, _ = ko.greedy_krylov(A, k, Q, cen, "min", 1e-6 * np.exp(w[-1]), 100,
+                                     miobi="make")
+    vals["collegemsg"]["oracle_greedy_make"] = {
+        "k": k, "Q": Q, "order": "min", "tol": 1e-6 * float(np.exp(w[-1])), "it": 100,
+        "centrality": "abs(leading eigenvector), dense eigh",
+        "edges": np.asarray(edges).tolist(), "rob": float(rob)}
+    print("greedy", np.asarray(edges).tolist(), rob, f"{time.time() - t0:.1f}s")
+    save_csr(os.path.join(HERE, "v73_graphs.npz"), graphs)
+    with open(os.path.join(HERE, "v73_values.json"), "w") as f:
+        json.dump(vals, f, indent=1)
+
+
 def main():
     if "--hawaii" in sys.argv:
         return main_hawaii()
+    if "--v73" in sys.argv:
+        return main_v73()
     graphs = load_graphs()
     arrays = {}
     for k, A in graphs.items():
