@@ -443,23 +443,32 @@ __global__ void k_pair_eig(int C, int j, int it, int fun, double tol,
     }
 }
 
-// ---- one WAVE per candidate (2j <= 56): the two projections live in LDS ----
+// ---- one workgroup per candidate (2j <= 56): wave 0 solves the updated
+// projection T, wave 1 the plain one G, concurrently; both live in LDS ----
 __device__ __forceinline__ double wave_sum64(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 
-// Eigenvalues of the symmetric n x n row-major LDS matrix A (n <= 64,
-// destroyed): Householder tridiagonalisation with lane i owning row i of the
-// trailing block, then Sturm-count bisection with lane k finding the k-th
-// smallest eigenvalue (so the result is already sorted).  d, e, v, w: LDS
-// vectors of length n.  Returns this lane's eigenvalue (lanes >= n: 0).
-__device__ double wave_sym_eig(int n, double* A, double* d, double* e, double* v, double* w) {
+// LDS hand-off between the lanes of ONE wave (the two waves of the block run
+// data-dependent control flow, so no workgroup barrier inside the solvers)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Householder tridiagonalisation (dsytd2, lower) of the symmetric n x n LDS
+// matrix A (row stride n, n <= 64, destroyed) by one wave: lane i owns
+// COLUMN i of the trailing block (symmetry: reading A(k+1+j, k+1+lane) for a
+// fixed j is a contiguous, conflict-free LDS row).  d, e: diagonal and
+// off-diagonal out; v, w: scratch (n each).
+__device__ void wave_tridiag(int n, double* A, double* d, double* e, double* v, double* w) {
     const int lane = threadIdx.x & 63;
-    for (int k = 0; k + 2 < n; ++k) {  // dsytd2 (lower), reflector on A(k+1:n, k)
+    for (int k = 0; k + 2 < n; ++k) {  // reflector on A(k+1:n, k) = A(k, k+1:n)'
         const int m = n - k - 1;
-        const double xi = (lane < m) ? A[(k + 1 + lane) * n + k] : 0.0;
+        const double xi = (lane < m) ? A[k * n + (k + 1 + lane)] : 0.0;
         const double alpha = __shfl(xi, 0, 64);
         const double xn2 = wave_sum64(lane >= 1 ? xi * xi : 0.0);
         double tau = 0.0, beta = alpha, scal = 1.0;
@@ -472,85 +481,128 @@ __device__ double wave_sym_eig(int n, double* A, double* d, double* e, double* v
             d[k] = A[k * n + k];
             e[k] = beta;
         }
-        if (lane < m) v[lane] = (lane == 0) ? 1.0 : xi * scal;
-        __syncthreads();
+        const double vi = (lane == 0) ? 1.0 : xi * scal;
+        if (lane < m) v[lane] = vi;
+        wave_sync();
         if (tau != 0.0) {
-            // p = tau * A22 v ; w = p - (tau/2)(p'v) v ; A22 -= v w' + w v'
+            // p = tau A22 v ; w = p - (tau/2)(p'v) v ; A22 -= v w' + w v'
             double p = 0.0;
             if (lane < m)
-                for (int j = 0; j < m; ++j) p = fma(A[(k + 1 + lane) * n + (k + 1 + j)], v[j], p);
+                for (int j = 0; j < m; ++j) p = fma(A[(k + 1 + j) * n + (k + 1 + lane)], v[j], p);
             p *= tau;
-            const double pv = wave_sum64(lane < m ? p * v[lane] : 0.0);
-            const double wi = p - 0.5 * tau * pv * (lane < m ? v[lane] : 0.0);
+            const double pv = wave_sum64(lane < m ? p * vi : 0.0);
+            const double wi = p - 0.5 * tau * pv * (lane < m ? vi : 0.0);
             if (lane < m) w[lane] = wi;
-            __syncthreads();
-            if (lane < m) {
-                const double vi = v[lane];
+            wave_sync();
+            if (lane < m)
                 for (int j = 0; j < m; ++j)
-                    A[(k + 1 + lane) * n + (k + 1 + j)] -= vi * w[j] + wi * v[j];
-            }
+                    A[(k + 1 + j) * n + (k + 1 + lane)] -= v[j] * wi + w[j] * vi;
         }
-        __syncthreads();
+        wave_sync();
     }
     if (lane == 0) {
         if (n >= 2) {
             d[n - 2] = A[(n - 2) * n + (n - 2)];
-            e[n - 2] = A[(n - 1) * n + (n - 2)];
+            e[n - 2] = A[(n - 2) * n + (n - 1)];
         }
         d[n - 1] = A[(n - 1) * n + (n - 1)];
     }
-    __syncthreads();
-    // Gershgorin interval, then bisection on the Sturm count
+    wave_sync();
+}
+
+// Eigenvalues of the symmetric tridiagonal (d, e) (LDS, n <= 64) by Sturm
+// multisection: g = 64 / n lanes per eigenvalue, each counting at kMs
+// interleaved shifts, so one round splits the bracket into g*kMs + 1 parts.
+// Rounds stop once the bracket is 2 ulp of the spectral radius wide (the
+// absolute accuracy tql2 / dstebz deliver), or stops shrinking.  The Sturm
+// pivots use rcp + one Newton step (only their signs count).  Writes
+// lambda_k (ascending) to out[k].
+constexpr int kMs = 4;
+__device__ void wave_multisect(int n, const double* d, const double* e, double* e2, double* out) {
+    const int lane = threadIdx.x & 63;
+    if (lane + 1 < n) e2[lane] = e[lane] * e[lane];
+    wave_sync();
     double lo = 0.0, hi = 0.0, emax2 = 0.0;
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n; ++i) {  // Gershgorin interval
         const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i + 1 < n ? fabs(e[i]) : 0.0);
         lo = (i == 0) ? d[i] - r : fmin(lo, d[i] - r);
         hi = (i == 0) ? d[i] + r : fmax(hi, d[i] + r);
-        if (i + 1 < n) emax2 = fmax(emax2, e[i] * e[i]);
+        if (i + 1 < n) emax2 = fmax(emax2, e2[i]);
     }
     const double span = fmax(hi - lo, 1e-300);
     lo -= 2.2e-16 * span + 1e-300;
     hi += 2.2e-16 * span + 1e-300;
     const double pivmin = fmax(2.2250738585072014e-308 * fmax(1.0, emax2), 1e-300);
-    if (lane >= n) return 0.0;
+    const double atol = 4.4e-16 * fmax(fabs(lo), fabs(hi)) + 1e-300;
+    const int g = 64 / n;
+    const int k = lane / g, sub = lane % g;
+    const int M = g * kMs;  // points per round
     double a = lo, b = hi;
-    for (int itb = 0; itb < 80; ++itb) {
-        const double x = 0.5 * (a + b);
-        if (x <= a || x >= b) break;
-        int cnt = 0;  // eigenvalues < x
-        double q = d[0] - x;
-        if (fabs(q) < pivmin) q = -pivmin;
-        cnt += q < 0.0;
-        for (int i = 1; i < n; ++i) {
-            q = d[i] - x - e[i - 1] * e[i - 1] / q;
-            if (fabs(q) < pivmin) q = -pivmin;
-            cnt += q < 0.0;
+    const bool live = k < n;
+    bool done = !live;  // identical across a group: it shares (a, b)
+    for (int round = 0; round < 64; ++round) {
+        if (!done && !(b - a > atol)) done = true;
+        if (__ballot(!done) == 0ull) break;  // wave-uniform exit
+        double x[kMs], q[kMs];
+        int cnt[kMs];
+        const double h = (b - a) / (double)(M + 1);
+#pragma unroll
+        for (int s = 0; s < kMs; ++s) {
+            x[s] = a + h * (double)(sub * kMs + s + 1);
+            q[s] = d[0] - x[s];
+            if (fabs(q[s]) < pivmin) q[s] = -pivmin;
+            cnt[s] = q[s] < 0.0;
         }
-        if (cnt > lane) b = x;  // the (lane+1)-th smallest is below x
-        else a = x;
+        for (int i = 1; i < n; ++i) {
+            const double di = d[i], ei = e2[i - 1];
+#pragma unroll
+            for (int s = 0; s < kMs; ++s) {
+                double r = __builtin_amdgcn_rcp(q[s]);
+                r = fma(fma(-q[s], r, 1.0), r, r);
+                q[s] = (di - x[s]) - ei * r;
+                if (fabs(q[s]) < pivmin) q[s] = -pivmin;
+                cnt[s] += q[s] < 0.0;
+            }
+        }
+        // first point (group-wide index) whose count exceeds k: lambda_k < x_p
+        int mine = M;
+#pragma unroll
+        for (int s = kMs - 1; s >= 0; --s)
+            if (cnt[s] > k) mine = sub * kMs + s;
+        int first = mine;
+        for (int o = 1; o < g; ++o) first = min(first, __shfl(mine, k * g + (sub + o) % g, 64));
+        if (!done) {
+            const double na = first == 0 ? a : a + h * (double)first;
+            const double nb = first == M ? b : fmin(b, a + h * (double)(first + 1));
+            if (!(na > a || nb < b)) {
+                done = true;  // bracket at machine resolution
+            } else {
+                a = na;
+                b = nb;
+            }
+        }
     }
-    return 0.5 * (a + b);
+    if (live && sub == 0) out[k] = 0.5 * (a + b);
+    wave_sync();
 }
 
-__global__ __launch_bounds__(64) void k_pair_eig_wave(int C, int j, int it, int fun, double tol,
-                                                      const double* __restrict__ hist,
-                                                      const double* __restrict__ Cm,
-                                                      double* __restrict__ state) {
+__global__ __launch_bounds__(128) void k_pair_eig_wave(int C, int j, int it, int fun, double tol,
+                                                       const double* __restrict__ hist,
+                                                       const double* __restrict__ Cm,
+                                                       double* __restrict__ state) {
     extern __shared__ double sm[];
     const int c = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
     double* st = state + (int64_t)c * PS_N;
     if (st[PS_DONE] != 0.0) return;
     const int nn = 2 * j;
     double* G = sm;
     double* T = G + nn * nn;
-    double* d = T + nn * nn;
-    double* e = d + nn;
-    double* v = e + nn;
-    double* w = v + nn;
-    for (int t = lane; t < nn * nn; t += 64) G[t] = 0.0;
+    double* vec = T + nn * nn;  // per wave: d, e, v, w, e2, lam  (6 nn)
+    for (int t = tid; t < nn * nn; t += 128) G[t] = 0.0;
     __syncthreads();
-    for (int b = lane; b < j; b += 64) {  // row-major G[r * nn + col]
+    for (int b = tid; b < j; b += 128) {  // row-major G[r * nn + col]
         const double* h = hist + ((int64_t)b * C + c) * 11;
         G[(2 * b) * nn + 2 * b] = h[2];
         G[(2 * b + 1) * nn + 2 * b] = h[3];
@@ -569,9 +621,9 @@ __global__ __launch_bounds__(64) void k_pair_eig_wave(int C, int j, int it, int 
         }
     }
     __syncthreads();
-    for (int t = lane; t < nn * nn; t += 64) T[t] = G[t];
+    for (int t = tid; t < nn * nn; t += 128) T[t] = G[t];
     __syncthreads();
-    if (lane == 0) {
+    if (tid == 0) {
         const double* cm = Cm + (int64_t)c * 4;  // column-major 2x2
         T[0] += cm[0];
         T[nn] += cm[1];
@@ -579,7 +631,7 @@ __global__ __launch_bounds__(64) void k_pair_eig_wave(int C, int j, int it, int 
         T[nn + 1] += cm[3];
     }
     __syncthreads();
-    for (int t = lane; t < nn * nn; t += 64) {  // (X + X') / 2   :78-81
+    for (int t = tid; t < nn * nn; t += 128) {  // (X + X') / 2   :78-81
         const int r = t / nn, q = t % nn;
         if (q < r) {
             const double g = 0.5 * (G[r * nn + q] + G[q * nn + r]);
@@ -589,12 +641,23 @@ __global__ __launch_bounds__(64) void k_pair_eig_wave(int C, int j, int it, int 
         }
     }
     __syncthreads();
-    const double l1 = wave_sym_eig(nn, T, d, e, v, w);
+    double* my = vec + (size_t)wave * 6 * nn;
+    double* d = my;
+    double* e = d + nn;
+    double* v = e + nn;
+    double* w = v + nn;
+    double* e2 = w + nn;
+    double* lam = e2 + nn;
+    wave_tridiag(nn, wave == 0 ? T : G, d, e, v, w);
+    wave_multisect(nn, d, e, e2, lam);
     __syncthreads();
-    const double l2 = wave_sym_eig(nn, G, d, e, v, w);
-    double term = 0.0;  // :85-89 (lane k holds the k-th smallest of each)
+    if (wave != 0) return;
+    const double* l1 = vec + 5 * nn;           // wave 0: eig(T), ascending
+    const double* l2 = vec + 6 * nn + 5 * nn;  // wave 1: eig(G)
+    double term = 0.0;  // :85-89 (k-th smallest of each)
     if (lane < nn)
-        term = (fun == 0) ? exp(l1) * (1.0 - exp(l2 - l1)) : dev_fscalar(fun, l1) - dev_fscalar(fun, l2);
+        term = (fun == 0) ? exp(l1[lane]) * (1.0 - exp(l2[lane] - l1[lane]))
+                          : dev_fscalar(fun, l1[lane]) - dev_fscalar(fun, l2[lane]);
     const double xm = wave_sum64(term);
     if (lane == 0) {
         const double* hj = hist + ((int64_t)(j - 1) * C + c) * 11;
@@ -634,9 +697,9 @@ __global__ void k_pair_active(int C, const double* __restrict__ state, int* __re
 hipError_t launch_pair_eig(int C, int j, int it, int fun, double tol, const double* hist,
                            const double* Cm, double* scratch, int64_t sstride, double* state,
                            int* active, hipStream_t st) {
-    if (2 * j <= 56) {  // 2 nn^2 + 4 nn doubles <= 52 KB of LDS
-        const size_t lds = sizeof(double) * (2 * (size_t)(2 * j) * (2 * j) + 4 * (size_t)(2 * j));
-        k_pair_eig_wave<<<C, 64, lds, st>>>(C, j, it, fun, tol, hist, Cm, state);
+    if (2 * j <= 56) {  // 2 nn^2 + 12 nn doubles <= 55 KB of LDS
+        const size_t lds = sizeof(double) * (2 * (size_t)(2 * j) * (2 * j) + 12 * (size_t)(2 * j));
+        k_pair_eig_wave<<<C, 128, lds, st>>>(C, j, it, fun, tol, hist, Cm, state);
     } else {
         k_pair_eig<<<(C + 63) / 64, 64, 0, st>>>(C, j, it, fun, tol, hist, Cm, scratch, sstride, state);
     }

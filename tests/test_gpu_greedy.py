@@ -165,15 +165,18 @@ def test_krylov_miobi_sharded_world1(kra, gpu_ctx):
 
 
 def test_pairs_device_and_host_eig_agree(kra, gpu_ctx, monkeypatch):
-    """The device-resident per-candidate eig (one wavefront per candidate,
-    Sturm bisection) and the host path (tred2/tql2 pool) give the same scores
-    and iteration counts."""
+    """The device-resident per-candidate eig (one workgroup per candidate,
+    Sturm multisection) and the host path (tred2/tql2 pool) give the same
+    scores and iteration counts.  Both solvers deliver eigenvalues to an
+    absolute O(eps ||T||); Xm = sum exp(l1) (1 - exp(l2 - l1)) scales that by
+    up to exp(lambda_max) (~1e3 here), so the scores agree to ~1e-12
+    absolute on |Xm| ~ 1-10: rtol 1e-11."""
     A, c = _india(kra)
     E = kra.find_top_edges(A, c, 96, "min")
     D = kra.DeviceMatrix(A, gpu_ctx)
     x_dev, it_dev, l_dev = kra.trace_fun_update_pairs(D, E, BREAK, 1e-10, 100, ctx=gpu_ctx)
     monkeypatch.setenv("KT_PAIRS_HOST", "1")
     x_host, it_host, l_host = kra.trace_fun_update_pairs(D, E, BREAK, 1e-10, 100, ctx=gpu_ctx)
-    np.testing.assert_allclose(x_dev, x_host, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(x_dev, x_host, rtol=1e-11, atol=1e-13)
     np.testing.assert_array_equal(it_dev, it_host)
     np.testing.assert_array_equal(l_dev, l_host)
