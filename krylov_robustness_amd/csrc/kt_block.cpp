@@ -114,6 +114,36 @@ void spmm(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols
                              ctx->stream));
 }
 
+// Y[:, 0:cols] = A X[:, 0:cols] for cols > 128 in ONE launch: ceil(cols/128)
+// column slices of width 128 on grid.y (ldx, ldy >= slices * 128; columns
+// past `cols` are computed too, they must hold finite values).  skip: see
+// k_spmm_block.
+void spmm_slices(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols,
+                 const int* skip) {
+    if (cols <= 128) {
+        kt_context_s* ctx = A->ctx;
+        const int P = pow2_at_least(std::max(cols, 1));
+        const int n = (int)A->n;
+        const int grid = spmm_grid(n, P, ctx->num_cu * 4);
+        const DevCSR& M = natural_csr(A);
+        const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
+        KT_HIP(launch_spmm_block(P, (A->unit_values ? 2 : 0) | (ctx->k1_flags & 4), grid + lblocks,
+                                 M.rowptr, M.col, M.val, n, X, ldx, Y, ldy, M.long_rows, M.n_long,
+                                 A->long_thresh, lblocks, ctx->stream, 1, skip));
+        return;
+    }
+    const int slices = (cols + 127) / 128;
+    if (ldx < slices * 128 || ldy < slices * 128) fail(KT_ERR_ARG, "spmm_slices: leading dimension");
+    kt_context_s* ctx = A->ctx;
+    const int n = (int)A->n;
+    const int grid = spmm_grid(n, 128, ctx->num_cu * 4);
+    const DevCSR& M = natural_csr(A);
+    const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
+    KT_HIP(launch_spmm_block(128, (A->unit_values ? 2 : 0) | (ctx->k1_flags & 4), grid + lblocks,
+                             M.rowptr, M.col, M.val, n, X, ldx, Y, ldy, M.long_rows, M.n_long,
+                             A->long_thresh, lblocks, ctx->stream, slices, skip));
+}
+
 void copy_cols(kt_context_s* ctx, int64_t n, const double* X, int ldx, double* Y, int ldy,
                int cols) {
     if (n == 0 || cols == 0) return;

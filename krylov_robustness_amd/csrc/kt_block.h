@@ -35,6 +35,10 @@ void combine(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px,
              const std::vector<double>& C, int q, double beta, double* Y, int ldy);
 // Y[:, 0:P] = A X[:, 0:P], P = pow2 >= cols (columns cols..P-1 of X must be 0)
 void spmm(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols);
+// cols > 128 in one launch (128-wide column slices); skip: device flag, the
+// launch is a no-op when *skip == 0 (nullptr: always run)
+void spmm_slices(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols,
+                 const int* skip = nullptr);
 // copy a column slice (n x cols) between device arrays
 void copy_cols(kt_context_s* ctx, int64_t n, const double* X, int ldx, double* Y, int ldy, int cols);
 void zero_cols(kt_context_s* ctx, int64_t n, double* X, int ldx, int cols);

@@ -204,8 +204,9 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
             for (auto& x : e)
                 if (x) (void)hipEventDestroy(x);
         }
-    } evs;
+    } evs, evhs;
     hipEvent_t* ev = evs.e;
+    hipEvent_t* evh = evhs.e;
     auto fetch = [&]() {
         KT_HIP(hipMemcpyAsync(hr, dhr, sizeof(double) * 11 * (size_t)C, hipMemcpyDeviceToHost,
                               ctx->stream));
@@ -248,18 +249,32 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
             for (int t = 0; t < 4; ++t) cm[(size_t)4 * c + t] = run[c].Cm[t];
         KT_HIP(hipMemsetAsync(state, 0, sizeof(double) * (size_t)C * 8, ctx->stream));
         KT_HIP(hipMemcpyAsync(dcm, cm.data(), sizeof(double) * cm.size(), hipMemcpyHostToDevice, ctx->stream));
+        const int act0[2] = {C, C};  // counts only fall: a stale read never skips early
+        KT_HIP(hipMemcpyAsync(act_dev, act0, sizeof(act0), hipMemcpyHostToDevice, ctx->stream));
+        // The projected eigenproblems of step j (k_pair_eig) only decide when
+        // to stop; the recurrence of step j+1 does not need them.  They run
+        // on a side stream, gated by an event after step j's coefficients, so
+        // they overlap step j+1's SpMM and sweeps.
+        if (!ctx->aux_stream[0])
+            KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[0], hipStreamNonBlocking));
+        hipStream_t side = ctx->aux_stream[0];
         int cur = 0, prev = -1, w = 1;
         for (int j = 1; j <= it; ++j) {
-            for (int c0 = 0; c0 < CP; c0 += 128)  // w = A * w   (lanczos_krylov.m:81)
-                spmm(A, S[cur] + c0, CP, S[w] + c0, CP, std::min(128, cols - c0));
+            // a step queued after every candidate stopped (the host polls one
+            // step behind) exits at once on an earlier step's active count
+            const int* skip = j >= 2 ? act_dev + ((j - 1) & 1) : nullptr;
+            spmm_slices(A, S[cur], CP, S[w], CP, cols, skip);  // w = A * w   (lanczos_krylov.m:81)
             double* hj = hist + (size_t)(j - 1) * C * 11;
             KT_HIP(launch_pairs_orth(C, (int)n, ctx->num_cu, prev >= 0 ? S[prev] : nullptr, S[cur], S[w], CP,
-                                     ws.pair_coef.as<double>(), ws.pair_part.as<double>(), hj, ctx->stream));
+                                     ws.pair_coef.as<double>(), ws.pair_part.as<double>(), hj, ctx->stream,
+                                     skip));
+            KT_HIP(hipEventRecord(evh[j & 1], ctx->stream));  // hist[j-1] complete
+            KT_HIP(hipStreamWaitEvent(side, evh[j & 1], 0));
             KT_HIP(launch_pair_eig(C, j, it, fun, tol, hist, dcm, ws.pair_scratch.as<double>(), sstride,
-                                   state, act_dev + (j & 1), ctx->stream));
+                                   state, act_dev + (j & 1), side));
             KT_HIP(hipMemcpyAsync(act_host + (j & 1), act_dev + (j & 1), sizeof(int), hipMemcpyDeviceToHost,
-                                  ctx->stream));
-            KT_HIP(hipEventRecord(ev[j & 1], ctx->stream));
+                                  side));
+            KT_HIP(hipEventRecord(ev[j & 1], side));
             const int freed = prev >= 0 ? prev : 3 - cur - w;
             prev = cur;
             cur = w;
@@ -269,6 +284,7 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
                 if (act_host[(j - 1) & 1] == 0) break;
             }
         }
+        KT_HIP(hipStreamSynchronize(side));
         KT_HIP(hipStreamSynchronize(ctx->stream));
         lap(t_gpu);
         std::vector<double> sv((size_t)C * 8);
@@ -291,8 +307,7 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
     PinnedBuf* hbuf = ws.pair_host;
     auto launch_step = [&](int slot) {
         // w = A * w over every candidate (lanczos_krylov.m:81)
-        for (int c0 = 0; c0 < CP; c0 += 128)
-            spmm(A, S[cur] + c0, CP, S[w] + c0, CP, std::min(128, cols - c0));
+        spmm_slices(A, S[cur], CP, S[w], CP, cols);
         orth(prev >= 0 ? S[prev] : nullptr, S[cur], S[w]);
         KT_HIP(hipMemcpyAsync(hbuf[slot].ptr, dhr, sizeof(double) * 11 * (size_t)C,
                               hipMemcpyDeviceToHost, ctx->stream));
@@ -511,11 +526,15 @@ int kt_krylov_miobi(kt_matrix_t A, int k, int64_t nE, const int64_t* ei, const i
     double total = 0.0;
     int64_t done = 0;
     const int64_t steps = std::min<int64_t>(k, nE);
+    static const bool timing = getenv("KT_PAIRS_TIMING") != nullptr;
+    using clk = std::chrono::steady_clock;
     for (int64_t s = 0; s < steps; ++s) {  // :70
         const int64_t m = (int64_t)Ei.size();
         xm.assign(m, 0.0);
+        const auto t0 = clk::now();
         trace_fun_update_pairs(A, m, Ei.data(), Ej.data(), B, sg, tol, it, KT_FUN_EXP, xm.data(),
                                nullptr, nullptr);  // :76-99
+        const auto t1 = clk::now();
         int64_t best = -1;  // :112-124 (strict comparison: first extreme wins)
         double bv = make ? -INFINITY : INFINITY;
         for (int64_t h = 0; h < m; ++h)
@@ -528,6 +547,10 @@ int kt_krylov_miobi(kt_matrix_t A, int k, int64_t nE, const int64_t* ei, const i
         Ei.erase(Ei.begin() + best);  // :127
         Ej.erase(Ej.begin() + best);
         set_pairs(A, 1, &ci, &cj, make ? 1.0 : 0.0);  // :129-135
+        if (timing)
+            fprintf(stderr, "[kt miobi] step %lld score %.3f ms  select+edit %.3f ms\n", (long long)s,
+                    std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                    std::chrono::duration<double, std::milli>(clk::now() - t1).count());
         if (sel_i) sel_i[done] = ci;
         if (sel_j) sel_j[done] = cj;
         total += bv;

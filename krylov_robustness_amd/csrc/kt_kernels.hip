@@ -318,10 +318,14 @@ template <int P, int BLOCK, int FLAGS>
 __global__ __launch_bounds__(BLOCK) void k_spmm_block(
     const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
     int n, const double* __restrict__ X, int ldx, double* __restrict__ Y, int ldy,
-    const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks) {
+    const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks,
+    const int* __restrict__ skip) {
     using G = Geo<P>;
     using V = VecT<G::VEC>;
     constexpr int WAVES = BLOCK / 64;
+    if (skip && *skip == 0) return;  // every consumer of this step already stopped
+    X += (int64_t)blockIdx.y * P;    // column slice blockIdx.y of a wider block
+    Y += (int64_t)blockIdx.y * P;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int sub = lane % G::LPR;
@@ -659,12 +663,13 @@ hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int*
 hipError_t launch_spmm_block(int P, int flags, int grid, const int* rp, const int* ci,
                              const double* va, int n, const double* X, int ldx, double* Y, int ldy,
                              const int* long_rows, int n_long, int long_thresh, int long_blocks,
-                             hipStream_t st) {
+                             hipStream_t st, int slices, const int* skip) {
+    const dim3 g(grid, slices);
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
 #define KT_SB(F)                                                                      \
-    k_spmm_block<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, X, ldx, Y, ldy,    \
-                                                         long_rows, n_long, long_thresh, long_blocks)
+    k_spmm_block<PP, kBlock, F><<<g, kBlock, 0, st>>>(rp, ci, va, n, X, ldx, Y, ldy, long_rows, \
+                                                      n_long, long_thresh, long_blocks, skip)
         switch (flags & (KF_UNIT | KF_MLP)) {
         case 0: KT_SB(0); break;
         case KF_UNIT: KT_SB(KF_UNIT); break;

@@ -17,7 +17,8 @@ hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int*
 hipError_t launch_spmm_block(int P, int flags, int grid, const int* rp, const int* ci,
                              const double* va, int n, const double* X, int ldx, double* Y, int ldy,
                              const int* long_rows, int n_long, int long_thresh, int long_blocks,
-                             hipStream_t st);
+                             hipStream_t st, int slices = 1,
+                             const int* skip = nullptr);
 hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, const double* k2s,
                             const double* sc, const double* sp, double* coef, double* t_alpha,
                             double* t_up, hipStream_t st);
@@ -39,7 +40,8 @@ hipError_t launch_pair_select(int C, const int* ii, const int* jj, double* X, in
 // per candidate; hr[c*11 + 0..10] = (h [8], R11, R12, R22)
 hipError_t launch_pairs_orth(int C, int n, int num_cu, const double* prev, const double* cur,
                              double* W, int ld, double* coef, double* part, double* hr,
-                             hipStream_t st);
+                             hipStream_t st,
+                             const int* skip = nullptr);
 size_t pairs_part_doubles(int n, int C, int num_cu);
 // per-candidate projected eigenproblems + stop logic; state C x 8 doubles
 hipError_t launch_pair_eig(int C, int j, int it, int fun, double tol, const double* hist,

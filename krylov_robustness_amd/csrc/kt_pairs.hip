@@ -66,9 +66,10 @@ template <int PH>
 __global__ __launch_bounds__(kSweepBlock) void k_pairs_sweep(
     int n, int C, int rows_per_blk, const double* __restrict__ prev,
     const double* __restrict__ cur, double* __restrict__ W, int ld,
-    const double* __restrict__ coef, double* __restrict__ part) {
+    const double* __restrict__ coef, double* __restrict__ part, const int* __restrict__ skip) {
     constexpr int NV = PhaseNV<PH>::v;
     __shared__ double lds[NV > 0 ? NV * kSweepWaves * 64 : 1];
+    if (skip && *skip == 0) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + lane;
     const bool valid = c < C;
@@ -153,17 +154,29 @@ __global__ __launch_bounds__(kSweepBlock) void k_pairs_sweep(
     }
 }
 
-// sum of the nrb partials of (k, c): one wave, fixed order (lane-strided
-// sums, then a fixed xor tree) -> identical result in every lane
-__device__ __forceinline__ double wave_sum_part(const double* __restrict__ part, int C, int nrb,
-                                                int k, int c) {
+// NV partial sums of candidate c at once (k = k0 .. k0+NV-1): the loads of
+// every k are issued together each round, same per-lane order as
+// wave_sum_part, so the results are bit-identical
+template <int NV>
+__device__ __forceinline__ void wave_sum_parts(const double* __restrict__ part, int C, int nrb,
+                                               int k0, int c, double* out) {
     const int lane = threadIdx.x & 63;
-    const double* p = part + ((int64_t)k * C + c) * nrb;
-    double s = 0.0;
-    for (int i = lane; i < nrb; i += 64) s += p[i];
+    double s[NV];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    return s;
+    for (int k = 0; k < NV; ++k) s[k] = 0.0;
+    for (int i = lane; i < nrb; i += 64) {
+        double x[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) x[k] = part[((int64_t)(k0 + k) * C + c) * nrb + i];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) s[k] += x[k];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) s[k] += __shfl_xor(s[k], o, 64);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[k] = s[k];
 }
 
 // LAPACK dlarfg on (alpha, ||x||^2 = xx): beta, tau and 1/(alpha - beta)
@@ -188,24 +201,25 @@ template <int PH>
 __global__ __launch_bounds__(256) void k_pairs_coef(int C, int nrb, const double* __restrict__ part,
                                                     const double* __restrict__ W, int ld,
                                                     double* __restrict__ coef,
-                                                    double* __restrict__ hr) {
+                                                    double* __restrict__ hr,
+                                                    const int* __restrict__ skip) {
     const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (c >= C) return;
+    if (c >= C || (skip && *skip == 0)) return;
     double* cf = coef + (int64_t)c * CF_NCOEF;
     const int64_t off = 2 * (int64_t)c;
     if (PH == PH_A || PH == PH_B) {
         double v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = wave_sum_part(part, C, nrb, k, c);
+        wave_sum_parts<8>(part, C, nrb, 0, c, v);
         if (lane == 0) {
             const int base = PH == PH_A ? CF_G1 : CF_G2;
 #pragma unroll
             for (int k = 0; k < 8; ++k) cf[base + k] = v[k];
         }
     } else if (PH == PH_C || PH == PH_C0) {
-        const double s1 = wave_sum_part(part, C, nrb, 0, c);
-        const double ab = wave_sum_part(part, C, nrb, 1, c);
+        double v2[2];
+        wave_sum_parts<2>(part, C, nrb, 0, c, v2);
+        const double s1 = v2[0], ab = v2[1];
         if (lane == 0) {
             const double2 w0 = ld2(W, 0, ld, off), w1 = ld2(W, 1, ld, off);
             double beta1, tau1, scal1;
@@ -223,8 +237,9 @@ __global__ __launch_bounds__(256) void k_pairs_coef(int C, int nrb, const double
             }
         }
     } else {  // PH_D
-        const double s2 = wave_sum_part(part, C, nrb, 0, c);
-        const double dz = wave_sum_part(part, C, nrb, 1, c);
+        double v2[2];
+        wave_sum_parts<2>(part, C, nrb, 0, c, v2);
+        const double s2 = v2[0], dz = v2[1];
         if (lane == 0) {
             const double2 w1 = ld2(W, 1, ld, off);
             const double z1 = w1.y - cf[CF_KAPPA] * w1.x;
@@ -459,17 +474,30 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// lane l's double, broadcast to the wave (l uniform): two v_readlane, no LDS
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // Householder tridiagonalisation (dsytd2, lower) of the symmetric n x n LDS
 // matrix A (row stride n, n <= 64, destroyed) by one wave: lane i owns
 // COLUMN i of the trailing block (symmetry: reading A(k+1+j, k+1+lane) for a
-// fixed j is a contiguous, conflict-free LDS row).  d, e: diagonal and
-// off-diagonal out; v, w: scratch (n each).
-__device__ void wave_tridiag(int n, double* A, double* d, double* e, double* v, double* w) {
+// fixed j is a contiguous, conflict-free LDS row); the reflector v and the
+// rank-2 update vector w stay in registers (lane i holds element i) and are
+// broadcast with v_readlane.  Returns this lane's (d_lane, e_lane) in the
+// references: the diagonal and off-diagonal of the tridiagonal.
+__device__ void wave_tridiag(int n, double* A, double& d_out, double& e_out) {
     const int lane = threadIdx.x & 63;
+    d_out = 0.0;
+    e_out = 0.0;
     for (int k = 0; k + 2 < n; ++k) {  // reflector on A(k+1:n, k) = A(k, k+1:n)'
         const int m = n - k - 1;
         const double xi = (lane < m) ? A[k * n + (k + 1 + lane)] : 0.0;
-        const double alpha = __shfl(xi, 0, 64);
+        const double akk = A[k * n + k];
+        const double alpha = readlane_d(xi, 0);
         const double xn2 = wave_sum64(lane >= 1 ? xi * xi : 0.0);
         double tau = 0.0, beta = alpha, scal = 1.0;
         if (xn2 != 0.0) {
@@ -477,69 +505,97 @@ __device__ void wave_tridiag(int n, double* A, double* d, double* e, double* v, 
             tau = (beta - alpha) / beta;
             scal = 1.0 / (alpha - beta);
         }
-        if (lane == 0) {
-            d[k] = A[k * n + k];
-            e[k] = beta;
+        if (lane == k) {
+            d_out = akk;
+            e_out = beta;
         }
-        const double vi = (lane == 0) ? 1.0 : xi * scal;
-        if (lane < m) v[lane] = vi;
-        wave_sync();
+        const double vi = (lane == 0) ? 1.0 : (lane < m ? xi * scal : 0.0);
         if (tau != 0.0) {
             // p = tau A22 v ; w = p - (tau/2)(p'v) v ; A22 -= v w' + w v'
+            double* col = A + (k + 1) * n + (k + 1) + lane;  // A(k+1+j, k+1+lane) = col[j n]
             double p = 0.0;
-            if (lane < m)
-                for (int j = 0; j < m; ++j) p = fma(A[(k + 1 + j) * n + (k + 1 + lane)], v[j], p);
+            if (lane < m) {  // by 4: the LDS loads issue together, fma order unchanged
+                int j = 0;
+                for (; j + 4 <= m; j += 4) {
+                    const double a0 = col[j * n], a1 = col[(j + 1) * n];
+                    const double a2 = col[(j + 2) * n], a3 = col[(j + 3) * n];
+                    p = fma(a0, readlane_d(vi, j), p);
+                    p = fma(a1, readlane_d(vi, j + 1), p);
+                    p = fma(a2, readlane_d(vi, j + 2), p);
+                    p = fma(a3, readlane_d(vi, j + 3), p);
+                }
+                for (; j < m; ++j) p = fma(col[j * n], readlane_d(vi, j), p);
+            }
             p *= tau;
             const double pv = wave_sum64(lane < m ? p * vi : 0.0);
-            const double wi = p - 0.5 * tau * pv * (lane < m ? vi : 0.0);
-            if (lane < m) w[lane] = wi;
+            const double wi = p - 0.5 * tau * pv * vi;
+            if (lane < m) {
+                int j = 0;
+                for (; j + 4 <= m; j += 4) {
+                    double a[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) a[t] = col[(j + t) * n];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        col[(j + t) * n] = a[t] - (readlane_d(vi, j + t) * wi + readlane_d(wi, j + t) * vi);
+                }
+                for (; j < m; ++j) col[j * n] -= readlane_d(vi, j) * wi + readlane_d(wi, j) * vi;
+            }
             wave_sync();
-            if (lane < m)
-                for (int j = 0; j < m; ++j)
-                    A[(k + 1 + j) * n + (k + 1 + lane)] -= v[j] * wi + w[j] * vi;
         }
-        wave_sync();
     }
-    if (lane == 0) {
-        if (n >= 2) {
-            d[n - 2] = A[(n - 2) * n + (n - 2)];
-            e[n - 2] = A[(n - 2) * n + (n - 1)];
-        }
-        d[n - 1] = A[(n - 1) * n + (n - 1)];
+    // last 2 x 2 block
+    if (n >= 2 && lane == n - 2) {
+        d_out = A[(n - 2) * n + (n - 2)];
+        e_out = A[(n - 2) * n + (n - 1)];
     }
-    wave_sync();
+    if (lane == n - 1) d_out = A[(n - 1) * n + (n - 1)];
 }
 
-// Eigenvalues of the symmetric tridiagonal (d, e) (LDS, n <= 64) by Sturm
-// multisection: g = 64 / n lanes per eigenvalue, each counting at kMs
-// interleaved shifts, so one round splits the bracket into g*kMs + 1 parts.
-// Rounds stop once the bracket is 2 ulp of the spectral radius wide (the
-// absolute accuracy tql2 / dstebz deliver), or stops shrinking.  The Sturm
-// pivots use rcp + one Newton step (only their signs count).  Writes
-// lambda_k (ascending) to out[k].
-constexpr int kMs = 4;
-__device__ void wave_multisect(int n, const double* d, const double* e, double* e2, double* out) {
+// Eigenvalues of the symmetric tridiagonal held in registers (lane i: d_i,
+// e_i) by Sturm multisection: g = 64 / n lanes per eigenvalue, each
+// counting at kMs interleaved shifts, so one round splits the bracket into
+// g*kMs + 1 parts.  Rounds stop once the bracket is 2 ulp of the spectral
+// radius wide (the absolute accuracy tql2 / dstebz deliver), or stops
+// shrinking.  The Sturm pivots use rcp + one Newton step (only their signs
+// count).  The wave solves eigenvalues k0 .. k0+ne-1 (g = 64 / ne lanes
+// each); returns lambda_{k0 + lane / g} in lanes with lane % g == 0
+// (others: unspecified).
+template <int kMs>
+__device__ double wave_multisect(int n, double di_reg, double ei_reg, int k0, int ne) {
     const int lane = threadIdx.x & 63;
-    if (lane + 1 < n) e2[lane] = e[lane] * e[lane];
-    wave_sync();
+    const double e2_reg = (lane + 1 < n) ? ei_reg * ei_reg : 0.0;
     double lo = 0.0, hi = 0.0, emax2 = 0.0;
-    for (int i = 0; i < n; ++i) {  // Gershgorin interval
-        const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i + 1 < n ? fabs(e[i]) : 0.0);
-        lo = (i == 0) ? d[i] - r : fmin(lo, d[i] - r);
-        hi = (i == 0) ? d[i] + r : fmax(hi, d[i] + r);
-        if (i + 1 < n) emax2 = fmax(emax2, e2[i]);
+    {  // Gershgorin interval (lane-parallel, then wave min/max)
+        const double eprev = __shfl(ei_reg, lane > 0 ? lane - 1 : 0, 64);
+        const double ep = (lane >= 1 && lane < n) ? fabs(eprev) : 0.0;
+        const double en = (lane + 1 < n) ? fabs(ei_reg) : 0.0;
+        double l = (lane < n) ? di_reg - ep - en : INFINITY;
+        double h = (lane < n) ? di_reg + ep + en : -INFINITY;
+        double m2 = e2_reg;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            l = fmin(l, __shfl_xor(l, o, 64));
+            h = fmax(h, __shfl_xor(h, o, 64));
+            m2 = fmax(m2, __shfl_xor(m2, o, 64));
+        }
+        lo = l;
+        hi = h;
+        emax2 = m2;
     }
     const double span = fmax(hi - lo, 1e-300);
     lo -= 2.2e-16 * span + 1e-300;
     hi += 2.2e-16 * span + 1e-300;
     const double pivmin = fmax(2.2250738585072014e-308 * fmax(1.0, emax2), 1e-300);
     const double atol = 4.4e-16 * fmax(fabs(lo), fabs(hi)) + 1e-300;
-    const int g = 64 / n;
-    const int k = lane / g, sub = lane % g;
+    const int g = 64 / ne;  // lanes per eigenvalue; this wave owns k0 .. k0+ne-1
+    const int kl = lane / g, sub = lane % g;
+    const int k = k0 + kl;
     const int M = g * kMs;  // points per round
     double a = lo, b = hi;
-    const bool live = k < n;
+    const bool live = kl < ne;
     bool done = !live;  // identical across a group: it shares (a, b)
+    const double d0 = readlane_d(di_reg, 0);
     for (int round = 0; round < 64; ++round) {
         if (!done && !(b - a > atol)) done = true;
         if (__ballot(!done) == 0ull) break;  // wave-uniform exit
@@ -549,12 +605,12 @@ __device__ void wave_multisect(int n, const double* d, const double* e, double* 
 #pragma unroll
         for (int s = 0; s < kMs; ++s) {
             x[s] = a + h * (double)(sub * kMs + s + 1);
-            q[s] = d[0] - x[s];
+            q[s] = d0 - x[s];
             if (fabs(q[s]) < pivmin) q[s] = -pivmin;
             cnt[s] = q[s] < 0.0;
         }
         for (int i = 1; i < n; ++i) {
-            const double di = d[i], ei = e2[i - 1];
+            const double di = readlane_d(di_reg, i), ei = readlane_d(e2_reg, i - 1);
 #pragma unroll
             for (int s = 0; s < kMs; ++s) {
                 double r = __builtin_amdgcn_rcp(q[s]);
@@ -570,7 +626,7 @@ __device__ void wave_multisect(int n, const double* d, const double* e, double* 
         for (int s = kMs - 1; s >= 0; --s)
             if (cnt[s] > k) mine = sub * kMs + s;
         int first = mine;
-        for (int o = 1; o < g; ++o) first = min(first, __shfl(mine, k * g + (sub + o) % g, 64));
+        for (int o = 1; o < g; ++o) first = min(first, __shfl(mine, kl * g + (sub + o) % g, 64));
         if (!done) {
             const double na = first == 0 ? a : a + h * (double)first;
             const double nb = first == M ? b : fmin(b, a + h * (double)(first + 1));
@@ -582,27 +638,31 @@ __device__ void wave_multisect(int n, const double* d, const double* e, double* 
             }
         }
     }
-    if (live && sub == 0) out[k] = 0.5 * (a + b);
-    wave_sync();
+    return 0.5 * (a + b);
 }
 
-__global__ __launch_bounds__(128) void k_pair_eig_wave(int C, int j, int it, int fun, double tol,
+// W waves per projection (block 128 W): wave 0 of each tridiagonalises, then
+// all W multisect disjoint eigenvalue ranges with MS counts per lane.
+template <int W, int MS>
+__global__ __launch_bounds__(128 * W) void k_pair_eig_wave(int C, int j, int it, int fun, double tol,
                                                        const double* __restrict__ hist,
                                                        const double* __restrict__ Cm,
                                                        double* __restrict__ state) {
     extern __shared__ double sm[];
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
+    constexpr int NT = 128 * W;
     const int wave = tid >> 6, lane = tid & 63;
     double* st = state + (int64_t)c * PS_N;
     if (st[PS_DONE] != 0.0) return;
     const int nn = 2 * j;
     double* G = sm;
     double* T = G + nn * nn;
-    double* vec = T + nn * nn;  // per wave: d, e, v, w, e2, lam  (6 nn)
-    for (int t = tid; t < nn * nn; t += 128) G[t] = 0.0;
+    double* de = T + nn * nn;  // per projection: d (nn), e (nn)
+    double* vec = de + 4 * nn;  // eigenvalues: eig(T) (nn), then eig(G) (nn)
+    for (int t = tid; t < nn * nn; t += NT) G[t] = 0.0;
     __syncthreads();
-    for (int b = tid; b < j; b += 128) {  // row-major G[r * nn + col]
+    for (int b = tid; b < j; b += NT) {  // row-major G[r * nn + col]
         const double* h = hist + ((int64_t)b * C + c) * 11;
         G[(2 * b) * nn + 2 * b] = h[2];
         G[(2 * b + 1) * nn + 2 * b] = h[3];
@@ -621,7 +681,7 @@ __global__ __launch_bounds__(128) void k_pair_eig_wave(int C, int j, int it, int
         }
     }
     __syncthreads();
-    for (int t = tid; t < nn * nn; t += 128) T[t] = G[t];
+    for (int t = tid; t < nn * nn; t += NT) T[t] = G[t];
     __syncthreads();
     if (tid == 0) {
         const double* cm = Cm + (int64_t)c * 4;  // column-major 2x2
@@ -631,7 +691,7 @@ __global__ __launch_bounds__(128) void k_pair_eig_wave(int C, int j, int it, int
         T[nn + 1] += cm[3];
     }
     __syncthreads();
-    for (int t = tid; t < nn * nn; t += 128) {  // (X + X') / 2   :78-81
+    for (int t = tid; t < nn * nn; t += NT) {  // (X + X') / 2   :78-81
         const int r = t / nn, q = t % nn;
         if (q < r) {
             const double g = 0.5 * (G[r * nn + q] + G[q * nn + r]);
@@ -641,19 +701,32 @@ __global__ __launch_bounds__(128) void k_pair_eig_wave(int C, int j, int it, int
         }
     }
     __syncthreads();
-    double* my = vec + (size_t)wave * 6 * nn;
-    double* d = my;
-    double* e = d + nn;
-    double* v = e + nn;
-    double* w = v + nn;
-    double* e2 = w + nn;
-    double* lam = e2 + nn;
-    wave_tridiag(nn, wave == 0 ? T : G, d, e, v, w);
-    wave_multisect(nn, d, e, e2, lam);
+    const int mat = wave / W, wv = wave % W;  // mat 0: T (updated), 1: G
+    if (wv == 0) {
+        double dl, el;
+        wave_tridiag(nn, mat == 0 ? T : G, dl, el);
+        if (lane < nn) {
+            de[mat * 2 * nn + lane] = dl;
+            de[mat * 2 * nn + nn + lane] = el;
+        }
+    }
+    __syncthreads();
+    {
+        const double dreg = lane < nn ? de[mat * 2 * nn + lane] : 0.0;
+        const double ereg = lane < nn ? de[mat * 2 * nn + nn + lane] : 0.0;
+        const int per = (nn + W - 1) / W;
+        const int k0 = wv * per;
+        const int ne = min(per, nn - k0);
+        if (ne > 0) {  // wave-uniform
+            const double lam = wave_multisect<MS>(nn, dreg, ereg, k0, ne);
+            const int g = 64 / ne;
+            if (lane % g == 0 && lane / g < ne) vec[mat * nn + k0 + lane / g] = lam;
+        }
+    }
     __syncthreads();
     if (wave != 0) return;
-    const double* l1 = vec + 5 * nn;           // wave 0: eig(T), ascending
-    const double* l2 = vec + 6 * nn + 5 * nn;  // wave 1: eig(G)
+    const double* l1 = vec;       // wave 0: eig(T), ascending
+    const double* l2 = vec + nn;  // wave 1: eig(G)
     double term = 0.0;  // :85-89 (k-th smallest of each)
     if (lane < nn)
         term = (fun == 0) ? exp(l1[lane]) * (1.0 - exp(l2[lane] - l1[lane]))
@@ -697,9 +770,12 @@ __global__ void k_pair_active(int C, const double* __restrict__ state, int* __re
 hipError_t launch_pair_eig(int C, int j, int it, int fun, double tol, const double* hist,
                            const double* Cm, double* scratch, int64_t sstride, double* state,
                            int* active, hipStream_t st) {
-    if (2 * j <= 56) {  // 2 nn^2 + 12 nn doubles <= 55 KB of LDS
-        const size_t lds = sizeof(double) * (2 * (size_t)(2 * j) * (2 * j) + 12 * (size_t)(2 * j));
-        k_pair_eig_wave<<<C, 128, lds, st>>>(C, j, it, fun, tol, hist, Cm, state);
+    if (2 * j <= 56) {  // 2 nn^2 + 6 nn doubles <= 52 KB of LDS
+        const size_t lds = sizeof(double) * (2 * (size_t)(2 * j) * (2 * j) + 6 * (size_t)(2 * j));
+        // W = 1, MS = 4 measured fastest (profiles/r01_greedy_eig_variants.txt):
+        // the Sturm rounds are VALU-issue-bound, more waves per SIMD only
+        // evaluate more points per round
+        k_pair_eig_wave<1, 4><<<C, 128, lds, st>>>(C, j, it, fun, tol, hist, Cm, state);
     } else {
         k_pair_eig<<<(C + 63) / 64, 64, 0, st>>>(C, j, it, fun, tol, hist, Cm, scratch, sstride, state);
     }
@@ -742,26 +818,26 @@ size_t pairs_coef_doubles(int C) { return (size_t)CF_NCOEF * C; }
 
 hipError_t launch_pairs_orth(int C, int n, int num_cu, const double* prev, const double* cur,
                              double* W, int ld, double* coef, double* part, double* hr,
-                             hipStream_t st) {
+                             hipStream_t st, const int* skip) {
     if (C <= 0) return hipSuccess;
     int nrb, rpb;
     pairs_orth_geometry(n, C, num_cu, &nrb, &rpb);
     const dim3 grid((C + 63) / 64, nrb);
     const int cgrid = (C + 3) / 4;
     if (cur) {
-        k_pairs_sweep<PH_A><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, prev, cur, W, ld, coef, part);
-        k_pairs_coef<PH_A><<<cgrid, 256, 0, st>>>(C, nrb, part, W, ld, coef, hr);
-        k_pairs_sweep<PH_B><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, prev, cur, W, ld, coef, part);
-        k_pairs_coef<PH_B><<<cgrid, 256, 0, st>>>(C, nrb, part, W, ld, coef, hr);
-        k_pairs_sweep<PH_C><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, prev, cur, W, ld, coef, part);
-        k_pairs_coef<PH_C><<<cgrid, 256, 0, st>>>(C, nrb, part, W, ld, coef, hr);
+        k_pairs_sweep<PH_A><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, prev, cur, W, ld, coef, part, skip);
+        k_pairs_coef<PH_A><<<cgrid, 256, 0, st>>>(C, nrb, part, W, ld, coef, hr, skip);
+        k_pairs_sweep<PH_B><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, prev, cur, W, ld, coef, part, skip);
+        k_pairs_coef<PH_B><<<cgrid, 256, 0, st>>>(C, nrb, part, W, ld, coef, hr, skip);
+        k_pairs_sweep<PH_C><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, prev, cur, W, ld, coef, part, skip);
+        k_pairs_coef<PH_C><<<cgrid, 256, 0, st>>>(C, nrb, part, W, ld, coef, hr, skip);
     } else {
-        k_pairs_sweep<PH_C0><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, nullptr, nullptr, W, ld, coef, part);
-        k_pairs_coef<PH_C0><<<cgrid, 256, 0, st>>>(C, nrb, part, W, ld, coef, hr);
+        k_pairs_sweep<PH_C0><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, nullptr, nullptr, W, ld, coef, part, skip);
+        k_pairs_coef<PH_C0><<<cgrid, 256, 0, st>>>(C, nrb, part, W, ld, coef, hr, skip);
     }
-    k_pairs_sweep<PH_D><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, nullptr, nullptr, W, ld, coef, part);
-    k_pairs_coef<PH_D><<<cgrid, 256, 0, st>>>(C, nrb, part, W, ld, coef, hr);
-    k_pairs_sweep<PH_E><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, nullptr, nullptr, W, ld, coef, part);
+    k_pairs_sweep<PH_D><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, nullptr, nullptr, W, ld, coef, part, skip);
+    k_pairs_coef<PH_D><<<cgrid, 256, 0, st>>>(C, nrb, part, W, ld, coef, hr, skip);
+    k_pairs_sweep<PH_E><<<grid, kSweepBlock, 0, st>>>(n, C, rpb, nullptr, nullptr, W, ld, coef, part, skip);
     return hipGetLastError();
 }
 
