@@ -139,6 +139,22 @@ enum kt_afun { /* the Afun argument of mc_trace.m:1 */
 int kt_mc_trace(kt_matrix_t A, int afun, int fun, int m, double tol, int maxit, int isAreal,
                 uint64_t seed, double* tr, double* res, int* it);
 
+/* All-reduce (sum) of `count` doubles in place across the ranks of a job;
+ * supplied by the caller (torch.distributed / RCCL, MPI, ...).  0 = ok. */
+typedef int (*kt_reduce_fn)(double* buf, int64_t count, void* user);
+
+/* mc_trace on `world` GPUs (Hutch++ structure): every rank
+ * recomputes S, Q and tr(Q' Afun Q) from the shared seed; the 10 G-probe
+ * columns of each round are dealt round-robin (column c to rank c % world),
+ * their quadratic forms all-reduced with `allreduce` (one call per round,
+ * count = 10) and summed in column order, so every rank returns the same
+ * tr / res / it.  KT_AFUN_EXPMV is computed replicated (its Taylor degree is
+ * chosen per block, expmv.m:41) and never calls `allreduce`.  Replaces
+ * mc_trace.m:1-63 on a multi-GPU node; world = 1 equals kt_mc_trace. */
+int kt_mc_trace_sharded(kt_matrix_t A, int afun, int fun, int m, double tol, int maxit,
+                        int isAreal, uint64_t seed, int rank, int world, kt_reduce_fn allreduce,
+                        void* user, double* tr, double* res, int* it);
+
 /* tr = trace_exp(A) (trace_exp.m:1-7) = mc_trace(Afun, n, 1e-4, 1000, 1) with
  * Afun = KT_AFUN_EXPMV (the reference composition) or KT_AFUN_LANCZOS (m steps). */
 int kt_trace_exp(kt_matrix_t A, int afun, int m, uint64_t seed, double* tr);

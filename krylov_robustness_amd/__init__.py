@@ -18,6 +18,7 @@ from .greedy import (compute_centrality, default_greedy_tol, find_top_edges,
                      find_top_missing_edges, greedy_krylov, krylov_miobi, krylov_miobi_sharded,
                      miobi_loop, select_extreme, trace_fun_update_pairs)
 from . import datasets, matv73
+from .dist import mc_trace_sharded, trace_exp_sharded
 from .datasets import load_problem, load_unweighted, prepare_unweighted, prepare_weighted
 
 __all__ = [
@@ -29,4 +30,5 @@ __all__ = [
     "default_greedy_tol", "krylov_miobi_sharded", "miobi_loop", "select_extreme", "function_multiple_entries", "householder_qr", "frechet_entries",
     "hessianfcn", "hessianfcn_exp", "hessianfcn_fun", "eigs_leading", "datasets", "matv73",
     "load_problem", "load_unweighted", "prepare_unweighted", "prepare_weighted",
+    "mc_trace_sharded", "trace_exp_sharded",
 ]

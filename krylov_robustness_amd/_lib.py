@@ -42,6 +42,9 @@ _i64p = C.POINTER(C.c_int64)
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int)
 
+# kt_reduce_fn: in-place sum of `count` doubles across ranks; 0 = ok
+REDUCE_FN = C.CFUNCTYPE(C.c_int, _dp, C.c_int64, C.c_void_p)
+
 # (name, restype, argtypes) -- every symbol include/krylov_trace.h declares
 SIGNATURES = [
     ("kt_abi_version", C.c_int, []),
@@ -66,6 +69,9 @@ SIGNATURES = [
                                              C.c_double, C.c_int, _dp, _dp]),
     ("kt_mc_trace", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int,
                               C.c_uint64, _dp, _dp, _ip]),
+    ("kt_mc_trace_sharded", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int,
+                                      C.c_uint64, C.c_int, C.c_int, REDUCE_FN, C.c_void_p, _dp, _dp,
+                                      _ip]),
     ("kt_trace_exp", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_uint64, _dp]),
     ("kt_expmv", C.c_int, [_mat_p, C.c_double, C.c_int64, _dp, _dp, _ip, _ip, _ip]),
     ("kt_lanczos_fmv", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_int64, _dp, _dp]),

@@ -179,24 +179,39 @@ struct AfunDev {
         default: expmv_device(A, 1.0, X, ld, nc, Y); break;
         }
     }
-    // sum_c x_c' F(x_c)
-    double trace_quad(const double* X, int ld, int nc) {
+    // q[c] = x_c' F(x_c), c < nc
+    void quad_cols(const double* X, int ld, int nc, double* q) {
         if (kind == AFUN_LANCZOS) {
-            std::vector<double> q(nc);
-            lanczos_columns(A, X, ld, nc, m, fun, q.data(), nullptr, 0);
-            double s = 0.0;
-            for (double v : q) s += v;
-            return s;
+            lanczos_columns(A, X, ld, nc, m, fun, q, nullptr, 0);
+            return;
         }
         DevMat Y;
         Y.alloc(A->ctx, A->n, ld);
         apply(X, ld, nc, Y.col(0));
         std::vector<double> G;
         gram(A->ctx, A->n, X, ld, nc, Y.col(0), ld, nc, G);
+        for (int c = 0; c < nc; ++c) q[c] = G[c + (size_t)c * nc];
+    }
+    // sum_c x_c' F(x_c), summed in column order
+    double trace_quad(const double* X, int ld, int nc) {
+        std::vector<double> q(nc);
+        quad_cols(X, ld, nc, q.data());
         double s = 0.0;
-        for (int c = 0; c < nc; ++c) s += G[c + (size_t)c * nc];
+        for (double v : q) s += v;
         return s;
     }
+};
+
+// Multi-GPU form of mc_trace: every rank recomputes S, Q
+// and tr(Q' Afun Q) from the shared seed; the G term's columns are dealt
+// round-robin (column c to rank c % world) and their quadratic forms
+// summed by one all-reduce of the 10-vector, then added in column order
+// on every rank.  expmv picks its Taylor degree from the whole block
+// (expmv.m:41), so that Afun stays replicated.
+struct Shard {
+    int rank = 0, world = 1;
+    kt_reduce_fn allreduce = nullptr;
+    void* user = nullptr;
 };
 
 // X <- X - Q (Q' X)  on nc columns (the deflation aux of mc_trace.m:47)
@@ -209,7 +224,7 @@ static void project(kt_context_s* ctx, int64_t n, const double* Q, int ld, int n
 
 // mc_trace.m:1-63
 void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isAreal, uint64_t seed,
-                   double* tr_out, double* res_out, int* it_out) {
+                   double* tr_out, double* res_out, int* it_out, const Shard& sh = Shard()) {
     kt_context_s* ctx = A->ctx;
     const int64_t n = A->n;
     const int mb = 10, ld = 16;                    // :36
@@ -245,7 +260,23 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
         // tr_new = tr + trace(G' Afun_{it+1}(G)) / m                              :49
         copy_cols(ctx, n, G.col(0), ld, Z.col(0), ld, mb);
         for (int q = (int)Qs.size() - 1; q >= 0; --q) project(ctx, n, Qs[q].col(0), ld, mb, Z.col(0), mb);
-        tr_new = tr + F.trace_quad(Z.col(0), ld, mb) / mb;
+        double gsum = 0.0;
+        if (sh.world > 1 && F.kind != AFUN_EXPMV) {
+            std::vector<double> qv(mb, 0.0), qm;
+            int nm = 0;
+            for (int c = sh.rank; c < mb; c += sh.world) copy_cols(ctx, n, Z.col(c), ld, Y.col(nm++), ld, 1);
+            if (nm > 0) {
+                zero_cols(ctx, n, Y.col(nm), ld, ld - nm);
+                qm.assign(nm, 0.0);
+                F.quad_cols(Y.col(0), ld, nm, qm.data());
+                for (int c = sh.rank, t = 0; c < mb; c += sh.world, ++t) qv[c] = qm[t];
+            }
+            if (sh.allreduce(qv.data(), mb, sh.user) != 0) fail(KT_ERR_ARG, "mc_trace: all-reduce callback failed");
+            for (double v : qv) gsum += v;
+        } else {
+            gsum = F.trace_quad(Z.col(0), ld, mb);
+        }
+        tr_new = tr + gsum / mb;
         res = std::fabs(tr_new - tr_old) / std::max(std::fabs(tr_new), std::fabs(tr_old));  // :50
         if (res < tol) break;                                                      // :54-56
         tr_old = tr_new;
@@ -288,6 +319,25 @@ int kt_mc_trace(kt_matrix_t A, int afun, int fun, int m, double tol, int maxit, 
     KT_HIP(hipSetDevice(A->ctx->device));
     AfunDev F{A, afun, fun, m};
     mc_trace_impl(A, F, tol, maxit, isAreal, seed, tr, res, it);
+    KT_CATCH
+}
+
+int kt_mc_trace_sharded(kt_matrix_t A, int afun, int fun, int m, double tol, int maxit, int isAreal,
+                        uint64_t seed, int rank, int world, kt_reduce_fn allreduce, void* user,
+                        double* tr, double* res, int* it) {
+    KT_TRY
+    if (!A || !tr) fail(KT_ERR_ARG, "NULL argument");
+    if (world < 1 || rank < 0 || rank >= world) fail(KT_ERR_ARG, "bad rank / world");
+    if (world > 1 && !allreduce) fail(KT_ERR_ARG, "world > 1 needs an all-reduce callback");
+    if (afun < AFUN_MATRIX || afun > AFUN_EXPMV) fail(KT_ERR_ARG, "unknown Afun kind");
+    if (fun < KT_FUN_EXP || fun > KT_FUN_SQRT) fail(KT_ERR_ARG, "unknown fun code");
+    if (afun == AFUN_LANCZOS && (m < 1 || m > 256)) fail(KT_ERR_ARG, "m must be in [1, 256]");
+    if (maxit < 1) fail(KT_ERR_ARG, "maxit must be >= 1");
+    if (A->n < 10) fail(KT_ERR_UNSUPPORTED, "mc_trace needs n >= 10 (qr of an n x 10 block)");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    AfunDev F{A, afun, fun, m};
+    Shard sh{rank, world, allreduce, user};
+    mc_trace_impl(A, F, tol, maxit, isAreal, seed, tr, res, it, sh);
     KT_CATCH
 }
 

@@ -60,3 +60,72 @@ def allgather_concat(x, counts, group=None):
     parts = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(parts, t, group=group)
     return np.concatenate([p[:int(c)].cpu().numpy() for p, c in zip(parts, counts)])
+
+
+def reduce_callback(group=None):
+    """A kt_reduce_fn (include/krylov_trace.h) that sums the buffer over the
+    torch.distributed group: device tensors on RCCL ("nccl"), CPU tensors
+    on gloo.  Keep the returned object alive for the duration of the call."""
+    import ctypes as C
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from . import _lib
+
+    def _cb(buf, count, user):
+        try:
+            arr = np.ctypeslib.as_array(buf, shape=(int(count),))
+            backend = dist.get_backend(group)
+            dev = (torch.device("cuda", torch.cuda.current_device()) if backend == "nccl"
+                   else torch.device("cpu"))
+            t = torch.from_numpy(arr.copy()).to(dev)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+            arr[:] = t.cpu().numpy()
+            return 0
+        except Exception:  # reported to the caller as a kt status
+            return 1
+
+    return _lib.REDUCE_FN(_cb)
+
+
+def mc_trace_sharded(Afun, n=None, tol=1e-3, maxit=10, isAreal=0, debug=0, seed=0, fun="exp",
+                     m=30, A=None, rank=None, world=None, allreduce=None, group=None, ctx=None):
+    """[tr, res, it] = mc_trace(...) on `world` GPUs: every
+    rank recomputes S, Q and tr(Q' Afun Q) from the shared seed, the G-probe
+    columns are dealt round-robin and their quadratic forms summed by one
+    all-reduce per round (kt_mc_trace_sharded).  Afun as in core.mc_trace.
+    rank / world default to the torch.distributed group; `allreduce` is a
+    _lib.REDUCE_FN (default: reduce_callback(group))."""
+    import ctypes as C
+    from . import _lib
+    from .core import _dev
+    if rank is None or world is None:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            rank, world = dist.get_rank(group), dist.get_world_size(group)
+        else:
+            rank, world = 0, 1
+    if isinstance(Afun, str):
+        kind = _lib.AFUN_CODES[Afun]
+        D = _dev(A, ctx)
+    else:
+        kind = _lib.AFUN_CODES["matrix"]
+        D = _dev(Afun, ctx)
+    if n is not None and int(n) != D.n:
+        raise _lib.KrylovError(_lib.KT_ERR_ARG, "n does not match the matrix")
+    cb = allreduce if allreduce is not None else (reduce_callback(group) if world > 1
+                                                  else _lib.REDUCE_FN(0))
+    tr, res, it = C.c_double(), C.c_double(), C.c_int()
+    _lib.check(_lib.load().kt_mc_trace_sharded(
+        D.handle, kind, _lib.FUN_CODES[fun] if isinstance(fun, str) else int(fun), int(m), float(tol),
+        int(maxit), int(isAreal), int(seed) & 0xFFFFFFFFFFFFFFFF, int(rank), int(world), cb, None,
+        C.byref(tr), C.byref(res), C.byref(it)))
+    return float(tr.value), float(res.value), int(it.value)
+
+
+def trace_exp_sharded(A, method="lanczos", m=30, seed=0, rank=None, world=None, allreduce=None,
+                      group=None, ctx=None):
+    """trace_exp.m:1-7 (mc_trace(Afun, n, 1e-4, 1000, 1)) on `world` GPUs."""
+    tr, _, _ = mc_trace_sharded(method, None, 1e-4, 1000, 1, 0, seed, "exp", m, A=A, rank=rank,
+                                world=world, allreduce=allreduce, group=group, ctx=ctx)
+    return tr

@@ -79,6 +79,8 @@ def test_every_entry_point_rejects_null_handles():
                 vals.append(1)
             elif a is C.c_double:
                 vals.append(1e-8)
+            elif a is _lib.REDUCE_FN:
+                vals.append(_lib.REDUCE_FN(0))  # NULL callback
             else:
                 vals.append(None)
         st = getattr(lib, name)(*vals)

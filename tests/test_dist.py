@@ -123,3 +123,38 @@ def test_gloo_world2_sharded_greedy_matches_single():
     eo, ro, _ = ko.krylov_miobi(A, 3, E, 1e-10, 60, np.inf, 0, "break", 1.0)
     assert edges == eo.tolist()
     assert rob == pytest.approx(ro, rel=1e-12)
+
+
+def _reduce_worker(rank, world, port, out):
+    """kt_reduce_fn plumbing: the ctypes callback mc_trace_sharded hands to
+    the library sums its buffer over the gloo group in place."""
+    import ctypes as C
+    import torch.distributed as dist
+    from krylov_robustness_amd.dist import reduce_callback
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cb = reduce_callback()
+    buf = (C.c_double * 10)(*[0.0] * 10)
+    for c in range(rank, 10, world):  # the round-robin G-column deal
+        buf[c] = 1.5 * c + 0.25
+    st = cb(buf, 10, None)
+    if rank == 0:
+        out.put((st, list(buf)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_reduce_callback():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reduce_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    st, vals = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert st == 0
+    assert vals == [1.5 * c + 0.25 for c in range(10)]
