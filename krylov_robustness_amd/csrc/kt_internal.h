@@ -117,7 +117,10 @@ struct kt_context_s {
     hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};  // extra probe-sweep lanes (lazy)
     int num_cu = 256;
     bool profile = false;
-    int k1_flags = 0;  // KT_K1_FLAGS: bit 0 = non-temporal stream hints in K1
+    // KT_K1_FLAGS: bit 0 = non-temporal CSR streams in K1, bit 2 = deep gather
+    // issue, bit 3 = non-temporal y store (default: profiles/r01_sweep_nt.txt)
+    int k1_flags = 8;
+    bool k2_nt = true;  // KT_K2_NT=0 disables: K2 loads y and u_prev non-temporal
     void* blas = nullptr;  // rocblas_handle, created on first block-Krylov use
     kt::ProfSlot prof[kt::PROF_NSLOTS];
     kt::Workspace ws;

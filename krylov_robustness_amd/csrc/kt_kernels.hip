@@ -58,7 +58,11 @@ template <int P> struct Geo {
 // FLAGS bit 2: deep gather issue -- up to 8 column indices, then up to 8 row
 // gathers in flight per row group per round trip (predicated tails, no
 // serial remainder loop), for graphs whose rows are mostly short.
-enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4 };
+// FLAGS bit 0: the CSR index/value streams are loaded nontemporal (read once
+// per launch; keeps L2/MALL for the gathered rows).  Bit 3: y is stored
+// nontemporal.  The own-row load of u_cur is always a normal load (it is the
+// gathered table).
+enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4, KF_NTY = 8 };
 
 template <int VEC> struct VecT;
 template <> struct VecT<1> {
@@ -220,9 +224,7 @@ __device__ __forceinline__ void row_epilogue(int row, int p0, const double* s, c
     using G = Geo<P>;
     using V = VecT<G::VEC>;
     const int64_t off = (int64_t)row * P + p0;
-    typename V::T ui;
-    if constexpr (FLAGS & KF_NT) ui = V::load_nt(ucur + off);
-    else ui = V::load(ucur + off);
+    const typename V::T ui = V::load(ucur + off);
     typename V::T yo;
     double* yp = reinterpret_cast<double*>(&yo);
 #pragma unroll
@@ -231,7 +233,7 @@ __device__ __forceinline__ void row_epilogue(int row, int p0, const double* s, c
         yp[e] = yv;
         acc[e] = fma(V::get(ui, e) * sc[e], yv, acc[e]);
     }
-    if constexpr (FLAGS & KF_NT) V::store_nt(y + off, yo);
+    if constexpr (FLAGS & KF_NTY) V::store_nt(y + off, yo);
     else V::store(y + off, yo);
 }
 
@@ -437,7 +439,7 @@ __global__ __launch_bounds__(256) void k_coef_cgs2(const double* __restrict__ pa
 // Pure streaming: rows are contiguous, so lanes cover 16 B each.
 // ---------------------------------------------------------------------------
 
-template <int P, int BLOCK>
+template <int P, int BLOCK, bool NT>
 __global__ __launch_bounds__(BLOCK) void k_update(
     int n, const double* __restrict__ y, double* __restrict__ uprev,
     const double* __restrict__ ucur, const double* __restrict__ scale_cur,
@@ -461,10 +463,11 @@ __global__ __launch_bounds__(BLOCK) void k_update(
     const int groups_total = gridDim.x * WAVES * G::GPW;
     for (int row = (blockIdx.x * WAVES + wave) * G::GPW + grp; row < n; row += groups_total) {
         const int64_t off = (int64_t)row * P + p0;
-        const typename V::T yv = V::load(y + off);
+        // y and u_prev are dead after this pass (u_next overwrites u_prev)
+        const typename V::T yv = NT ? V::load_nt(y + off) : V::load(y + off);
         const typename V::T cv = V::load(ucur + off);
         typename V::T pv;
-        if (!first) pv = V::load(uprev + off);
+        if (!first) pv = NT ? V::load_nt(uprev + off) : V::load(uprev + off);
         typename V::T o;
         double* op = reinterpret_cast<double*>(&o);
 #pragma unroll
@@ -646,15 +649,19 @@ hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int*
 #define KT_K1(F)                                                                              \
     k_spmm_dot<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, ucur, sc, y, partial,      \
                                                        long_rows, n_long, long_thresh, long_blocks)
-        switch (flags & 7) {
+        switch (flags & 15) {
         case 0: KT_K1(0); break;
-        case KF_NT: KT_K1(KF_NT); break;
         case KF_UNIT: KT_K1(KF_UNIT); break;
+        case KF_NT: KT_K1(KF_NT); break;
         case KF_NT | KF_UNIT: KT_K1(KF_NT | KF_UNIT); break;
+        case KF_NTY | KF_UNIT: KT_K1(KF_NTY | KF_UNIT); break;
+        case KF_NT | KF_NTY | KF_UNIT: KT_K1(KF_NT | KF_NTY | KF_UNIT); break;
         case KF_MLP: KT_K1(KF_MLP); break;
-        case KF_MLP | KF_NT: KT_K1(KF_MLP | KF_NT); break;
         case KF_MLP | KF_UNIT: KT_K1(KF_MLP | KF_UNIT); break;
-        default: KT_K1(KF_MLP | KF_NT | KF_UNIT); break;
+        default:  // unsupported combination: keep only the unit bit (exactness)
+            if (flags & KF_UNIT) KT_K1(KF_UNIT);
+            else KT_K1(0);
+            break;
         }
 #undef KT_K1
     });
@@ -692,10 +699,14 @@ hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, c
 
 hipError_t launch_update(int P, int grid, int n, const double* y, double* uprev,
                          const double* ucur, const double* sc, const double* sp,
-                         const double* coef, int first, double* partial, hipStream_t st) {
+                         const double* coef, int first, double* partial, hipStream_t st, bool nt) {
     return dispatch_p(P, [&](auto c) {
-        k_update<decltype(c)::value, kBlock><<<grid, kBlock, 0, st>>>(n, y, uprev, ucur, sc, sp,
-                                                                      coef, first, partial);
+        if (nt)
+            k_update<decltype(c)::value, kBlock, true><<<grid, kBlock, 0, st>>>(n, y, uprev, ucur, sc,
+                                                                                sp, coef, first, partial);
+        else
+            k_update<decltype(c)::value, kBlock, false><<<grid, kBlock, 0, st>>>(n, y, uprev, ucur, sc,
+                                                                                 sp, coef, first, partial);
     });
 }
 

@@ -24,7 +24,8 @@ hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, c
                             double* t_up, hipStream_t st);
 hipError_t launch_update(int P, int grid, int n, const double* y, double* uprev,
                          const double* ucur, const double* sc, const double* sp,
-                         const double* coef, int first, double* partial, hipStream_t st);
+                         const double* coef, int first, double* partial, hipStream_t st,
+                         bool nt = false);
 hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, double* scale_next,
                        double* t_low, hipStream_t st);
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st);

@@ -197,6 +197,7 @@ int kt_context_create(int device, kt_context_t* out) {
     KT_HIP(hipGetDeviceProperties(&prop, device));
     ctx->num_cu = prop.multiProcessorCount;
     if (const char* f = getenv("KT_K1_FLAGS")) ctx->k1_flags = atoi(f);
+    if (const char* f = getenv("KT_K2_NT")) ctx->k2_nt = f[0] == '1';
     KT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     *out = ctx;
     KT_GUARD_END

@@ -111,7 +111,7 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
                                 trec + (size_t)(0 * m + j) * P, trec + (size_t)(1 * m + j) * P, st));
         prof_begin(ctx, PROF_UPDATE, st);
         KT_HIP(launch_update(P, grid, n, w.Y.as<double>(), uprev, ucur, sc, sp, coef, first, part2,
-                             st));
+                             st, ctx->k2_nt));
         prof_end(ctx, PROF_UPDATE, st);
         KT_HIP(launch_norm(P, part2, grid, k2s, sn, trec + (size_t)(2 * m + j) * P, st));
         std::swap(ucur, uprev);  // uprev now holds u_{j+1}
