@@ -98,6 +98,7 @@ struct SweepBufs {
 struct Workspace {
     SweepBufs sweep[4];
     DevBuf small, small2, qrtmp, eigA, eigW, eigInfo;  // block-Krylov scratch
+    DevBuf expm;                                       // batched device expm (6 x batch x n^2)
     DevBuf hist, norm_part;                             // sweep scale history, inf-norm partials
     PinnedBuf host_trec;
     // batched greedy candidates (kt_greedy.cpp): 3 pair blocks, indices,

@@ -18,6 +18,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <thread>
 
 #include "kt_krylov.h"
 #include "kt_launch.h"
@@ -38,22 +40,35 @@ struct EigStats {
     }
 };
 static EigStats g_eig;
+static std::mutex g_eig_mu;  // the projection pairs are solved on two host threads
 
 struct EigTimer {
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     ~EigTimer() {
-        g_eig.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::lock_guard<std::mutex> lk(g_eig_mu);
+        g_eig.ms += ms;
     }
 };
 
 static void sym_eig_dispatch(kt_context_s* ctx, int n, const double* A, double* w, double* V);
 
 static void sym_eig(kt_context_s* ctx, int n, const double* A, double* w, double* V) {
-    EigTimer tm;
-    g_eig.calls++;
-    g_eig.maxn = std::max(g_eig.maxn, n);
-    if (n > (V ? 160 : 320)) g_eig.dev_calls++;
-    sym_eig_dispatch(ctx, n, A, w, V);
+    static const bool log = getenv("KT_EIG_STATS") && getenv("KT_EIG_STATS")[0] == '2';
+    const auto t0 = std::chrono::steady_clock::now();
+    {
+        EigTimer tm;
+        {
+            std::lock_guard<std::mutex> lk(g_eig_mu);
+            g_eig.calls++;
+            g_eig.maxn = std::max(g_eig.maxn, n);
+            if (n > (V ? 160 : 320)) g_eig.dev_calls++;
+        }
+        sym_eig_dispatch(ctx, n, A, w, V);
+    }
+    if (log)
+        fprintf(stderr, "[kt eig] n %d %s %.3f ms\n", n, V ? "vec" : "val",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
 static void sym_eig_dispatch(kt_context_s* ctx, int n, const double* A, double* w, double* V) {
@@ -90,63 +105,87 @@ static std::vector<double> sym_eigvals(kt_context_s* ctx, int n, const std::vect
     return w;
 }
 
-// exp(sgn * M) for an n x n matrix M (host, column-major) on the device:
-// truncated Taylor of degree 18 evaluated by Paterson-Stockmeyer (powers X^2,
-// X^3, X^4 and four Horner steps in X^4) on X = sgn M / 2^s, then s
-// squarings; s = max(0, ceil(log2(||M||_1 / theta_18))) with theta_18 the
-// double-precision Taylor bound of Al-Mohy & Higham (expm(M) of
-// fun_update.m:43-59 is a scaling-and-squaring method too).
-static std::vector<double> expm_device(kt_context_s* ctx, int n, const std::vector<double>& M,
-                                       double sgn) {
+// exp(sgn_b * M_b) for a batch of n x n matrices (host, column-major) on the
+// device: truncated Taylor of degree 18 evaluated by Paterson-Stockmeyer
+// (powers X^2, X^3, X^4 and four Horner steps in X^4) on X = sgn M / 2^s,
+// then s squarings; s = max(0, ceil(log2(||M||_1 / theta_18))) per matrix
+// with theta_18 the double-precision Taylor bound of Al-Mohy & Higham
+// (expm(M) of fun_update.m:43-59 is a scaling-and-squaring method too).  The
+// batch shares every launch (strided-batched dgemm, batched k_poly4); the
+// squarings run on the prefix of matrices (sorted by s) that still need one.
+static std::vector<std::vector<double>> expm_device_batch(kt_context_s* ctx, int n,
+                                                          const std::vector<const double*>& Ms,
+                                                          const std::vector<double>& sgns) {
     const double theta18 = 1.0908637192900361;
-    double nrm1 = 0.0;
-    for (int j = 0; j < n; ++j) {
-        double c = 0.0;
-        for (int i = 0; i < n; ++i) c += std::fabs(M[i + (size_t)j * n]);
-        nrm1 = std::max(nrm1, c);
+    const int nb = (int)Ms.size();
+    std::vector<int> sv(nb, 0);
+    for (int b = 0; b < nb; ++b) {
+        double nrm1 = 0.0;
+        for (int j = 0; j < n; ++j) {
+            double c = 0.0;
+            for (int i = 0; i < n; ++i) c += std::fabs(Ms[b][i + (size_t)j * n]);
+            nrm1 = std::max(nrm1, c);
+        }
+        if (nrm1 > theta18) sv[b] = (int)std::ceil(std::log2(nrm1 / theta18));
     }
-    int s = 0;
-    if (nrm1 > theta18) s = (int)std::ceil(std::log2(nrm1 / theta18));
-    const double scale = sgn * std::ldexp(1.0, -s);
-    std::vector<double> Xh(M.size());
-    for (size_t t = 0; t < M.size(); ++t) Xh[t] = scale * M[t];
-    const size_t nn = (size_t)n * n;
-    DevBuf buf;
-    buf.ensure(sizeof(double) * nn * 6);
+    std::vector<int> ord(nb);
+    for (int b = 0; b < nb; ++b) ord[b] = b;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return sv[a] > sv[b]; });
+    const size_t nn = (size_t)n * n, bn = nn * nb;
+    std::vector<double> Xh(bn);
+    for (int k = 0; k < nb; ++k) {
+        const int b = ord[k];
+        const double scale = sgns[b] * std::ldexp(1.0, -sv[b]);
+        for (size_t t = 0; t < nn; ++t) Xh[k * nn + t] = scale * Ms[b][t];
+    }
+    DevBuf& buf = ctx->ws.expm;
+    buf.ensure(sizeof(double) * bn * 6);
     double* X1 = buf.as<double>();
-    double* X2 = X1 + nn;
-    double* X3 = X2 + nn;
-    double* X4 = X3 + nn;
-    double* T = X4 + nn;
-    double* U = T + nn;
+    double* X2 = X1 + bn;
+    double* X3 = X2 + bn;
+    double* X4 = X3 + bn;
+    double* T = X4 + bn;
+    double* U = T + bn;
     hipStream_t st = ctx->stream;
-    KT_HIP(hipMemcpyAsync(X1, Xh.data(), sizeof(double) * nn, hipMemcpyHostToDevice, st));
+    KT_HIP(hipMemcpyAsync(X1, Xh.data(), sizeof(double) * bn, hipMemcpyHostToDevice, st));
     const double one = 1.0, zero = 0.0;
-    auto mm = [&](const double* A, const double* B, double* C) {
-        if (rocblas_dgemm(blas(ctx), rocblas_operation_none, rocblas_operation_none, n, n, n, &one, A, n,
-                          B, n, &zero, C, n) != rocblas_status_success)
-            fail(KT_ERR_HIP, "rocblas_dgemm(expm) failed");
+    auto mm = [&](const double* A, const double* B, double* C, int cnt) {
+        if (rocblas_dgemm_strided_batched(blas(ctx), rocblas_operation_none, rocblas_operation_none, n, n, n,
+                                          &one, A, n, (rocblas_stride)nn, B, n, (rocblas_stride)nn, &zero, C,
+                                          n, (rocblas_stride)nn, cnt) != rocblas_status_success)
+            fail(KT_ERR_HIP, "rocblas_dgemm_strided_batched(expm) failed");
     };
-    mm(X1, X1, X2);
-    mm(X2, X1, X3);
-    mm(X2, X2, X4);
+    mm(X1, X1, X2, nb);
+    mm(X2, X1, X3, nb);
+    mm(X2, X2, X4, nb);
     double c[19];
     c[0] = 1.0;
     for (int k = 1; k <= 18; ++k) c[k] = c[k - 1] / k;
     // T = B_4 = c16 I + c17 X + c18 X^2;  T = T X^4 + B_k, k = 3..0
-    KT_HIP(launch_poly4(n, 0.0, nullptr, c[16], c[17], X1, c[18], X2, 0.0, nullptr, T, st));
+    KT_HIP(launch_poly4(n, 0.0, nullptr, c[16], c[17], X1, c[18], X2, 0.0, nullptr, T, st, nb));
     for (int k = 3; k >= 0; --k) {
-        mm(T, X4, U);
-        KT_HIP(launch_poly4(n, 1.0, U, c[4 * k], c[4 * k + 1], X1, c[4 * k + 2], X2, c[4 * k + 3], X3, T, st));
+        mm(T, X4, U, nb);
+        KT_HIP(launch_poly4(n, 1.0, U, c[4 * k], c[4 * k + 1], X1, c[4 * k + 2], X2, c[4 * k + 3], X3, T, st,
+                            nb));
     }
-    for (int q = 0; q < s; ++q) {  // squaring
-        mm(T, T, U);
-        std::swap(T, U);
+    for (int q = 0;; ++q) {  // squarings of the matrices with s > q (a prefix)
+        int cnt = 0;
+        while (cnt < nb && sv[ord[cnt]] > q) ++cnt;
+        if (cnt == 0) break;
+        mm(T, T, U, cnt);
+        KT_HIP(hipMemcpyAsync(T, U, sizeof(double) * nn * cnt, hipMemcpyDeviceToDevice, st));
     }
-    std::vector<double> F(nn);
-    KT_HIP(hipMemcpyAsync(F.data(), T, sizeof(double) * nn, hipMemcpyDeviceToHost, st));
+    std::vector<double> Fh(bn);
+    KT_HIP(hipMemcpyAsync(Fh.data(), T, sizeof(double) * bn, hipMemcpyDeviceToHost, st));
     KT_HIP(hipStreamSynchronize(st));
-    return F;
+    std::vector<std::vector<double>> out(nb);
+    for (int k = 0; k < nb; ++k) out[ord[k]].assign(Fh.begin() + k * nn, Fh.begin() + (k + 1) * nn);
+    return out;
+}
+
+static std::vector<double> expm_device(kt_context_s* ctx, int n, const std::vector<double>& M,
+                                       double sgn) {
+    return std::move(expm_device_batch(ctx, n, {M.data()}, {sgn})[0]);
 }
 
 // f(M) for symmetric M (fun_update.m:43-59 maps exp/sinh/cosh/sin/cos/log/sqrt
@@ -226,6 +265,90 @@ void require_symmetric(kt_matrix_s* A, const char* msg) {
 }
 
 // dense host copy of A (original numbering), column-major
+// The two projections of a Krylov step (tGm with the low-rank update, Gm
+// without, trace_fun_update.m:83-84 / fun_update.m:106) are independent:
+// host-size problems are solved on two host threads; exp/sinh/cosh above
+// kDevExpm go through ONE batched device expm (2 matrices for exp, 4 for
+// sinh/cosh = (expm(M) -+ expm(-M)) / 2).
+constexpr int kDevExpm = 64;
+constexpr int kPairThreads = 48;  // below this a second thread costs more than it saves
+
+template <class F1, class F2>
+static void run_pair(bool parallel, F1&& f1, F2&& f2) {
+    if (!parallel) {
+        f1();
+        f2();
+        return;
+    }
+    std::exception_ptr err;
+    std::thread th([&] {
+        try {
+            f2();
+        } catch (...) {
+            err = std::current_exception();
+        }
+    });
+    try {
+        f1();
+    } catch (...) {
+        th.join();
+        throw;
+    }
+    th.join();
+    if (err) std::rethrow_exception(err);
+}
+
+// f(M1) - f(M2) for symmetric n x n M1, M2
+static std::vector<double> sym_matfun_diff(kt_context_s* ctx, int n, const std::vector<double>& M1,
+                                           const std::vector<double>& M2, int fun) {
+    const bool expfam = fun == KT_FUN_EXP || fun == KT_FUN_SINH || fun == KT_FUN_COSH;
+    if (expfam && n > kDevExpm) {
+        std::vector<std::vector<double>> E;
+        if (fun == KT_FUN_EXP) {
+            E = expm_device_batch(ctx, n, {M1.data(), M2.data()}, {1.0, 1.0});
+            for (size_t t = 0; t < E[0].size(); ++t) E[0][t] -= E[1][t];
+            return std::move(E[0]);
+        }
+        E = expm_device_batch(ctx, n, {M1.data(), M1.data(), M2.data(), M2.data()}, {1.0, -1.0, 1.0, -1.0});
+        const double sg = fun == KT_FUN_SINH ? -1.0 : 1.0;
+        std::vector<double> D(E[0].size());
+        for (size_t t = 0; t < D.size(); ++t)
+            D[t] = 0.5 * (E[0][t] + sg * E[1][t]) - 0.5 * (E[2][t] + sg * E[3][t]);
+        return D;
+    }
+    std::vector<double> F1, F2;
+    const bool host = n <= 160;  // sym_matfun's host-eig range (no device work)
+    run_pair(host && n >= kPairThreads, [&] { F1 = sym_matfun(ctx, n, M1, fun); },
+             [&] { F2 = sym_matfun(ctx, n, M2, fun); });
+    for (size_t t = 0; t < F1.size(); ++t) F1[t] -= F2[t];
+    return F1;
+}
+
+// sorted eigenvalues of both projections
+static void sym_eigvals_pair(kt_context_s* ctx, int n, const std::vector<double>& M1,
+                             const std::vector<double>& M2, std::vector<double>& w1,
+                             std::vector<double>& w2) {
+    const bool host = n <= 320;  // sym_eig_dispatch's values-only host range
+    run_pair(host && n >= kPairThreads, [&] { w1 = sym_eigvals(ctx, n, M1); },
+             [&] { w2 = sym_eigvals(ctx, n, M2); });
+}
+
+// ||D||_2 < tol for symmetric n x n D, decided from bounds when they settle
+// it (max column 2-norm <= ||D||_2 <= ||D||_F), else from the spectrum
+static bool sym_norm2_below(kt_context_s* ctx, int n, const std::vector<double>& D, double tol) {
+    double fro2 = 0.0, col2max = 0.0;
+    for (int j = 0; j < n; ++j) {
+        double c2 = 0.0;
+        for (int i = 0; i < n; ++i) c2 += D[i + (size_t)j * n] * D[i + (size_t)j * n];
+        fro2 += c2;
+        col2max = std::max(col2max, c2);
+    }
+    if (std::sqrt(fro2) < tol) return true;
+    if (std::sqrt(col2max) >= tol) return false;
+    const std::vector<double> ev = sym_eigvals(ctx, n, D);
+    return std::max(std::fabs(ev.front()), std::fabs(ev.back())) < tol;
+}
+
 static std::vector<double> dense_A(const kt_matrix_s* A) {
     const int64_t n = A->n;
     std::vector<double> D((size_t)n * n, 0.0);
@@ -483,7 +606,9 @@ double trace_fun_update_impl(kt_matrix_s* A, int rk, const double* U, const doub
                 const double s = 0.5 * (fAt[i + j * n] + fAt[j + i * n]);
                 fAt[i + j * n] = fAt[j + i * n] = s;
             }
-        const double x = trace_diff(sym_eigvals(ctx, (int)n, fAt), sym_eigvals(ctx, (int)n, fA), fun);
+        std::vector<double> w1, w2;
+        sym_eigvals_pair(ctx, (int)n, fAt, fA, w1, w2);
+        const double x = trace_diff(w1, w2, fun);
         if (iter_out) *iter_out = 0;
         if (lucky_out) *lucky_out = 0;
         return x;
@@ -515,7 +640,9 @@ double trace_fun_update_impl(kt_matrix_s* A, int rk, const double* U, const doub
                 s = 0.5 * (tGm[a + (size_t)b * nn] + tGm[b + (size_t)a * nn]);
                 tGm[a + (size_t)b * nn] = tGm[b + (size_t)a * nn] = s;
             }
-        Xm = trace_diff(sym_eigvals(ctx, nn, tGm), sym_eigvals(ctx, nn, Gm), fun);  // :83-89
+        std::vector<double> w1, w2;
+        sym_eigvals_pair(ctx, nn, tGm, Gm, w1, w2);
+        Xm = trace_diff(w1, w2, fun);  // :83-89
         if (j <= d) {                                                          // :104-118
             Xstop[j - 1] = Xm;
         } else {
@@ -569,8 +696,7 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
         if (2 * (int64_t)Ar.nblk * rk >= n) {  // size(Um,2) >= size(Um,1)/2   :85-90
             std::vector<double> fA = dense_A(A), fAt = fA;
             add_UBUt(fAt, n, rk, U, B);
-            std::vector<double> F1 = sym_matfun(ctx, (int)n, fAt, fun), F2 = sym_matfun(ctx, (int)n, fA, fun);
-            for (size_t t = 0; t < F1.size(); ++t) F1[t] -= F2[t];
+            std::vector<double> F1 = sym_matfun_diff(ctx, (int)n, fAt, fA, fun);
             res.Xm.swap(F1);
             res.nx = (int)n;
             res.iter = j;
@@ -591,8 +717,7 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
                 tGm[ii + (size_t)jj * nn] += herm ? 0.5 * (Cm[ii + (size_t)jj * rk] + Cm[jj + (size_t)ii * rk])
                                                   : Cm[ii + (size_t)jj * rk];
         if (!herm) fail(KT_ERR_UNSUPPORTED, "fun_update: non-Hermitian B");
-        std::vector<double> F1 = sym_matfun(ctx, nn, tGm, fun), F2 = sym_matfun(ctx, nn, Gm, fun);
-        for (size_t t = 0; t < F1.size(); ++t) F1[t] -= F2[t];               // :106
+        std::vector<double> F1 = sym_matfun_diff(ctx, nn, tGm, Gm, fun);     // :106
         res.Xm = F1;
         res.nx = nn;
         if (j <= d) {                                                        // :109-126
@@ -602,10 +727,8 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
             std::vector<double> D = F1;
             for (int b = 0; b < n0; ++b)
                 for (int a = 0; a < n0; ++a) D[a + (size_t)b * nn] -= Xstop[0][a + (size_t)b * n0];
-            // 2-norm of the symmetric difference = max |eig|
-            const std::vector<double> ev = sym_eigvals(ctx, nn, D);
-            const double err = std::max(std::fabs(ev.front()), std::fabs(ev.back()));
-            if (err < tol) break;
+            // 2-norm of the symmetric difference (= max |eig|) below tol?
+            if (sym_norm2_below(ctx, nn, D, tol)) break;
             Xstop.erase(Xstop.begin());
             Xstop.push_back(F1);
         }

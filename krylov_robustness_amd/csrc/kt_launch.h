@@ -58,7 +58,8 @@ hipError_t launch_ts_formq(int n, int bs, int BP, const double* V, const double*
 hipError_t launch_sum_slabs(int count, int S, const double* part, double* G, hipStream_t st);
 hipError_t launch_poly4(int n, double beta, const double* in, double c0, double c1, const double* X1,
                         double c2, const double* X2, double c3, const double* X3, double* out,
-                        hipStream_t st);
+                        hipStream_t st,
+                        int batch = 1);
 // column-batched single-vector Arnoldi (kt_colbatch.hip); V blocks at stride vstride
 int col_nrb(int n, int num_cu);
 hipError_t launch_col_dots(int n, int P, int nb, int64_t vstride, const double* V, const double* W,

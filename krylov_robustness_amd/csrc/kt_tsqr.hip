@@ -186,29 +186,32 @@ hipError_t launch_sum_slabs(int count, int S, const double* part, double* G, hip
 }
 
 // out = beta * in + c0 I + c1 X1 + c2 X2 + c3 X3   (n x n column-major; in,
-// X2, X3 nullable) -- the Paterson-Stockmeyer blocks of the device expm
+// X2, X3 nullable) -- the Paterson-Stockmeyer blocks of the device expm;
+// blockIdx.y = matrix of a batch, consecutive matrices n*n apart
 __global__ void k_poly4(int n, double beta, const double* __restrict__ in, double c0, double c1,
                         const double* __restrict__ X1, double c2, const double* __restrict__ X2,
                         double c3, const double* __restrict__ X3, double* __restrict__ out) {
     const int64_t total = (int64_t)n * n;
+    const int64_t b = (int64_t)blockIdx.y * total;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = t % n, j = t / n;
         double v = (i == j) ? c0 : 0.0;
-        v += c1 * X1[t];
-        if (X2) v += c2 * X2[t];
-        if (X3) v += c3 * X3[t];
-        if (in) v += beta * in[t];
-        out[t] = v;
+        v += c1 * X1[b + t];
+        if (X2) v += c2 * X2[b + t];
+        if (X3) v += c3 * X3[b + t];
+        if (in) v += beta * in[b + t];
+        out[b + t] = v;
     }
 }
 
 hipError_t launch_poly4(int n, double beta, const double* in, double c0, double c1, const double* X1,
                         double c2, const double* X2, double c3, const double* X3, double* out,
-                        hipStream_t st) {
+                        hipStream_t st, int batch) {
     int64_t g = ((int64_t)n * n + 255) / 256;
     if (g > 4096) g = 4096;
-    k_poly4<<<(int)g, 256, 0, st>>>(n, beta, in, c0, c1, X1, c2, X2, c3, X3, out);
+    k_poly4<<<dim3((unsigned)g, (unsigned)batch), 256, 0, st>>>(n, beta, in, c0, c1, X1, c2, X2, c3, X3,
+                                                               out);
     return hipGetLastError();
 }
 
