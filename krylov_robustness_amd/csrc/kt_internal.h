@@ -137,7 +137,11 @@ struct DevCSR {
     int n_long = 0;
     int* perm = nullptr;       // device row -> original row (nullptr: identity)
     bool built = false;
+    // allocation sizes in elements: a rebuild after edge edits (greedy) reuses
+    // the buffers instead of a hipFree / hipMalloc round trip
+    size_t cap_rp = 0, cap_col = 0, cap_val = 0, cap_lr = 0, cap_perm = 0;
     void release();
+    void invalidate() { built = false; }  // contents stale, buffers kept
 };
 }  // namespace kt
 

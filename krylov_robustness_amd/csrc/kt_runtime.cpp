@@ -60,6 +60,17 @@ void DevCSR::release() {
     val = nullptr;
     n_long = 0;
     built = false;
+    cap_rp = cap_col = cap_val = cap_lr = cap_perm = 0;
+}
+
+template <class T>
+static void ensure_dev(T*& p, size_t& cap, size_t want) {
+    if (want <= cap && p) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    KT_HIP(hipMalloc(&p, sizeof(T) * want));
+    cap = want;
 }
 
 void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out) {
@@ -91,11 +102,15 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
     std::stable_sort(lr.begin(), lr.end(), [&](int32_t a, int32_t b) {
         return rp32[a + 1] - rp32[a] > rp32[b + 1] - rp32[b];
     });
+    // buffers may be reused: nothing of this context may still read them
+    KT_HIP(hipStreamSynchronize(A->ctx->stream));
+    for (hipStream_t st : A->ctx->aux_stream)
+        if (st) KT_HIP(hipStreamSynchronize(st));
     try {
-        KT_HIP(hipMalloc(&out.rowptr, sizeof(int) * (n + 1)));
-        KT_HIP(hipMalloc(&out.col, sizeof(int) * c32.size()));
-        KT_HIP(hipMalloc(&out.val, sizeof(double) * v64.size()));
-        KT_HIP(hipMalloc(&out.long_rows, sizeof(int) * std::max<size_t>(lr.size(), 1)));
+        ensure_dev(out.rowptr, out.cap_rp, (size_t)n + 1);
+        ensure_dev(out.col, out.cap_col, c32.size());
+        ensure_dev(out.val, out.cap_val, v64.size());
+        ensure_dev(out.long_rows, out.cap_lr, std::max<size_t>(lr.size(), 1));
         KT_HIP(hipMemcpy(out.rowptr, rp32.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice));
         KT_HIP(hipMemcpy(out.col, c32.data(), sizeof(int) * c32.size(), hipMemcpyHostToDevice));
         KT_HIP(hipMemcpy(out.val, v64.data(), sizeof(double) * v64.size(), hipMemcpyHostToDevice));
@@ -103,7 +118,7 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
             KT_HIP(hipMemcpy(out.long_rows, lr.data(), sizeof(int) * lr.size(), hipMemcpyHostToDevice));
         out.n_long = (int)lr.size();
         if (!ident) {
-            KT_HIP(hipMalloc(&out.perm, sizeof(int) * std::max<int64_t>(n, 1)));
+            ensure_dev(out.perm, out.cap_perm, (size_t)std::max<int64_t>(n, 1));
             if (n) KT_HIP(hipMemcpy(out.perm, new2old.data(), sizeof(int) * n, hipMemcpyHostToDevice));
         }
     } catch (...) {
@@ -116,8 +131,8 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
 // Drop the device copies after the host CSR changed; hub_csr / natural_csr
 // rebuild them on next use.
 void refresh_device(kt_matrix_s* A) {
-    A->hub.release();
-    A->nat.release();
+    A->hub.invalidate();
+    A->nat.invalidate();
     A->unit_values = std::all_of(A->h_val.begin(), A->h_val.end(), [](double v) { return v == 1.0; });
     const char* un = getenv("KT_UNIT");
     if (un && un[0] == '0') A->unit_values = false;
