@@ -49,9 +49,6 @@ template <int P> struct Geo {
     static constexpr int GPW = 64 / LPR;          // row groups per wave
 };
 
-// FLAGS bit 0: non-temporal hints on the streamed (read-once) traffic of K1
-// (CSR arrays, own-row vector read, y store) so it does not evict the
-// gathered probe block from L2.
 // FLAGS bit 1: unit-weight adjacency (every stored value is 1.0, detected at
 // matrix creation): the values array is never read (4 B per nonzero instead
 // of 12).
