@@ -14,7 +14,7 @@ from .core import (Context, DeviceMatrix, default_context, device_count, expmv,
                    fun_and_grad_krylov_exp, fun_and_grad_krylov_fun, fun_update, lanczos_fmv,
                    mc_trace, normest, slq_plan, slq_quadforms, slq_trace, trace_exp,
                    trace_fun_update)
-from .greedy import (compute_centrality, default_greedy_tol, find_top_edges,
+from .greedy import (compute_centrality, default_greedy_tol, edge2low_rank, find_top_edges,
                      find_top_missing_edges, greedy_krylov, krylov_miobi, krylov_miobi_sharded,
                      miobi_loop, select_extreme, trace_fun_update_pairs)
 from . import datasets, matv73
@@ -30,5 +30,5 @@ __all__ = [
     "default_greedy_tol", "krylov_miobi_sharded", "miobi_loop", "select_extreme", "function_multiple_entries", "householder_qr", "frechet_entries",
     "hessianfcn", "hessianfcn_exp", "hessianfcn_fun", "eigs_leading", "datasets", "matv73",
     "load_problem", "load_unweighted", "prepare_unweighted", "prepare_weighted",
-    "mc_trace_sharded", "trace_exp_sharded",
+    "mc_trace_sharded", "trace_exp_sharded", "edge2low_rank",
 ]

@@ -201,6 +201,9 @@ def _dptr(a):
 
 
 def _colmajor(a, rows=None):
+    import scipy.sparse as sp
+    if sp.issparse(a):  # e.g. U of edge2low_rank (the callers pass full(U))
+        a = a.toarray()
     a = np.asarray(a, dtype=np.float64)
     if a.ndim == 1:
         a = a[:, None]

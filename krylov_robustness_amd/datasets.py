@@ -14,8 +14,10 @@ test_unweighted_make.m:41-52 / test_unweighted_break.m:42-52:
     A = A - spdiags(diag(A), 0, n, n);        % no self loops
     ind = max_connected_component(A); A = A(ind, ind);
 
-(max_connected_component is not part of the reference; the largest
-component is kept, the lowest-labelled one on a tie).  ``prepare_weighted``
+(max_connected_component is the drivers' local function,
+Tests/test_unweighted_make.m:159-168: conncomp bins numbered in discovery
+order from node 1, the first largest bin kept -- scipy labels components in
+the same order, and argmax keeps the first maximum).  ``prepare_weighted``
 is test_weighted_exp_lbfgs.m:34-36 (A / max(A(:))).  Host-side input
 preparation only: the result is handed to DeviceMatrix.
 """

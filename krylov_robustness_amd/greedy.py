@@ -213,6 +213,29 @@ def find_top_missing_edges(A, centrality, num, order="min"):
     raise ValueError(f"unknown order {order!r}")
 
 
+def edge2low_rank(E, n, value=-1.0):
+    """[U, B] = edge2low_rank(E, n): the low-rank factors of an edge edit,
+    A + U B U' (functions/edge2low_rank.m:1-13, value = -1: remove the edges;
+    the make drivers' local copy, Tests/test_unweighted_make.m:171-183, uses
+    +1: add them).  E: m x 2 1-based node pairs.  U: n x k sparse selector of
+    the k distinct nodes (ascending, as unique()), B: k x k dense with
+    B(a, b) = B(b, a) = value for every edge."""
+    import scipy.sparse as sp
+    E = np.asarray(E, dtype=np.int64).reshape(-1, 2)
+    t1, t2 = E[:, 0], E[:, 1]
+    ut = np.unique(np.concatenate([t1, t2]))
+    if ut.size and (ut[0] < 1 or ut[-1] > n):
+        raise _lib.KrylovError(_lib.KT_ERR_ARG, "edge2low_rank: node index out of range")
+    k = ut.size
+    U = sp.csc_matrix((np.ones(k), (ut - 1, np.arange(k))), shape=(int(n), k))
+    B = np.zeros((k, k))
+    a = np.searchsorted(ut, t1)
+    b = np.searchsorted(ut, t2)
+    B[a, b] = value
+    B[b, a] = value
+    return U, B
+
+
 def compute_centrality(A, kind="eig", ctx: Optional[Context] = None):
     """compute_centrality.m: 'eig' = abs(leading eigenvector) (:15-17), on the
     device when A is a DeviceMatrix (kt_eigs_leading), else scipy eigsh;

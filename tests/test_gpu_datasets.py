@@ -67,3 +67,22 @@ def test_device_centrality_as_735(kra, gpu_ctx):
     c = kra.compute_centrality(kra.DeviceMatrix(A, gpu_ctx), "eig", ctx=gpu_ctx)
     w, V = np.linalg.eigh(A.toarray())
     np.testing.assert_allclose(c, np.abs(V[:, -1]), rtol=0, atol=1e-8)
+
+
+def test_selected_edges_delta_trace(kra, gpu_ctx, vals):
+    """The drivers' check of a selected edge set (test_unweighted_make.m:92-93):
+    [U, B] = edge2low_rank(edges, n) (+1: the make drivers' copy, :171-183),
+    delta = trace_fun_update(A, full(U), B, tol*nrm) -- against the exact
+    tr exp(A + U B U') - tr exp(A) from dense spectra.  tol*nrm = 1e-6 e^48
+    on a difference of ~1e20: 1e-5 relative."""
+    A = load_v73_graph("collegemsg")
+    g = vals["collegemsg"]["oracle_greedy_make"]
+    E = np.array(g["edges"])
+    U, B = kra.edge2low_rank(E, A.shape[0], value=1.0)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    xm, it, lucky = kra.trace_fun_update(D, U, B, g["tol"], 100, ctx=gpu_ctx)
+    Ad = A.toarray()
+    Ud = U.toarray()
+    exact = (np.exp(np.linalg.eigvalsh(Ad + Ud @ B @ Ud.T)).sum()
+             - np.exp(np.linalg.eigvalsh(Ad)).sum())
+    assert xm == pytest.approx(exact, rel=1e-5)

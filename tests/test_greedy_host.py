@@ -53,3 +53,29 @@ def test_find_top_missing_edges_mult_are_missing():
     assert all(A[i - 1, j - 1] == 0 and i != j for i, j in E)
     s = c[E[:, 0] - 1] * c[E[:, 1] - 1]
     assert np.all(np.diff(s) <= 1e-15)            # descending products
+
+
+def test_edge2low_rank_matches_edit():
+    """edge2low_rank.m:1-13: A + U B U' removes (value -1) / adds (+1) the
+    edges, U selects the distinct nodes in ascending order."""
+    import scipy.sparse as sp
+    from conftest import load_graph
+    from krylov_robustness_amd.greedy import edge2low_rank
+    A = load_graph("anaheim").tocsr()
+    n = A.shape[0]
+    I, J = sp.triu(A, 1).nonzero()
+    E = np.stack([I[[3, 7, 11]] + 1, J[[3, 7, 11]] + 1], axis=1)
+    U, B = edge2low_rank(E, n)
+    assert U.shape == (n, len(np.unique(E)))
+    assert np.array_equal(sp.find(U)[0], np.unique(E) - 1)
+    Ud = U.toarray()
+    R = A.toarray() + Ud @ B @ Ud.T
+    for i, j in E:
+        assert R[i - 1, j - 1] == 0 and R[j - 1, i - 1] == 0
+    assert abs(R - R.T).max() == 0
+    assert (A.toarray() - R).sum() == 2 * len(E)
+    U2, B2 = edge2low_rank(E, n, value=1.0)
+    assert np.array_equal(B2, -B)
+    # shared endpoint: node appears once in U
+    U3, B3 = edge2low_rank([[1, 2], [2, 3]], 5)
+    assert U3.shape == (5, 3) and B3[0, 1] == -1 and B3[1, 2] == -1 and B3[0, 2] == 0
