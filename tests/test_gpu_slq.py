@@ -108,3 +108,22 @@ def test_slq_hub_rows_long_mode(kra, gpu_ctx, block):
     _, _, q = kra.slq_quadforms(D, 6, 30, seed=8, block=block, ctx=gpu_ctx)
     _, q_ref = slq_ref.slq_trace(A, 6, 30, seed=8)
     np.testing.assert_allclose(q, q_ref, rtol=RTOL)
+
+
+def test_slq_full_size_config4(kra, gpu_ctx, monkeypatch):
+    """BASELINE.json config 4 at full size (Chung-Lu n=1M, nnz=10M, m=30,
+    the bench workload): the first probes match the C oracle; probes
+    evaluated at an offset (a rank's shard) equal the same probes inside a
+    wider run; 1 and 3 sweep lanes give bit-identical per-probe values."""
+    from krylov_robustness_amd import graphs
+    A = graphs.chung_lu(1_000_000, 10_000_000, seed=0)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    monkeypatch.setenv("KT_SLQ_LANES", "3")
+    _, _, q3 = kra.slq_quadforms(D, 64, 30, seed=5, block=16, ctx=gpu_ctx)
+    monkeypatch.setenv("KT_SLQ_LANES", "1")
+    _, _, q1 = kra.slq_quadforms(D, 64, 30, seed=5, block=16, ctx=gpu_ctx)
+    assert np.array_equal(q1, q3)
+    _, _, qs = kra.slq_quadforms(D, 16, 30, seed=5, probe_offset=32, block=16, ctx=gpu_ctx)
+    assert np.array_equal(qs, q1[32:48])
+    _, q_ref = slq_ref.slq_trace(A, 3, 30, seed=5, probe_offset=32)
+    np.testing.assert_allclose(qs[:3], q_ref, rtol=RTOL)
