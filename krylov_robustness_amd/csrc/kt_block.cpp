@@ -101,17 +101,31 @@ void combine(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px,
     KT_HIP(hipStreamSynchronize(ctx->stream));
 }
 
-void spmm(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols) {
+// Every block SpMM: Y[:, 0:slices P] = A X over `slices` P-wide column slices
+// of the natural-order CSR, hub rows through the chunk table + combine.
+static void block_spmm(kt_matrix_s* A, int P, const double* X, int ldx, double* Y, int ldy, int slices,
+                       const int* skip) {
     kt_context_s* ctx = A->ctx;
+    const int n = (int)A->n;
+    const DevCSR& M = natural_csr(A);  // block paths run in the reference's row order
+    const int grid = spmm_grid(n, P, ctx->num_cu * 4);
+    const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
+    const int cblocks = M.n_chunks ? std::min((M.n_chunks + 7) / 8, ctx->num_cu * 2) : 0;
+    double* ck_part = nullptr;
+    if (M.n_chunks) {
+        ctx->ws.ck_part.ensure(sizeof(double) * (size_t)M.n_chunks * P * slices);
+        ck_part = ctx->ws.ck_part.as<double>();
+    }
+    const CsrView V{M.rowptr, M.col, M.val, n, M.long_rows, M.n_long, A->long_thresh, kSplitThresh,
+                    M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split};
+    KT_HIP(launch_spmm_block(P, (A->unit_values ? 2 : 0) | (ctx->k1_flags & 4), grid + lblocks + cblocks, V,
+                             X, ldx, Y, ldy, lblocks, cblocks, ck_part, ctx->stream, slices, skip));
+}
+
+void spmm(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols) {
     const int P = pow2_at_least(std::max(cols, 1));
     if (P > 128) fail(KT_ERR_UNSUPPORTED, "block width > 128");
-    const int n = (int)A->n;
-    const int grid = spmm_grid(n, P, ctx->num_cu * 4);
-    const DevCSR& M = natural_csr(A);  // block paths run in the reference's row order
-    const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
-    KT_HIP(launch_spmm_block(P, (A->unit_values ? 2 : 0) | (ctx->k1_flags & 4), grid + lblocks, M.rowptr, M.col, M.val, n,
-                             X, ldx, Y, ldy, M.long_rows, M.n_long, A->long_thresh, lblocks,
-                             ctx->stream));
+    block_spmm(A, P, X, ldx, Y, ldy, 1, nullptr);
 }
 
 // Y[:, 0:cols] = A X[:, 0:cols] for cols > 128 in ONE launch: ceil(cols/128)
@@ -121,27 +135,12 @@ void spmm(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols
 void spmm_slices(kt_matrix_s* A, const double* X, int ldx, double* Y, int ldy, int cols,
                  const int* skip) {
     if (cols <= 128) {
-        kt_context_s* ctx = A->ctx;
-        const int P = pow2_at_least(std::max(cols, 1));
-        const int n = (int)A->n;
-        const int grid = spmm_grid(n, P, ctx->num_cu * 4);
-        const DevCSR& M = natural_csr(A);
-        const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
-        KT_HIP(launch_spmm_block(P, (A->unit_values ? 2 : 0) | (ctx->k1_flags & 4), grid + lblocks,
-                                 M.rowptr, M.col, M.val, n, X, ldx, Y, ldy, M.long_rows, M.n_long,
-                                 A->long_thresh, lblocks, ctx->stream, 1, skip));
+        block_spmm(A, pow2_at_least(std::max(cols, 1)), X, ldx, Y, ldy, 1, skip);
         return;
     }
     const int slices = (cols + 127) / 128;
     if (ldx < slices * 128 || ldy < slices * 128) fail(KT_ERR_ARG, "spmm_slices: leading dimension");
-    kt_context_s* ctx = A->ctx;
-    const int n = (int)A->n;
-    const int grid = spmm_grid(n, 128, ctx->num_cu * 4);
-    const DevCSR& M = natural_csr(A);
-    const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
-    KT_HIP(launch_spmm_block(128, (A->unit_values ? 2 : 0) | (ctx->k1_flags & 4), grid + lblocks,
-                             M.rowptr, M.col, M.val, n, X, ldx, Y, ldy, M.long_rows, M.n_long,
-                             A->long_thresh, lblocks, ctx->stream, slices, skip));
+    block_spmm(A, 128, X, ldx, Y, ldy, slices, skip);
 }
 
 void copy_cols(kt_context_s* ctx, int64_t n, const double* X, int ldx, double* Y, int ldy,

@@ -99,6 +99,7 @@ struct Workspace {
     SweepBufs sweep[4];
     DevBuf small, small2, qrtmp, eigA, eigW, eigInfo;  // block-Krylov scratch
     DevBuf expm;                                       // batched device expm (6 x batch x n^2)
+    DevBuf ck_part;                                    // block SpMM hub-row chunk partials
     DevBuf hist, norm_part;                             // sweep scale history, inf-norm partials
     PinnedBuf host_trec;
     // batched greedy candidates (kt_greedy.cpp): 3 pair blocks, indices,
@@ -136,10 +137,16 @@ struct DevCSR {
     int* long_rows = nullptr;  // rows with degree > long_thresh, heaviest first
     int n_long = 0;
     int* perm = nullptr;       // device row -> original row (nullptr: identity)
+    // hub rows (degree > kSplitThresh) cut into kChunkNnz-nonzero chunks for
+    // the block SpMM: chunk c = nonzeros [ck_beg[c], ck_end[c]); split row i =
+    // device row sp_rows[i], its chunks [sp_first[i], sp_first[i+1])
+    int *ck_beg = nullptr, *ck_end = nullptr, *sp_rows = nullptr, *sp_first = nullptr;
+    int n_chunks = 0, n_split = 0;
     bool built = false;
     // allocation sizes in elements: a rebuild after edge edits (greedy) reuses
     // the buffers instead of a hipFree / hipMalloc round trip
     size_t cap_rp = 0, cap_col = 0, cap_val = 0, cap_lr = 0, cap_perm = 0;
+    size_t cap_ckb = 0, cap_cke = 0, cap_spr = 0, cap_spf = 0;
     void release();
     void invalidate() { built = false; }  // contents stale, buffers kept
 };

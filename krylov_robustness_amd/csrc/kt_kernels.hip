@@ -313,12 +313,19 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
 // strides ldx, ldy (blocks are column slices of a wider row-major basis).
 // Same row-group / long-row mapping as K1, no reductions.
 // ---------------------------------------------------------------------------
+// Rows longer than split_thresh (every long row) are cut into chunks of
+// kChunkNnz nonzeros, one WAVE per chunk in blocks [0, chunk_blocks); each
+// writes its partial row to ck_part[slice][chunk][P] and k_spmm_combine sums
+// a row's chunks in chunk order (deterministic).  With P = 128 a wave holds a
+// single row group, so a hub row of 1,500 nonzeros would otherwise be one
+// wave's serial gather chain (180 us on as_735 vs 9 us for the rest).
 template <int P, int BLOCK, int FLAGS>
 __global__ __launch_bounds__(BLOCK) void k_spmm_block(
     const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
     int n, const double* __restrict__ X, int ldx, double* __restrict__ Y, int ldy,
     const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks,
-    const int* __restrict__ skip) {
+    const int* __restrict__ skip, const int* __restrict__ ck_beg, const int* __restrict__ ck_end,
+    int n_chunks, int chunk_blocks, int split_thresh, double* __restrict__ ck_part) {
     using G = Geo<P>;
     using V = VecT<G::VEC>;
     constexpr int WAVES = BLOCK / 64;
@@ -330,9 +337,27 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_block(
     const int sub = lane % G::LPR;
     const int grp = lane / G::LPR;
     const int p0 = sub * G::VEC;
-    if ((int)blockIdx.x < long_blocks) {
-        for (int li = blockIdx.x * WAVES + wave; li < n_long; li += long_blocks * WAVES) {
+    if ((int)blockIdx.x < chunk_blocks) {
+        double* part = ck_part + (int64_t)blockIdx.y * n_chunks * P;
+        for (int ci = blockIdx.x * WAVES + wave; ci < n_chunks; ci += chunk_blocks * WAVES) {
+            double s[G::VEC];
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+            gather_row<P, FLAGS>(ck_beg[ci] + grp, ck_end[ci], G::GPW, p0, col, val, X, s, ldx);
+#pragma unroll
+            for (int o = G::LPR; o < 64; o <<= 1)
+#pragma unroll
+                for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
+            if (grp == 0) {
+#pragma unroll
+                for (int e = 0; e < G::VEC; ++e) part[(int64_t)ci * P + p0 + e] = s[e];
+            }
+        }
+    } else if ((int)blockIdx.x < chunk_blocks + long_blocks) {
+        const int lb = blockIdx.x - chunk_blocks;
+        for (int li = lb * WAVES + wave; li < n_long; li += long_blocks * WAVES) {
             const int row = long_rows[li];
+            if (row_ptr[row + 1] - row_ptr[row] > split_thresh) continue;  // chunked
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
@@ -351,8 +376,8 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_block(
             }
         }
     } else {
-        const int sb = blockIdx.x - long_blocks;
-        const int groups_total = (gridDim.x - long_blocks) * WAVES * G::GPW;
+        const int sb = blockIdx.x - chunk_blocks - long_blocks;
+        const int groups_total = (gridDim.x - chunk_blocks - long_blocks) * WAVES * G::GPW;
         for (int row = (sb * WAVES + wave) * G::GPW + grp; row < n; row += groups_total) {
             const int beg = row_ptr[row], end = row_ptr[row + 1];
             if (end - beg > long_thresh) continue;
@@ -367,6 +392,32 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_block(
             V::store(Y + (int64_t)row * ldy + p0, yo);
         }
     }
+}
+
+// Y[row, slice P + t] = sum of the row's chunk partials in chunk order
+template <int P>
+__global__ __launch_bounds__(128) void k_spmm_combine(const int* __restrict__ sp_rows,
+                                                      const int* __restrict__ sp_first, int n_chunks,
+                                                      const double* __restrict__ ck_part,
+                                                      double* __restrict__ Y, int ldy,
+                                                      const int* __restrict__ skip) {
+    if (skip && *skip == 0) return;
+    const int t = threadIdx.x;
+    if (t >= P) return;
+    const int i = blockIdx.x;
+    const double* part = ck_part + (int64_t)blockIdx.y * n_chunks * P;
+    double s = 0.0;
+    int c = sp_first[i];
+    const int ce = sp_first[i + 1];
+    for (; c + 8 <= ce; c += 8) {  // 8 loads in flight, summed in chunk order
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(c + u) * P + t];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; c < ce; ++c) s += part[(int64_t)c * P + t];
+    Y[(int64_t)sp_rows[i] * ldy + (int64_t)blockIdx.y * P + t] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -664,16 +715,16 @@ hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int*
     });
 }
 
-hipError_t launch_spmm_block(int P, int flags, int grid, const int* rp, const int* ci,
-                             const double* va, int n, const double* X, int ldx, double* Y, int ldy,
-                             const int* long_rows, int n_long, int long_thresh, int long_blocks,
+hipError_t launch_spmm_block(int P, int flags, int grid, const CsrView& M, const double* X, int ldx,
+                             double* Y, int ldy, int long_blocks, int chunk_blocks, double* ck_part,
                              hipStream_t st, int slices, const int* skip) {
     const dim3 g(grid, slices);
-    return dispatch_p(P, [&](auto c) {
+    hipError_t e = dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
-#define KT_SB(F)                                                                      \
-    k_spmm_block<PP, kBlock, F><<<g, kBlock, 0, st>>>(rp, ci, va, n, X, ldx, Y, ldy, long_rows, \
-                                                      n_long, long_thresh, long_blocks, skip)
+#define KT_SB(F)                                                                                   \
+    k_spmm_block<PP, kBlock, F><<<g, kBlock, 0, st>>>(                                              \
+        M.rp, M.ci, M.va, M.n, X, ldx, Y, ldy, M.long_rows, M.n_long, M.long_thresh, long_blocks, skip, \
+        M.ck_beg, M.ck_end, M.n_chunks, chunk_blocks, M.split_thresh, ck_part)
         switch (flags & (KF_UNIT | KF_MLP)) {
         case 0: KT_SB(0); break;
         case KF_UNIT: KT_SB(KF_UNIT); break;
@@ -681,6 +732,12 @@ hipError_t launch_spmm_block(int P, int flags, int grid, const int* rp, const in
         default: KT_SB(KF_UNIT | KF_MLP); break;
         }
 #undef KT_SB
+    });
+    if (e != hipSuccess || M.n_split == 0 || chunk_blocks == 0) return e;
+    return dispatch_p(P, [&](auto c) {
+        constexpr int PP = decltype(c)::value;
+        k_spmm_combine<PP><<<dim3(M.n_split, slices), 128, 0, st>>>(M.sp_rows, M.sp_first, M.n_chunks, ck_part,
+                                                                    Y, ldy, skip);
     });
 }
 

@@ -14,11 +14,26 @@ hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int*
                            const double* va, int n, const double* ucur, const double* sc,
                            double* y, double* partial, const int* long_rows, int n_long,
                            int long_thresh, int long_blocks, hipStream_t st);
-hipError_t launch_spmm_block(int P, int flags, int grid, const int* rp, const int* ci,
-                             const double* va, int n, const double* X, int ldx, double* Y, int ldy,
-                             const int* long_rows, int n_long, int long_thresh, int long_blocks,
-                             hipStream_t st, int slices = 1,
-                             const int* skip = nullptr);
+// device CSR + its long-row list and hub-row chunk table (kt_internal.h DevCSR)
+struct CsrView {
+    const int* rp;
+    const int* ci;
+    const double* va;
+    int n;
+    const int* long_rows;
+    int n_long, long_thresh, split_thresh;
+    const int* ck_beg;
+    const int* ck_end;
+    int n_chunks;
+    const int* sp_rows;
+    const int* sp_first;
+    int n_split;
+};
+constexpr int kChunkNnz = 32;      // nonzeros per hub-row chunk
+constexpr int kSplitThresh = 64;   // rows longer than this are chunked (block SpMM)
+hipError_t launch_spmm_block(int P, int flags, int grid, const CsrView& M, const double* X, int ldx,
+                             double* Y, int ldy, int long_blocks, int chunk_blocks, double* ck_part,
+                             hipStream_t st, int slices = 1, const int* skip = nullptr);
 hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, const double* k2s,
                             const double* sc, const double* sp, double* coef, double* t_alpha,
                             double* t_up, hipStream_t st);

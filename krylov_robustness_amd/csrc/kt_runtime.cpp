@@ -10,6 +10,7 @@
 #include <rocblas/rocblas.h>
 
 #include "kt_internal.h"
+#include "kt_launch.h"
 
 namespace kt {
 
@@ -56,6 +57,11 @@ void DevCSR::release() {
     if (val) (void)hipFree(val);
     if (long_rows) (void)hipFree(long_rows);
     if (perm) (void)hipFree(perm);
+    for (int* q : {ck_beg, ck_end, sp_rows, sp_first})
+        if (q) (void)hipFree(q);
+    ck_beg = ck_end = sp_rows = sp_first = nullptr;
+    n_chunks = n_split = 0;
+    cap_ckb = cap_cke = cap_spr = cap_spf = 0;
     rowptr = col = long_rows = perm = nullptr;
     val = nullptr;
     n_long = 0;
@@ -117,6 +123,30 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
         if (!lr.empty())
             KT_HIP(hipMemcpy(out.long_rows, lr.data(), sizeof(int) * lr.size(), hipMemcpyHostToDevice));
         out.n_long = (int)lr.size();
+        // hub-row chunk table (block SpMM)
+        std::vector<int32_t> ckb, cke, spr, spf(1, 0);
+        for (int32_t r : lr) {  // heaviest first
+            const int32_t b = rp32[r], e = rp32[r + 1];
+            if (e - b <= kSplitThresh) continue;
+            spr.push_back(r);
+            for (int32_t k = b; k < e; k += kChunkNnz) {
+                ckb.push_back(k);
+                cke.push_back(std::min(e, k + kChunkNnz));
+            }
+            spf.push_back((int32_t)ckb.size());
+        }
+        out.n_split = (int)spr.size();
+        out.n_chunks = (int)ckb.size();
+        if (out.n_split) {
+            ensure_dev(out.ck_beg, out.cap_ckb, ckb.size());
+            ensure_dev(out.ck_end, out.cap_cke, cke.size());
+            ensure_dev(out.sp_rows, out.cap_spr, spr.size());
+            ensure_dev(out.sp_first, out.cap_spf, spf.size());
+            KT_HIP(hipMemcpy(out.ck_beg, ckb.data(), sizeof(int) * ckb.size(), hipMemcpyHostToDevice));
+            KT_HIP(hipMemcpy(out.ck_end, cke.data(), sizeof(int) * cke.size(), hipMemcpyHostToDevice));
+            KT_HIP(hipMemcpy(out.sp_rows, spr.data(), sizeof(int) * spr.size(), hipMemcpyHostToDevice));
+            KT_HIP(hipMemcpy(out.sp_first, spf.data(), sizeof(int) * spf.size(), hipMemcpyHostToDevice));
+        }
         if (!ident) {
             ensure_dev(out.perm, out.cap_perm, (size_t)std::max<int64_t>(n, 1));
             if (n) KT_HIP(hipMemcpy(out.perm, new2old.data(), sizeof(int) * n, hipMemcpyHostToDevice));
