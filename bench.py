@@ -179,6 +179,10 @@ def main():
                     "measured": "HIP events on an isolated single-lane pass (4 sweeps x m steps) "
                                 "after the timed region",
                     "timed_region_avg_launch_us_overlapped": k1_overlapped}
+            if traffic:  # memory-side rate: PMC bytes per launch over the same duration
+                tgbs = traffic / (k1_ms * 1e-3) / 1e9
+                roof["traffic_GBs"] = round(tgbs, 1)
+                roof["traffic_frac"] = round(tgbs / HBM_PEAK_GBS, 4)
             extra["k2_update_avg_us"] = round(ms2 / max(l2, 1) * 1e3, 2)
     eval_gbs = b_eval_rank / (ms_per_step * 1e-3) / 1e9
     extra["eval_roofline"] = {"B_eval_bytes_per_rank": b_eval_rank, "achieved_GBs_per_rank":
