@@ -43,11 +43,19 @@ __device__ __forceinline__ uint64_t sm64(uint64_t x) {
     return z ^ (z >> 31);
 }
 
-template <int P> struct Geo {
-    static constexpr int VEC = (P >= 2) ? 2 : 1;  // doubles per lane
-    static constexpr int LPR = P / VEC;           // lanes per row group
-    static constexpr int GPW = 64 / LPR;          // row groups per wave
+// Lane geometry of a P-wide row-major block: VW doubles per lane, LPR lanes
+// per row group, GPW row groups per wave.
+template <int P, int VW> struct GeoW {
+    static constexpr int VEC = VW;       // doubles per lane
+    static constexpr int LPR = P / VEC;  // lanes per row group
+    static constexpr int GPW = 64 / LPR; // row groups per wave
 };
+// streaming kernels and the block SpMM: 16 B per lane
+template <int P> using Geo = GeoW<P, (P >= 2) ? 2 : 1>;
+// K1: 32 B per lane from P = 16 on -- a 128-B probe row is 4 lanes, 16 rows
+// in flight per wave (K1 -4 %, profiles/r01_sweep_vec4.txt; K2 is faster
+// with 16 B per lane and keeps Geo)
+template <int P> using GeoK1 = GeoW<P, (P >= 16) ? 4 : (P >= 2) ? 2 : 1>;
 
 // FLAGS bit 1: unit-weight adjacency (every stored value is 1.0, detected at
 // matrix creation): the values array is never read (4 B per nonzero instead
@@ -94,6 +102,32 @@ template <> struct VecT<2> {
     __device__ static __forceinline__ double get(const T& v, int e) { return e ? v.y : v.x; }
 };
 
+struct Dbl4 {
+    double2 a, b;
+};
+template <> struct VecT<4> {
+    using T = Dbl4;
+    __device__ static __forceinline__ T load(const double* p) {
+        const double2* q = reinterpret_cast<const double2*>(p);
+        return Dbl4{q[0], q[1]};
+    }
+    __device__ static __forceinline__ T load_nt(const double* p) {
+        return Dbl4{VecT<2>::load_nt(p), VecT<2>::load_nt(p + 2)};
+    }
+    __device__ static __forceinline__ void store(double* p, const T& v) {
+        double2* q = reinterpret_cast<double2*>(p);
+        q[0] = v.a;
+        q[1] = v.b;
+    }
+    __device__ static __forceinline__ void store_nt(double* p, const T& v) {
+        VecT<2>::store_nt(p, v.a);
+        VecT<2>::store_nt(p + 2, v.b);
+    }
+    __device__ static __forceinline__ double get(const T& v, int e) {
+        return e == 0 ? v.a.x : e == 1 ? v.a.y : e == 2 ? v.b.x : v.b.y;
+    }
+};
+
 template <int FLAGS, class T> __device__ __forceinline__ T ld_stream(const T* p) {
     if constexpr (FLAGS & KF_NT) return __builtin_nontemporal_load(p);
     else return *p;
@@ -126,13 +160,12 @@ __global__ __launch_bounds__(256) void k_rademacher(int n, uint64_t seed, int64_
 // K1
 // ---------------------------------------------------------------------------
 // Gather-accumulate nonzeros k = k0, k0 + stride, ... < end of one row.
-template <int P, int FLAGS>
+template <int P, int FLAGS, class G = Geo<P>>
 __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
                                            const int* __restrict__ col,
                                            const double* __restrict__ val,
                                            const double* __restrict__ ucur, double* s,
                                            int ld = P) {
-    using G = Geo<P>;
     using V = VecT<G::VEC>;
     int k = k0;
     for (; k + 3 * stride < end; k += 4 * stride) {  // 4 independent gathers in flight
@@ -171,13 +204,12 @@ __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
 // Same sum as row_gather, issued 8 deep: the 8 column indices of a chunk are
 // loaded together, then the 8 row gathers (a tail entry re-reads the chunk's
 // first row with weight 0, so no lane branches), then the 8 FMAs.
-template <int P, int FLAGS>
+template <int P, int FLAGS, class G = Geo<P>>
 __device__ __forceinline__ void row_gather8(int k0, int end, int stride, int p0,
                                             const int* __restrict__ col,
                                             const double* __restrict__ val,
                                             const double* __restrict__ ucur, double* s,
                                             int ld = P) {
-    using G = Geo<P>;
     using V = VecT<G::VEC>;
     for (int k = k0; k < end; k += 8 * stride) {
         int c[8];
@@ -203,22 +235,21 @@ __device__ __forceinline__ void row_gather8(int k0, int end, int stride, int p0,
     }
 }
 
-template <int P, int FLAGS>
+template <int P, int FLAGS, class G = Geo<P>>
 __device__ __forceinline__ void gather_row(int k0, int end, int stride, int p0,
                                            const int* __restrict__ col,
                                            const double* __restrict__ val,
                                            const double* __restrict__ ucur, double* s,
                                            int ld = P) {
-    if constexpr (FLAGS & KF_MLP) row_gather8<P, FLAGS>(k0, end, stride, p0, col, val, ucur, s, ld);
-    else row_gather<P, FLAGS>(k0, end, stride, p0, col, val, ucur, s, ld);
+    if constexpr (FLAGS & KF_MLP) row_gather8<P, FLAGS, G>(k0, end, stride, p0, col, val, ucur, s, ld);
+    else row_gather<P, FLAGS, G>(k0, end, stride, p0, col, val, ucur, s, ld);
 }
 
 // y_r = s_cur * sum; accumulate v_cur . y.
-template <int P, int FLAGS>
+template <int P, int FLAGS, class G = Geo<P>>
 __device__ __forceinline__ void row_epilogue(int row, int p0, const double* s, const double* sc,
                                              const double* __restrict__ ucur,
                                              double* __restrict__ y, double* acc) {
-    using G = Geo<P>;
     using V = VecT<G::VEC>;
     const int64_t off = (int64_t)row * P + p0;
     const typename V::T ui = V::load(ucur + off);
@@ -244,7 +275,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
     int n, const double* __restrict__ ucur, const double* __restrict__ scale_cur,
     double* __restrict__ y, double* __restrict__ partial, const int* __restrict__ long_rows,
     int n_long, int long_thresh, int long_blocks) {
-    using G = Geo<P>;
+    using G = GeoK1<P>;
     constexpr int WAVES = BLOCK / 64;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -267,12 +298,12 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            gather_row<P, FLAGS>(beg + grp, end, G::GPW, p0, col, val, ucur, s);
+            gather_row<P, FLAGS, G>(beg + grp, end, G::GPW, p0, col, val, ucur, s);
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
                 for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
-            if (grp == 0) row_epilogue<P, FLAGS>(row, p0, s, sc, ucur, y, acc);
+            if (grp == 0) row_epilogue<P, FLAGS, G>(row, p0, s, sc, ucur, y, acc);
         }
     } else {
         const int sb = blockIdx.x - long_blocks;
@@ -284,8 +315,8 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            gather_row<P, FLAGS>(beg, end, 1, p0, col, val, ucur, s);
-            row_epilogue<P, FLAGS>(row, p0, s, sc, ucur, y, acc);
+            gather_row<P, FLAGS, G>(beg, end, 1, p0, col, val, ucur, s);
+            row_epilogue<P, FLAGS, G>(row, p0, s, sc, ucur, y, acc);
         }
     }
 
