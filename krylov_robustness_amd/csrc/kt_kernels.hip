@@ -55,7 +55,10 @@ template <int P> using Geo = GeoW<P, (P >= 2) ? 2 : 1>;
 // K1: 32 B per lane from P = 16 on -- a 128-B probe row is 4 lanes, 16 rows
 // in flight per wave (K1 -4 %, profiles/r01_sweep_vec4.txt; K2 is faster
 // with 16 B per lane and keeps Geo)
-template <int P> using GeoK1 = GeoW<P, (P >= 16) ? 4 : (P >= 2) ? 2 : 1>;
+#ifndef KT_K1_VW
+#define KT_K1_VW 4
+#endif
+template <int P> using GeoK1 = GeoW<P, (P >= 16) ? (KT_K1_VW < P ? KT_K1_VW : P) : (P >= 2) ? 2 : 1>;
 
 // FLAGS bit 1: unit-weight adjacency (every stored value is 1.0, detected at
 // matrix creation): the values array is never read (4 B per nonzero instead
@@ -125,6 +128,30 @@ template <> struct VecT<4> {
     }
     __device__ static __forceinline__ double get(const T& v, int e) {
         return e == 0 ? v.a.x : e == 1 ? v.a.y : e == 2 ? v.b.x : v.b.y;
+    }
+};
+
+struct Dbl8 {
+    Dbl4 a, b;
+};
+template <> struct VecT<8> {
+    using T = Dbl8;
+    __device__ static __forceinline__ T load(const double* p) {
+        return Dbl8{VecT<4>::load(p), VecT<4>::load(p + 4)};
+    }
+    __device__ static __forceinline__ T load_nt(const double* p) {
+        return Dbl8{VecT<4>::load_nt(p), VecT<4>::load_nt(p + 4)};
+    }
+    __device__ static __forceinline__ void store(double* p, const T& v) {
+        VecT<4>::store(p, v.a);
+        VecT<4>::store(p + 4, v.b);
+    }
+    __device__ static __forceinline__ void store_nt(double* p, const T& v) {
+        VecT<4>::store_nt(p, v.a);
+        VecT<4>::store_nt(p + 4, v.b);
+    }
+    __device__ static __forceinline__ double get(const T& v, int e) {
+        return e < 4 ? VecT<4>::get(v.a, e) : VecT<4>::get(v.b, e - 4);
     }
 };
 
@@ -737,6 +764,7 @@ hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int*
         case KF_NT | KF_NTY | KF_UNIT: KT_K1(KF_NT | KF_NTY | KF_UNIT); break;
         case KF_MLP: KT_K1(KF_MLP); break;
         case KF_MLP | KF_UNIT: KT_K1(KF_MLP | KF_UNIT); break;
+        case KF_MLP | KF_NTY | KF_UNIT: KT_K1(KF_MLP | KF_NTY | KF_UNIT); break;
         default:  // unsupported combination: keep only the unit bit (exactness)
             if (flags & KF_UNIT) KT_K1(KF_UNIT);
             else KT_K1(0);

@@ -28,8 +28,8 @@ def main():
     for var in a.variants.split(","):
       os.environ["KT_RELABEL"] = "0" if var == "natural" else "1"
       os.environ["KT_K1_FLAGS"] = {"nt": "1", "mlp": "4", "mlpnt": "5", "nty": "8", "ntboth": "9",
-                                   "ntall": "9", "ntyk2": "8"}.get(var.split("_")[0], "0")
-      os.environ["KT_K2_NT"] = "1" if var.startswith(("k2nt", "ntall", "ntyk2")) else "0"
+                                   "ntall": "9", "ntyk2": "8", "mlpk2": "12"}.get(var.split("_")[0], "0")
+      os.environ["KT_K2_NT"] = "1" if var.startswith(("k2nt", "ntall", "ntyk2", "mlpk2")) else "0"
       os.environ["KT_SLQ_LANES"] = (var[5:] if var.startswith("lanes")
                                     else var.split("_lanes")[1] if "_lanes" in var else "1")
       os.environ["KT_UNIT"] = "0" if var == "valued" else "1"
