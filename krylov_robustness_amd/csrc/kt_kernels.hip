@@ -59,6 +59,11 @@ template <int P> using Geo = GeoW<P, (P >= 2) ? 2 : 1>;
 #define KT_K1_VW 4
 #endif
 template <int P> using GeoK1 = GeoW<P, (P >= 16) ? (KT_K1_VW < P ? KT_K1_VW : P) : (P >= 2) ? 2 : 1>;
+// block SpMM lane width (doubles per lane) from P = 16 on
+#ifndef KT_BLK_VW
+#define KT_BLK_VW 2
+#endif
+template <int P> using GeoB = GeoW<P, (P >= 16) ? KT_BLK_VW : (P >= 2) ? 2 : 1>;
 
 // FLAGS bit 1: unit-weight adjacency (every stored value is 1.0, detected at
 // matrix creation): the values array is never read (4 B per nonzero instead
@@ -384,7 +389,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_block(
     const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks,
     const int* __restrict__ skip, const int* __restrict__ ck_beg, const int* __restrict__ ck_end,
     int n_chunks, int chunk_blocks, int split_thresh, double* __restrict__ ck_part) {
-    using G = Geo<P>;
+    using G = GeoB<P>;
     using V = VecT<G::VEC>;
     constexpr int WAVES = BLOCK / 64;
     if (skip && *skip == 0) return;  // every consumer of this step already stopped
@@ -401,7 +406,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_block(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            gather_row<P, FLAGS>(ck_beg[ci] + grp, ck_end[ci], G::GPW, p0, col, val, X, s, ldx);
+            gather_row<P, FLAGS, G>(ck_beg[ci] + grp, ck_end[ci], G::GPW, p0, col, val, X, s, ldx);
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
@@ -419,7 +424,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_block(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            gather_row<P, FLAGS>(row_ptr[row] + grp, row_ptr[row + 1], G::GPW, p0, col, val, X, s,
+            gather_row<P, FLAGS, G>(row_ptr[row] + grp, row_ptr[row + 1], G::GPW, p0, col, val, X, s,
                                  ldx);
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
@@ -442,7 +447,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_block(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            gather_row<P, FLAGS>(beg, end, 1, p0, col, val, X, s, ldx);
+            gather_row<P, FLAGS, G>(beg, end, 1, p0, col, val, X, s, ldx);
             typename V::T yo;
             double* yp = reinterpret_cast<double*>(&yo);
 #pragma unroll
