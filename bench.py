@@ -40,6 +40,8 @@ def parse():
                     help="CPU-baseline time budget (rank 0, N=1 only); 0 disables")
     ap.add_argument("--lanes", type=int, default=3,
                     help="probe sweeps in flight on separate HIP streams (KT_SLQ_LANES, 1..4)")
+    ap.add_argument("--explicit", action="store_true",
+                    help="explicit K1/K2 CGS2 sweep instead of the y-form pass (KT_SLQ_YFORM=0)")
     ap.add_argument("--no-profile", action="store_true")
     return ap.parse_args()
 
@@ -94,6 +96,7 @@ def _pmc_traffic(kernel_prefix):
 def main():
     args = parse()
     os.environ["KT_SLQ_LANES"] = str(args.lanes)
+    os.environ["KT_SLQ_YFORM"] = "0" if args.explicit else "1"
     import torch  # noqa: F401  -- load torch's HIP runtime first (one runtime per process)
     import torch.distributed as dist
 
@@ -158,8 +161,12 @@ def main():
 
     ms_per_step = el_max * 1e3 / args.steps
     value = args.steps / el_max
-    # algorithmic bytes: one K1 launch = one Lanczos step of one
-    # P-probe sweep: CSR (12 nnz + 4(n+1)) + gather source, v_{j-1}, y (8nP each)
+    # algorithmic bytes: one launch of the dominant kernel = one
+    # Lanczos step of one P-probe sweep: CSR (12 nnz + 4(n+1)) + gather source,
+    # previous vector, next vector (8nP each).  The y-form pass
+    # (k_spmm_lanczos) moves exactly these streams; the explicit sweep's K1 is
+    # charged the whole step although its K2 streams two of them.
+    kname = f"k_spmm_dot<{P}" if args.explicit else f"k_spmm_lanczos<{P}"
     k1_bytes = 12 * nnz + 4 * (n + 1) + 24 * n * P
     sweeps = math.ceil(cnt / P)
     b_eval_rank = m * (sweeps * (12 * nnz + 4 * (n + 1)) + 24 * n * cnt)
@@ -171,10 +178,10 @@ def main():
         if l1:
             k1_ms = ms1 / l1
             achieved = k1_bytes / (k1_ms * 1e-3) / 1e9
-            traffic = _pmc_traffic(f"k_spmm_dot<{P}")
+            traffic = _pmc_traffic(kname)
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": f"k_spmm_dot<{P}>", "avg_launch_us": round(k1_ms * 1e3, 2),
+                    "kernel": kname + ">", "avg_launch_us": round(k1_ms * 1e3, 2),
                     "launches": l1, "algorithmic_bytes_per_launch": k1_bytes,
                     "measured": "HIP events on an isolated single-lane pass (4 sweeps x m steps) "
                                 "after the timed region",
@@ -183,7 +190,10 @@ def main():
                 tgbs = traffic / (k1_ms * 1e-3) / 1e9
                 roof["traffic_GBs"] = round(tgbs, 1)
                 roof["traffic_frac"] = round(tgbs / HBM_PEAK_GBS, 4)
-            extra["k2_update_avg_us"] = round(ms2 / max(l2, 1) * 1e3, 2)
+            if l2:
+                extra["k2_update_avg_us"] = round(ms2 / l2 * 1e3, 2)
+    extra["sweep"] = "explicit K1/K2 CGS2" if args.explicit else "y-form single pass"
+    extra["yform_redone_sweeps"] = ctx.yform_redone()
     eval_gbs = b_eval_rank / (ms_per_step * 1e-3) / 1e9
     extra["eval_roofline"] = {"B_eval_bytes_per_rank": b_eval_rank, "achieved_GBs_per_rank":
                               round(eval_gbs, 1), "frac": round(eval_gbs / HBM_PEAK_GBS, 4)}

@@ -259,6 +259,12 @@ int kt_profile_enable(kt_context_t ctx, int enable);
 int kt_profile_read(kt_context_t ctx, int kernel, int64_t* launches, double* total_ms);
 int kt_profile_reset(kt_context_t ctx);
 
+/* Hot-path statistics.  stat 0: kt_slq_trace sweeps whose y-form probe
+ * Lanczos tripped the cancellation guard (a lucky breakdown, or a beta^2
+ * below 1e-4 ||A v||^2) and were recomputed by the explicit CGS2 sweep,
+ * counted since context creation. */
+int kt_context_stat(kt_context_t ctx, int stat, int64_t* value);
+
 #ifdef __cplusplus
 }
 #endif

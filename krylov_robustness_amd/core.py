@@ -56,6 +56,13 @@ class Context:
         _lib.check(_lib.load().kt_profile_read(self._h, kernel, C.byref(n), C.byref(ms)))
         return int(n.value), float(ms.value)
 
+    def yform_redone(self) -> int:
+        """Sweeps of the y-form hot path recomputed by the explicit CGS2 sweep
+        (cancellation guard / lucky breakdown), since context creation."""
+        v = C.c_int64()
+        _lib.check(_lib.load().kt_context_stat(self._h, 0, C.byref(v)))
+        return int(v.value)
+
 
 _default_ctx: Optional[Context] = None
 

@@ -372,6 +372,130 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
 }
 
 // ---------------------------------------------------------------------------
+// KY: the A-image ("y-form") probe Lanczos step -- the whole step in ONE
+// streaming pass (no K2).  With y_j = A v_j the three-term recurrence
+//   beta_{j+1} v_{j+1} = A v_j - alpha_j v_j - beta_j v_{j-1}
+// multiplied by A gives
+//   y_{j+1} = (A y_j - alpha_j y_j - beta_j y_{j-1}) / beta_{j+1},
+// and every coefficient follows from three dots of this pass (symmetry of A,
+// see k_ycoef): the v_j are never formed.  The kernel gathers X = y_j,
+// reads the own rows X[r], Yold[r] = y_{j-1}[r] (dead after this pass: NT)
+// and writes Out[r] = g t_r - a X[r] - b Yold[r] in place over Yold, with
+// per-probe (g, a, b) = (1, alpha_j, beta_j) / beta_{j+1}.  Start mode
+// (has_old = 0): X = the probe block z, (g, a, b) = (1/||z||, 0, 0), Out =
+// y_0 = A v_0.  partial slabs [3][P][grid]: X.t, X.Out, Out.Out.
+// ---------------------------------------------------------------------------
+template <int P, int FLAGS, class G = Geo<P>>
+__device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s, const double* cg,
+                                               const double* ca, const double* cb, bool has_old,
+                                               const double* __restrict__ X,
+                                               const double* __restrict__ Yold,
+                                               double* __restrict__ Out, double* d0, double* d1,
+                                               double* d2) {
+    using V = VecT<G::VEC>;
+    const int64_t off = (int64_t)row * P + p0;
+    const typename V::T xi = V::load(X + off);
+    typename V::T yo;
+    if (has_old) yo = V::load_nt(Yold + off);
+    typename V::T o;
+    double* op = reinterpret_cast<double*>(&o);
+#pragma unroll
+    for (int e = 0; e < G::VEC; ++e) {
+        const double x = V::get(xi, e);
+        double u = fma(-ca[e], x, cg[e] * s[e]);
+        if (has_old) u = fma(-cb[e], V::get(yo, e), u);
+        op[e] = u;
+        d0[e] = fma(x, s[e], d0[e]);
+        d1[e] = fma(x, u, d1[e]);
+        d2[e] = fma(u, u, d2[e]);
+    }
+    if constexpr (FLAGS & KF_NTY) V::store_nt(Out + off, o);
+    else V::store(Out + off, o);
+}
+
+template <int P, int BLOCK, int FLAGS>
+__global__ __launch_bounds__(BLOCK) void k_spmm_lanczos(
+    const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
+    int n, const double* __restrict__ X, const double* __restrict__ Yold, double* __restrict__ Out,
+    const double* __restrict__ coef, double* __restrict__ partial,
+    const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks) {
+    using G = GeoK1<P>;
+    constexpr int WAVES = BLOCK / 64;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int sub = lane % G::LPR;
+    const int grp = lane / G::LPR;
+    const int p0 = sub * G::VEC;
+    const bool has_old = Yold != nullptr;
+
+    double cg[G::VEC], ca[G::VEC], cb[G::VEC], d0[G::VEC], d1[G::VEC], d2[G::VEC];
+#pragma unroll
+    for (int e = 0; e < G::VEC; ++e) {
+        cg[e] = coef[p0 + e];
+        ca[e] = coef[P + p0 + e];
+        cb[e] = coef[2 * P + p0 + e];
+        d0[e] = d1[e] = d2[e] = 0.0;
+    }
+
+    if ((int)blockIdx.x < long_blocks) {
+        for (int li = blockIdx.x * WAVES + wave; li < n_long; li += long_blocks * WAVES) {
+            const int row = long_rows[li];
+            const int beg = row_ptr[row];
+            const int end = row_ptr[row + 1];
+            double s[G::VEC];
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+            gather_row<P, FLAGS, G>(beg + grp, end, G::GPW, p0, col, val, X, s);
+#pragma unroll
+            for (int o = G::LPR; o < 64; o <<= 1)
+#pragma unroll
+                for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
+            if (grp == 0)
+                row_epilogue_y<P, FLAGS, G>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2);
+        }
+    } else {
+        const int sb = blockIdx.x - long_blocks;
+        const int groups_total = (gridDim.x - long_blocks) * WAVES * G::GPW;
+        for (int row = (sb * WAVES + wave) * G::GPW + grp; row < n; row += groups_total) {
+            const int beg = ld_stream<FLAGS>(row_ptr + row);
+            const int end = ld_stream<FLAGS>(row_ptr + row + 1);
+            if (end - beg > long_thresh) continue;  // owned by a long-row wave
+            double s[G::VEC];
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+            gather_row<P, FLAGS, G>(beg, end, 1, p0, col, val, X, s);
+            row_epilogue_y<P, FLAGS, G>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2);
+        }
+    }
+
+#pragma unroll
+    for (int o = G::LPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) {
+            d0[e] += __shfl_xor(d0[e], o, 64);
+            d1[e] += __shfl_xor(d1[e], o, 64);
+            d2[e] += __shfl_xor(d2[e], o, 64);
+        }
+    __shared__ double red[WAVES][3][P];
+    if (grp == 0) {
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) {
+            red[wave][0][p0 + e] = d0[e];
+            red[wave][1][p0 + e] = d1[e];
+            red[wave][2][p0 + e] = d2[e];
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < 3 * P; t += BLOCK) {  // slot t = q * P + p
+        const int q = t / P, p = t % P;
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) v += red[w][q][p];
+        partial[(int64_t)t * gridDim.x + blockIdx.x] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Block SpMM for the block-Krylov paths: Y[:, 0:P] = A X[:, 0:P] with row
 // strides ldx, ldy (blocks are column slices of a wider row-major basis).
 // Same row-group / long-row mapping as K1, no reductions.
@@ -645,6 +769,76 @@ __global__ __launch_bounds__(256) void k_norm(const double* __restrict__ partial
     }
 }
 
+// y-form coefficients (one workgroup per probe, one wave per dot).  State
+// ys[k][P]: 0 alpha_j, 1 beta_j, 2 alpha_{j-1}, 3 ||y_j||^2, 4 y_{j-1}.y_j,
+// 5 beta_{j+1}, 6..8 the next pass's (g, a, b).  Identities (A = A',
+// v_i orthonormal, y_i = A v_i):
+//   alpha_0 = v_0.y_0,  beta_1^2 = ||y_0||^2 - alpha_0^2,
+//   alpha_{j+1} beta_{j+1}^2 = y_j'A y_j - 2 alpha_j ||y_j||^2
+//        - 2 beta_j y_{j-1}.y_j + alpha_j^3 + 2 alpha_j beta_j^2 + beta_j^2 alpha_{j-1},
+//   beta_{j+2}^2 = ||y_{j+1}||^2 - alpha_{j+1}^2 - beta_{j+1}^2.
+// guard[p] = min over the used beta_k of beta_k^2 / ||y_{k-1}||^2: a small
+// ratio (cancellation; a lucky breakdown) sends the sweep back to the
+// explicit CGS2 path on the host (kt_slq.cpp), so breakdowns keep the
+// reference's semantics (lanczos_krylov.m:91-93).
+// Records: alpha[j], up[j] = beta_j, low[j] = beta_{j+1}.
+template <int P>
+__global__ __launch_bounds__(192) void k_ycoef(const double* __restrict__ partial, int nblk,
+                                               int start, int last, double s0,
+                                               double* __restrict__ ys,
+                                               double* __restrict__ t_alpha,
+                                               double* __restrict__ t_up,
+                                               double* __restrict__ t_low,
+                                               double* __restrict__ guard) {
+    const int p = blockIdx.x;
+    const int q = threadIdx.x >> 6;
+    const double r = wave_reduce_slot(partial, nblk, q * P + p);
+    __shared__ double d[3];
+    if ((threadIdx.x & 63) == 0) d[q] = r;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double an, bn, bnext_sq, ny2;
+    if (start) {
+        an = d[1] * s0;  // v_0 . y_0 with v_0 = s0 z
+        ny2 = d[2];
+        bn = 0.0;        // beta_0
+        bnext_sq = ny2 - an * an;
+        ys[1 * P + p] = 0.0;
+        ys[2 * P + p] = 0.0;
+        ys[4 * P + p] = 0.0;
+        guard[p] = 1.0;
+    } else {
+        const double aj = ys[0 * P + p], bj = ys[1 * P + p], am1 = ys[2 * P + p];
+        const double nyj = ys[3 * P + p], ydj = ys[4 * P + p], b1 = ys[5 * P + p];
+        const double b1sq = b1 * b1;
+        an = (d[0] - 2.0 * aj * nyj - 2.0 * bj * ydj + aj * aj * aj + 2.0 * aj * bj * bj +
+              bj * bj * am1) / b1sq;
+        ny2 = d[2];
+        bn = b1;
+        bnext_sq = ny2 - an * an - b1sq;
+        ys[1 * P + p] = b1;
+        ys[2 * P + p] = aj;
+        ys[4 * P + p] = d[1];
+    }
+    const double bnext = sqrt(fmax(bnext_sq, 0.0));
+    ys[0 * P + p] = an;
+    ys[3 * P + p] = ny2;
+    ys[5 * P + p] = bnext;
+    t_alpha[p] = an;
+    t_up[p] = bn;
+    t_low[p] = bnext;
+    if (!last) {
+        const double ratio = bnext_sq / ny2;
+        const double g = guard[p];
+        guard[p] = (ratio < g || !(ratio == ratio)) ? ratio : g;  // NaN sticks
+    }
+    const bool ok = bnext > 0.0 && bnext < INFINITY;
+    const double inv = ok ? 1.0 / bnext : 0.0;
+    ys[6 * P + p] = inv;
+    ys[7 * P + p] = an * inv;
+    ys[8 * P + p] = bn * inv;
+}
+
 // ---------------------------------------------------------------------------
 // Small streaming kernels for the Afun paths (mc_trace.m / expmv.m).
 // ---------------------------------------------------------------------------
@@ -833,6 +1027,36 @@ hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, doub
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
         k_norm<PP><<<(3 * PP + 3) / 4, 256, 0, st>>>(partial, nblk, k2s, scale_next, t_low);
+    });
+}
+
+hipError_t launch_spmm_lanczos(int P, int flags, int grid, const int* rp, const int* ci,
+                               const double* va, int n, const double* X, const double* Yold,
+                               double* Out, const double* coef, double* partial,
+                               const int* long_rows, int n_long, int long_thresh, int long_blocks,
+                               hipStream_t st) {
+    return dispatch_p(P, [&](auto c) {
+        constexpr int PP = decltype(c)::value;
+#define KT_KY(F)                                                                                   \
+    k_spmm_lanczos<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, X, Yold, Out, coef, partial, \
+                                                           long_rows, n_long, long_thresh, long_blocks)
+        switch (flags & (KF_UNIT | KF_NTY)) {
+        case 0: KT_KY(0); break;
+        case KF_UNIT: KT_KY(KF_UNIT); break;
+        case KF_NTY: KT_KY(KF_NTY); break;
+        default: KT_KY(KF_UNIT | KF_NTY); break;
+        }
+#undef KT_KY
+    });
+}
+
+hipError_t launch_ycoef(int P, const double* partial, int nblk, int start, int last, double s0,
+                        double* ys, double* t_alpha, double* t_up, double* t_low, double* guard,
+                        hipStream_t st) {
+    return dispatch_p(P, [&](auto c) {
+        constexpr int PP = decltype(c)::value;
+        k_ycoef<PP><<<PP, 192, 0, st>>>(partial, nblk, start, last, s0, ys, t_alpha, t_up, t_low,
+                                        guard);
     });
 }
 

@@ -43,6 +43,16 @@ hipError_t launch_update(int P, int grid, int n, const double* y, double* uprev,
                          bool nt = false);
 hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, double* scale_next,
                        double* t_low, hipStream_t st);
+// y-form probe Lanczos (one pass per step) and its per-probe coefficients;
+// Yold == nullptr selects start mode
+hipError_t launch_spmm_lanczos(int P, int flags, int grid, const int* rp, const int* ci,
+                               const double* va, int n, const double* X, const double* Yold,
+                               double* Out, const double* coef, double* partial,
+                               const int* long_rows, int n_long, int long_thresh, int long_blocks,
+                               hipStream_t st);
+hipError_t launch_ycoef(int P, const double* partial, int nblk, int start, int last, double s0,
+                        double* ys, double* t_alpha, double* t_up, double* t_low, double* guard,
+                        hipStream_t st);
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st);
 hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int ldu,
                                const double* W, double* Y, int ldy, hipStream_t st);

@@ -243,6 +243,8 @@ int kt_context_create(int device, kt_context_t* out) {
     ctx->num_cu = prop.multiProcessorCount;
     if (const char* f = getenv("KT_K1_FLAGS")) ctx->k1_flags = atoi(f);
     if (const char* f = getenv("KT_K2_NT")) ctx->k2_nt = f[0] == '1';
+    if (const char* f = getenv("KT_KY_FLAGS")) ctx->ky_flags = atoi(f);
+    if (const char* f = getenv("KT_SLQ_YFORM")) ctx->yform = f[0] != '0';
     KT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     *out = ctx;
     KT_GUARD_END
@@ -380,6 +382,13 @@ int kt_profile_read(kt_context_t ctx, int kernel, int64_t* launches, double* tot
     if (!ctx || kernel < 0 || kernel >= PROF_NSLOTS) fail(KT_ERR_ARG, "bad profile query");
     if (launches) *launches = ctx->prof[kernel].launches;
     if (total_ms) *total_ms = ctx->prof[kernel].total_ms;
+    KT_GUARD_END
+}
+
+int kt_context_stat(kt_context_t ctx, int stat, int64_t* value) {
+    KT_GUARD_BEGIN
+    if (!ctx || !value || stat != 0) fail(KT_ERR_ARG, "bad stat query");
+    *value = ctx->yform_redone;
     KT_GUARD_END
 }
 

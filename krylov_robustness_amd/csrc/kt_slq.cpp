@@ -126,6 +126,70 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
                               hipMemcpyDeviceToHost, st));
 }
 
+// y-form sweep (RNG-seeded probes only): one fused pass + one coefficient
+// launch per Lanczos step (kt_kernels.hip, k_spmm_lanczos / k_ycoef).
+// rec_host receives [alpha | up | low][m][P] followed by guard[P].
+void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
+                     int64_t probe_base, double* rec_host, int lane) {
+    kt_context_s* ctx = A->ctx;
+    const int n = (int)A->n;
+    if (lane < 0 || lane > 3) fail(KT_ERR_ARG, "sweep lane out of range");
+    if (lane && !ctx->aux_stream[lane - 1])
+        KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[lane - 1], hipStreamNonBlocking));
+    hipStream_t st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
+    const int grid = spmm_grid(n, P, ctx->num_cu * 4);
+    const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
+    const int grid1 = grid + lblocks;
+    SweepBufs& w = ctx->ws.sweep[lane];
+    const size_t blk_bytes = sizeof(double) * (size_t)n * P;
+    w.X0.ensure(blk_bytes);
+    w.X1.ensure(blk_bytes);
+    w.Y.ensure(blk_bytes);
+    w.partial.ensure(sizeof(double) * (size_t)3 * grid1 * P);
+    w.coef.ensure(sizeof(double) * 9 * P);
+    const size_t rec = (size_t)3 * m * P + P;
+    w.trec.ensure(sizeof(double) * rec);
+    double* part = w.partial.as<double>();
+    double* ys = w.coef.as<double>();
+    double* trec = w.trec.as<double>();
+    double* guard = trec + (size_t)3 * m * P;
+    auto rec_at = [&](int row, int j) { return trec + (size_t)(row * m + j) * P; };
+    const int flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
+    const double s0 = 1.0 / std::sqrt((double)n);  // v_0 = z / ||z||, ||z||^2 = n
+
+    double* Z = w.X1.as<double>();
+    KT_HIP(launch_rademacher(P, n, seed, probe_base, M.perm, Z, st));
+    KT_HIP(launch_fill(ys + 6 * P, P, s0, st));        // (g, a, b) = (s0, 0, 0)
+    KT_HIP(launch_fill(ys + 7 * P, 2 * P, 0.0, st));
+    double* Xc = w.Y.as<double>();   // y_j
+    double* Yo = nullptr;            // y_{j-1} (none at j = 0)
+    double* Ot = w.X0.as<double>();  // y_{j+1}
+    prof_begin(ctx, PROF_SPMM, st);
+    KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Z, nullptr, Xc, ys + 6 * P,
+                               part, M.long_rows, M.n_long, A->long_thresh, lblocks, st));
+    prof_end(ctx, PROF_SPMM, st);
+    KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, s0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0),
+                        guard, st));
+    for (int j = 0; j + 1 < m; ++j) {
+        prof_begin(ctx, PROF_SPMM, st);
+        KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, Yo, Ot, ys + 6 * P,
+                                   part, M.long_rows, M.n_long, A->long_thresh, lblocks, st));
+        prof_end(ctx, PROF_SPMM, st);
+        KT_HIP(launch_ycoef(P, part, grid1, 0, j + 2 == m, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1),
+                            rec_at(2, j + 1), guard, st));
+        Yo = Xc;  // y_{j+1} overwrites y_{j-1} from the next pass on
+        Xc = Ot;
+        Ot = Yo;
+    }
+    KT_HIP(hipMemcpyAsync(rec_host, trec, sizeof(double) * rec, hipMemcpyDeviceToHost, st));
+}
+
+// A y-form probe is accepted when every used beta_k^2 kept at least this
+// fraction of ||y_{k-1}||^2 (its Gram-identity cancellation then costs at most
+// ~1e4 ulp); otherwise its sweep is recomputed by the explicit CGS2 sweep.
+// Measured minimum on the golden graphs and Chung-Lu up to m = 100: 6.4e-3.
+constexpr double kYformGuard = 1e-4;
+
 // Column c of a sweep record -> symmetric tridiagonal (alpha, off); returns
 // the number of steps before a lucky breakdown (lanczos_krylov.m:91-93).
 int record_tridiag(const double* R, int m, int P, int c, double* al, double* off) {
@@ -241,22 +305,42 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         const int P = block ? block : slq_auto_block(n, nprobes);
         const int64_t nsweeps = (nprobes + P - 1) / P;
         KT_HIP(hipSetDevice(ctx->device));
-        const size_t rec = (size_t)3 * m * P;
+        // record per sweep: [alpha | up | low][m][P] (+ guard[P] in y-form)
+        const size_t rec = (size_t)3 * m * P + P;
         Workspace& w = ctx->ws;
         w.host_trec.ensure(sizeof(double) * rec * nsweeps);
         double* htrec = w.host_trec.as<double>();
         // KT_SLQ_LANES=L (<= 4): sweeps round-robin over L streams, so one
-        // sweep's streaming K2 and small launches overlap another sweep's
-        // gather-bound K1
+        // sweep's small launches (and, in the explicit sweep, its streaming
+        // K2) overlap another sweep's gather-bound pass
         const char* le = getenv("KT_SLQ_LANES");
         const int lanes_env = le ? std::max(1, std::min(4, atoi(le))) : 3;  // measured best: 3
         const int lanes = (int)std::min<int64_t>(nsweeps, lanes_env);
         const DevCSR& H = hub_csr(A);
-        for (int64_t s = 0; s < nsweeps; ++s)
-            lanczos_sweep(A, H, P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr, htrec + rec * s,
-                          nullptr, nullptr, (int)(s % lanes));
+        for (int64_t s = 0; s < nsweeps; ++s) {
+            if (ctx->yform)
+                lanczos_sweep_y(A, H, P, m, seed, probe_offset + s * P, htrec + rec * s, (int)(s % lanes));
+            else
+                lanczos_sweep(A, H, P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr,
+                              htrec + rec * s, nullptr, nullptr, (int)(s % lanes));
+        }
         KT_HIP(hipStreamSynchronize(ctx->stream));
         for (int l = 1; l < lanes; ++l) KT_HIP(hipStreamSynchronize(ctx->aux_stream[l - 1]));
+        if (ctx->yform) {  // sweeps with a guarded probe are redone by the explicit CGS2 sweep
+            int64_t redone = 0;
+            for (int64_t s = 0; s < nsweeps; ++s) {
+                const double* g = htrec + rec * s + (size_t)3 * m * P;
+                const int64_t live = std::min<int64_t>(P, nprobes - s * P);
+                bool bad = false;
+                for (int64_t c = 0; c < live; ++c) bad |= !(g[c] >= kYformGuard);
+                if (!bad) continue;
+                lanczos_sweep(A, H, P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr,
+                              htrec + rec * s, nullptr, nullptr, 0);
+                KT_HIP(hipStreamSynchronize(ctx->stream));
+                ++redone;
+            }
+            ctx->yform_redone += redone;
+        }
         prof_collect(ctx);
 
         std::vector<double> qv((size_t)nprobes);

@@ -127,3 +127,56 @@ def test_slq_full_size_config4(kra, gpu_ctx, monkeypatch):
     assert np.array_equal(qs, q1[32:48])
     _, q_ref = slq_ref.slq_trace(A, 3, 30, seed=5, probe_offset=32)
     np.testing.assert_allclose(qs[:3], q_ref, rtol=RTOL)
+
+
+def _ctx_with(monkeypatch, kra, **env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    return kra.Context(0)
+
+
+@pytest.mark.parametrize("name", GRAPHS + ["oregon_A6"])
+def test_slq_yform_matches_explicit_sweep(kra, monkeypatch, name):
+    """The y-form hot path (one fused pass per step, coefficients from Gram
+    identities) and the explicit CGS2 sweep give the same quadratures; no
+    sweep on these graphs trips the cancellation guard."""
+    A = load_graph(name)
+    cy = _ctx_with(monkeypatch, kra, KT_SLQ_YFORM="1")
+    cx = _ctx_with(monkeypatch, kra, KT_SLQ_YFORM="0")
+    for m in (2, 30, 60):
+        if m >= A.shape[0]:
+            continue
+        qy = kra.slq_quadforms(kra.DeviceMatrix(A, cy), 24, m, seed=11, fun="exp", ctx=cy)[2]
+        qx = kra.slq_quadforms(kra.DeviceMatrix(A, cx), 24, m, seed=11, fun="exp", ctx=cx)[2]
+        np.testing.assert_allclose(qy, qx, rtol=1e-10)
+    assert cy.yform_redone() == 0
+
+
+def test_slq_yform_single_step(kra, gpu_ctx):
+    """m = 1: the start pass alone (alpha_0 = z'Az/n), as the oracle."""
+    A = load_graph("india")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    _, _, q = kra.slq_quadforms(D, 5, 1, seed=4, ctx=gpu_ctx)
+    _, q_ref = slq_ref.slq_trace(A, 5, 1, seed=4)
+    np.testing.assert_allclose(q, q_ref, rtol=1e-12)
+
+
+def test_slq_yform_breakdown_falls_back(kra, monkeypatch):
+    """Complete graph K_50 (two distinct eigenvalues): the Krylov space is
+    exhausted after 2 steps, the y-form guard trips, and the sweep is redone
+    by the explicit CGS2 sweep with the reference's lucky-breakdown stop
+    (lanczos_krylov.m:91-93) -- the result equals the oracle and exp exactly."""
+    A = sp.csr_matrix(np.ones((50, 50)) - np.eye(50))
+    ctx = _ctx_with(monkeypatch, kra, KT_SLQ_YFORM="1")
+    D = kra.DeviceMatrix(A, ctx)
+    _, _, q = kra.slq_quadforms(D, 20, 30, seed=6, block=16, ctx=ctx)
+    assert ctx.yform_redone() == 2  # both sweeps of 16 probes
+    _, q_ref = slq_ref.slq_trace(A, 20, 30, seed=6)
+    np.testing.assert_allclose(q, q_ref, rtol=1e-10)
+    from oracle import krylov_oracle as ko
+    Z = ko.rademacher(50, np.arange(20), 6)
+    # K_n spectrum: n-1 on the ones vector, -1 on its complement (closed form;
+    # a dense expm loses the small forms to cancellation against e^49)
+    s = Z.sum(axis=0)
+    exact = s ** 2 / 50 * np.exp(49.0) + (50 - s ** 2 / 50) * np.exp(-1.0)
+    np.testing.assert_allclose(q, exact, rtol=1e-10)

@@ -33,6 +33,12 @@ def main():
       os.environ["KT_SLQ_LANES"] = (var[5:] if var.startswith("lanes")
                                     else var.split("_lanes")[1] if "_lanes" in var else "1")
       os.environ["KT_UNIT"] = "0" if var == "valued" else "1"
+      # y-form variants: "y", "ynt" (nontemporal y_{j+1} store), "_lanesL" suffix
+      os.environ["KT_SLQ_YFORM"] = "1" if var.startswith("y") else "0"
+      os.environ["KT_KY_FLAGS"] = "8" if var.startswith("ynt") else "0"
+      if var.startswith("y"):
+          os.environ["KT_K1_FLAGS"] = "8"
+          os.environ["KT_K2_NT"] = "1"
       ctx = kra.Context(0)
       D = kra.DeviceMatrix(A, ctx)
       print(f"--- variant {var}", flush=True)
@@ -51,8 +57,8 @@ def main():
           per_eval_1024 = el / a.nprobes * 1024
           print(f"P={P:4d} total {el*1e3:9.1f} ms  ({1/per_eval_1024:7.3f} evals/s @1024 probes) "
                 f"K1 {k1*1e3:8.1f} us {k1_bytes/k1/1e6:7.0f} GB/s  K2 {k2*1e3:8.1f} us "
-                f"{k2_bytes/k2/1e6:7.0f} GB/s  launches {l1}  K1+K2 share {(ms1+ms2)/(el*1e3):.2f}  "
-                f"tr~{s1/a.nprobes:.4e}", flush=True)
+                f"{k2_bytes/max(k2, 1e-9)/1e6:7.0f} GB/s  launches {l1}  K1+K2 share {(ms1+ms2)/(el*1e3):.2f}  "
+                f"tr~{s1/a.nprobes:.4e}  redone {ctx.yform_redone()}", flush=True)
 
 
 if __name__ == "__main__":
