@@ -38,8 +38,9 @@ def parse():
     ap.add_argument("--block", type=int, default=0, help="probes per SpMM sweep (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline time budget (rank 0, N=1 only); 0 disables")
-    ap.add_argument("--lanes", type=int, default=3,
-                    help="probe sweeps in flight on separate HIP streams (KT_SLQ_LANES, 1..4)")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="probe sweeps in flight on separate HIP streams (KT_SLQ_LANES, 1..4; "
+                         "0 = the library default: 2 for the y-form pass, 3 for the explicit sweep)")
     ap.add_argument("--explicit", action="store_true",
                     help="explicit K1/K2 CGS2 sweep instead of the y-form pass (KT_SLQ_YFORM=0)")
     ap.add_argument("--no-profile", action="store_true")
@@ -95,6 +96,8 @@ def _pmc_traffic(kernel_prefix):
 
 def main():
     args = parse()
+    if args.lanes == 0:
+        args.lanes = 3 if args.explicit else 2
     os.environ["KT_SLQ_LANES"] = str(args.lanes)
     os.environ["KT_SLQ_YFORM"] = "0" if args.explicit else "1"
     import torch  # noqa: F401  -- load torch's HIP runtime first (one runtime per process)

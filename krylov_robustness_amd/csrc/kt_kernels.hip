@@ -188,6 +188,31 @@ __global__ __launch_bounds__(256) void k_rademacher(int n, uint64_t seed, int64_
     }
 }
 
+// Packed form of the same probe block for the y-form start pass: bit p of
+// S[r * W + p / 32] (W = ceil(P / 32) words per row) is set where X[r, p] = -1.
+// n x 4W bytes (2 MB at n = 1M, P = 16) instead of the 8nP-byte fp64 block.
+template <int P>
+__global__ __launch_bounds__(256) void k_rademacher_signs(int n, uint64_t seed, int64_t probe_base,
+                                                          const int* __restrict__ perm,
+                                                          uint32_t* __restrict__ S) {
+    constexpr int W = (P + 31) / 32;
+    __shared__ uint64_t keys[P];
+    for (int p = threadIdx.x; p < P; p += blockDim.x)
+        keys[p] = sm64(sm64(seed) + (uint64_t)(probe_base + p));
+    __syncthreads();
+    const int64_t total = (int64_t)n * W;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = t / W;
+        const int w = (int)(t % W);
+        const uint64_t i = perm ? (uint64_t)perm[r] : (uint64_t)r;
+        uint32_t bits = 0;
+        for (int b = 0; b < 32 && w * 32 + b < P; ++b)
+            bits |= (uint32_t)(sm64(keys[w * 32 + b] + i) >> 63) << b;
+        S[t] = bits;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // K1
 // ---------------------------------------------------------------------------
@@ -383,7 +408,9 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
 // and writes Out[r] = g t_r - a X[r] - b Yold[r] in place over Yold, with
 // per-probe (g, a, b) = (1, alpha_j, beta_j) / beta_{j+1}.  Start mode
 // (has_old = 0): X = the probe block z, (g, a, b) = (1/||z||, 0, 0), Out =
-// y_0 = A v_0.  partial slabs [3][P][grid]: X.t, X.Out, Out.Out.
+// y_0 = A v_0.  partial slabs [3][P][grid]: X.t, X.Out, Out.Out.  Out ==
+// nullptr (the last pass of a sweep): only X.t is formed -- Yold is not read
+// and nothing is stored.
 // ---------------------------------------------------------------------------
 template <int P, int FLAGS, class G = Geo<P>>
 __device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s, const double* cg,
@@ -395,6 +422,11 @@ __device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s,
     using V = VecT<G::VEC>;
     const int64_t off = (int64_t)row * P + p0;
     const typename V::T xi = V::load(X + off);
+    if (!Out) {  // last pass: only alpha (X.t) is still needed
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) d0[e] = fma(V::get(xi, e), s[e], d0[e]);
+        return;
+    }
     typename V::T yo;
     if (has_old) yo = V::load_nt(Yold + off);
     typename V::T o;
@@ -411,6 +443,141 @@ __device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s,
     }
     if constexpr (FLAGS & KF_NTY) V::store_nt(Out + off, o);
     else V::store(Out + off, o);
+}
+
+// Start-pass gather from the packed sign table: the lane's VEC probe bits of
+// column c are one 4-byte load (VEC <= 32, VEC | 32).
+template <int P, class G>
+__device__ __forceinline__ double sign_of(uint32_t w, int p0, int e) {
+    return ((w >> ((p0 + e) & 31)) & 1u) ? -1.0 : 1.0;
+}
+template <int P, int FLAGS, class G>
+__device__ __forceinline__ void row_gather_signs(int k0, int end, int stride, int p0,
+                                                 const int* __restrict__ col,
+                                                 const double* __restrict__ val,
+                                                 const uint32_t* __restrict__ S, double* s) {
+    constexpr int W = (P + 31) / 32;
+    const int wo = p0 >> 5;
+    int k = k0;
+    for (; k + 3 * stride < end; k += 4 * stride) {
+        const int c0 = ld_stream<FLAGS>(col + k), c1 = ld_stream<FLAGS>(col + k + stride);
+        const int c2 = ld_stream<FLAGS>(col + k + 2 * stride);
+        const int c3 = ld_stream<FLAGS>(col + k + 3 * stride);
+        double a0 = 1.0, a1 = 1.0, a2 = 1.0, a3 = 1.0;
+        if constexpr (!(FLAGS & KF_UNIT)) {
+            a0 = ld_stream<FLAGS>(val + k);
+            a1 = ld_stream<FLAGS>(val + k + stride);
+            a2 = ld_stream<FLAGS>(val + k + 2 * stride);
+            a3 = ld_stream<FLAGS>(val + k + 3 * stride);
+        }
+        const uint32_t w0 = S[(int64_t)c0 * W + wo], w1 = S[(int64_t)c1 * W + wo];
+        const uint32_t w2 = S[(int64_t)c2 * W + wo], w3 = S[(int64_t)c3 * W + wo];
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) {
+            s[e] = fma(a0, sign_of<P, G>(w0, p0, e), s[e]);
+            s[e] = fma(a1, sign_of<P, G>(w1, p0, e), s[e]);
+            s[e] = fma(a2, sign_of<P, G>(w2, p0, e), s[e]);
+            s[e] = fma(a3, sign_of<P, G>(w3, p0, e), s[e]);
+        }
+    }
+    for (; k < end; k += stride) {
+        const int c0 = ld_stream<FLAGS>(col + k);
+        double a0 = 1.0;
+        if constexpr (!(FLAGS & KF_UNIT)) a0 = ld_stream<FLAGS>(val + k);
+        const uint32_t w0 = S[(int64_t)c0 * W + wo];
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) s[e] = fma(a0, sign_of<P, G>(w0, p0, e), s[e]);
+    }
+}
+
+// Start pass (y-form): y_0 = s0 A z from the packed signs; partials as
+// k_spmm_lanczos with X = z (X.t, X.y_0, y_0.y_0).
+template <int P, int BLOCK, int FLAGS>
+__global__ __launch_bounds__(BLOCK) void k_spmm_lanczos_start(
+    const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
+    int n, const uint32_t* __restrict__ S, double s0, double* __restrict__ Out,
+    double* __restrict__ partial, const int* __restrict__ long_rows, int n_long, int long_thresh,
+    int long_blocks) {
+    using G = GeoK1<P>;
+    using V = VecT<G::VEC>;
+    constexpr int WAVES = BLOCK / 64;
+    constexpr int W = (P + 31) / 32;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int sub = lane % G::LPR;
+    const int grp = lane / G::LPR;
+    const int p0 = sub * G::VEC;
+    double d0[G::VEC], d1[G::VEC], d2[G::VEC];
+#pragma unroll
+    for (int e = 0; e < G::VEC; ++e) d0[e] = d1[e] = d2[e] = 0.0;
+    auto epilogue = [&](int row, const double* sum) {
+        const uint32_t wr = S[(int64_t)row * W + (p0 >> 5)];
+        typename V::T o;
+        double* op = reinterpret_cast<double*>(&o);
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) {
+            const double x = sign_of<P, G>(wr, p0, e);
+            const double u = s0 * sum[e];
+            op[e] = u;
+            d0[e] = fma(x, sum[e], d0[e]);
+            d1[e] = fma(x, u, d1[e]);
+            d2[e] = fma(u, u, d2[e]);
+        }
+        if constexpr (FLAGS & KF_NTY) V::store_nt(Out + (int64_t)row * P + p0, o);
+        else V::store(Out + (int64_t)row * P + p0, o);
+    };
+    if ((int)blockIdx.x < long_blocks) {
+        for (int li = blockIdx.x * WAVES + wave; li < n_long; li += long_blocks * WAVES) {
+            const int row = long_rows[li];
+            double sm[G::VEC];
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) sm[e] = 0.0;
+            row_gather_signs<P, FLAGS, G>(row_ptr[row] + grp, row_ptr[row + 1], G::GPW, p0, col, val, S, sm);
+#pragma unroll
+            for (int o = G::LPR; o < 64; o <<= 1)
+#pragma unroll
+                for (int e = 0; e < G::VEC; ++e) sm[e] += __shfl_xor(sm[e], o, 64);
+            if (grp == 0) epilogue(row, sm);
+        }
+    } else {
+        const int sb = blockIdx.x - long_blocks;
+        const int groups_total = (gridDim.x - long_blocks) * WAVES * G::GPW;
+        for (int row = (sb * WAVES + wave) * G::GPW + grp; row < n; row += groups_total) {
+            const int beg = ld_stream<FLAGS>(row_ptr + row);
+            const int end = ld_stream<FLAGS>(row_ptr + row + 1);
+            if (end - beg > long_thresh) continue;
+            double sm[G::VEC];
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) sm[e] = 0.0;
+            row_gather_signs<P, FLAGS, G>(beg, end, 1, p0, col, val, S, sm);
+            epilogue(row, sm);
+        }
+    }
+#pragma unroll
+    for (int o = G::LPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) {
+            d0[e] += __shfl_xor(d0[e], o, 64);
+            d1[e] += __shfl_xor(d1[e], o, 64);
+            d2[e] += __shfl_xor(d2[e], o, 64);
+        }
+    __shared__ double red[WAVES][3][P];
+    if (grp == 0) {
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) {
+            red[wave][0][p0 + e] = d0[e];
+            red[wave][1][p0 + e] = d1[e];
+            red[wave][2][p0 + e] = d2[e];
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < 3 * P; t += BLOCK) {
+        const int q = t / P, p = t % P;
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) v += red[w][q][p];
+        partial[(int64_t)t * gridDim.x + blockIdx.x] = v;
+    }
 }
 
 template <int P, int BLOCK, int FLAGS>
@@ -1047,6 +1214,37 @@ hipError_t launch_spmm_lanczos(int P, int flags, int grid, const int* rp, const 
         default: KT_KY(KF_UNIT | KF_NTY); break;
         }
 #undef KT_KY
+    });
+}
+
+hipError_t launch_rademacher_signs(int P, int n, uint64_t seed, int64_t probe_base,
+                                  const int* perm, uint32_t* S, hipStream_t st) {
+    const int64_t total = (int64_t)n * ((P + 31) / 32);
+    int grid = (int)((total + 255) / 256);
+    if (grid > 8192) grid = 8192;
+    if (grid < 1) grid = 1;
+    return dispatch_p(P, [&](auto c) {
+        k_rademacher_signs<decltype(c)::value><<<grid, 256, 0, st>>>(n, seed, probe_base, perm, S);
+    });
+}
+
+hipError_t launch_spmm_lanczos_start(int P, int flags, int grid, const int* rp, const int* ci,
+                                     const double* va, int n, const uint32_t* S, double s0,
+                                     double* Out, double* partial, const int* long_rows, int n_long,
+                                     int long_thresh, int long_blocks, hipStream_t st) {
+    return dispatch_p(P, [&](auto c) {
+        constexpr int PP = decltype(c)::value;
+#define KT_KS(F)                                                                                 \
+    k_spmm_lanczos_start<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, S, s0, Out, partial, \
+                                                                 long_rows, n_long, long_thresh,  \
+                                                                 long_blocks)
+        switch (flags & (KF_UNIT | KF_NTY)) {
+        case 0: KT_KS(0); break;
+        case KF_UNIT: KT_KS(KF_UNIT); break;
+        case KF_NTY: KT_KS(KF_NTY); break;
+        default: KT_KS(KF_UNIT | KF_NTY); break;
+        }
+#undef KT_KS
     });
 }
 

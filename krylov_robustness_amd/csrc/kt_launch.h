@@ -50,6 +50,12 @@ hipError_t launch_spmm_lanczos(int P, int flags, int grid, const int* rp, const 
                                double* Out, const double* coef, double* partial,
                                const int* long_rows, int n_long, int long_thresh, int long_blocks,
                                hipStream_t st);
+hipError_t launch_rademacher_signs(int P, int n, uint64_t seed, int64_t probe_base,
+                                  const int* perm, uint32_t* S, hipStream_t st);
+hipError_t launch_spmm_lanczos_start(int P, int flags, int grid, const int* rp, const int* ci,
+                                     const double* va, int n, const uint32_t* S, double s0,
+                                     double* Out, double* partial, const int* long_rows, int n_long,
+                                     int long_thresh, int long_blocks, hipStream_t st);
 hipError_t launch_ycoef(int P, const double* partial, int nblk, int start, int last, double s0,
                         double* ys, double* t_alpha, double* t_up, double* t_low, double* guard,
                         hipStream_t st);

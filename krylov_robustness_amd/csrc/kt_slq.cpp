@@ -157,25 +157,27 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     const int flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
     const double s0 = 1.0 / std::sqrt((double)n);  // v_0 = z / ||z||, ||z||^2 = n
 
-    double* Z = w.X1.as<double>();
-    KT_HIP(launch_rademacher(P, n, seed, probe_base, M.perm, Z, st));
-    KT_HIP(launch_fill(ys + 6 * P, P, s0, st));        // (g, a, b) = (s0, 0, 0)
-    KT_HIP(launch_fill(ys + 7 * P, 2 * P, 0.0, st));
+    // probes as a packed sign table (n x ceil(P/32) words), gathered by the
+    // start pass instead of an 8nP-byte fp64 block
+    uint32_t* Z = w.X1.as<uint32_t>();
+    KT_HIP(launch_rademacher_signs(P, n, seed, probe_base, M.perm, Z, st));
     double* Xc = w.Y.as<double>();   // y_j
     double* Yo = nullptr;            // y_{j-1} (none at j = 0)
     double* Ot = w.X0.as<double>();  // y_{j+1}
     prof_begin(ctx, PROF_SPMM, st);
-    KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Z, nullptr, Xc, ys + 6 * P,
-                               part, M.long_rows, M.n_long, A->long_thresh, lblocks, st));
+    KT_HIP(launch_spmm_lanczos_start(P, flags, grid1, M.rowptr, M.col, M.val, n, Z, s0, Xc, part,
+                                     M.long_rows, M.n_long, A->long_thresh, lblocks, st));
     prof_end(ctx, PROF_SPMM, st);
     KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, s0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0),
                         guard, st));
     for (int j = 0; j + 1 < m; ++j) {
         prof_begin(ctx, PROF_SPMM, st);
-        KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, Yo, Ot, ys + 6 * P,
-                                   part, M.long_rows, M.n_long, A->long_thresh, lblocks, st));
+        const bool last = j + 2 == m;  // y_{m} is never used: alpha_{m-1} needs only X.t
+        KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
+                                   last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long,
+                                   A->long_thresh, lblocks, st));
         prof_end(ctx, PROF_SPMM, st);
-        KT_HIP(launch_ycoef(P, part, grid1, 0, j + 2 == m, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1),
+        KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1),
                             rec_at(2, j + 1), guard, st));
         Yo = Xc;  // y_{j+1} overwrites y_{j-1} from the next pass on
         Xc = Ot;
@@ -314,7 +316,9 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         // sweep's small launches (and, in the explicit sweep, its streaming
         // K2) overlap another sweep's gather-bound pass
         const char* le = getenv("KT_SLQ_LANES");
-        const int lanes_env = le ? std::max(1, std::min(4, atoi(le))) : 3;  // measured best: 3
+        // measured best (profiles/r01_yform_lanes.txt): 2 for the y-form pass, 3 for
+        // the explicit K1/K2 sweep
+        const int lanes_env = le ? std::max(1, std::min(4, atoi(le))) : (ctx->yform ? 2 : 3);
         const int lanes = (int)std::min<int64_t>(nsweeps, lanes_env);
         const DevCSR& H = hub_csr(A);
         for (int64_t s = 0; s < nsweeps; ++s) {
