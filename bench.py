@@ -195,6 +195,9 @@ def main():
                 roof["traffic_frac"] = round(tgbs / HBM_PEAK_GBS, 4)
             if l2:
                 extra["k2_update_avg_us"] = round(ms2 / l2 * 1e3, 2)
+            l3, ms3 = ctx.profile_read(2)
+            if l3:
+                extra["start_pass_avg_us"] = round(ms3 / l3 * 1e3, 2)
     extra["sweep"] = "explicit K1/K2 CGS2" if args.explicit else "y-form single pass"
     extra["yform_redone_sweeps"] = ctx.yform_redone()
     eval_gbs = b_eval_rank / (ms_per_step * 1e-3) / 1e9

@@ -253,8 +253,11 @@ int kt_hessianfcn(kt_matrix_t A, int64_t nomega, const double* X, const double* 
 int kt_eigs_leading(kt_matrix_t A, double tol, int maxit, double* lambda, double* v, int* steps);
 
 /* Per-kernel timing (HIP events recorded on the library's stream around each
- * launch of the named kernel while enabled).  kernel: 0 = spmm_gram (K1),
- * 1 = update_norm (K2).  Returns launch count and summed milliseconds. */
+ * launch of the named kernel while enabled).  kernel: 0 = the probe-Lanczos
+ * gather pass (k_spmm_lanczos in the y-form sweep, k_spmm_dot = K1 in the
+ * explicit sweep), 1 = K2 (k_update, explicit sweep only), 2 = the y-form
+ * start pass (k_spmm_lanczos_start).  Returns launch count and summed
+ * milliseconds. */
 int kt_profile_enable(kt_context_t ctx, int enable);
 int kt_profile_read(kt_context_t ctx, int kernel, int64_t* launches, double* total_ms);
 int kt_profile_reset(kt_context_t ctx);

@@ -87,7 +87,7 @@ struct ProfSlot {
     double total_ms = 0.0;
 };
 
-enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_NSLOTS = 2 };
+enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_START = 2, PROF_NSLOTS = 3 };
 
 // Buffers of one probe-sweep lane (kt_slq.cpp); two lanes let two sweeps
 // run on two streams.

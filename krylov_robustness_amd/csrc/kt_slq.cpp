@@ -164,10 +164,10 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     double* Xc = w.Y.as<double>();   // y_j
     double* Yo = nullptr;            // y_{j-1} (none at j = 0)
     double* Ot = w.X0.as<double>();  // y_{j+1}
-    prof_begin(ctx, PROF_SPMM, st);
+    prof_begin(ctx, PROF_START, st);
     KT_HIP(launch_spmm_lanczos_start(P, flags, grid1, M.rowptr, M.col, M.val, n, Z, s0, Xc, part,
                                      M.long_rows, M.n_long, A->long_thresh, lblocks, st));
-    prof_end(ctx, PROF_SPMM, st);
+    prof_end(ctx, PROF_START, st);
     KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, s0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0),
                         guard, st));
     for (int j = 0; j + 1 < m; ++j) {

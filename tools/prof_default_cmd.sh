@@ -1,4 +1,4 @@
-# rocprofv3 kernel stats of the exact default bench command (3 lanes, timed
+# rocprofv3 kernel stats of the exact default bench command (default lanes, timed
 # region + the isolated single-lane roofline pass + CPU baseline).
 set -e
 OUT=$PWD/gpurun_out/defcmd

@@ -1,0 +1,43 @@
+"""Split a rocprofv3 kernel trace of the default bench command into the timed
+region and the isolated single-lane roofline pass, for the dominant kernel,
+and compare each with the bench line it produced.
+Usage: python tools/reconcile_trace.py KERNEL_TRACE_CSV BENCH_JSON OUT_JSON"""
+import csv
+import json
+import sys
+
+
+def main(trace_csv, bench_json, out_json):
+    b = json.loads(open(bench_json).read().strip().splitlines()[-1])
+    roof = b["roofline"]
+    kname = roof["kernel"].rstrip(">")  # e.g. k_spmm_lanczos<16
+    rows = [r for r in csv.DictReader(open(trace_csv)) if f"kt::{kname}," in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]  # us
+    iso = roof["launches"]
+    timed = b["steps"] * (b["config"]["probes_per_eval"] // b["config"]["probes_per_sweep"]) * \
+        (b["config"]["lanczos_m"] - 1)
+    t_iso, t_timed = dur[-iso:], dur[-iso - timed:-iso]
+    out = {
+        "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py (default command)",
+        "kernel": kname,
+        "bench_value": b["value"],
+        "launches_total": len(dur),
+        "isolated_pass": {"launches": len(t_iso), "rocprof_avg_us": round(sum(t_iso) / len(t_iso), 2),
+                          "bench_avg_launch_us": roof["avg_launch_us"]},
+        "timed_region": {"launches": len(t_timed),
+                         "rocprof_avg_us": round(sum(t_timed) / len(t_timed), 2),
+                         "bench_timed_region_avg_launch_us_overlapped":
+                             roof["timed_region_avg_launch_us_overlapped"],
+                         "note": f"{b['config']['sweep_lanes']} sweep lanes in flight: launches "
+                                 "share the chip"},
+        "_doc": "rocprofv3 kernel trace of the default bench command split into the timed region "
+                "(the steps x sweeps x (m-1) launches before the isolated pass) and the isolated "
+                "single-lane roofline pass (the last `launches` launches)",
+    }
+    json.dump(out, open(out_json, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
