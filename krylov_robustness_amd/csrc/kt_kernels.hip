@@ -75,7 +75,27 @@ template <int P> using GeoB = GeoW<P, (P >= 16) ? KT_BLK_VW : (P >= 2) ? 2 : 1>;
 // per launch; keeps L2/MALL for the gathered rows).  Bit 3: y is stored
 // nontemporal.  The own-row load of u_cur is always a normal load (it is the
 // gathered table).
-enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4, KF_NTY = 8 };
+// FLAGS bit 4 (y-form passes): y_{j+1} is stored write-through (buffer store
+// with sc1), which drops the line from the XCD's L2 instead of keeping it
+// (MI355X_MICROARCH.md: plain / nt stores keep the line), leaving L2 to the
+// gathered table.
+enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4, KF_NTY = 8, KF_SC1 = 16 };
+
+typedef unsigned int kt_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int kt_u32x2 __attribute__((ext_vector_type(2)));
+// VEC doubles of one lane at byte offset `boff` of the buffer, sc1 (write-through)
+template <int VEC>
+__device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t r, uint32_t boff, const double* v) {
+#pragma unroll
+    for (int e = 0; e + 1 < VEC; e += 2) {
+        const double2 d = make_double2(v[e], v[e + 1]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kt_u32x4, d), r, boff + 8 * e, 0, 16);
+    }
+    if constexpr (VEC & 1) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(kt_u32x2, v[VEC - 1]), r,
+                                              boff + 8 * (VEC - 1), 0, 16);
+    }
+}
 
 template <int VEC> struct VecT;
 template <> struct VecT<1> {
@@ -418,7 +438,7 @@ __device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s,
                                                const double* __restrict__ X,
                                                const double* __restrict__ Yold,
                                                double* __restrict__ Out, double* d0, double* d1,
-                                               double* d2) {
+                                               double* d2, __amdgpu_buffer_rsrc_t orsrc) {
     using V = VecT<G::VEC>;
     const int64_t off = (int64_t)row * P + p0;
     const typename V::T xi = V::load(X + off);
@@ -441,7 +461,8 @@ __device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s,
         d1[e] = fma(x, u, d1[e]);
         d2[e] = fma(u, u, d2[e]);
     }
-    if constexpr (FLAGS & KF_NTY) V::store_nt(Out + off, o);
+    if constexpr (FLAGS & KF_SC1) store_sc1<G::VEC>(orsrc, (uint32_t)(off * 8), op);
+    else if constexpr (FLAGS & KF_NTY) V::store_nt(Out + off, o);
     else V::store(Out + off, o);
 }
 
@@ -510,6 +531,8 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos_start(
     double d0[G::VEC], d1[G::VEC], d2[G::VEC];
 #pragma unroll
     for (int e = 0; e < G::VEC; ++e) d0[e] = d1[e] = d2[e] = 0.0;
+    __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        Out, 0, (FLAGS & KF_SC1) ? (int)((int64_t)n * P * 8) : 0, 0x00020000);
     auto epilogue = [&](int row, const double* sum) {
         const uint32_t wr = S[(int64_t)row * W + (p0 >> 5)];
         typename V::T o;
@@ -523,7 +546,8 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos_start(
             d1[e] = fma(x, u, d1[e]);
             d2[e] = fma(u, u, d2[e]);
         }
-        if constexpr (FLAGS & KF_NTY) V::store_nt(Out + (int64_t)row * P + p0, o);
+        if constexpr (FLAGS & KF_SC1) store_sc1<G::VEC>(orsrc, (uint32_t)(((int64_t)row * P + p0) * 8), op);
+        else if constexpr (FLAGS & KF_NTY) V::store_nt(Out + (int64_t)row * P + p0, o);
         else V::store(Out + (int64_t)row * P + p0, o);
     };
     if ((int)blockIdx.x < long_blocks) {
@@ -594,6 +618,9 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos(
     const int grp = lane / G::LPR;
     const int p0 = sub * G::VEC;
     const bool has_old = Yold != nullptr;
+    // Out spans n*P doubles (< 2^32 bytes when KF_SC1 is selected, kt_slq.cpp)
+    __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        Out, 0, (FLAGS & KF_SC1) ? (int)((int64_t)n * P * 8) : 0, 0x00020000);
 
     double cg[G::VEC], ca[G::VEC], cb[G::VEC], d0[G::VEC], d1[G::VEC], d2[G::VEC];
 #pragma unroll
@@ -618,7 +645,8 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos(
 #pragma unroll
                 for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
             if (grp == 0)
-                row_epilogue_y<P, FLAGS, G>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2);
+                row_epilogue_y<P, FLAGS, G>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2,
+                                           orsrc);
         }
     } else {
         const int sb = blockIdx.x - long_blocks;
@@ -631,7 +659,8 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos(
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
             gather_row<P, FLAGS, G>(beg, end, 1, p0, col, val, X, s);
-            row_epilogue_y<P, FLAGS, G>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2);
+            row_epilogue_y<P, FLAGS, G>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2,
+                                           orsrc);
         }
     }
 
@@ -1207,11 +1236,14 @@ hipError_t launch_spmm_lanczos(int P, int flags, int grid, const int* rp, const 
 #define KT_KY(F)                                                                                   \
     k_spmm_lanczos<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, X, Yold, Out, coef, partial, \
                                                            long_rows, n_long, long_thresh, long_blocks)
-        switch (flags & (KF_UNIT | KF_NTY)) {
+        switch (flags & (KF_UNIT | KF_NTY | KF_SC1)) {
         case 0: KT_KY(0); break;
         case KF_UNIT: KT_KY(KF_UNIT); break;
         case KF_NTY: KT_KY(KF_NTY); break;
-        default: KT_KY(KF_UNIT | KF_NTY); break;
+        case KF_UNIT | KF_NTY: KT_KY(KF_UNIT | KF_NTY); break;
+        case KF_SC1:
+        case KF_SC1 | KF_NTY: KT_KY(KF_SC1); break;
+        default: KT_KY(KF_UNIT | KF_SC1); break;
         }
 #undef KT_KY
     });
@@ -1238,11 +1270,14 @@ hipError_t launch_spmm_lanczos_start(int P, int flags, int grid, const int* rp, 
     k_spmm_lanczos_start<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, S, s0, Out, partial, \
                                                                  long_rows, n_long, long_thresh,  \
                                                                  long_blocks)
-        switch (flags & (KF_UNIT | KF_NTY)) {
+        switch (flags & (KF_UNIT | KF_NTY | KF_SC1)) {
         case 0: KT_KS(0); break;
         case KF_UNIT: KT_KS(KF_UNIT); break;
         case KF_NTY: KT_KS(KF_NTY); break;
-        default: KT_KS(KF_UNIT | KF_NTY); break;
+        case KF_UNIT | KF_NTY: KT_KS(KF_UNIT | KF_NTY); break;
+        case KF_SC1:
+        case KF_SC1 | KF_NTY: KT_KS(KF_SC1); break;
+        default: KT_KS(KF_UNIT | KF_SC1); break;
         }
 #undef KT_KS
     });

@@ -154,7 +154,8 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     double* trec = w.trec.as<double>();
     double* guard = trec + (size_t)3 * m * P;
     auto rec_at = [&](int row, int j) { return trec + (size_t)(row * m + j) * P; };
-    const int flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
+    int flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
+    if (blk_bytes >= ((size_t)1 << 31)) flags &= ~16;  // sc1 buffer stores take 32-bit offsets
     const double s0 = 1.0 / std::sqrt((double)n);  // v_0 = z / ||z||, ||z||^2 = n
 
     // probes as a packed sign table (n x ceil(P/32) words), gathered by the

@@ -33,9 +33,11 @@ def main():
       os.environ["KT_SLQ_LANES"] = (var[5:] if var.startswith("lanes")
                                     else var.split("_lanes")[1] if "_lanes" in var else "1")
       os.environ["KT_UNIT"] = "0" if var == "valued" else "1"
-      # y-form variants: "y", "ynt" (nontemporal y_{j+1} store), "_lanesL" suffix
+      # y-form variants: "y", "ynt" (nontemporal y_{j+1} store), "ysc1" (write-through
+      # y_{j+1} store), "_lanesL" suffix
       os.environ["KT_SLQ_YFORM"] = "1" if var.startswith("y") else "0"
-      os.environ["KT_KY_FLAGS"] = "8" if var.startswith("ynt") else "0"
+      os.environ["KT_KY_FLAGS"] = ("8" if var.startswith("ynt") else "16" if var.startswith("ysc1")
+                                   else "0")
       if var.startswith("y"):
           os.environ["KT_K1_FLAGS"] = "8"
           os.environ["KT_K2_NT"] = "1"
