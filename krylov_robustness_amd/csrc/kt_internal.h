@@ -101,6 +101,7 @@ struct Workspace {
     DevBuf expm;                                       // batched device expm (6 x batch x n^2)
     DevBuf ck_part;                                    // block SpMM hub-row chunk partials
     DevBuf hist, norm_part;                             // sweep scale history, inf-norm partials
+    DevBuf expmv_state;                                 // expmv stage stop state (device)
     PinnedBuf host_trec;
     // batched greedy candidates (kt_greedy.cpp): 3 pair blocks, indices,
     // per-candidate coefficients / partials / host records

@@ -1088,6 +1088,102 @@ __global__ void k_fill(double* __restrict__ x, int count, double v) {
     if (t < count) x[t] = v;
 }
 
+// ---------------------------------------------------------------------------
+// expmv.m:71-92 Taylor loop with its stop test on the device, so the host
+// queues a whole stage without a round trip per term.  State (ExpmvState):
+// active = 1 while the stage runs; every kernel of a term (the SpMM through
+// its skip flag, k_expmv_term, k_expmv_check) is a no-op once active = 0.
+// ---------------------------------------------------------------------------
+struct ExpmvState {
+    int active;
+    int mv;
+    double c1;
+};
+
+// stage start: c1 = norm(b, inf) from k_inf_norm partials; active = 1   (:73)
+__global__ __launch_bounds__(256) void k_expmv_begin(const double* __restrict__ partial, int nb,
+                                                     ExpmvState* st) {
+    double mx = 0.0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) mx = fmax(mx, partial[i]);
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    __shared__ double red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        st->c1 = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+        st->active = 1;
+    }
+}
+
+// b = coef (Ab - mu b) (in place), f = f + b; partial maxima of the row sums
+// of |b| (partial[0, nb)) and |f| (partial[nb, 2 nb))   (:75-78)
+__global__ __launch_bounds__(256) void k_expmv_term(int n, int nc, double mu, double coef,
+                                                    const double* __restrict__ Ab, double* __restrict__ b,
+                                                    double* __restrict__ F, int ld,
+                                                    double* __restrict__ partial,
+                                                    const ExpmvState* __restrict__ st) {
+    if (!st->active) return;
+    double mb = 0.0, mf = 0.0;
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+        double sb = 0.0, sf = 0.0;
+        for (int c = 0; c < nc; ++c) {
+            const int64_t o = (int64_t)r * ld + c;
+            double t = Ab[o];
+            if (mu != 0.0) t = fma(-mu, b[o], t);  // (A - mu I) b, as launch_axpby(-mu, b, 1, Ab)
+            const double bn = fma(coef, t, 0.0);
+            const double f = fma(1.0, bn, F[o]);
+            b[o] = bn;
+            F[o] = f;
+            sb += fabs(bn);
+            sf += fabs(f);
+        }
+        mb = fmax(mb, sb);
+        mf = fmax(mf, sf);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        mb = fmax(mb, __shfl_xor(mb, o, 64));
+        mf = fmax(mf, __shfl_xor(mf, o, 64));
+    }
+    __shared__ double red[2][4];
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = mb;
+        red[1][threadIdx.x >> 6] = mf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        partial[blockIdx.x] = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
+        partial[gridDim.x + blockIdx.x] = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+    }
+}
+
+// mv = mv + 1; c2 = norm(b, inf); if c1 + c2 <= tol*norm(f, inf) break; c1 = c2   (:76-82)
+__global__ __launch_bounds__(256) void k_expmv_check(const double* __restrict__ partial, int nb,
+                                                     double tol, ExpmvState* st) {
+    if (!st->active) return;
+    double mb = 0.0, mf = 0.0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+        mb = fmax(mb, partial[i]);
+        mf = fmax(mf, partial[nb + i]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        mb = fmax(mb, __shfl_xor(mb, o, 64));
+        mf = fmax(mf, __shfl_xor(mf, o, 64));
+    }
+    __shared__ double red[2][4];
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = mb;
+        red[1][threadIdx.x >> 6] = mf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double c2 = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
+        const double nf = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+        st->mv += 1;
+        if (st->c1 + c2 <= tol * nf) st->active = 0;
+        else st->c1 = c2;
+    }
+}
+
 }  // namespace kt
 
 // ---------------------------------------------------------------------------
@@ -1318,6 +1414,32 @@ hipError_t launch_inf_norm(int n, int nc, const double* X, int ldx, double* part
     k_inf_norm<<<inf_norm_blocks(), 256, 0, st>>>(n, nc, X, ldx, partial);
     return hipGetLastError();
 }
+
+// one row per thread: no idle blocks on small matrices (the check reduces
+// only these partials)
+static int expmv_term_blocks(int n) {
+    const int b = (n + 255) / 256;
+    return b < 1 ? 1 : (b > inf_norm_blocks() ? inf_norm_blocks() : b);
+}
+
+hipError_t launch_expmv_begin(const double* partial, int nb, void* state, hipStream_t st) {
+    k_expmv_begin<<<1, 256, 0, st>>>(partial, nb, static_cast<ExpmvState*>(state));
+    return hipGetLastError();
+}
+
+hipError_t launch_expmv_term(int n, int nc, double mu, double coef, const double* Ab, double* b,
+                             double* F, int ld, double* partial, const void* state, hipStream_t st) {
+    k_expmv_term<<<expmv_term_blocks(n), 256, 0, st>>>(n, nc, mu, coef, Ab, b, F, ld, partial,
+                                                       static_cast<const ExpmvState*>(state));
+    return hipGetLastError();
+}
+
+hipError_t launch_expmv_check(int n, const double* partial, double tol, void* state, hipStream_t st) {
+    k_expmv_check<<<1, 256, 0, st>>>(partial, expmv_term_blocks(n), tol, static_cast<ExpmvState*>(state));
+    return hipGetLastError();
+}
+
+size_t expmv_state_bytes() { return sizeof(ExpmvState); }
 
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st) {
     int grid = (count + 255) / 256;

@@ -103,5 +103,12 @@ hipError_t launch_col_select(int C, int P, const int* idx, double* X, hipStream_
 size_t pairs_coef_doubles(int C);
 hipError_t launch_inf_norm(int n, int nc, const double* X, int ldx, double* partial,
                            hipStream_t st);
+// expmv Taylor stage with the stop test on the device (state: expmv_state_bytes();
+// layout {int active; int mv; double c1;}); partial: 2 * inf_norm_blocks() doubles
+size_t expmv_state_bytes();
+hipError_t launch_expmv_begin(const double* partial, int nb, void* state, hipStream_t st);
+hipError_t launch_expmv_term(int n, int nc, double mu, double coef, const double* Ab, double* b,
+                             double* F, int ld, double* partial, const void* state, hipStream_t st);
+hipError_t launch_expmv_check(int n, const double* partial, double tol, void* state, hipStream_t st);
 
 }  // namespace kt

@@ -149,22 +149,33 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
     Ab.alloc(ctx, n, ld);
     copy_cols(ctx, n, Bsrc, ld, b.col(0), ld, nc);
     copy_cols(ctx, n, Bsrc, ld, F, ld, nc);
+    // The stop test `c1 + c2 <= tol*norm(f, inf)` runs on the device
+    // (k_expmv_check clears state.active; the remaining terms of the stage
+    // are no-ops), so a stage is queued without host round trips.  Same
+    // arithmetic as the host-tested loop: b = (t/(s k)) (A b - mu b),
+    // f = f + b, row sums of |.| in column order.
+    const int nb = inf_norm_blocks();
+    ctx->ws.norm_part.ensure(sizeof(double) * 2 * nb);
+    ctx->ws.expmv_state.ensure(expmv_state_bytes());
+    double* part = ctx->ws.norm_part.as<double>();
+    void* state = ctx->ws.expmv_state.ptr;
+    KT_HIP(hipMemsetAsync(state, 0, expmv_state_bytes(), st));
     for (int i = 0; i < r.s; ++i) {
-        double c1 = inf_norm(A, b.col(0), ld, nc);
+        KT_HIP(launch_inf_norm((int)n, nc, b.col(0), ld, part, st));   // c1 = norm(b, inf)
+        KT_HIP(launch_expmv_begin(part, nb, state, st));
         for (int k = 1; k <= r.m; ++k) {
-            spmm(A, b.col(0), ld, Ab.col(0), ld, nc);
-            if (mu != 0.0) KT_HIP(launch_axpby((int)n, nc, -mu, b.col(0), ld, 1.0, Ab.col(0), ld, st));
-            KT_HIP(launch_axpby((int)n, nc, t / ((double)r.s * k), Ab.col(0), ld, 0.0, b.col(0), ld, st));
-            r.mv += 1;
-            KT_HIP(launch_axpby((int)n, nc, 1.0, b.col(0), ld, 1.0, F, ld, st));
-            const double c2 = inf_norm(A, b.col(0), ld, nc);
-            if (c1 + c2 <= tol * inf_norm(A, F, ld, nc)) break;
-            c1 = c2;
+            spmm_slices(A, b.col(0), ld, Ab.col(0), ld, nc, static_cast<const int*>(state));
+            KT_HIP(launch_expmv_term((int)n, nc, mu, t / ((double)r.s * k), Ab.col(0), b.col(0), F, ld,
+                                     part, state, st));
+            KT_HIP(launch_expmv_check((int)n, part, tol, state, st));
         }
         KT_HIP(launch_axpby((int)n, nc, eta, F, ld, 0.0, F, ld, st));  // f = eta f
         copy_cols(ctx, n, F, ld, b.col(0), ld, nc);                    // b = f
     }
+    int hstate[2] = {0, 0};  // {active, mv}
+    KT_HIP(hipMemcpyAsync(hstate, state, sizeof(hstate), hipMemcpyDeviceToHost, st));
     KT_HIP(hipStreamSynchronize(st));
+    r.mv += hstate[1];
     return r;
 }
 
