@@ -44,6 +44,10 @@ def parse():
     ap.add_argument("--explicit", action="store_true",
                     help="explicit K1/K2 CGS2 sweep instead of the y-form pass (KT_SLQ_YFORM=0)")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse the multi-rank path, e.g. several ranks sharing one GPU with "
+                         "KT_BENCH_ONE_DEVICE=1)")
     return ap.parse_args()
 
 
@@ -105,11 +109,17 @@ def main():
 
     from krylov_robustness_amd import dist as kdist
     rank, world, local_rank = kdist.env_rank()
+    if os.environ.get("KT_BENCH_ONE_DEVICE") == "1":  # rehearsal: every rank on GPU 0
+        local_rank = 0
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", local_rank)
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # where the sums meet
 
     import krylov_robustness_amd as kra
     A, N, wl = make_graph(args.config)
@@ -124,7 +134,7 @@ def main():
 
     def step(seed):
         s1, s2, _ = kra.slq_quadforms(D, cnt, m, seed=seed, probe_offset=off, block=P, ctx=ctx)
-        s1, s2 = kdist.allreduce_sums([s1, s2], device=dev)
+        s1, s2 = kdist.allreduce_sums([s1, s2], device=coll_dev)
         return s1 / N, s2
 
     def barrier():
@@ -146,7 +156,7 @@ def main():
     el = time.perf_counter() - t0
     if not args.no_profile:
         ctx.profile(False)
-    el_max = kdist.allreduce_max(el, device=dev)
+    el_max = kdist.allreduce_max(el, device=coll_dev)
     k1_overlapped = None
     if not args.no_profile:
         l1, ms1 = ctx.profile_read(0)
