@@ -140,6 +140,8 @@ struct DevCSR {
     double* val = nullptr;
     int* long_rows = nullptr;  // rows with degree > long_thresh, heaviest first
     int n_long = 0;
+    int* med_rows = nullptr;   // rows with kMedThresh < degree <= long_thresh (expmv terms)
+    int n_med = 0;
     int* perm = nullptr;       // device row -> original row (nullptr: identity)
     // hub rows (degree > kSplitThresh) cut into kChunkNnz-nonzero chunks for
     // the block SpMM: chunk c = nonzeros [ck_beg[c], ck_end[c]); split row i =
@@ -149,7 +151,7 @@ struct DevCSR {
     bool built = false;
     // allocation sizes in elements: a rebuild after edge edits (greedy) reuses
     // the buffers instead of a hipFree / hipMalloc round trip
-    size_t cap_rp = 0, cap_col = 0, cap_val = 0, cap_lr = 0, cap_perm = 0;
+    size_t cap_rp = 0, cap_col = 0, cap_val = 0, cap_lr = 0, cap_perm = 0, cap_med = 0;
     size_t cap_ckb = 0, cap_cke = 0, cap_spr = 0, cap_spf = 0;
     void release();
     void invalidate() { built = false; }  // contents stale, buffers kept

@@ -30,6 +30,8 @@
 // All reductions are deterministic: per-block partial slabs summed in a fixed
 // order by column-reduction kernels (no float atomics).
 #include <hip/hip_runtime.h>
+
+#include "kt_launch.h"
 #include <stdint.h>
 
 #include <type_traits>
@@ -1098,6 +1100,7 @@ struct ExpmvState {
     int active;
     int mv;
     double c1;
+    double c1s[2];  // fused path: c1 of the check of term j in c1s[j & 1]
 };
 
 // stage start: c1 = norm(b, inf) from k_inf_norm partials; active = 1   (:73)
@@ -1111,6 +1114,7 @@ __global__ __launch_bounds__(256) void k_expmv_begin(const double* __restrict__ 
     __syncthreads();
     if (threadIdx.x == 0) {
         st->c1 = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+        st->c1s[1] = st->c1;
         st->active = 1;
     }
 }
@@ -1153,6 +1157,211 @@ __global__ __launch_bounds__(256) void k_expmv_term(int n, int nc, double mu, do
     if (threadIdx.x == 0) {
         partial[blockIdx.x] = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
         partial[gridDim.x + blockIdx.x] = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+    }
+}
+
+// bout = coef (A bin - mu bin), F = F + bout on one row (VEC columns from p0);
+// row sums of |bout| and |F| of those columns into sb, sf   (expmv.m:75-78)
+// The row's own F and b values are loaded before the gathers (expmv_row_prefetch).
+template <int VEC>
+__device__ __forceinline__ void expmv_row_prefetch(int row, int p0, int nc, int ld, double mu,
+                                                   const double* __restrict__ bin,
+                                                   const double* __restrict__ F, double* fo, double* bo) {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+        const int c = p0 + e;
+        const int64_t o = (int64_t)row * ld + c;
+        fo[e] = (c < nc) ? F[o] : 0.0;
+        bo[e] = (c < nc && mu != 0.0) ? bin[o] : 0.0;
+    }
+}
+template <int VEC>
+__device__ __forceinline__ void expmv_row_update(int row, int p0, const double* s, const double* fo,
+                                                 const double* bo, int nc, int ld, double mu, double coef,
+                                                 double* __restrict__ bout, double* __restrict__ F,
+                                                 double& sb, double& sf) {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+        const int c = p0 + e;
+        const int64_t o = (int64_t)row * ld + c;
+        if (c < nc) {
+            double t = s[e];
+            if (mu != 0.0) t = fma(-mu, bo[e], t);  // (A - mu I) b, as launch_axpby(-mu, b, 1, Ab)
+            const double bn = fma(coef, t, 0.0);
+            const double f = fma(1.0, bn, fo[e]);
+            bout[o] = bn;
+            F[o] = f;
+            sb += fabs(bn);
+            sf += fabs(f);
+        } else {
+            bout[o] = 0.0;
+        }
+    }
+}
+
+// One whole Taylor term in one launch (SpMM fused with the update and with
+// the previous term's stop test):
+//   the check of term k-1 (expmv.m:79-82) from that term's norm partials
+//   (pin, 2 x gridDim.x) and c1 = st->c1s[(k-1) & 1] -- stop: st->active = 0;
+//   otherwise c1s[k & 1] = c2 (every block stores the same value);
+//   bout = coef (A bin - mu bin), F = F + bout, and the partial maxima of the
+//   row sums of |bout| and |F| into pout; block 0 counts the term (mv).
+// A small matrix makes this a chain of dependent memory latencies, so the
+// reads of the check and the gathers are issued before anything is decided
+// (only the writes wait for the decision), and no row is a long serial
+// chain: blocks [0, n_long) take one row longer than long_thresh each (64
+// row groups of 32 B per lane, 8 deep, summed through LDS), the next
+// ceil(n_med / 4) blocks one row of kMedThresh < degree <= long_thresh per
+// WAVE (16 row groups, 8 deep: one round trip), the rest one row of degree
+// <= kMedThresh per row group (8 deep).
+// bin / bout and pin / pout ping-pong between terms; columns nc..P-1 of the
+// blocks stay zero so the P-wide gathers read finite values.
+template <int P, int FLAGS>
+__global__ __launch_bounds__(256) void k_expmv_step(
+    const int* __restrict__ rp, const int* __restrict__ ci, const double* __restrict__ va, int n,
+    const int* __restrict__ long_rows, int n_long, const int* __restrict__ med_rows, int n_med,
+    int nc, int ld, double mu, double coef, double tol, int k, const double* __restrict__ bin,
+    double* __restrict__ bout, double* __restrict__ F, const double* __restrict__ pin,
+    double* __restrict__ pout, ExpmvState* st) {
+    constexpr int WAVES = 4;
+    using G = GeoW<P, (P >= 2) ? 2 : 1>;                          // short rows
+    using GL = GeoW<P, (P >= 4) ? 4 : (P >= 2) ? 2 : 1>;          // medium / long rows
+    __shared__ double red[2][WAVES];
+    __shared__ double lred[WAVES][P];
+    __shared__ int decide;  // 0 = skip (stopped), 1 = run
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int nb = (int)gridDim.x;
+    const int med_blocks = (n_med + WAVES - 1) / WAVES;
+    const int kind = ((int)blockIdx.x < n_long) ? 2 : ((int)blockIdx.x < n_long + med_blocks) ? 1 : 0;
+    // (1) reads of the check, consumed after the gathers
+    const int act = (threadIdx.x == 0) ? st->active : 0;
+    const double c1 = (k > 1) ? st->c1s[(k - 1) & 1] : 0.0;
+    double pb[4], pf[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int i = (int)threadIdx.x + u * 256;
+        const bool ok = k > 1 && i < nb;
+        pb[u] = ok ? pin[i] : 0.0;
+        pf[u] = ok ? pin[nb + i] : 0.0;
+    }
+    // (2) the gathers of this term
+    const int subL = lane % GL::LPR, grpL = lane / GL::LPR, p0L = subL * GL::VEC;
+    const int sub = lane % G::LPR, grp = lane / G::LPR, p0 = sub * G::VEC;
+    double sl[GL::VEC], s[G::VEC], fo[GL::VEC], bo[GL::VEC];  // fo / bo: the row's own F, b
+#pragma unroll
+    for (int e = 0; e < GL::VEC; ++e) sl[e] = fo[e] = bo[e] = 0.0;
+#pragma unroll
+    for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+    int row = -1;
+    bool mine = false;  // this lane holds a finished row (of its row class)
+    if (kind == 2) {
+        row = long_rows[blockIdx.x];
+        if (wave == 0 && grpL == 0) expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
+        row_gather8<P, FLAGS, GL>(rp[row] + wave * GL::GPW + grpL, rp[row + 1], WAVES * GL::GPW, p0L, ci,
+                                  va, bin, sl, ld);
+    } else if (kind == 1) {
+        const int mi = ((int)blockIdx.x - n_long) * WAVES + wave;
+        if (mi < n_med) {
+            row = med_rows[mi];
+            if (grpL == 0) expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
+            row_gather8<P, FLAGS, GL>(rp[row] + grpL, rp[row + 1], GL::GPW, p0L, ci, va, bin, sl, ld);
+            mine = grpL == 0;
+        }
+    } else {
+        row = (((int)blockIdx.x - n_long - med_blocks) * WAVES + wave) * G::GPW + grp;
+        if (row < n) {
+            const int beg = rp[row], end = rp[row + 1];
+            if (end - beg <= kMedThresh) {
+                expmv_row_prefetch<G::VEC>(row, p0, nc, ld, mu, bin, F, fo, bo);
+                row_gather8<P, FLAGS, G>(beg, end, 1, p0, ci, va, bin, s, ld);
+                mine = true;
+            }
+        }
+    }
+    if (kind != 0) {  // sum the row groups of the wave
+#pragma unroll
+        for (int o = GL::LPR; o < 64; o <<= 1)
+#pragma unroll
+            for (int e = 0; e < GL::VEC; ++e) sl[e] += __shfl_xor(sl[e], o, 64);
+    }
+    if (kind == 2 && grpL == 0)
+#pragma unroll
+        for (int e = 0; e < GL::VEC; ++e) lred[wave][p0L + e] = sl[e];
+    // (3) the check, block-uniform
+    double mb = 0.0, mf = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        mb = fmax(mb, pb[u]);
+        mf = fmax(mf, pf[u]);
+    }
+    for (int i = (int)threadIdx.x + 1024; k > 1 && i < nb; i += 256) {  // grids above 1024 blocks
+        mb = fmax(mb, pin[i]);
+        mf = fmax(mf, pin[nb + i]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mb = fmax(mb, __shfl_xor(mb, o, 64));
+        mf = fmax(mf, __shfl_xor(mf, o, 64));
+    }
+    if (lane == 0) {
+        red[0][wave] = mb;
+        red[1][wave] = mf;
+    }
+    if (threadIdx.x == 0) decide = act;
+    __syncthreads();
+    if (threadIdx.x == 0 && act && k > 1) {
+        const double c2 = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
+        const double nf = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+        if (c1 + c2 <= tol * nf) {
+            st->active = 0;
+            decide = 0;
+        } else {
+            st->c1s[k & 1] = c2;
+        }
+    }
+    __syncthreads();
+    if (!decide) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->mv += 1;
+    // (4) update, norm partials of this term
+    double sb = 0.0, sf = 0.0;
+    if (kind == 0) {
+        if (mine) expmv_row_update<G::VEC>(row, p0, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+#pragma unroll
+        for (int o = 1; o < G::LPR; o <<= 1) {
+            sb += __shfl_xor(sb, o, 64);
+            sf += __shfl_xor(sf, o, 64);
+        }
+    } else {
+        if (kind == 2 && wave == 0 && grpL == 0) {
+#pragma unroll
+            for (int e = 0; e < GL::VEC; ++e)
+                sl[e] = lred[0][p0L + e] + lred[1][p0L + e] + lred[2][p0L + e] + lred[3][p0L + e];
+            mine = true;
+        }
+        if (mine) expmv_row_update<GL::VEC>(row, p0L, sl, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+#pragma unroll
+        for (int o = 1; o < GL::LPR; o <<= 1) {
+            sb += __shfl_xor(sb, o, 64);
+            sf += __shfl_xor(sf, o, 64);
+        }
+    }
+    mb = sb;
+    mf = sf;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mb = fmax(mb, __shfl_xor(mb, o, 64));
+        mf = fmax(mf, __shfl_xor(mf, o, 64));
+    }
+    __syncthreads();  // red reused
+    if (lane == 0) {
+        red[0][wave] = mb;
+        red[1][wave] = mf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        pout[blockIdx.x] = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
+        pout[gridDim.x + blockIdx.x] = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
     }
 }
 
@@ -1440,6 +1649,40 @@ hipError_t launch_expmv_check(int n, const double* partial, double tol, void* st
 }
 
 size_t expmv_state_bytes() { return sizeof(ExpmvState); }
+
+int expmv_step_blocks(int n, int P, int n_long, int n_med) {
+    const int gpw = (P >= 2) ? 64 / (P / 2) : 64;
+    return n_long + (n_med + 3) / 4 + (n + 4 * gpw - 1) / (4 * gpw);
+}
+
+hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_rows, int n_med, int nc,
+                             int ld, double mu, double coef, double tol, int k, const double* bin,
+                             double* bout, double* F, const double* pin, double* pout, void* state,
+                             hipStream_t st) {
+    const int grid = expmv_step_blocks(M.n, P, M.n_long, n_med);
+    ExpmvState* s = static_cast<ExpmvState*>(state);
+#define KT_EXPMV_STEP(PP)                                                                          \
+    if (unit)                                                                                      \
+        k_expmv_step<PP, KF_UNIT><<<grid, 256, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long,  \
+                                                        med_rows, n_med, nc, ld, mu, coef, tol, k,    \
+                                                        bin, bout, F, pin, pout, s);                 \
+    else                                                                                           \
+        k_expmv_step<PP, 0><<<grid, 256, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long,        \
+                                                  med_rows, n_med, nc, ld, mu, coef, tol, k, bin,    \
+                                                  bout, F, pin, pout, s);
+    switch (P) {
+    case 1: KT_EXPMV_STEP(1) break;
+    case 2: KT_EXPMV_STEP(2) break;
+    case 4: KT_EXPMV_STEP(4) break;
+    case 8: KT_EXPMV_STEP(8) break;
+    case 16: KT_EXPMV_STEP(16) break;
+    case 32: KT_EXPMV_STEP(32) break;
+    default: return hipErrorInvalidValue;
+    }
+#undef KT_EXPMV_STEP
+    return hipGetLastError();
+}
+
 
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st) {
     int grid = (count + 255) / 256;

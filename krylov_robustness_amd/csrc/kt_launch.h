@@ -31,6 +31,7 @@ struct CsrView {
 };
 constexpr int kChunkNnz = 32;      // nonzeros per hub-row chunk
 constexpr int kSplitThresh = 64;   // rows longer than this are chunked (block SpMM)
+constexpr int kMedThresh = 16;     // expmv terms: rows longer than this get a wave (or a workgroup)
 hipError_t launch_spmm_block(int P, int flags, int grid, const CsrView& M, const double* X, int ldx,
                              double* Y, int ldy, int long_blocks, int chunk_blocks, double* ck_part,
                              hipStream_t st, int slices = 1, const int* skip = nullptr);
@@ -110,5 +111,13 @@ hipError_t launch_expmv_begin(const double* partial, int nb, void* state, hipStr
 hipError_t launch_expmv_term(int n, int nc, double mu, double coef, const double* Ab, double* b,
                              double* F, int ld, double* partial, const void* state, hipStream_t st);
 hipError_t launch_expmv_check(int n, const double* partial, double tol, void* state, hipStream_t st);
+// one fused launch per Taylor term k (P = pow2 >= nc, P <= 32, ld >= P): the
+// check of term k-1 (from pin), SpMM of the natural-order CSR (M), update,
+// norm partials of term k into pout (each 2 * expmv_step_blocks doubles)
+int expmv_step_blocks(int n, int P, int n_long, int n_med);
+hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_rows, int n_med, int nc,
+                             int ld, double mu, double coef,
+                             double tol, int k, const double* bin, double* bout, double* F,
+                             const double* pin, double* pout, void* state, hipStream_t st);
 
 }  // namespace kt

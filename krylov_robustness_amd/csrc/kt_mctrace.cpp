@@ -10,6 +10,7 @@
 // [10,20) of the build's counter RNG (oracle/krylov_oracle.py:mc_trace).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "kt_launch.h"
 #include "kt_slq.h"
@@ -48,31 +49,33 @@ static const double kTheta[100] = {
 
 enum { AFUN_MATRIX = 0, AFUN_LANCZOS = 1, AFUN_EXPMV = 2 };
 
-static double inf_norm(kt_matrix_s* A, const double* X, int ld, int nc) {
-    kt_context_s* ctx = A->ctx;
-    const int nb = inf_norm_blocks();
-    ctx->ws.norm_part.ensure(sizeof(double) * nb);
-    KT_HIP(launch_inf_norm((int)A->n, nc, X, ld, ctx->ws.norm_part.as<double>(), ctx->stream));
-    std::vector<double> h(nb);
-    KT_HIP(hipMemcpyAsync(h.data(), ctx->ws.norm_part.ptr, sizeof(double) * nb, hipMemcpyDeviceToHost,
-                          ctx->stream));
-    KT_HIP(hipStreamSynchronize(ctx->stream));
-    return *std::max_element(h.begin(), h.end());
-}
-
-// normAm.m: ||A^m||_1 for A >= 0 (exact: e = A'^m ones, c = ||e||_inf).
-static double normAm(kt_matrix_s* A, int m) {
+// normAm.m: ||A^m||_1 for A >= 0 (exact: e = A'^m ones, c = ||e||_inf), for
+// every m = 2..mmax at once: select_taylor_degree.m:48-53 asks for
+// m = p + 1, p = 1..p_max, each from ones -- the same vectors A^m ones, so
+// one chain of mmax SpMVs gives them all (one host round trip).
+static std::vector<double> normAm_chain(kt_matrix_s* A, int mmax) {
     kt_context_s* ctx = A->ctx;
     const int64_t n = A->n;
+    const int nb = inf_norm_blocks();
     DevMat e, t;
     e.alloc(ctx, n, 1);
     t.alloc(ctx, n, 1);
+    DevBuf& part = ctx->ws.norm_part;
+    part.ensure(sizeof(double) * (size_t)nb * (mmax + 1));
     KT_HIP(launch_fill(e.col(0), (int)n, 1.0, ctx->stream));
-    for (int j = 0; j < m; ++j) {  // A symmetric: A' = A
+    for (int j = 1; j <= mmax; ++j) {  // A symmetric: A' = A
         spmm(A, e.col(0), 1, t.col(0), 1, 1);
         copy_cols(ctx, n, t.col(0), 1, e.col(0), 1, 1);
+        KT_HIP(launch_inf_norm((int)n, 1, e.col(0), 1, part.as<double>() + (size_t)j * nb, ctx->stream));
     }
-    return inf_norm(A, e.col(0), 1, 1);
+    std::vector<double> h((size_t)nb * (mmax + 1));
+    KT_HIP(hipMemcpyAsync(h.data() + nb, part.as<double>() + nb, sizeof(double) * (size_t)nb * mmax,
+                          hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<double> c(mmax + 1, 0.0);
+    for (int j = 1; j <= mmax; ++j)
+        c[j] = *std::max_element(h.begin() + (size_t)j * nb, h.begin() + (size_t)(j + 1) * nb);
+    return c;
 }
 
 struct Expmv {
@@ -113,9 +116,10 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
         if (mu != 0.0 || minv < 0.0)
             fail(KT_ERR_UNSUPPORTED, "expmv: normest1 branch of normAm.m (A - mu I not >= 0) is not built");
         std::vector<double> eta(p_max);
+        const std::vector<double> nAm = normAm_chain(A, p_max + 1);
         for (int p = 1; p <= p_max; ++p) {
-            const double c = normAm(A, p + 1) * std::pow(std::fabs(t), p + 1);
-            r.mv += p + 1;
+            const double c = nAm[p + 1] * std::pow(std::fabs(t), p + 1);
+            r.mv += p + 1;  // as normAm.m counts them (one chain per m)
             eta[p - 1] = std::pow(c, 1.0 / (p + 1));
         }
         for (int p = 1; p < p_max; ++p) alpha[p - 1] = std::max(eta[p - 1], eta[p]);
@@ -160,6 +164,36 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
     double* part = ctx->ws.norm_part.as<double>();
     void* state = ctx->ws.expmv_state.ptr;
     KT_HIP(hipMemsetAsync(state, 0, expmv_state_bytes(), st));
+    const int P = pow2_at_least(std::max(nc, 1));
+    if (P <= 32 && ld >= P && !std::getenv("KT_EXPMV_UNFUSED")) {
+        // One launch per term (k_expmv_step: the previous term's stop test,
+        // SpMM, update, norm partials); b and the partials ping-pong.
+        const DevCSR& M = natural_csr(A);
+        const CsrView V{M.rowptr, M.col, M.val, (int)n, M.long_rows, M.n_long, A->long_thresh,
+                        kSplitThresh, M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split};
+        const int nbs = expmv_step_blocks((int)n, P, M.n_long, M.n_med);
+        ctx->ws.norm_part.ensure(sizeof(double) * std::max(2 * nb, 4 * nbs));
+        part = ctx->ws.norm_part.as<double>();
+        for (int i = 0; i < r.s; ++i) {
+            KT_HIP(launch_inf_norm((int)n, nc, b.col(0), ld, part, st));   // c1 = norm(b, inf)
+            KT_HIP(launch_expmv_begin(part, nb, state, st));
+            double* cur = b.col(0);
+            double* nxt = Ab.col(0);
+            for (int k = 1; k <= r.m; ++k) {
+                KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu, t / ((double)r.s * k), tol, k, cur,
+                                         nxt, F, part + (size_t)((k - 1) & 1) * 2 * nbs,
+                                         part + (size_t)(k & 1) * 2 * nbs, state, st));
+                std::swap(cur, nxt);
+            }
+            KT_HIP(launch_axpby((int)n, nc, eta, F, ld, 0.0, F, ld, st));  // f = eta f
+            copy_cols(ctx, n, F, ld, b.col(0), ld, nc);                    // b = f
+        }
+        int hstate[2] = {0, 0};  // {active, mv}
+        KT_HIP(hipMemcpyAsync(hstate, state, sizeof(hstate), hipMemcpyDeviceToHost, st));
+        KT_HIP(hipStreamSynchronize(st));
+        r.mv += hstate[1];
+        return r;
+    }
     for (int i = 0; i < r.s; ++i) {
         KT_HIP(launch_inf_norm((int)n, nc, b.col(0), ld, part, st));   // c1 = norm(b, inf)
         KT_HIP(launch_expmv_begin(part, nb, state, st));

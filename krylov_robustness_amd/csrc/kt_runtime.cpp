@@ -62,6 +62,10 @@ void DevCSR::release() {
     ck_beg = ck_end = sp_rows = sp_first = nullptr;
     n_chunks = n_split = 0;
     cap_ckb = cap_cke = cap_spr = cap_spf = 0;
+    if (med_rows) (void)hipFree(med_rows);
+    med_rows = nullptr;
+    n_med = 0;
+    cap_med = 0;
     rowptr = col = long_rows = perm = nullptr;
     val = nullptr;
     n_long = 0;
@@ -108,6 +112,11 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
     std::stable_sort(lr.begin(), lr.end(), [&](int32_t a, int32_t b) {
         return rp32[a + 1] - rp32[a] > rp32[b + 1] - rp32[b];
     });
+    std::vector<int32_t> mr;  // medium rows (expmv terms), row order
+    for (int64_t r = 0; r < n; ++r) {
+        const int32_t d = rp32[r + 1] - rp32[r];
+        if (d > kMedThresh && d <= A->long_thresh) mr.push_back((int32_t)r);
+    }
     // buffers may be reused: nothing of this context may still read them
     KT_HIP(hipStreamSynchronize(A->ctx->stream));
     for (hipStream_t st : A->ctx->aux_stream)
@@ -123,6 +132,10 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
         if (!lr.empty())
             KT_HIP(hipMemcpy(out.long_rows, lr.data(), sizeof(int) * lr.size(), hipMemcpyHostToDevice));
         out.n_long = (int)lr.size();
+        ensure_dev(out.med_rows, out.cap_med, std::max<size_t>(mr.size(), 1));
+        if (!mr.empty())
+            KT_HIP(hipMemcpy(out.med_rows, mr.data(), sizeof(int) * mr.size(), hipMemcpyHostToDevice));
+        out.n_med = (int)mr.size();
         // hub-row chunk table (block SpMM)
         std::vector<int32_t> ckb, cke, spr, spf(1, 0);
         for (int32_t r : lr) {  // heaviest first
