@@ -30,6 +30,26 @@ def test_expmv_matches_oracle(kra, gpu_ctx, name):
     np.testing.assert_allclose(F, Fo, rtol=1e-11, atol=1e-13 * np.abs(Fo).max())
 
 
+def test_expmv_wide_block_and_unfused_form(kra, gpu_ctx, monkeypatch):
+    """Blocks wider than 32 columns run the four-launch Taylor term (block SpMM
+    + combine + k_expmv_term + k_expmv_check); KT_EXPMV_UNFUSED=1 selects it
+    for narrow blocks too.  Both agree with the oracle and with the fused
+    k_expmv_step (same s, m, mv; 1e-13)."""
+    A = load_graph("oregon_A0")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    b = np.random.default_rng(3).normal(size=(A.shape[0], 40))
+    F, s, m, mv = kra.expmv(1.0, D, b, ctx=gpu_ctx)
+    Fo, so, mo, mvo = ko.expmv(1.0, A, b)
+    assert (s, m, mv) == (so, mo, mvo)
+    np.testing.assert_allclose(F, Fo, rtol=1e-11, atol=1e-13 * np.abs(Fo).max())
+    b3 = b[:, :3]
+    Ff, *rf = kra.expmv(1.0, D, b3, ctx=gpu_ctx)
+    monkeypatch.setenv("KT_EXPMV_UNFUSED", "1")
+    Fu, *ru = kra.expmv(1.0, D, b3, ctx=gpu_ctx)
+    assert rf == ru
+    np.testing.assert_allclose(Fu, Ff, rtol=1e-13, atol=1e-15 * np.abs(Ff).max())
+
+
 def test_lanczos_fmv_matches_oracle(kra, gpu_ctx):
     A = load_graph("rome")
     X = np.random.default_rng(2).normal(size=(A.shape[0], 4))
