@@ -76,8 +76,14 @@ def cpu_baseline(A, m, budget_s, nprobes_eval):
         if el >= budget_s or done >= nprobes_eval:
             break
     probes_per_s = done / el
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        pass
     return {"value": probes_per_s / nprobes_eval, "unit": "evals/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": model, "host_cpus": os.cpu_count(),
             "sample": f"{done} of the {nprobes_eval} probes of one evaluation (m={m}) in "
                       f"{el:.1f} s with {threads} OpenMP threads, extrapolated"}
 
