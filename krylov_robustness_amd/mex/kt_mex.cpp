@@ -28,6 +28,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <cmath>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -124,6 +127,125 @@ int fun_arg(const mxArray* h, int dflt) {
 
 mxArray* scalar(double v) { return mxCreateDoubleScalar(v); }
 
+// ---- mc_trace with a function-handle Afun --------------------------------
+// One MATLAB call with owned results (inputs borrowed).
+mxArray* call1(const char* fn, std::initializer_list<mxArray*> args) {
+    std::vector<mxArray*> in(args);
+    mxArray* out = nullptr;
+    if (mexCallMATLAB(1, &out, (int)in.size(), in.data(), fn) != 0)
+        mexErrMsgIdAndTxt("krylov_hip:mc_trace", "MATLAB call %s failed", fn);
+    return out;
+}
+
+// The matrix A captured by a handle of the form @(x) expmv(1, A, x, ...)
+// (trace_exp.m:5), or nullptr: func2str names the call, functions(h)
+// .workspace{1}.A holds the captured matrix.
+const mxArray* expmv_handle_matrix(const mxArray* h, mxArray** keep) {
+    mxArray* in = const_cast<mxArray*>(h);
+    mxArray* str = call1("func2str", {in});
+    char buf[128] = {0};
+    mxGetString(str, buf, sizeof(buf));
+    mxDestroyArray(str);
+    std::string f;
+    for (const char* c = buf; *c; ++c)
+        if (*c != ' ') f.push_back(*c);
+    if (f.rfind("@(x)expmv(1,A,x", 0) != 0) return nullptr;
+    mxArray* info = call1("functions", {in});
+    mxArray* ws = mxGetField(info, 0, "workspace");
+    const mxArray* A = nullptr;
+    if (ws && mxIsCell(ws) && mxGetNumberOfElements(ws) > 0) {
+        const mxArray* w0 = mxGetCell(ws, 0);
+        if (w0 && mxIsStruct(w0)) A = mxGetField(w0, 0, "A");
+    }
+    if (!A || !mxIsDouble(A) || mxIsComplex(A)) {
+        mxDestroyArray(info);
+        return nullptr;
+    }
+    *keep = info;  // A lives inside info
+    return A;
+}
+
+// Afun_k(x) = P_k(Afun_{k-1}(P_k x)), P_k x = x - Q_k (Q_k' x), Afun_0 = h
+// (mc_trace.m:47-48 nests one projector per round).  Returns an owned array.
+mxArray* apply_deflated(const mxArray* h, const std::vector<mxArray*>& Q, size_t k, mxArray* x) {
+    if (k == 0) return call1("feval", {const_cast<mxArray*>(h), x});
+    mxArray* Qt = call1("ctranspose", {Q[k - 1]});
+    auto proj = [&](mxArray* v) {
+        mxArray* c = call1("mtimes", {Qt, v});
+        mxArray* qc = call1("mtimes", {Q[k - 1], c});
+        mxArray* r = call1("minus", {v, qc});
+        mxDestroyArray(c);
+        mxDestroyArray(qc);
+        return r;
+    };
+    mxArray* px = proj(x);
+    mxArray* y = apply_deflated(h, Q, k - 1, px);
+    mxArray* py = proj(y);
+    mxDestroyArray(px);
+    mxDestroyArray(y);
+    mxDestroyArray(Qt);
+    return py;
+}
+
+// trace(X' * Y)
+double trace_xty(mxArray* X, mxArray* Y) {
+    mxArray* Xt = call1("ctranspose", {X});
+    mxArray* M = call1("mtimes", {Xt, Y});
+    mxArray* t = call1("trace", {M});
+    const double v = mxGetScalar(t);
+    mxDestroyArray(Xt);
+    mxDestroyArray(M);
+    mxDestroyArray(t);
+    return v;
+}
+
+// mc_trace.m:33-63 for a handle Afun nothing on the device can evaluate,
+// replayed with MATLAB's own built-ins (randn stream, qr, mtimes, trace),
+// so the result is the .m file's.  The MEX shadows mc_trace.m, which is why
+// the .m cannot simply be called back.
+void mc_trace_host(const mxArray* h, double n, double tol, int maxit, int isAreal, int debug,
+                   double* tr_out, double* res_out, int* it_out) {
+    const int m = 10;
+    const int K = (maxit + 3 * m - 1) / (3 * m);  // ceil(maxit / (3 m))
+    mxArray* nn = scalar(n);
+    mxArray* mm = scalar(m);
+    mxArray* zero = scalar(0);
+    std::vector<mxArray*> Q;
+    double tr = 0.0, tr_old = 0.0, tr_new = 0.0, res = 0.0;
+    int it = 0;
+    if (debug == 1) mexPrintf("------------- Trace estimation convergence history -------------\n");
+    for (it = 1; it <= K; ++it) {
+        mxArray* r1 = call1("randn", {nn, mm});
+        mxArray* S = call1("sign", {r1});
+        mxArray* r2 = call1("randn", {nn, mm});
+        mxArray* G = call1("sign", {r2});
+        mxArray* Y = apply_deflated(h, Q, Q.size(), S);
+        mxArray* qr_out[2] = {nullptr, nullptr};
+        mxArray* qr_in[2] = {Y, zero};
+        if (mexCallMATLAB(2, qr_out, 2, qr_in, "qr") != 0)
+            mexErrMsgIdAndTxt("krylov_hip:mc_trace", "MATLAB call qr failed");
+        mxArray* AQ = apply_deflated(h, Q, Q.size(), qr_out[0]);
+        tr += trace_xty(qr_out[0], AQ);
+        Q.push_back(qr_out[0]);
+        mxArray* AG = apply_deflated(h, Q, Q.size(), G);
+        tr_new = tr + trace_xty(G, AG) / m;
+        res = std::fabs(tr_new - tr_old) / std::max(std::fabs(tr_new), std::fabs(tr_old));
+        if (debug == 1)
+            mexPrintf("Number of quadrature pts: %d, Trace estimate: %1.4e, Error: %e\n", it * 3 * m, tr_new,
+                      res);
+        for (mxArray* a : {r1, S, r2, G, Y, qr_out[1], AQ, AG}) mxDestroyArray(a);
+        if (res < tol) break;
+        tr_old = tr_new;
+    }
+    if (it > K) it = K;
+    for (mxArray* q : Q) mxDestroyArray(q);
+    for (mxArray* a : {nn, mm, zero}) mxDestroyArray(a);
+    (void)isAreal;  // real arithmetic throughout: real(tr_new) == tr_new
+    *tr_out = tr_new;
+    *res_out = res;
+    *it_out = it;
+}
+
 // k x 2 MATLAB index matrix (1-based doubles) -> 0-based columns
 void pairs_arg(const mxArray* E, std::vector<int64_t>& a, std::vector<int64_t>& b) {
     const mwSize k = mxGetM(E);
@@ -178,14 +300,36 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     // [tr, res, it] = mc_trace(Afun, n, tol, maxit, isAreal, debug)   mc_trace.m:1
     // Afun: a matrix (mc_trace.m:32-34), or a handle @(x) expmv(1, A, x, ...)
     // whose matrix is passed by the caller through the workspace variable A.
+    // Afun: a matrix (mc_trace.m:32-34) -> device; the handle trace_exp.m:5
+    // builds, @(x) expmv(1, A, x, [], 'double') -> device expmv Afun on its
+    // captured A; any other handle -> mc_trace.m replayed with MATLAB's own
+    // built-ins (mc_trace_host).  Device paths draw the probes from the
+    // build's counter RNG (oracle/krylov_oracle.py:rademacher), the host
+    // replay from MATLAB's randn as the .m does.
     if (nrhs < 2) mexErrMsgIdAndTxt("krylov_hip:nargin", "mc_trace(Afun, n, ...)");
-    if (!mxIsDouble(prhs[0]))
-        mexErrMsgIdAndTxt("krylov_hip:Afun", "mc_trace MEX: Afun must be a matrix; keep mc_trace.m for handles");
+    const double tol = scalar_or(nrhs, prhs, 2, 1e-3);
+    const int maxit = (int)scalar_or(nrhs, prhs, 3, 10);
+    const int isAreal = (int)scalar_or(nrhs, prhs, 4, 0);
+    const int debug = (int)scalar_or(nrhs, prhs, 5, 0);
     double tr = 0.0, res = 0.0;
     int it = 0;
-    check(kt_mc_trace(matrix_arg(prhs[0]), KT_AFUN_MATRIX, KT_FUN_EXP, 0, scalar_or(nrhs, prhs, 2, 1e-3),
-                      (int)scalar_or(nrhs, prhs, 3, 10), (int)scalar_or(nrhs, prhs, 4, 0), 0, &tr, &res, &it),
-          "mc_trace");
+    if (mxIsDouble(prhs[0])) {
+        check(kt_mc_trace(matrix_arg(prhs[0]), KT_AFUN_MATRIX, KT_FUN_EXP, 0, tol, maxit, isAreal, 0, &tr, &res,
+                          &it),
+              "mc_trace");
+    } else if (mxIsClass(prhs[0], "function_handle")) {
+        mxArray* keep = nullptr;
+        const mxArray* A = expmv_handle_matrix(prhs[0], &keep);
+        if (A) {
+            check(kt_mc_trace(matrix_arg(A), KT_AFUN_EXPMV, KT_FUN_EXP, 0, tol, maxit, isAreal, 0, &tr, &res, &it),
+                  "mc_trace");
+            mxDestroyArray(keep);
+        } else {
+            mc_trace_host(prhs[0], mxGetScalar(prhs[1]), tol, maxit, isAreal, debug, &tr, &res, &it);
+        }
+    } else {
+        mexErrMsgIdAndTxt("krylov_hip:Afun", "mc_trace: Afun must be a matrix or a function handle");
+    }
     plhs[0] = scalar(tr);
     if (nlhs > 1) plhs[1] = scalar(res);
     if (nlhs > 2) plhs[2] = scalar(it);

@@ -25,6 +25,13 @@ mxArray* mxCreateSparse(mwSize, mwSize, mwSize, mxComplexity);
 double mxGetInf(void);
 void mxDestroyArray(mxArray*);
 int mexCallMATLAB(int, mxArray**, int, mxArray**, const char*);
+bool mxIsClass(const mxArray*, const char*);
+bool mxIsCell(const mxArray*);
+bool mxIsStruct(const mxArray*);
+size_t mxGetNumberOfElements(const mxArray*);
+mxArray* mxGetCell(const mxArray*, mwIndex);
+mxArray* mxGetField(const mxArray*, mwIndex, const char*);
+int mexPrintf(const char*, ...);
 void mexErrMsgIdAndTxt(const char*, const char*, ...);
 void mexWarnMsgIdAndTxt(const char*, const char*, ...);
 int mexAtExit(void (*)(void));
