@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sf1m", choices=["sf1m", "er100k"])
     ap.add_argument("--nprobes", type=int, default=None)
-    ap.add_argument("--m", type=int, default=30)
+    ap.add_argument("--m", "--lanczos-m", dest="m", type=int, default=30)
     ap.add_argument("--block", type=int, default=0, help="probes per SpMM sweep (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="CPU-baseline time budget (rank 0, N=1 only); 0 disables")
@@ -197,7 +197,9 @@ def main():
         if l1:
             k1_ms = ms1 / l1
             achieved = k1_bytes / (k1_ms * 1e-3) / 1e9
-            traffic = _pmc_traffic(kname)
+            # PMC bytes were profiled on the sf1m graph (tools/gpu_prof.sh); other
+            # graphs report traffic null
+            traffic = _pmc_traffic(kname) if args.config == "sf1m" else None
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": kname + ">", "avg_launch_us": round(k1_ms * 1e3, 2),

@@ -1,0 +1,57 @@
+"""GPU: bench.py keeps the driver's contract -- ONE JSON line on rank 0 with
+the metric, whole-job value, roofline (algorithmic + PMC-traffic rates of the
+dominant kernel) and cpu_baseline objects -- on a small configuration (the
+config-2 graph, 32 probes, m = 5), single process and two torchrun ranks
+sharing the GPU over gloo (the N > 1 launch the driver uses, rehearsed)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+SMALL = ["--config", "er100k", "--nprobes", "32", "--lanczos-m", "5", "--steps", "2", "--warmup", "1"]
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
+
+
+def _json_lines(out):
+    return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+
+
+def test_bench_single_process_line():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, "--cpu-seconds", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["value"] > 0 and d["higher_is_better"] is True and d["dtype"] == "f64"
+    assert d["value"] == pytest.approx(d["steps"] / (d["steps"] * d["ms_per_step"] * 1e-3), rel=1e-3)
+    roof = d["roofline"]
+    assert roof["bound"] == "hbm" and roof["unit"] == "GB/s" and roof["peak"] == 8000.0
+    assert roof["frac"] == pytest.approx(roof["achieved"] / roof["peak"], rel=1e-3)
+    assert roof["avg_launch_us"] > 0
+    cpu = d["cpu_baseline"]
+    assert cpu["kind"] == "port" and cpu["value"] > 0 and cpu["cores"] >= 1
+    assert d["yform_redone_sweeps"] == 0
+
+
+def test_bench_two_ranks_one_gpu_gloo():
+    env = dict(os.environ, KT_BENCH_ONE_DEVICE="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29531", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", *SMALL, "--dist-backend", "gloo", "--no-profile"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1  # rank 0 only
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "probes sharded x2"
+    assert d["cpu_baseline"] is None and d["value"] > 0
