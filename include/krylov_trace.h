@@ -103,6 +103,17 @@ int kt_normest(kt_matrix_t A, double tol, double* nrm);
 int kt_trace_fun_update(kt_matrix_t A, int64_t rk, const double* U, const double* B, double tol,
                         int it, int fun, double* Xm, int* iter, int* lucky);
 
+/* Elementwise scalar function for a function handle outside enum kt_fun:
+ * y[i] = f(x[i]), i < count; called on the host, on the calling thread. */
+typedef void (*kt_scalar_fn)(const double* x, double* y, int64_t count, void* user);
+
+/* trace_fun_update with an arbitrary elementwise handle (trace_fun_update.m:
+ * 85-89 `Xm = sum(fun(d1) - fun(d2))`; the same call as kt_trace_fun_update
+ * otherwise): f is applied to the two sorted eigenvalue vectors of each
+ * projected pair (tGm, Gm), or of A + UBU' and A on the dense path. */
+int kt_trace_fun_update_fn(kt_matrix_t A, int64_t rk, const double* U, const double* B, double tol,
+                           int it, kt_scalar_fn f, void* user, double* Xm, int* iter, int* lucky);
+
 /* [Xm, iter, lucky, Um] = fun_update(A, U, B, fun, tol, it, debug) with four
  * outputs (fun_update.m:1, Arnoldi branch :77-91): f(A+UBU') - f(A) ~= Um Xm Um'.
  * Xm is ncols x ncols (column-major, buffer of max_cols^2 doubles); Um (may be

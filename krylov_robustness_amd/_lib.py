@@ -42,6 +42,8 @@ _i64p = C.POINTER(C.c_int64)
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int)
 
+# kt_scalar_fn: y[i] = f(x[i]) for an elementwise handle outside kt_fun
+SCALAR_FN = C.CFUNCTYPE(None, _dp, _dp, C.c_int64, C.c_void_p)
 # kt_reduce_fn: in-place sum of `count` doubles across ranks; 0 = ok
 REDUCE_FN = C.CFUNCTYPE(C.c_int, _dp, C.c_int64, C.c_void_p)
 
@@ -61,6 +63,8 @@ SIGNATURES = [
     ("kt_normest", C.c_int, [_mat_p, C.c_double, _dp]),
     ("kt_trace_fun_update", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_double, C.c_int, C.c_int,
                                       _dp, _ip, _ip]),
+    ("kt_trace_fun_update_fn", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_double, C.c_int,
+                                         C.c_void_p, C.c_void_p, _dp, _ip, _ip]),
     ("kt_fun_update", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_int, C.c_double, C.c_int,
                                 C.c_int64, _dp, _i64p, _ip, _ip, _dp]),
     ("kt_fun_and_grad_krylov_exp", C.c_int, [_mat_p, C.c_int64, _dp, _dp, _dp, C.c_double, C.c_int,

@@ -235,9 +235,22 @@ def trace_fun_update(A, U, B, tol=1e-12, it=None, debug=0, fun="exp", ctx: Optio
     xm = C.c_double()
     itr = C.c_int()
     lk = C.c_int()
-    _lib.check(_lib.load().kt_trace_fun_update(
-        D.handle, U.shape[1], _dptr(U), _dptr(B), float(tol), int(it or 0), _fun_code(fun),
-        C.byref(xm), C.byref(itr), C.byref(lk)))
+    name = getattr(fun, "__name__", fun) if callable(fun) else fun
+    if callable(fun) and name not in _lib.FUN_CODES:
+        # any elementwise handle (trace_fun_update.m:88 sum(fun(d1) - fun(d2))):
+        # evaluated on the host eigenvalue vectors through kt_trace_fun_update_fn
+        def _f(x, y, count, user):
+            k = int(count)
+            xs = np.ctypeslib.as_array(x, shape=(k,))
+            np.ctypeslib.as_array(y, shape=(k,))[:] = np.asarray(fun(xs.copy()), dtype=np.float64)
+        cb = _lib.SCALAR_FN(_f)
+        _lib.check(_lib.load().kt_trace_fun_update_fn(
+            D.handle, U.shape[1], _dptr(U), _dptr(B), float(tol), int(it or 0),
+            C.cast(cb, C.c_void_p), None, C.byref(xm), C.byref(itr), C.byref(lk)))
+    else:
+        _lib.check(_lib.load().kt_trace_fun_update(
+            D.handle, U.shape[1], _dptr(U), _dptr(B), float(tol), int(it or 0), _fun_code(fun),
+            C.byref(xm), C.byref(itr), C.byref(lk)))
     its = int(it) if it else min(100, D.n)
     if lk.value and debug:  # trace_fun_update.m:119-124
         warnings.warn("TRACE_FUN_UPDATE:: Detected lucky breakdown")

@@ -233,9 +233,24 @@ static std::vector<double> sym_matfun(kt_context_s* ctx, int n, const std::vecto
     return F;
 }
 
+// The elementwise handle of kt_trace_fun_update_fn, for the duration of the call.
+struct ScalarFn {
+    kt_scalar_fn f = nullptr;
+    void* user = nullptr;
+};
+static thread_local ScalarFn tl_scalar_fn;
+
 // trace_fun_update.m:43-47 / :85-89 with d1, d2 ascending
 double trace_diff(const std::vector<double>& d1, const std::vector<double>& d2, int fun) {
     double x = 0.0;
+    if (fun == kFunCallback) {  // sum(fun(d1) - fun(d2))
+        if (!tl_scalar_fn.f) fail(KT_ERR_ARG, "no scalar function set");
+        std::vector<double> f1(d1.size()), f2(d2.size());
+        tl_scalar_fn.f(d1.data(), f1.data(), (int64_t)d1.size(), tl_scalar_fn.user);
+        tl_scalar_fn.f(d2.data(), f2.data(), (int64_t)d2.size(), tl_scalar_fn.user);
+        for (size_t i = 0; i < d1.size(); ++i) x += f1[i] - f2[i];
+        return x;
+    }
     if (fun == KT_FUN_EXP) {
         for (size_t i = 0; i < d1.size(); ++i) x += std::exp(d1[i]) * (1.0 - std::exp(d2[i] - d1[i]));
     } else {
@@ -889,6 +904,20 @@ int kt_trace_fun_update(kt_matrix_t A, int64_t rk, const double* U, const double
     if (fun < KT_FUN_EXP || fun > KT_FUN_SQRT) fail(KT_ERR_ARG, "unknown fun code");
     KT_HIP(hipSetDevice(A->ctx->device));
     *Xm = trace_fun_update_impl(A, (int)rk, U, B, tol, it, fun, iter, lucky);
+    KT_CATCH
+}
+
+int kt_trace_fun_update_fn(kt_matrix_t A, int64_t rk, const double* U, const double* B, double tol,
+                           int it, kt_scalar_fn f, void* user, double* Xm, int* iter, int* lucky) {
+    KT_TRY
+    if (!A || !U || !B || !Xm || !f || rk < 1) fail(KT_ERR_ARG, "NULL argument or empty U");
+    if (rk > 128) fail(KT_ERR_UNSUPPORTED, "rank > 128");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    struct Scope {  // the handle is visible to trace_diff for this call only
+        explicit Scope(ScalarFn s) { tl_scalar_fn = s; }
+        ~Scope() { tl_scalar_fn = ScalarFn{}; }
+    } scope(ScalarFn{f, user});
+    *Xm = trace_fun_update_impl(A, (int)rk, U, B, tol, it, kFunCallback, iter, lucky);
     KT_CATCH
 }
 

@@ -4,6 +4,8 @@
 
 namespace kt {
 
+// fun code of kt_trace_fun_update_fn: the caller's elementwise handle
+constexpr int kFunCallback = 100;
 // trace_fun_update.m:43-47 / :85-89 with d1, d2 ascending
 double trace_diff(const std::vector<double>& d1, const std::vector<double>& d2, int fun);
 // fails with KT_ERR_NOT_HERMITIAN and `msg` unless A is symmetric (cached)

@@ -108,8 +108,9 @@ double scalar_or(int nrhs, const mxArray* prhs[], int k, double dflt) {
     return (nrhs > k && !mxIsEmpty(prhs[k])) ? mxGetScalar(prhs[k]) : dflt;
 }
 
-// function_handle -> kt_fun via func2str (fun_update.m:43-59 identities).
-int fun_arg(const mxArray* h, int dflt) {
+// function_handle -> kt_fun via func2str (fun_update.m:43-59 identities);
+// -2 for any other handle when `generic` (callers that take a kt_scalar_fn).
+int fun_arg(const mxArray* h, int dflt, bool generic = false) {
     if (!h || mxIsEmpty(h)) return dflt;
     mxArray* out = nullptr;
     mxArray* in = const_cast<mxArray*>(h);
@@ -121,11 +122,34 @@ int fun_arg(const mxArray* h, int dflt) {
     static const char* names[] = {"exp", "sinh", "cosh", "sin", "cos", "log", "sqrt"};
     for (int i = 0; i < 7; ++i)
         if (strcmp(s, names[i]) == 0) return i;
+    if (generic) return -2;
     mexErrMsgIdAndTxt("krylov_hip:fun", "unsupported function handle %s (exp/sinh/cosh/sin/cos/log/sqrt)", buf);
     return -1;
 }
 
 mxArray* scalar(double v) { return mxCreateDoubleScalar(v); }
+
+// kt_scalar_fn over a MATLAB handle: y = feval(h, x) on a count x 1 column.
+// Runs inside the library call, so a failure is only recorded (NaN result)
+// and raised after the call returns: no MATLAB error unwinds library frames.
+bool g_feval_failed = false;
+void feval_scalar_fn(const double* x, double* y, int64_t count, void* user) {
+    mxArray* h = static_cast<mxArray*>(user);
+    mxArray* in = mxCreateDoubleMatrix((mwSize)count, 1, mxREAL);
+    memcpy(mxGetDoubles(in), x, sizeof(double) * (size_t)count);
+    mxArray* args[2] = {h, in};
+    mxArray* out = nullptr;
+    const bool ok = mexCallMATLAB(1, &out, 2, args, "feval") == 0 && out && mxIsDouble(out) &&
+                    !mxIsComplex(out) && mxGetNumberOfElements(out) == (size_t)count;
+    if (ok) {
+        memcpy(y, mxGetDoubles(out), sizeof(double) * (size_t)count);
+    } else {
+        g_feval_failed = true;
+        for (int64_t i = 0; i < count; ++i) y[i] = mxGetNaN();
+    }
+    mxDestroyArray(in);
+    if (out) mxDestroyArray(out);
+}
 
 // ---- mc_trace with a function-handle Afun --------------------------------
 // One MATLAB call with owned results (inputs borrowed).
@@ -342,10 +366,22 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     if (mxIsSparse(U) || mxIsSparse(B)) mexErrMsgIdAndTxt("krylov_hip:U", "U and B must be full");
     double xm = 0.0;
     int iter = 0, lucky = 0;
-    check(kt_trace_fun_update(A, (int64_t)mxGetN(U), mxGetDoubles(U), mxGetDoubles(B),
-                              scalar_or(nrhs, prhs, 3, 1e-12), (int)scalar_or(nrhs, prhs, 4, 0),
-                              fun_arg(nrhs > 6 ? prhs[6] : nullptr, KT_FUN_EXP), &xm, &iter, &lucky),
-          "trace_fun_update");
+    const mxArray* fh = nrhs > 6 ? prhs[6] : nullptr;
+    const int fcode = fun_arg(fh, KT_FUN_EXP, true);
+    if (fcode >= 0)
+        check(kt_trace_fun_update(A, (int64_t)mxGetN(U), mxGetDoubles(U), mxGetDoubles(B),
+                                  scalar_or(nrhs, prhs, 3, 1e-12), (int)scalar_or(nrhs, prhs, 4, 0), fcode,
+                                  &xm, &iter, &lucky),
+              "trace_fun_update");
+    else {  // any elementwise handle: sum(fun(d1) - fun(d2)) with fun evaluated by MATLAB (:88)
+        g_feval_failed = false;
+        check(kt_trace_fun_update_fn(A, (int64_t)mxGetN(U), mxGetDoubles(U), mxGetDoubles(B),
+                                     scalar_or(nrhs, prhs, 3, 1e-12), (int)scalar_or(nrhs, prhs, 4, 0),
+                                     feval_scalar_fn, const_cast<mxArray*>(fh), &xm, &iter, &lucky),
+              "trace_fun_update");
+        if (g_feval_failed)
+            mexErrMsgIdAndTxt("krylov_hip:fun", "fun must map a real double vector elementwise");
+    }
     {  // warnings stay warnings (trace_fun_update.m:119-130)
         const int it_arg = (int)scalar_or(nrhs, prhs, 4, 0);
         const int it_eff = it_arg > 0 ? it_arg : (int)(mxGetM(prhs[0]) < 100 ? mxGetM(prhs[0]) : 100);

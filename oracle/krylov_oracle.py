@@ -76,7 +76,11 @@ _SCALAR = {"exp": np.exp, "sinh": np.sinh, "cosh": np.cosh, "sin": np.sin,
            "cos": np.cos, "log": np.log, "sqrt": np.sqrt}
 
 
-def scalar_fun(name: str):
+def scalar_fun(name):
+    """A fun_update.m:43-59 name, or any elementwise callable (a generic
+    handle, trace_fun_update.m:88)."""
+    if callable(name):
+        return name
     return _SCALAR[name]
 
 
@@ -238,7 +242,7 @@ def arnoldi_krylov_extend(st: ArnoldiState) -> ArnoldiState:
 # ---------------------------------------------------------------------------
 def _trace_diff(d1, d2, fun):
     """trace_fun_update.m:43-47 / :85-89."""
-    if fun == "exp":
+    if isinstance(fun, str) and fun == "exp":
         return float(np.sum(np.exp(d1) * (1 - np.exp(d2 - d1))))
     f = scalar_fun(fun)
     return float(np.sum(f(d1) - f(d2)))

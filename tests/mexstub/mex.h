@@ -23,6 +23,7 @@ mxArray* mxCreateDoubleMatrix(mwSize, mwSize, mxComplexity);
 mxArray* mxCreateDoubleScalar(double);
 mxArray* mxCreateSparse(mwSize, mwSize, mwSize, mxComplexity);
 double mxGetInf(void);
+double mxGetNaN(void);
 void mxDestroyArray(mxArray*);
 int mexCallMATLAB(int, mxArray**, int, mxArray**, const char*);
 bool mxIsClass(const mxArray*, const char*);

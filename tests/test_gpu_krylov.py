@@ -61,6 +61,35 @@ def test_trace_fun_update_dense_shortcut(kra, gpu_ctx):
         assert xm == pytest.approx(ko.exact_trace_update(A, U, B, fun), rel=1e-11)
 
 
+def test_trace_fun_update_generic_handle(kra, gpu_ctx, values):
+    """A handle outside fun_update.m's list (trace_fun_update.m:88,
+    sum(fun(d1) - fun(d2))) goes through kt_trace_fun_update_fn: the Lanczos
+    path (rome) and the dense shortcut (denmark) vs the oracle with the same
+    callable and vs the exact update; a renamed sinh equals fun='sinh'."""
+    f = lambda x: np.tanh(x) + 0.1 * x ** 3  # noqa: E731
+    A = load_graph("rome")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    n = A.shape[0]
+    i, j = values["rome"]["trace_fun_update_break"][0]["edge"]
+    U = np.zeros((n, 2)); U[i - 1, 0] = 1; U[j - 1, 1] = 1
+    B = -np.array([[0.0, 1.0], [1.0, 0.0]])
+    xm, it, lucky = kra.trace_fun_update(D, U, B, 1e-12, min(100, n), fun=f, ctx=gpu_ctx)
+    xo, ito, _ = ko.trace_fun_update(A, U, B, 1e-12, min(100, n), 0, f)
+    assert it == ito
+    assert xm == pytest.approx(xo, rel=1e-9, abs=1e-11)
+    assert xm == pytest.approx(ko.exact_trace_update(A, U, B, f), rel=1e-8, abs=1e-10)
+    sinh_like = lambda x: np.sinh(x)  # noqa: E731
+    xs, _, _ = kra.trace_fun_update(D, U, B, 1e-12, min(100, n), fun=sinh_like, ctx=gpu_ctx)
+    xr, _, _ = kra.trace_fun_update(D, U, B, 1e-12, min(100, n), fun="sinh", ctx=gpu_ctx)
+    assert xs == pytest.approx(xr, rel=1e-12)
+    Ad = load_graph("denmark")
+    nd = Ad.shape[0]
+    Ud = np.zeros((nd, 2)); Ud[3, 0] = 1; Ud[7, 1] = 1
+    xd, itd, _ = kra.trace_fun_update(kra.DeviceMatrix(Ad, gpu_ctx), Ud, B, fun=f, ctx=gpu_ctx)
+    assert itd == 0
+    assert xd == pytest.approx(ko.exact_trace_update(Ad, Ud, B, f), rel=1e-11)
+
+
 def test_trace_fun_update_rank6_sinh(kra, gpu_ctx):
     A = load_graph("india")
     n = A.shape[0]
