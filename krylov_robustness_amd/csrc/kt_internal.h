@@ -177,6 +177,13 @@ struct kt_matrix_s {
     std::vector<int64_t> h_rowptr;
     std::vector<int32_t> h_col;
     std::vector<double> h_val;
+    uint64_t version = 0;  // bumped when the host copy is edited (refresh_device)
+    // twin: a second context (own stream + workspace) holding another device
+    // copy of this matrix, built on first use, so that two independent Krylov
+    // runs of one call overlap (fun_and_grad_krylov_fun.m:64-65)
+    kt_context_s* twin_ctx = nullptr;
+    kt_matrix_s* twin = nullptr;
+    uint64_t twin_version = 0;
 };
 
 namespace kt {

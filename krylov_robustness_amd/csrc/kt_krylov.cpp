@@ -983,6 +983,30 @@ int kt_fun_and_grad_krylov_exp(kt_matrix_t A, int64_t nom, const double* X, cons
     KT_CATCH
 }
 
+// Second device copy of A on its own context (stream + workspace), rebuilt
+// when A was edited since; nullptr when KT_FG_SERIAL=1.
+static kt_matrix_s* twin_of(kt_matrix_s* A) {
+    static const bool serial = getenv("KT_FG_SERIAL") && getenv("KT_FG_SERIAL")[0] == '1';
+    if (serial) return nullptr;
+    if (A->twin && A->twin_version == A->version) return A->twin;
+    if (A->twin) {
+        kt_matrix_destroy(A->twin);
+        A->twin = nullptr;
+    }
+    if (!A->twin_ctx && kt_context_create(A->ctx->device, &A->twin_ctx) != KT_OK)
+        fail(KT_ERR_HIP, std::string("twin context: ") + kt_last_error());
+    const int64_t n = A->n;
+    std::vector<int64_t> ir(A->h_col.begin(), A->h_col.end());
+    if (kt_matrix_create_csc(A->twin_ctx, n, A->h_rowptr.data(), ir.data(), A->h_val.data(), 0, &A->twin) !=
+        KT_OK)
+        fail(KT_ERR_HIP, std::string("twin matrix: ") + kt_last_error());
+    A->twin->symmetric = A->symmetric;
+    A->twin->long_thresh = A->long_thresh;
+    A->twin_version = A->version;
+    KT_HIP(hipSetDevice(A->ctx->device));
+    return A->twin;
+}
+
 int kt_fun_and_grad_krylov_fun(kt_matrix_t A, int64_t nom, const double* X, const double* Omega,
                                int fun, int dfun, const double* dfA, double tol, int it, double* f,
                                double* gr) {
@@ -1004,9 +1028,39 @@ int kt_fun_and_grad_krylov_fun(kt_matrix_t A, int64_t nom, const double* X, cons
     std::vector<double> U, B;
     lowrank_from_edges(A->n, nom, X, Omega, aux, U, B);
     const int k = (int)aux.size();
-    FunUpdateResult fu = fun_update_impl(A, k, U.data(), B.data(), dfun, tol * fscalar(dfun, nrmA), it);  // :64
-    *f = -trace_fun_update_impl(A, k, U.data(), B.data(), tol * fscalar(fun, nrmA), it, fun, nullptr,
-                                nullptr);                                                   // :65
+    // :64 and :65 are independent Krylov runs on the same A: trace_fun_update
+    // runs on the twin context (own stream) on a second host thread while
+    // fun_update runs here, so their kernels and host eigensolves overlap.
+    const double tol_f = tol * fscalar(fun, nrmA), tol_df = tol * fscalar(dfun, nrmA);
+    kt_matrix_s* A2 = twin_of(A);
+    double fval = 0.0;
+    Status terr{KT_OK, ""};
+    std::thread th;
+    if (A2)
+        th = std::thread([&] {
+            try {
+                KT_HIP(hipSetDevice(A2->ctx->device));
+                fval = trace_fun_update_impl(A2, k, U.data(), B.data(), tol_f, it, fun, nullptr, nullptr);
+            } catch (const Status& s) {
+                terr = s;
+            } catch (...) {
+                terr = Status{KT_ERR_HIP, "trace_fun_update (twin) failed"};
+            }
+        });
+    struct Join {
+        std::thread& t;
+        ~Join() {
+            if (t.joinable()) t.join();
+        }
+    } join{th};
+    FunUpdateResult fu = fun_update_impl(A, k, U.data(), B.data(), dfun, tol_df, it);          // :64
+    if (A2) {
+        th.join();
+        if (terr.code != KT_OK) throw terr;
+    } else {
+        fval = trace_fun_update_impl(A, k, U.data(), B.data(), tol_f, it, fun, nullptr, nullptr);  // :65
+    }
+    *f = -fval;
     gradient(A, fu, nom, Omega, dfA, gr);                                                   // :67-70
     KT_CATCH
 }

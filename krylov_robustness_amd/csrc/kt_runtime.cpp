@@ -176,6 +176,7 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
 void refresh_device(kt_matrix_s* A) {
     A->hub.invalidate();
     A->nat.invalidate();
+    A->version++;  // a twin copy (kt_krylov.cpp) is now stale
     A->unit_values = std::all_of(A->h_val.begin(), A->h_val.end(), [](double v) { return v == 1.0; });
     const char* un = getenv("KT_UNIT");
     if (un && un[0] == '0') A->unit_values = false;
@@ -369,6 +370,9 @@ int kt_matrix_destroy(kt_matrix_t A) {
     if (!A) return KT_OK;
     (void)hipSetDevice(A->ctx->device);
     (void)hipStreamSynchronize(A->ctx->stream);
+    if (A->twin) kt_matrix_destroy(A->twin);
+    if (A->twin_ctx) kt_context_destroy(A->twin_ctx);
+    (void)hipSetDevice(A->ctx->device);
     A->hub.release();
     A->nat.release();
     delete A;

@@ -180,6 +180,14 @@ def test_fun_and_grad_fun_matches_oracle(kra, gpu_ctx, fun, dfun):
     fo, gro = ko.fun_and_grad_krylov_fun(X, A, Om, fun, dfun, dfA, tol, 100)
     assert f == pytest.approx(fo, rel=1e-7)
     np.testing.assert_allclose(gr, gro, rtol=1e-7, atol=1e-10)
+    # f comes from trace_fun_update on the matrix's twin context (second
+    # stream, overlapped with fun_update): bit-identical to the plain call
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    U, B = ko.lowrank_from_edges(X, Om, A.shape[0])
+    nrm_d = kra.normest(D, 1e-2, ctx=gpu_ctx)
+    f2, _ = kra.fun_and_grad_krylov_fun(X, D, Om, fun, dfun, dfA, tol, 100, ctx=gpu_ctx)
+    xm, _, _ = kra.trace_fun_update(D, U, B, tol * ko.scalar_fun(fun)(nrm_d), 100, fun=fun, ctx=gpu_ctx)
+    assert f2 == -xm
 
 
 def test_trace_fun_update_leaf_candidates(kra, gpu_ctx):
