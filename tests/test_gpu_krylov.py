@@ -190,6 +190,33 @@ def test_fun_and_grad_fun_matches_oracle(kra, gpu_ctx, fun, dfun):
     assert f2 == -xm
 
 
+def test_fun_and_grad_fun_after_edge_edit(kra, gpu_ctx):
+    """The twin device copy that fun_and_grad_krylov_fun's trace_fun_update
+    runs on is rebuilt after an edge edit of the matrix (kt_matrix_set_pairs):
+    the edited DeviceMatrix gives what a fresh upload of the edited A gives."""
+    A = load_graph("india")
+    Om = edges(A, 5, offset=100)
+    rng = np.random.default_rng(7)
+    X = rng.uniform(-0.5, 1.0, 5)
+    dfA = rng.normal(size=5)
+    tol = 1e-6 * np.sinh(ko.normest(A, 1e-2))
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    f0, _ = kra.fun_and_grad_krylov_fun(X, D, Om, "sinh", "cosh", dfA, tol, 100, ctx=gpu_ctx)
+    cut = edges(A, 1, offset=400)
+    D.set_pairs(cut, 0.0)
+    f1, g1 = kra.fun_and_grad_krylov_fun(X, D, Om, "sinh", "cosh", dfA, tol, 100, ctx=gpu_ctx)
+    A1 = A.tolil()
+    A1[cut[0, 0] - 1, cut[0, 1] - 1] = 0
+    A1[cut[0, 1] - 1, cut[0, 0] - 1] = 0
+    A1 = A1.tocsr()
+    A1.eliminate_zeros()
+    f2, g2 = kra.fun_and_grad_krylov_fun(X, kra.DeviceMatrix(A1, gpu_ctx), Om, "sinh", "cosh", dfA, tol, 100,
+                                         ctx=gpu_ctx)
+    assert f1 != f0
+    assert f1 == pytest.approx(f2, rel=1e-12)
+    np.testing.assert_allclose(g1, g2, rtol=1e-12, atol=1e-14)
+
+
 def test_trace_fun_update_leaf_candidates(kra, gpu_ctx):
     """Break candidates at leaf nodes of the India grid (krylov_miobi.m:77-99):
     A*U has an exactly dependent column after CGS2, so qr(w, 0) completes the
