@@ -399,6 +399,10 @@ void set_entry(kt_matrix_s* A, int64_t r, int32_t col, double value) {
 
 }  // namespace
 
+static void run_pairs_range(kt_matrix_s* A, const std::vector<int64_t>& pairs, size_t p0, size_t p1,
+                            const int64_t* ei, const int64_t* ej, const double* B, double tol, int it,
+                            int fun, double* Xm, int* iter, int* lucky);
+
 void trace_fun_update_pairs(kt_matrix_s* A, int64_t nC, const int64_t* ei, const int64_t* ej,
                             const double* B, double B1, double tol, int it, int fun, double* Xm,
                             int* iter, int* lucky) {
@@ -424,9 +428,20 @@ void trace_fun_update_pairs(kt_matrix_s* A, int64_t nC, const int64_t* ei, const
     }
     if (pairs.empty()) return;
     if (B[1] != B[2]) fail(KT_ERR_UNSUPPORTED, "trace_fun_update: non-Hermitian B (needs a general eig)");
+    // One batch sequence on A's own stream.  Splitting the candidates over A
+    // and its twin (second stream + host thread) was measured slower: config
+    // 5 47 -> 60 ms (profiles/r01_greedy_twin_split.txt) -- each half keeps
+    // every launch of a Lanczos step, so the launch count doubles.
+    run_pairs_range(A, pairs, 0, pairs.size(), ei, ej, B, tol, it, fun, Xm, iter, lucky);
+}
+
+// candidates pairs[p0, p1) in device batches of <= kMaxPairs
+static void run_pairs_range(kt_matrix_s* A, const std::vector<int64_t>& pairs, size_t p0, size_t p1,
+                            const int64_t* ei, const int64_t* ej, const double* B, double tol, int it,
+                            int fun, double* Xm, int* iter, int* lucky) {
     (void)natural_csr(A);
-    for (size_t b0 = 0; b0 < pairs.size(); b0 += kMaxPairs) {
-        const int C = (int)std::min<size_t>(kMaxPairs, pairs.size() - b0);
+    for (size_t b0 = p0; b0 < p1; b0 += kMaxPairs) {
+        const int C = (int)std::min<size_t>(kMaxPairs, p1 - b0);
         std::vector<int64_t> bi(C), bj(C);
         std::vector<double> xm(C);
         std::vector<int> itv(C), lv(C);
@@ -453,7 +468,13 @@ void set_pairs(kt_matrix_s* A, int64_t count, const int64_t* ei, const int64_t* 
         set_entry(A, ei[t], (int32_t)ej[t], value);
         if (ei[t] != ej[t]) set_entry(A, ej[t], (int32_t)ei[t], value);
     }
+    const bool twin_current = A->twin && A->twin_version == A->version;
     refresh_device(A);
+    if (twin_current) {  // the same edit on the twin copy instead of a rebuild
+        set_pairs(A->twin, count, ei, ej, value);
+        A->twin_version = A->version;
+        KT_HIP(hipSetDevice(A->ctx->device));
+    }
 }
 
 }  // namespace kt

@@ -847,6 +847,30 @@ static void gradient(kt_matrix_s* A, FunUpdateResult& fu, int64_t nom, const dou
     }
 }
 
+// Second device copy of A on its own context (stream + workspace), rebuilt
+// when A was edited since (set_pairs keeps it current); nullptr when KT_TWIN=0.
+kt_matrix_s* twin_of(kt_matrix_s* A) {
+    static const bool off = getenv("KT_TWIN") && getenv("KT_TWIN")[0] == '0';
+    if (off) return nullptr;
+    if (A->twin && A->twin_version == A->version) return A->twin;
+    if (A->twin) {
+        kt_matrix_destroy(A->twin);
+        A->twin = nullptr;
+    }
+    if (!A->twin_ctx && kt_context_create(A->ctx->device, &A->twin_ctx) != KT_OK)
+        fail(KT_ERR_HIP, std::string("twin context: ") + kt_last_error());
+    const int64_t n = A->n;
+    std::vector<int64_t> ir(A->h_col.begin(), A->h_col.end());
+    if (kt_matrix_create_csc(A->twin_ctx, n, A->h_rowptr.data(), ir.data(), A->h_val.data(), 0, &A->twin) !=
+        KT_OK)
+        fail(KT_ERR_HIP, std::string("twin matrix: ") + kt_last_error());
+    A->twin->symmetric = A->symmetric;
+    A->twin->long_thresh = A->long_thresh;
+    A->twin_version = A->version;
+    KT_HIP(hipSetDevice(A->ctx->device));
+    return A->twin;
+}
+
 }  // namespace kt
 
 using namespace kt;
@@ -981,30 +1005,6 @@ int kt_fun_and_grad_krylov_exp(kt_matrix_t A, int64_t nom, const double* X, cons
     *f = -tr;                                                                 // :84
     gradient(A, fu, nom, Omega, eA, gr);                                      // :85-88
     KT_CATCH
-}
-
-// Second device copy of A on its own context (stream + workspace), rebuilt
-// when A was edited since; nullptr when KT_FG_SERIAL=1.
-static kt_matrix_s* twin_of(kt_matrix_s* A) {
-    static const bool serial = getenv("KT_FG_SERIAL") && getenv("KT_FG_SERIAL")[0] == '1';
-    if (serial) return nullptr;
-    if (A->twin && A->twin_version == A->version) return A->twin;
-    if (A->twin) {
-        kt_matrix_destroy(A->twin);
-        A->twin = nullptr;
-    }
-    if (!A->twin_ctx && kt_context_create(A->ctx->device, &A->twin_ctx) != KT_OK)
-        fail(KT_ERR_HIP, std::string("twin context: ") + kt_last_error());
-    const int64_t n = A->n;
-    std::vector<int64_t> ir(A->h_col.begin(), A->h_col.end());
-    if (kt_matrix_create_csc(A->twin_ctx, n, A->h_rowptr.data(), ir.data(), A->h_val.data(), 0, &A->twin) !=
-        KT_OK)
-        fail(KT_ERR_HIP, std::string("twin matrix: ") + kt_last_error());
-    A->twin->symmetric = A->symmetric;
-    A->twin->long_thresh = A->long_thresh;
-    A->twin_version = A->version;
-    KT_HIP(hipSetDevice(A->ctx->device));
-    return A->twin;
 }
 
 int kt_fun_and_grad_krylov_fun(kt_matrix_t A, int64_t nom, const double* X, const double* Omega,

@@ -21,6 +21,11 @@ void trace_fun_update_pairs(kt_matrix_s* A, int64_t nC, const int64_t* ei, const
                             const double* B, double B1, double tol, int it, int fun, double* Xm,
                             int* iter, int* lucky);
 
+// A's twin: a second device copy on its own context (stream, workspace),
+// built on first use and kept current through edits; nullptr when KT_TWIN=0.
+// Lets two independent Krylov runs of one call overlap on the GPU.
+kt_matrix_s* twin_of(kt_matrix_s* A);
+
 // set A(i,j) = A(j,i) = value for each pair (0 deletes the entry, as MATLAB
 // sparse assignment does) on the host copy and refresh the device copies.
 void set_pairs(kt_matrix_s* A, int64_t count, const int64_t* ei, const int64_t* ej, double value);
