@@ -168,18 +168,38 @@ void upload_rows(kt_matrix_s* A, const double* H, int cols, double* D, int ldd) 
     KT_HIP(hipStreamSynchronize(A->ctx->stream));
 }
 
+void download_elems(kt_context_s* ctx, const double* D, const std::vector<int64_t>& off,
+                    std::vector<double>& out) {
+    const size_t m = off.size();
+    out.assign(m, 0.0);
+    if (m == 0) return;
+    DevBuf& d = ctx->ws.qrtmp;
+    const size_t idx_bytes = (sizeof(int64_t) * m + 255) / 256 * 256;
+    d.ensure(idx_bytes + sizeof(double) * m);
+    int64_t* doff = d.as<int64_t>();
+    double* dout = reinterpret_cast<double*>(static_cast<char*>(d.ptr) + idx_bytes);
+    KT_HIP(hipMemcpyAsync(doff, off.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, ctx->stream));
+    KT_HIP(launch_gather_elems((int64_t)m, D, doff, dout, ctx->stream));
+    KT_HIP(hipMemcpyAsync(out.data(), dout, sizeof(double) * m, hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipStreamSynchronize(ctx->stream));
+}
+
 void download_rows(kt_matrix_s* A, const double* D, int ldd, int cols,
                    const std::vector<int64_t>& rows, std::vector<double>& out) {
     const int nr = (int)rows.size();
     out.assign((size_t)nr * cols, 0.0);
-    std::vector<double> row(cols);
-    for (int r = 0; r < nr; ++r) {
-        const int64_t dr = rows[r];
-        KT_HIP(hipMemcpyAsync(row.data(), D + (size_t)dr * ldd, sizeof(double) * cols,
-                              hipMemcpyDeviceToHost, A->ctx->stream));
-        KT_HIP(hipStreamSynchronize(A->ctx->stream));
-        for (int c = 0; c < cols; ++c) out[(size_t)c * nr + r] = row[c];
-    }
+    if (nr == 0 || cols == 0) return;
+    // one gather kernel + one copy (a copy and a sync per row cost ~40 us each)
+    kt_context_s* ctx = A->ctx;
+    DevBuf& d = ctx->ws.qrtmp;
+    const size_t idx_bytes = (sizeof(int64_t) * nr + 255) / 256 * 256;
+    d.ensure(idx_bytes + sizeof(double) * (size_t)nr * cols);
+    int64_t* drows = d.as<int64_t>();
+    double* dout = reinterpret_cast<double*>(static_cast<char*>(d.ptr) + idx_bytes);
+    KT_HIP(hipMemcpyAsync(drows, rows.data(), sizeof(int64_t) * nr, hipMemcpyHostToDevice, ctx->stream));
+    KT_HIP(launch_gather_rows(nr, cols, D, ldd, drows, dout, ctx->stream));
+    KT_HIP(hipMemcpyAsync(out.data(), dout, sizeof(double) * out.size(), hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipStreamSynchronize(ctx->stream));
 }
 
 void download_block(kt_matrix_s* A, const double* D, int ldd, int cols, double* out) {

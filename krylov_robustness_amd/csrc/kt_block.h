@@ -45,6 +45,9 @@ void zero_cols(kt_context_s* ctx, int64_t n, double* X, int ldx, int cols);
 // host column-major -> device row-major
 void upload_rows(kt_matrix_s* A, const double* H, int cols, double* D, int ldd);
 // device rows (row indices) -> host nrows x cols column-major
+// host out[i] = device D[off[i]] (one upload, one gather launch, one download)
+void download_elems(kt_context_s* ctx, const double* D, const std::vector<int64_t>& off,
+                    std::vector<double>& out);
 void download_rows(kt_matrix_s* A, const double* D, int ldd, int cols,
                    const std::vector<int64_t>& rows, std::vector<double>& out);
 // whole device block (n x cols at ldd) -> host column-major n x cols

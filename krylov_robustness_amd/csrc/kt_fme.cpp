@@ -52,11 +52,9 @@ ColArnoldi::ColArnoldi(kt_matrix_s* A, const std::vector<int64_t>& starts, int i
                           ctx_->stream));
     KT_HIP(launch_col_select(C_, P_, idx_.as<int>(), V, ctx_->stream));
     start_qr();
-    uaux_.assign(C_, 0.0);
-    for (int c = 0; c < C_; ++c)
-        KT_HIP(hipMemcpyAsync(&uaux_[c], V + starts[c] * P_ + c, sizeof(double),
-                              hipMemcpyDeviceToHost, ctx_->stream));
-    KT_HIP(hipStreamSynchronize(ctx_->stream));
+    std::vector<int64_t> off(C_);
+    for (int c = 0; c < C_; ++c) off[c] = starts[c] * P_ + c;
+    download_elems(ctx_, V, off, uaux_);
 }
 
 ColArnoldi::ColArnoldi(kt_matrix_s* A, const double* X, int C, int it)
@@ -141,17 +139,13 @@ void ColArnoldi::gm(int c, std::vector<double>& G) const {
 }
 
 void ColArnoldi::rows(const std::vector<int64_t>& rr, int nk, std::vector<double>& out) const {
-    out.assign(rr.size() * (size_t)nk * C_, 0.0);
-    std::vector<double> buf((size_t)nk * P_);
-    const double* V = static_cast<const double*>(basis_.ptr);
-    for (size_t ri = 0; ri < rr.size(); ++ri) {
-        KT_HIP(hipMemcpy2DAsync(buf.data(), sizeof(double) * P_, V + rr[ri] * P_,
-                                sizeof(double) * vs_, sizeof(double) * P_, (size_t)nk,
-                                hipMemcpyDeviceToHost, ctx_->stream));
-        KT_HIP(hipStreamSynchronize(ctx_->stream));
+    // one gather of every (row, block, column) element instead of a copy and
+    // a sync per row
+    std::vector<int64_t> off(rr.size() * (size_t)nk * C_);
+    for (size_t ri = 0; ri < rr.size(); ++ri)
         for (int k = 0; k < nk; ++k)
-            for (int c = 0; c < C_; ++c) out[(ri * nk + k) * C_ + c] = buf[(size_t)k * P_ + c];
-    }
+            for (int c = 0; c < C_; ++c) off[(ri * nk + k) * C_ + c] = rr[ri] * P_ + (int64_t)k * vs_ + c;
+    download_elems(ctx_, static_cast<const double*>(basis_.ptr), off, out);
 }
 
 void sym_eig_small(int j, const std::vector<double>& G, std::vector<double>& w,

@@ -1090,6 +1090,28 @@ __global__ void k_fill(double* __restrict__ x, int count, double v) {
     if (t < count) x[t] = v;
 }
 
+// out (nr x cols, column-major) = rows[r] of the row-major block D (ldd)
+__global__ __launch_bounds__(256) void k_gather_rows(int nr, int cols, const double* __restrict__ D,
+                                                     int ldd, const int64_t* __restrict__ rows,
+                                                     double* __restrict__ out) {
+    const int64_t total = (int64_t)nr * cols;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int r = (int)(t % nr);
+        const int c = (int)(t / nr);
+        out[t] = D[rows[r] * ldd + c];
+    }
+}
+
+// out[i] = D[off[i]]: scattered elements of a device array in one launch
+__global__ __launch_bounds__(256) void k_gather_elems(int64_t count, const double* __restrict__ D,
+                                                      const int64_t* __restrict__ off,
+                                                      double* __restrict__ out) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count;
+         t += (int64_t)gridDim.x * blockDim.x)
+        out[t] = D[off[t]];
+}
+
 // ---------------------------------------------------------------------------
 // expmv.m:71-92 Taylor loop with its stop test on the device, so the host
 // queues a whole stage without a round trip per term.  State (ExpmvState):
@@ -1683,6 +1705,19 @@ hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_
     return hipGetLastError();
 }
 
+
+hipError_t launch_gather_rows(int nr, int cols, const double* D, int ldd, const int64_t* rows, double* out,
+                              hipStream_t st) {
+    k_gather_rows<<<stream_grid((int64_t)nr * cols), 256, 0, st>>>(nr, cols, D, ldd, rows, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_elems(int64_t count, const double* D, const int64_t* off, double* out,
+                               hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    k_gather_elems<<<stream_grid(count), 256, 0, st>>>(count, D, off, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st) {
     int grid = (count + 255) / 256;

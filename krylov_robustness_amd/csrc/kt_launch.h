@@ -61,6 +61,12 @@ hipError_t launch_ycoef(int P, const double* partial, int nblk, int start, int l
                         double* ys, double* t_alpha, double* t_up, double* t_low, double* guard,
                         hipStream_t st);
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st);
+// out[i] = D[off[i]], i < count
+hipError_t launch_gather_elems(int64_t count, const double* D, const int64_t* off, double* out,
+                               hipStream_t st);
+// out (nr x cols, column-major) = rows[r] of the row-major block D (leading dimension ldd)
+hipError_t launch_gather_rows(int nr, int cols, const double* D, int ldd, const int64_t* rows, double* out,
+                              hipStream_t st);
 hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int ldu,
                                const double* W, double* Y, int ldy, hipStream_t st);
 hipError_t launch_axpby(int n, int nc, double a, const double* X, int ldx, double b, double* Y,
