@@ -178,6 +178,10 @@ struct kt_matrix_s {
     std::vector<int32_t> h_col;
     std::vector<double> h_val;
     uint64_t version = 0;  // bumped when the host copy is edited (refresh_device)
+    // last normest(A, tol) (kt_krylov.cpp normest_impl), valid for `normest_version`
+    bool normest_ok = false;
+    uint64_t normest_version = 0;
+    double normest_tol = 0.0, normest_val = 0.0;
     // twin: a second context (own stream + workspace) holding another device
     // copy of this matrix, built on first use, so that two independent Krylov
     // runs of one call overlap (fun_and_grad_krylov_fun.m:64-65)

@@ -757,7 +757,23 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
 
 // MATLAB normest (2-norm power estimate) on the device: x = sum(abs(A))',
 // repeat x = A'(A x)/||.|| until |e - e0| <= tol e.
+static double normest_compute(kt_matrix_s* A, double tol);
+
+// MATLAB normest is a deterministic function of (A, tol); the fmincon loops
+// call fun_and_grad_* (fun_and_grad_krylov_exp.m:26, _fun.m:27) with the same
+// A and tol every iteration, so the estimate is kept with the matrix (until an
+// edit bumps its version): the same value without a dozen host round trips.
 double normest_impl(kt_matrix_s* A, double tol) {
+    if (A->normest_ok && A->normest_version == A->version && A->normest_tol == tol) return A->normest_val;
+    const double e = normest_compute(A, tol);
+    A->normest_ok = true;
+    A->normest_version = A->version;
+    A->normest_tol = tol;
+    A->normest_val = e;
+    return e;
+}
+
+static double normest_compute(kt_matrix_s* A, double tol) {
     kt_context_s* ctx = A->ctx;
     const int64_t n = A->n;
     if (n == 0) return 0.0;

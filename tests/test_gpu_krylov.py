@@ -214,6 +214,9 @@ def test_fun_and_grad_fun_after_edge_edit(kra, gpu_ctx):
                                          ctx=gpu_ctx)
     assert f1 != f0
     assert f1 == pytest.approx(f2, rel=1e-12)
+    # normest is kept with the matrix per (version, tol): recomputed after the edit
+    assert kra.normest(D, 1e-2, ctx=gpu_ctx) == kra.normest(kra.DeviceMatrix(A1, gpu_ctx), 1e-2, ctx=gpu_ctx)
+    assert kra.normest(D, 1e-2, ctx=gpu_ctx) == pytest.approx(ko.normest(A1, 1e-2), rel=1e-9)
     np.testing.assert_allclose(g1, g2, rtol=1e-12, atol=1e-14)
 
 

@@ -50,9 +50,10 @@ def main():
     D = kra.DeviceMatrix(A, ctx, check_symmetric=True)
     out = {"workload": "config3 hawaii-lcc sinh/cosh", "n": n, "nnz": int(A.nnz)}
 
-    nrm, t = best(lambda: kra.normest(D, 1e-2, ctx=ctx), a.repeat)
+    t0 = time.perf_counter()  # first call: later calls return the estimate kept with A
+    nrm = kra.normest(D, 1e-2, ctx=ctx)
     out["normest"] = nrm
-    out["normest_s"] = t
+    out["normest_s"] = time.perf_counter() - t0
     # 1. tr(sinh(A)) by SLQ
     kra.slq_quadforms(D, 16, a.m, seed=3, fun="sinh", ctx=ctx)
     (tr, qdev), t = best(lambda: kra.slq_trace(D, a.probes, a.m, seed=3, fun="sinh", ctx=ctx), a.repeat)
