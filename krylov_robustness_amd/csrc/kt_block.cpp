@@ -46,7 +46,19 @@ void gram(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const 
           int ldy, int py, std::vector<double>& G) {
     G.assign((size_t)px * py, 0.0);
     if (px == 0 || py == 0 || n == 0) return;
+    const double* d = gram_device(ctx, n, X, ldx, px, Y, ldy, py);
+    KT_HIP(hipMemcpyAsync(G.data(), d, sizeof(double) * G.size(), hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+const double* gram_device(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* Y,
+                          int ldy, int py) {
     DevBuf& d = ctx->ws.small;
+    if (px == 0 || py == 0 || n == 0) {
+        d.ensure(sizeof(double) * (size_t)std::max(px * py, 1));
+        KT_HIP(hipMemsetAsync(d.ptr, 0, sizeof(double) * (size_t)std::max(px * py, 1), ctx->stream));
+        return d.as<double>();
+    }
     const double one = 1.0, zero = 0.0;
     const int64_t count = (int64_t)px * py;
     // column-major views: X is (ldx x n), Y is (ldy x n);  G = X(0:px,:) Y(0:py,:)'.
@@ -76,9 +88,16 @@ void gram(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const 
                "rocblas_dgemm(gram tail)");
         KT_HIP(launch_sum_slabs((int)count, slabs, part, d.as<double>(), ctx->stream));
     }
-    KT_HIP(hipMemcpyAsync(G.data(), d.ptr, sizeof(double) * G.size(), hipMemcpyDeviceToHost,
-                          ctx->stream));
-    KT_HIP(hipStreamSynchronize(ctx->stream));
+    return d.as<double>();
+}
+
+void combine_device(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* dC, int q,
+                    double alpha, double beta, double* Y, int ldy) {
+    if (q == 0 || px == 0) return;
+    // Yc (q x n) = beta Yc + alpha C' (q x px) * Xc (px x n), C on the device
+    rb(rocblas_dgemm(blas(ctx), rocblas_operation_transpose, rocblas_operation_none, q,
+                     (rocblas_int)n, px, &alpha, dC, px, X, ldx, &beta, Y, ldy),
+       "rocblas_dgemm(combine_device)");
 }
 
 void combine(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px,

@@ -30,6 +30,13 @@ struct DevMat {
 // G (host, px x py column-major) = X[:, 0:px]' Y[:, 0:py]   (synchronises)
 void gram(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* Y,
           int ldy, int py, std::vector<double>& G);
+// The same Gram matrix left on the device (ctx->ws.small, px x py column-major;
+// valid until the next gram on this context): no host round trip
+const double* gram_device(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* Y,
+                          int ldy, int py);
+// Y[:, 0:q] = beta * Y[:, 0:q] + alpha * X[:, 0:px] * C   (C device px x q column-major)
+void combine_device(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* dC, int q,
+                    double alpha, double beta, double* Y, int ldy);
 // Y[:, 0:q] = beta * Y[:, 0:q] + X[:, 0:px] * C   (C host px x q column-major)
 void combine(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px,
              const std::vector<double>& C, int q, double beta, double* Y, int ldy);

@@ -103,6 +103,7 @@ struct Workspace {
     DevBuf hist, norm_part;                             // sweep scale history, inf-norm partials
     DevBuf expmv_state;                                 // expmv stage stop state (device)
     PinnedBuf host_trec;
+    PinnedBuf pin_small;  // block-Krylov Gram blocks read back without a sync per pass
     // batched greedy candidates (kt_greedy.cpp): 3 pair blocks, indices,
     // per-candidate coefficients / partials / host records
     DevBuf pair_blk[3], pair_idx, pair_coef, pair_part, pair_hr;

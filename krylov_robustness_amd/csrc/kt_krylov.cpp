@@ -394,6 +394,13 @@ static void add_UBUt(std::vector<double>& M, int64_t n, int r, const double* U, 
 // BlockLanczos: lanczos_krylov.m (start :30-58, extend :60-67,
 // add_inf_pole :73-101, CGS2 :109-115).  Window slots 0/1 of `win`.
 // ---------------------------------------------------------------------------
+// KT_GRAM_HOST=1: the CGS2 Gram blocks go through the host (one round trip
+// per pass) instead of staying on the device -- the A/B switch of that change
+static bool gram_host_path() {
+    static const bool host = getenv("KT_GRAM_HOST") && getenv("KT_GRAM_HOST")[0] == '1';
+    return host;
+}
+
 struct BlockLanczos {
     kt_matrix_s* A;
     kt_context_s* ctx;
@@ -441,7 +448,20 @@ struct BlockLanczos {
         grow(bs);                                  // :85
         // CGS2 against the window (both slots in one Gram; absent slot -> 0)
         std::vector<double> h((size_t)2 * PB * bs, 0.0);
-        for (int pass = 0; pass < 2; ++pass) {  // :109-115
+        const size_t cnt = (size_t)2 * PB * bs;
+        double* hg = nullptr;
+        if (prev >= 0 && !gram_host_path()) {  // both slots live: Gram blocks stay on the device
+            PinnedBuf& hp = ctx->ws.pin_small;
+            hp.ensure(sizeof(double) * 2 * cnt);
+            hg = hp.as<double>();
+            for (int pass = 0; pass < 2; ++pass) {
+                const double* dG = gram_device(ctx, n, win.col(0), ld, 2 * PB, W.col(0), PB, bs);
+                KT_HIP(hipMemcpyAsync(hg + pass * cnt, dG, sizeof(double) * cnt, hipMemcpyDeviceToHost,
+                                      ctx->stream));
+                combine_device(ctx, n, win.col(0), ld, 2 * PB, dG, bs, -1.0, 1.0, W.col(0), PB);
+            }
+        }
+        for (int pass = 0; !hg && pass < 2; ++pass) {  // :109-115
             std::vector<double> g;
             gram(ctx, n, win.col(0), ld, 2 * PB, W.col(0), PB, bs, g);
             if (prev < 0)
@@ -454,6 +474,12 @@ struct BlockLanczos {
                 h[t] += g[t];
             }
             combine(ctx, n, win.col(0), ld, 2 * PB, C, bs, 1.0, W.col(0), PB);
+        }
+        std::vector<double> R;
+        householder_qr(ctx, n, W.col(0), PB, bs, R);  // [w, R] = qr(w, 0)   :90
+        if (hg) {
+            KT_HIP(hipStreamSynchronize(ctx->stream));  // (the QR's read of R has drained the copies)
+            for (size_t t = 0; t < cnt; ++t) h[t] = (0.0 + hg[t]) + hg[cnt + t];  // h += g, twice
         }
         // H(max(1,end-3bs+1):end-bs, end-bs+1:end) = h      :88
         const int c0 = Hc - bs;
@@ -468,8 +494,6 @@ struct BlockLanczos {
         } else {
             put(cur, Hr - 2 * bs);
         }
-        std::vector<double> R;
-        householder_qr(ctx, n, W.col(0), PB, bs, R);  // [w, R] = qr(w, 0)   :90
         for (int j = 0; j < bs; ++j)
             for (int i = 0; i < bs; ++i) H[(Hr - bs + i) + (size_t)(c0 + j) * Hr] = R[i + (size_t)j * bs];
         lucky = norm_fro(R) < 1e-8;  // :91-93
@@ -532,32 +556,46 @@ struct BlockArnoldi {
         const int L = ld();
         const int pv = nblk * PB;
         spmm(A, blk(last), L, W.col(0), PB, bs);  // w = A * w   :86
-        std::vector<double> h((size_t)pv * bs, 0.0);
-        for (int pass = 0; pass < 2; ++pass) {  // CGS2 :119-125
-            std::vector<double> g;
-            gram(ctx, n, V.col(0), L, pv, W.col(0), PB, bs, g);
-            std::vector<double> C(g.size());
-            for (size_t t = 0; t < g.size(); ++t) {
-                C[t] = -g[t];
-                h[t] += g[t];
+        // CGS2 :119-125 with the Gram blocks kept on the device: each pass's
+        // h_p = V'w feeds w = w - V h_p directly; the two blocks are read back
+        // (pinned, asynchronously) for H and summed once the QR below has synced
+        const size_t cnt = (size_t)pv * bs;
+        PinnedBuf& hp = ctx->ws.pin_small;
+        hp.ensure(sizeof(double) * 3 * cnt);
+        double* hg = hp.as<double>();
+        // w = w - V (V'w), the Gram block read back into hg + off
+        auto project = [&](size_t off) {
+            if (gram_host_path()) {  // A/B: through the host, one round trip per pass
+                std::vector<double> g;
+                gram(ctx, n, V.col(0), L, pv, W.col(0), PB, bs, g);
+                std::vector<double> C(g.size());
+                for (size_t t = 0; t < g.size(); ++t) C[t] = -g[t];
+                combine(ctx, n, V.col(0), L, pv, C, bs, 1.0, W.col(0), PB);
+                std::copy(g.begin(), g.end(), hg + off);
+                return;
             }
-            combine(ctx, n, V.col(0), L, pv, C, bs, 1.0, W.col(0), PB);
-        }
+            const double* dG = gram_device(ctx, n, V.col(0), L, pv, W.col(0), PB, bs);
+            KT_HIP(hipMemcpyAsync(hg + off, dG, sizeof(double) * cnt, hipMemcpyDeviceToHost, ctx->stream));
+            combine_device(ctx, n, V.col(0), L, pv, dG, bs, -1.0, 1.0, W.col(0), PB);
+        };
+        for (int pass = 0; pass < 2; ++pass) project(pass * cnt);
+        std::vector<double> r;
+        householder_qr(ctx, n, W.col(0), PB, bs, r);  // [w, r] = qr(w, 0)   :99
+        lucky = norm2_small(bs, bs, r.data()) < 1e-12;  // :100-102
+        KT_HIP(hipStreamSynchronize(ctx->stream));    // (the QR's read of r has drained the copies)
+        std::vector<double> h(cnt);
+        for (size_t t = 0; t < cnt; ++t) h[t] = (0.0 + hg[t]) + hg[cnt + t];  // h += g, twice
         grow(bs);  // :93-94
         const int c0 = Hc - bs;
         auto hrow = [&](int padded_row) { return (padded_row / PB) * bs + padded_row % PB; };
         for (int j = 0; j < bs; ++j)
             for (int i = 0; i < pv; ++i)
                 if (i % PB < bs) H[hrow(i) + (size_t)(c0 + j) * Hr] = h[i + (size_t)j * pv];  // :96
-        std::vector<double> r;
-        householder_qr(ctx, n, W.col(0), PB, bs, r);  // [w, r] = qr(w, 0)   :99
-        lucky = norm2_small(bs, bs, r.data()) < 1e-12;  // :100-102
         // reorthogonalise :104-106
-        std::vector<double> hh;
-        gram(ctx, n, V.col(0), L, pv, W.col(0), PB, bs, hh);
-        std::vector<double> C(hh.size());
-        for (size_t t = 0; t < hh.size(); ++t) C[t] = -hh[t];
-        combine(ctx, n, V.col(0), L, pv, C, bs, 1.0, W.col(0), PB);
+        project(2 * cnt);
+        copy_cols(ctx, n, W.col(0), PB, blk(nblk), L, PB);  // V = [V, w]   :110
+        KT_HIP(hipStreamSynchronize(ctx->stream));
+        std::vector<double> hh(hg + 2 * cnt, hg + 3 * cnt);
         std::vector<double> hr((size_t)pv * bs);
         matmul(pv, bs, bs, hh.data(), r.data(), hr.data());
         for (int j = 0; j < bs; ++j)
@@ -565,7 +603,6 @@ struct BlockArnoldi {
                 if (i % PB < bs) H[hrow(i) + (size_t)(c0 + j) * Hr] += hr[i + (size_t)j * pv];
         for (int j = 0; j < bs; ++j)  // :108
             for (int i = 0; i < bs; ++i) H[(Hr - bs + i) + (size_t)(c0 + j) * Hr] = r[i + (size_t)j * bs];
-        copy_cols(ctx, n, W.col(0), PB, blk(nblk), L, PB);  // V = [V, w]   :110
         nblk += 1;
     }
 };
