@@ -20,6 +20,7 @@
 #include <unordered_map>
 
 #include "kt_colarnoldi.h"
+#include "kt_pool.h"
 
 namespace kt {
 
@@ -125,22 +126,32 @@ int frechet_entries_impl(kt_matrix_s* A, int64_t k, const int64_t* oi, const int
     }
     const int d = 3;  // :80
     int j = 0;
-    std::vector<double> G;
     for (j = 1; j <= it; ++j) {
         for (auto& g : groups) g->step();
         // eigendecompositions of the live projections
         std::vector<char> live(T.size(), 0);
         for (const FEntry& e : ents)
             if (!e.conv) live[e.ti] = live[e.tj] = 1;
+        // the per-index eigensolves and the per-entry blocks are independent:
+        // spread over the host pool (they are the step's critical path on a
+        // small graph; the device step takes a fraction of it)
         std::vector<std::vector<double>> W(T.size()), Q(T.size());
-        for (size_t s = 0; s < T.size(); ++s) {
-            if (!live[s]) continue;
-            groups[slot[s].group]->gm(slot[s].col, G);
-            sym_eig_small(j, G, W[s], Q[s]);
-        }
-        bool stop = true;
-        for (FEntry& e : ents) {
-            if (e.conv) continue;
+        std::vector<int> ls;
+        for (size_t s = 0; s < T.size(); ++s)
+            if (live[s]) ls.push_back((int)s);
+        HostPool& pool = HostPool::get();
+        pool.run((int)ls.size(), [&](int i) {
+            const int s = ls[i];
+            std::vector<double> Gs;
+            groups[slot[s].group]->gm(slot[s].col, Gs);
+            sym_eig_small(j, Gs, W[s], Q[s]);
+        }, 4);
+        std::vector<int> act;
+        for (size_t h = 0; h < ents.size(); ++h)
+            if (!ents[h].conv) act.push_back((int)h);
+        std::vector<char> open_(act.size(), 0);  // entry not stopped at this step
+        pool.run((int)act.size(), [&](int i) {
+            FEntry& e = ents[act[i]];
             const double c = groups[slot[e.ti].group]->uaux(slot[e.ti].col) *
                              groups[slot[e.tj].group]->uaux(slot[e.tj].col);  // Cm(1,1)  :152
             const std::vector<double>& Q1 = Q[e.ti];
@@ -166,7 +177,7 @@ int frechet_entries_impl(kt_matrix_s* A, int64_t k, const int64_t* oi, const int
             e.nn = j;
             if (j <= d) {
                 e.stop[j - 1] = e.Xm;
-                stop = false;
+                open_[i] = 1;
             } else {
                 const std::vector<double>& old = e.stop[0];
                 const int no = (int)std::lround(std::sqrt((double)old.size()));
@@ -174,13 +185,15 @@ int frechet_entries_impl(kt_matrix_s* A, int64_t k, const int64_t* oi, const int
                 for (int b = 0; b < no; ++b)
                     for (int a = 0; a < no; ++a) D[a + (size_t)b * j] -= old[a + (size_t)b * no];
                 const double err = spectral_norm(j, D);  // norm(Xm - Xstop{1})   :172
-                if (err > tol) stop = false;
+                if (err > tol) open_[i] = 1;
                 else e.conv = true;
                 e.stop[0] = std::move(e.stop[1]);
                 e.stop[1] = std::move(e.stop[2]);
                 e.stop[2] = e.Xm;
             }
-        }
+        }, 4);
+        bool stop = true;
+        for (char o : open_) stop = stop && !o;
         if (stop) break;
     }
     const int iter = std::min(j, it);

@@ -22,6 +22,7 @@
 #include <thread>
 
 #include "kt_krylov.h"
+#include "kt_pool.h"
 #include "kt_launch.h"
 
 namespace kt {
@@ -75,82 +76,6 @@ double pair_xm(const PairRun& s, int j, int fun, std::vector<double>& G, std::ve
     std::sort(w2.begin(), w2.end());
     return trace_diff(w1, w2, fun);
 }
-
-// Persistent host worker pool for the per-candidate eig work (spawning
-// threads every Lanczos step costs more than the work itself).
-class HostPool {
-   public:
-    static HostPool& get() {
-        static HostPool pool;
-        return pool;
-    }
-    // f(i) for i in [0, count); the caller thread participates
-    void run(int count, const std::function<void(int)>& f) {
-        if (count <= 0) return;
-        if (workers_.empty() || count < 8) {
-            for (int i = 0; i < count; ++i) f(i);
-            return;
-        }
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            job_ = &f;
-            count_ = count;
-            next_.store(0);
-            pending_ = (int)workers_.size();
-            ++gen_;
-        }
-        cv_.notify_all();
-        drain(f, count);
-        std::unique_lock<std::mutex> lk(m_);
-        done_cv_.wait(lk, [&] { return pending_ == 0; });
-        job_ = nullptr;
-    }
-    ~HostPool() {
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            stop_ = true;
-            ++gen_;
-        }
-        cv_.notify_all();
-        for (auto& t : workers_) t.join();
-    }
-
-   private:
-    HostPool() {
-        int nt = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) - 1;
-        if (const char* e = getenv("KT_HOST_THREADS")) nt = std::max(0, atoi(e) - 1);
-        for (int t = 0; t < nt; ++t) workers_.emplace_back([this] { loop(); });
-    }
-    void drain(const std::function<void(int)>& f, int count) {
-        for (int i = next_.fetch_add(1); i < count; i = next_.fetch_add(1)) f(i);
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            const std::function<void(int)>* f;
-            int count;
-            {
-                std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return gen_ != seen; });
-                seen = gen_;
-                if (stop_) return;
-                f = job_;
-                count = count_;
-            }
-            if (f) drain(*f, count);
-            std::lock_guard<std::mutex> lk(m_);
-            if (--pending_ == 0) done_cv_.notify_one();
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex m_;
-    std::condition_variable cv_, done_cv_;
-    const std::function<void(int)>* job_ = nullptr;
-    int count_ = 0, pending_ = 0;
-    std::atomic<int> next_{0};
-    uint64_t gen_ = 0;
-    bool stop_ = false;
-};
 
 // One device batch of C <= kMaxPairs two-column candidates.
 void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej, const double* B,

@@ -1,5 +1,6 @@
-"""fun_and_grad_krylov_exp on voltage India as tools/bench_hessian.py sets it up,
-repeated (for rocprofv3 / KT_EIG_STATS timing)."""
+"""fun_and_grad_krylov_exp (or, with --hess, hessianfcn_exp) on voltage India
+as tools/bench_hessian.py sets it up, repeated (for rocprofv3 / KT_EIG_STATS
+timing)."""
 import os
 import sys
 import time
@@ -13,7 +14,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import krylov_robustness_amd as kra  # noqa: E402
 from conftest import load_graph  # noqa: E402
 
-A = load_graph(sys.argv[1] if len(sys.argv) > 1 else "india")
+hess = "--hess" in sys.argv
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+A = load_graph(args[0] if args else "india")
 ctx = kra.Context(0)
 D = kra.DeviceMatrix(A, ctx)
 tol = 1e-8 * np.exp(kra.normest(D, 1e-2, ctx=ctx))
@@ -28,5 +31,9 @@ if X.sum() > 10:
     X *= 10 / X.sum()
 for r in range(4):
     t0 = time.perf_counter()
-    f, gr = kra.fun_and_grad_krylov_exp(X, D, Om, eA, tol, 100, ctx=ctx)
-    print(f"fg_exp {time.perf_counter() - t0:.4f} s f={f:.10e}", flush=True)
+    if hess:
+        H = kra.hessianfcn_exp(X, D, Om, tol, 100, ctx=ctx)
+        print(f"hessianfcn_exp {time.perf_counter() - t0:.4f} s |H|={np.abs(H).sum():.10e}", flush=True)
+    else:
+        f, gr = kra.fun_and_grad_krylov_exp(X, D, Om, eA, tol, 100, ctx=ctx)
+        print(f"fg_exp {time.perf_counter() - t0:.4f} s f={f:.10e}", flush=True)
