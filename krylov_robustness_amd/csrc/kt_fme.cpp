@@ -15,6 +15,7 @@
 #include <unordered_map>
 
 #include "kt_colarnoldi.h"
+#include "kt_pool.h"
 #include "kt_launch.h"
 
 namespace kt {
@@ -191,15 +192,17 @@ int run_group(kt_matrix_s* A, const std::vector<int64_t>& rows, std::vector<Entr
     std::vector<char> col_live(C, 1);
     const int d = 3;  // lag (function_multiple_entries.m:63)
     int j = 0;
-    std::vector<double> G;
     for (j = 1; j <= it; ++j) {
         ca.step();
         std::vector<std::vector<double>> F(C);
-        for (int c = 0; c < C; ++c) {
-            if (!col_live[c]) continue;
-            ca.gm(c, G);
-            F[c] = fun_e1(j, G, fun);
-        }
+        std::vector<int> lc;  // live columns: f(G_c) e1 each, on the host worker pool
+        for (int c = 0; c < C; ++c)
+            if (col_live[c]) lc.push_back(c);
+        HostPool::get().run((int)lc.size(), [&](int i) {
+            std::vector<double> Gc;
+            ca.gm(lc[i], Gc);
+            F[lc[i]] = fun_e1(j, Gc, fun);
+        }, 4);
         bool stop = true;  // :113-156
         for (Entry& e : ents) {
             if (e.conv) continue;
