@@ -78,6 +78,22 @@ def test_trace_fun_update_dense_shortcut_exact():
     assert xs == pytest.approx(ko.exact_trace_update(A, U, B, "sinh"), rel=1e-12)
 
 
+def test_trace_fun_update_generic_handle_pinned():
+    """A handle outside fun_update.m's list (trace_fun_update.m:88) in the
+    oracle: the Lanczos path agrees with the exact update, and a callable
+    equal to sinh gives fun='sinh'."""
+    A = load_graph("rome")
+    n = A.shape[0]
+    U = np.zeros((n, 2)); U[5, 0] = 1; U[40, 1] = 1
+    B = -np.array([[0.0, 1.0], [1.0, 0.0]])
+    f = lambda x: np.tanh(x) + 0.1 * x ** 3  # noqa: E731
+    xf, _, _ = ko.trace_fun_update(A, U, B, 1e-12, 100, 0, f)
+    assert xf == pytest.approx(ko.exact_trace_update(A, U, B, f), rel=1e-9, abs=1e-10)
+    xs, _, _ = ko.trace_fun_update(A, U, B, 1e-12, 100, 0, lambda x: np.sinh(x))
+    xr, _, _ = ko.trace_fun_update(A, U, B, 1e-12, 100, 0, "sinh")
+    assert xs == xr
+
+
 def test_fun_update_arnoldi_vs_dense_expm():
     """fun_and_grad_krylov_exp.m:90-93 debug check: Um Xm Um' ~ expm(A+UBU') - expm(A)."""
     A = load_graph("austria")
