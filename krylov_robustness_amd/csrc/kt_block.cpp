@@ -1,5 +1,7 @@
 // kt_block.cpp -- tall-skinny device block operations (rocBLAS dgemm for the
 // plain GEMM shapes, the HIP SpMM kernel for A*X) and CholQR.
+#include <cstring>
+
 #include "kt_block.h"
 
 #include <rocsolver/rocsolver.h>
@@ -42,13 +44,28 @@ void DevMat::alloc(kt_context_s* ctx, int64_t n_, int ld_) {
                           ctx->stream));
 }
 
+// KT_PINNED_STAGING=0: gram / combine / the thin QR move their small blocks
+// through pageable host memory with a sync each (the A/B switch)
+static bool pinned_staging() {
+    static const bool on = !(getenv("KT_PINNED_STAGING") && getenv("KT_PINNED_STAGING")[0] == '0');
+    return on;
+}
+
 void gram(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* Y,
           int ldy, int py, std::vector<double>& G) {
     G.assign((size_t)px * py, 0.0);
     if (px == 0 || py == 0 || n == 0) return;
     const double* d = gram_device(ctx, n, X, ldx, px, Y, ldy, py);
-    KT_HIP(hipMemcpyAsync(G.data(), d, sizeof(double) * G.size(), hipMemcpyDeviceToHost, ctx->stream));
+    if (!pinned_staging()) {
+        KT_HIP(hipMemcpyAsync(G.data(), d, sizeof(double) * G.size(), hipMemcpyDeviceToHost, ctx->stream));
+        KT_HIP(hipStreamSynchronize(ctx->stream));
+        return;
+    }
+    PinnedBuf& pb = ctx->ws.pin_gram;
+    pb.ensure(sizeof(double) * G.size());
+    KT_HIP(hipMemcpyAsync(pb.ptr, d, sizeof(double) * G.size(), hipMemcpyDeviceToHost, ctx->stream));
     KT_HIP(hipStreamSynchronize(ctx->stream));
+    std::memcpy(G.data(), pb.ptr, sizeof(double) * G.size());
 }
 
 const double* gram_device(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* Y,
@@ -108,16 +125,34 @@ void combine(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px,
         return;
     }
     DevBuf& d = ctx->ws.small2;
-    d.ensure(sizeof(double) * (size_t)px * q);
-    KT_HIP(hipMemcpyAsync(d.ptr, C.data(), sizeof(double) * (size_t)px * q, hipMemcpyHostToDevice,
-                          ctx->stream));
+    const size_t bytes = sizeof(double) * (size_t)px * q;
+    // C goes through a pinned staging buffer, so the caller may free C at once
+    // and the stream is not drained; the staging buffer is only rewritten once
+    // the previous upload out of it has completed (event)
     const double one = 1.0;
+    if (!pinned_staging()) {
+        d.ensure(bytes);
+        KT_HIP(hipMemcpyAsync(d.ptr, C.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+        rb(rocblas_dgemm(blas(ctx), rocblas_operation_transpose, rocblas_operation_none, q,
+                         (rocblas_int)n, px, &one, d.as<double>(), px, X, ldx, &beta, Y, ldy),
+           "rocblas_dgemm(combine)");
+        KT_HIP(hipStreamSynchronize(ctx->stream));  // the caller may free C right after
+        return;
+    }
+    Workspace& ws = ctx->ws;
+    if (ws.comb_pending) KT_HIP(hipEventSynchronize(ws.comb_ev));
+    ws.comb_pending = false;
+    if (!ws.comb_ev) KT_HIP(hipEventCreateWithFlags(&ws.comb_ev, hipEventDisableTiming));
+    ws.pin_comb.ensure(bytes);
+    std::memcpy(ws.pin_comb.ptr, C.data(), bytes);
+    d.ensure(bytes);
+    KT_HIP(hipMemcpyAsync(d.ptr, ws.pin_comb.ptr, bytes, hipMemcpyHostToDevice, ctx->stream));
+    KT_HIP(hipEventRecord(ws.comb_ev, ctx->stream));
+    ws.comb_pending = true;
     // Yc (q x n) = beta Yc + C' (q x px) * Xc (px x n)
     rb(rocblas_dgemm(blas(ctx), rocblas_operation_transpose, rocblas_operation_none, q,
                      (rocblas_int)n, px, &one, d.as<double>(), px, X, ldx, &beta, Y, ldy),
        "rocblas_dgemm(combine)");
-    // the host vector C may be freed by the caller right after: finish the copy
-    KT_HIP(hipStreamSynchronize(ctx->stream));
 }
 
 // Every block SpMM: Y[:, 0:slices P] = A X over `slices` P-wide column slices
@@ -326,14 +361,20 @@ void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std
     KT_HIP(hipMemsetAsync(V, 0, sizeof(double) * (size_t)n * BP, ctx->stream));
     KT_HIP(launch_ts_reflectors((int)n, bs, BP, W, ld, V, pivot, sums, ws.ts_part.as<double>(), taus,
                                 ctx->num_cu, ctx->stream));
-    std::vector<double> top((size_t)bs * bs), V1((size_t)bs * BP), tau(bs);
-    KT_HIP(hipMemcpy2DAsync(top.data(), sizeof(double) * bs, W, sizeof(double) * ld,
-                            sizeof(double) * bs, (size_t)bs, hipMemcpyDeviceToHost, ctx->stream));
-    KT_HIP(hipMemcpyAsync(V1.data(), V, sizeof(double) * (size_t)bs * BP, hipMemcpyDeviceToHost,
-                          ctx->stream));
-    KT_HIP(hipMemcpyAsync(tau.data(), taus, sizeof(double) * bs, hipMemcpyDeviceToHost, ctx->stream));
+    // R's rows, V's top block and the taus come back through pinned staging
+    // (asynchronous); gram's synchronisation covers them
+    ws.pin_qr.ensure(sizeof(double) * ((size_t)bs * bs + (size_t)bs * BP + bs));
+    double* ptop = ws.pin_qr.as<double>();
+    double* pV1 = ptop + (size_t)bs * bs;
+    double* ptau = pV1 + (size_t)bs * BP;
+    KT_HIP(hipMemcpy2DAsync(ptop, sizeof(double) * bs, W, sizeof(double) * ld, sizeof(double) * bs, (size_t)bs,
+                            hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipMemcpyAsync(pV1, V, sizeof(double) * (size_t)bs * BP, hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipMemcpyAsync(ptau, taus, sizeof(double) * bs, hipMemcpyDeviceToHost, ctx->stream));
     std::vector<double> G;  // V' V (bs x bs), gram synchronises the stream
     gram(ctx, n, V, BP, bs, V, BP, bs, G);
+    const std::vector<double> top(ptop, ptop + (size_t)bs * bs), V1(pV1, pV1 + (size_t)bs * BP),
+        tau(ptau, ptau + bs);
     for (int i = 0; i < bs; ++i)
         for (int j = i; j < bs; ++j) R[i + (size_t)j * bs] = top[(size_t)i * bs + j];
     // dlarft (forward, columnwise): T upper bs x bs, column-major

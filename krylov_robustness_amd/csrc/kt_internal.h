@@ -104,6 +104,11 @@ struct Workspace {
     DevBuf expmv_state;                                 // expmv stage stop state (device)
     PinnedBuf host_trec;
     PinnedBuf pin_small;  // block-Krylov Gram blocks read back without a sync per pass
+    // pinned staging for gram() read-backs, combine() uploads and the thin-QR
+    // read-backs (pageable transfers are staged synchronously by the runtime)
+    PinnedBuf pin_gram, pin_comb, pin_qr;
+    hipEvent_t comb_ev = nullptr;  // last combine() upload out of pin_comb
+    bool comb_pending = false;
     // batched greedy candidates (kt_greedy.cpp): 3 pair blocks, indices,
     // per-candidate coefficients / partials / host records
     DevBuf pair_blk[3], pair_idx, pair_coef, pair_part, pair_hr;

@@ -282,6 +282,7 @@ int kt_context_destroy(kt_context_t ctx) {
     w.eigA.release(); w.eigW.release(); w.eigInfo.release();
     w.hist.release(); w.norm_part.release();
     if (ctx->blas) rocblas_destroy_handle(static_cast<rocblas_handle>(ctx->blas));
+    if (w.comb_ev) (void)hipEventDestroy(w.comb_ev);
     w.host_trec.release();
     for (auto a : ctx->aux_stream)
         if (a) (void)hipStreamDestroy(a);
