@@ -1,17 +1,17 @@
 """A/B of one environment switch on one GPU box: alternating runs of the
 block-Krylov / greedy / config-1 benches with VAR=a and VAR=b; best times.
-  python tools/ab_env.py VAR a b"""
+  python tests/perf/ab_env.py VAR a b"""
 import json
 import os
 import subprocess
 import sys
 
-ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
 var, vals = sys.argv[1], sys.argv[2:4]
 
 
 def run(tool, env, *args):
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", tool), *args], env=env,
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "perf", tool), *args], env=env,
                          capture_output=True, text=True, timeout=300, check=True).stdout
     return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
 

@@ -6,11 +6,11 @@ import os
 import subprocess
 import sys
 
-ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
 
 
 def run(tool, env, *args):
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", tool), *args], env=env,
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "perf", tool), *args], env=env,
                          capture_output=True, text=True, timeout=300, check=True).stdout
     return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
 

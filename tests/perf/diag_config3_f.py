@@ -1,7 +1,10 @@
+"""Config-3 objective diagnosis (GPU box): trace_fun_update(sinh) device vs
+oracle per iteration cap, and the exact dense value by torch eigvalsh on the
+GPU.  Test infrastructure: imports the oracle."""
 import os, sys, json
 import torch  # noqa
 import numpy as np
-ROOT = "/root/repo"
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
 sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tests"))
 import krylov_robustness_amd as kra
 from conftest import load_graph

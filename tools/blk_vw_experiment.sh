@@ -2,8 +2,8 @@
 set -e
 mkdir -p gpurun_out/bv
 run() {
-  timeout -k 10 300 python tools/bench_greedy.py --cpu-steps 0 --repeat 3 > gpurun_out/bv/india_$1.json 2>/dev/null
-  timeout -k 10 300 python tools/bench_greedy.py --graph as_735 --miobi make --cpu-steps 0 --repeat 2 > gpurun_out/bv/as735_$1.json 2>/dev/null
+  timeout -k 10 300 python tests/perf/bench_greedy.py --cpu-steps 0 --repeat 3 > gpurun_out/bv/india_$1.json 2>/dev/null
+  timeout -k 10 300 python tests/perf/bench_greedy.py --graph as_735 --miobi make --cpu-steps 0 --repeat 2 > gpurun_out/bv/as735_$1.json 2>/dev/null
   timeout -k 10 300 python tools/prof_fg.py > gpurun_out/bv/fg_$1.txt 2>&1
 }
 run vw2

@@ -1,5 +1,5 @@
 """fun_and_grad_krylov_exp (or, with --hess, hessianfcn_exp) on voltage India
-as tools/bench_hessian.py sets it up, repeated (for rocprofv3 / KT_EIG_STATS
+as tests/perf/bench_hessian.py sets it up, repeated (for rocprofv3 / KT_EIG_STATS
 timing)."""
 import os
 import sys
