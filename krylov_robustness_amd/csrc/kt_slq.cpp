@@ -137,7 +137,9 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     if (lane && !ctx->aux_stream[lane - 1])
         KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[lane - 1], hipStreamNonBlocking));
     hipStream_t st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
-    const int grid = spmm_grid(n, P, ctx->num_cu * 4);
+    // KT_KY_BPC: row-group workgroups per CU of the pass (default 4)
+    static const int bpc = getenv("KT_KY_BPC") ? std::max(1, atoi(getenv("KT_KY_BPC"))) : 4;
+    const int grid = spmm_grid(n, P, ctx->num_cu * bpc);
     const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
     const int grid1 = grid + lblocks;
     SweepBufs& w = ctx->ws.sweep[lane];
