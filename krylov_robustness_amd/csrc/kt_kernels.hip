@@ -813,17 +813,28 @@ __global__ __launch_bounds__(128) void k_spmm_combine(const int* __restrict__ sp
 // Slot-major slabs: partial[slot * nblk + b].  One WAVE per slot reads the
 // slot's nblk partials with coalesced loads (all in flight at once), sums
 // lane-wise in block order, then a fixed xor-tree -- deterministic.
+constexpr int kReduceDepth = 32;
 __device__ __forceinline__ double wave_reduce_slot(const double* __restrict__ partial, int nblk,
                                                    int slot) {
     const int lane = threadIdx.x & 63;
     const double* base = partial + (int64_t)slot * nblk;
     double v = 0.0;
-    int b = lane;
-    for (; b + 192 < nblk; b += 256) {
-        const double x0 = base[b], x1 = base[b + 64], x2 = base[b + 128], x3 = base[b + 192];
-        v += x0; v += x1; v += x2; v += x3;
+    // 32 predicated loads in flight per lane before the in-order adds: the
+    // slabs are read right after the producing pass, while the other sweep
+    // lane's pass loads the memory system, so each round trip costs
+    // microseconds (a 4-deep loop over the pass's ~1,500 blocks measured
+    // 21.6 us per k_ycoef under two lanes).  Each lane still adds its blocks
+    // in increasing order (out-of-range slots add +0.0), so sums are unchanged.
+    for (int b = lane; b < nblk; b += 64 * kReduceDepth) {
+        double x[kReduceDepth];
+#pragma unroll
+        for (int i = 0; i < kReduceDepth; ++i) {
+            const int bi = b + 64 * i;
+            x[i] = bi < nblk ? base[bi] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < kReduceDepth; ++i) v += x[i];
     }
-    for (; b < nblk; b += 64) v += base[b];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
@@ -990,6 +1001,18 @@ __global__ __launch_bounds__(192) void k_ycoef(const double* __restrict__ partia
                                                double* __restrict__ guard) {
     const int p = blockIdx.x;
     const int q = threadIdx.x >> 6;
+    // the recurrence state is loaded before the slab reduction so that its
+    // round trip overlaps the reduction's
+    double aj = 0.0, bj = 0.0, am1 = 0.0, nyj = 0.0, ydj = 0.0, b1 = 0.0, g = 1.0;
+    if (threadIdx.x == 0 && !start) {
+        aj = ys[0 * P + p];
+        bj = ys[1 * P + p];
+        am1 = ys[2 * P + p];
+        nyj = ys[3 * P + p];
+        ydj = ys[4 * P + p];
+        b1 = ys[5 * P + p];
+        g = guard[p];
+    }
     const double r = wave_reduce_slot(partial, nblk, q * P + p);
     __shared__ double d[3];
     if ((threadIdx.x & 63) == 0) d[q] = r;
@@ -1004,10 +1027,9 @@ __global__ __launch_bounds__(192) void k_ycoef(const double* __restrict__ partia
         ys[1 * P + p] = 0.0;
         ys[2 * P + p] = 0.0;
         ys[4 * P + p] = 0.0;
+        g = 1.0;
         guard[p] = 1.0;
     } else {
-        const double aj = ys[0 * P + p], bj = ys[1 * P + p], am1 = ys[2 * P + p];
-        const double nyj = ys[3 * P + p], ydj = ys[4 * P + p], b1 = ys[5 * P + p];
         const double b1sq = b1 * b1;
         an = (d[0] - 2.0 * aj * nyj - 2.0 * bj * ydj + aj * aj * aj + 2.0 * aj * bj * bj +
               bj * bj * am1) / b1sq;
@@ -1027,7 +1049,6 @@ __global__ __launch_bounds__(192) void k_ycoef(const double* __restrict__ partia
     t_low[p] = bnext;
     if (!last) {
         const double ratio = bnext_sq / ny2;
-        const double g = guard[p];
         guard[p] = (ratio < g || !(ratio == ratio)) ? ratio : g;  // NaN sticks
     }
     const bool ok = bnext > 0.0 && bnext < INFINITY;
