@@ -823,7 +823,10 @@ __device__ __forceinline__ double wave_reduce_slot(const double* __restrict__ pa
     // slabs are read right after the producing pass, while the other sweep
     // lane's pass loads the memory system, so each round trip costs
     // microseconds (a 4-deep loop over the pass's ~1,500 blocks measured
-    // 21.6 us per k_ycoef under two lanes).  Each lane still adds its blocks
+    // 21.6 us per k_ycoef under two lanes; this 32-deep form measured 25.4 us
+    // in a later profile, bench unchanged at 2.54 evals/s, so the slab read
+    // is bound by the concurrent pass, not by load depth -- see
+    // profiles/r01_final_kernel_stats.csv).  Each lane still adds its blocks
     // in increasing order (out-of-range slots add +0.0), so sums are unchanged.
     for (int b = lane; b < nblk; b += 64 * kReduceDepth) {
         double x[kReduceDepth];
