@@ -88,10 +88,18 @@ def cpu_baseline(A, m, budget_s, nprobes_eval):
                       f"{el:.1f} s with {threads} OpenMP threads, extrapolated"}
 
 
-def _pmc_traffic(kernel_prefix):
+def _kernel_template_args(name):
+    """'k_spmm_lanczos<16, 512, 10>' -> ('k_spmm_lanczos', ['16', '512', '10'])."""
+    base, _, rest = name.partition("<")
+    return base.strip(), [a.strip() for a in rest.rstrip(">").split(",")] if rest else []
+
+
+def _pmc_traffic(kernel, P):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
     counter summary (profiles/traffic.json, produced by tools/gpu_prof.sh +
-    tools/pmc_traffic.py on this same bench command), or None."""
+    tools/pmc_traffic.py on this same bench command), or None.  Matches the
+    kernel's name and its first template argument (the probe block P)
+    exactly, so P = 1 never picks up the P = 16 entry."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
@@ -99,9 +107,21 @@ def _pmc_traffic(kernel_prefix):
     except (OSError, ValueError):
         return None
     for k, v in t.items():
-        if k.startswith(kernel_prefix) and isinstance(v, dict):
+        base, targs = _kernel_template_args(k)
+        if base == kernel and targs[:1] == [str(P)] and isinstance(v, dict):
             return v.get("hbm_bytes_per_launch")
     return None
+
+
+def _metric_name(n, nnz):
+    def short(x):
+        for unit, div in (("M", 1_000_000), ("k", 1_000)):
+            if x >= div and x % (div // 10 or 1) == 0:
+                v = x / div
+                return f"{v:g}{unit}"
+        return str(x)
+    # BASELINE.json's metric string, with n / nnz of the graph actually used
+    return f"trace(exp(A)) evals/sec + achieved HBM GB/s, n={short(n)} nnz={short(nnz)}, 1/2/4/8 GPU"
 
 
 def main():
@@ -185,7 +205,8 @@ def main():
     # previous vector, next vector (8nP each).  The y-form pass
     # (k_spmm_lanczos) moves exactly these streams; the explicit sweep's K1 is
     # charged the whole step although its K2 streams two of them.
-    kname = f"k_spmm_dot<{P}" if args.explicit else f"k_spmm_lanczos<{P}"
+    kbase = "k_spmm_dot" if args.explicit else "k_spmm_lanczos"
+    kname = f"{kbase}<{P}"
     k1_bytes = 12 * nnz + 4 * (n + 1) + 24 * n * P
     sweeps = math.ceil(cnt / P)
     b_eval_rank = m * (sweeps * (12 * nnz + 4 * (n + 1)) + 24 * n * cnt)
@@ -199,7 +220,7 @@ def main():
             achieved = k1_bytes / (k1_ms * 1e-3) / 1e9
             # PMC bytes were profiled on the sf1m graph (tools/gpu_prof.sh); other
             # graphs report traffic null
-            traffic = _pmc_traffic(kname) if args.config == "sf1m" else None
+            traffic = _pmc_traffic(kbase, P) if args.config == "sf1m" else None
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": kname + ">", "avg_launch_us": round(k1_ms * 1e3, 2),
@@ -228,7 +249,7 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "trace(exp(A)) evals/sec (+ achieved HBM GB/s), n=1M nnz=10M",
+            "metric": _metric_name(n, nnz),
             "value": round(value, 4), "unit": "evals/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KT_ABI_VERSION 1
+#define KT_ABI_VERSION 2
 
 enum kt_status {
     KT_OK = 0,
@@ -38,7 +38,8 @@ enum kt_status {
     KT_ERR_NOT_HERMITIAN = 3, /* fun_and_grad_krylov_exp.m:21-23                */
     KT_ERR_NOT_SQUARE = 4,    /* lanczos_krylov.m:36-38                         */
     KT_ERR_ALLOC = 5,         /* device allocation failed                       */
-    KT_ERR_UNSUPPORTED = 6    /* size / option outside what the build supports  */
+    KT_ERR_UNSUPPORTED = 6,   /* size / option outside what the build supports  */
+    KT_ERR_CALLBACK = 7       /* a caller-supplied callback returned non-zero   */
 };
 
 enum kt_fun { /* fun_update.m:43-59 */
@@ -104,8 +105,10 @@ int kt_trace_fun_update(kt_matrix_t A, int64_t rk, const double* U, const double
                         int it, int fun, double* Xm, int* iter, int* lucky);
 
 /* Elementwise scalar function for a function handle outside enum kt_fun:
- * y[i] = f(x[i]), i < count; called on the host, on the calling thread. */
-typedef void (*kt_scalar_fn)(const double* x, double* y, int64_t count, void* user);
+ * y[i] = f(x[i]), i < count; called on the host, on the calling thread.
+ * Returns 0 on success; any other value aborts the call, which then returns
+ * KT_ERR_CALLBACK (the partial result is discarded, never summed). */
+typedef int (*kt_scalar_fn)(const double* x, double* y, int64_t count, void* user);
 
 /* trace_fun_update with an arbitrary elementwise handle (trace_fun_update.m:
  * 85-89 `Xm = sum(fun(d1) - fun(d2))`; the same call as kt_trace_fun_update

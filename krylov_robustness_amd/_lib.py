@@ -30,7 +30,8 @@ class KrylovError(RuntimeError):
 
 
 # kt_status
-KT_OK, KT_ERR_ARG, KT_ERR_HIP, KT_ERR_NOT_HERMITIAN, KT_ERR_NOT_SQUARE, KT_ERR_ALLOC, KT_ERR_UNSUPPORTED = range(7)
+(KT_OK, KT_ERR_ARG, KT_ERR_HIP, KT_ERR_NOT_HERMITIAN, KT_ERR_NOT_SQUARE, KT_ERR_ALLOC, KT_ERR_UNSUPPORTED,
+ KT_ERR_CALLBACK) = range(8)
 # kt_afun (mc_trace.m's Afun kinds)
 AFUN_CODES = {"matrix": 0, "lanczos": 1, "expmv": 2}
 # kt_fun (fun_update.m:43-59)
@@ -42,8 +43,8 @@ _i64p = C.POINTER(C.c_int64)
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int)
 
-# kt_scalar_fn: y[i] = f(x[i]) for an elementwise handle outside kt_fun
-SCALAR_FN = C.CFUNCTYPE(None, _dp, _dp, C.c_int64, C.c_void_p)
+# kt_scalar_fn: y[i] = f(x[i]) for an elementwise handle outside kt_fun; 0 = ok
+SCALAR_FN = C.CFUNCTYPE(C.c_int, _dp, _dp, C.c_int64, C.c_void_p)
 # kt_reduce_fn: in-place sum of `count` doubles across ranks; 0 = ok
 REDUCE_FN = C.CFUNCTYPE(C.c_int, _dp, C.c_int64, C.c_void_p)
 

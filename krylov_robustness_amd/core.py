@@ -238,15 +238,31 @@ def trace_fun_update(A, U, B, tol=1e-12, it=None, debug=0, fun="exp", ctx: Optio
     name = getattr(fun, "__name__", fun) if callable(fun) else fun
     if callable(fun) and name not in _lib.FUN_CODES:
         # any elementwise handle (trace_fun_update.m:88 sum(fun(d1) - fun(d2))):
-        # evaluated on the host eigenvalue vectors through kt_trace_fun_update_fn
+        # evaluated on the host eigenvalue vectors through kt_trace_fun_update_fn.
+        # ctypes would print and drop an exception raised in the callback, so
+        # it is kept here, reported to the library as a non-zero status (the
+        # call aborts with KT_ERR_CALLBACK) and re-raised once the call returns.
+        raised = []
+
         def _f(x, y, count, user):
-            k = int(count)
-            xs = np.ctypeslib.as_array(x, shape=(k,))
-            np.ctypeslib.as_array(y, shape=(k,))[:] = np.asarray(fun(xs.copy()), dtype=np.float64)
+            try:
+                k = int(count)
+                xs = np.ctypeslib.as_array(x, shape=(k,))
+                fx = np.asarray(fun(xs.copy()), dtype=np.float64)
+                if fx.shape != (k,):
+                    raise ValueError(f"fun must map a length-{k} vector elementwise, got shape {fx.shape}")
+                np.ctypeslib.as_array(y, shape=(k,))[:] = fx
+                return 0
+            except BaseException as e:  # noqa: BLE001 -- re-raised after the call
+                raised.append(e)
+                return 1
         cb = _lib.SCALAR_FN(_f)
-        _lib.check(_lib.load().kt_trace_fun_update_fn(
+        st = _lib.load().kt_trace_fun_update_fn(
             D.handle, U.shape[1], _dptr(U), _dptr(B), float(tol), int(it or 0),
-            C.cast(cb, C.c_void_p), None, C.byref(xm), C.byref(itr), C.byref(lk)))
+            C.cast(cb, C.c_void_p), None, C.byref(xm), C.byref(itr), C.byref(lk))
+        if raised:
+            raise raised[0]
+        _lib.check(st)
     else:
         _lib.check(_lib.load().kt_trace_fun_update(
             D.handle, U.shape[1], _dptr(U), _dptr(B), float(tol), int(it or 0), _fun_code(fun),

@@ -194,6 +194,8 @@ struct kt_matrix_s {
     kt_context_s* twin_ctx = nullptr;
     kt_matrix_s* twin = nullptr;
     uint64_t twin_version = 0;
+    bool twin_failed = false;  // the last build failed (twin_of falls back to serial)
+    uint64_t twin_failed_version = 0;
 };
 
 namespace kt {

@@ -246,8 +246,11 @@ double trace_diff(const std::vector<double>& d1, const std::vector<double>& d2, 
     if (fun == kFunCallback) {  // sum(fun(d1) - fun(d2))
         if (!tl_scalar_fn.f) fail(KT_ERR_ARG, "no scalar function set");
         std::vector<double> f1(d1.size()), f2(d2.size());
-        tl_scalar_fn.f(d1.data(), f1.data(), (int64_t)d1.size(), tl_scalar_fn.user);
-        tl_scalar_fn.f(d2.data(), f2.data(), (int64_t)d2.size(), tl_scalar_fn.user);
+        // a failed handle aborts the call: its zero-filled or partial output
+        // must never reach the sum or the stop test
+        if (tl_scalar_fn.f(d1.data(), f1.data(), (int64_t)d1.size(), tl_scalar_fn.user) != 0 ||
+            tl_scalar_fn.f(d2.data(), f2.data(), (int64_t)d2.size(), tl_scalar_fn.user) != 0)
+            fail(KT_ERR_CALLBACK, "trace_fun_update: fun callback failed");
         for (size_t i = 0; i < d1.size(); ++i) x += f1[i] - f2[i];
         return x;
     }
@@ -901,25 +904,48 @@ static void gradient(kt_matrix_s* A, FunUpdateResult& fu, int64_t nom, const dou
 }
 
 // Second device copy of A on its own context (stream + workspace), rebuilt
-// when A was edited since (set_pairs keeps it current); nullptr when KT_TWIN=0.
+// when A was edited since (set_pairs keeps it current); nullptr when KT_TWIN=0
+// or when the copy cannot be built (e.g. HBM too full for a second A and its
+// workspace): the caller then runs the serial order, which needs no second
+// copy, instead of failing.  A failed build is not retried until A changes.
 kt_matrix_s* twin_of(kt_matrix_s* A) {
     static const bool off = getenv("KT_TWIN") && getenv("KT_TWIN")[0] == '0';
     if (off) return nullptr;
     if (A->twin && A->twin_version == A->version) return A->twin;
+    if (A->twin_failed && A->twin_failed_version == A->version) return nullptr;
     if (A->twin) {
         kt_matrix_destroy(A->twin);
         A->twin = nullptr;
     }
-    if (!A->twin_ctx && kt_context_create(A->ctx->device, &A->twin_ctx) != KT_OK)
-        fail(KT_ERR_HIP, std::string("twin context: ") + kt_last_error());
+    auto give_up = [&] {
+        if (A->twin) {
+            kt_matrix_destroy(A->twin);
+            A->twin = nullptr;
+        }
+        A->twin_failed = true;
+        A->twin_failed_version = A->version;
+        (void)hipGetLastError();  // a failed allocation must not leak into later checks
+        KT_HIP(hipSetDevice(A->ctx->device));
+        return (kt_matrix_s*)nullptr;
+    };
+    // KT_TWIN_FAULT=1 (tests): act as if the twin's allocation had failed
+    const char* fault = getenv("KT_TWIN_FAULT");
+    if (fault && fault[0] == '1') return give_up();
+    if (!A->twin_ctx && kt_context_create(A->ctx->device, &A->twin_ctx) != KT_OK) {
+        A->twin_ctx = nullptr;
+        return give_up();
+    }
     const int64_t n = A->n;
     std::vector<int64_t> ir(A->h_col.begin(), A->h_col.end());
     if (kt_matrix_create_csc(A->twin_ctx, n, A->h_rowptr.data(), ir.data(), A->h_val.data(), 0, &A->twin) !=
-        KT_OK)
-        fail(KT_ERR_HIP, std::string("twin matrix: ") + kt_last_error());
+        KT_OK) {
+        A->twin = nullptr;
+        return give_up();
+    }
     A->twin->symmetric = A->symmetric;
     A->twin->long_thresh = A->long_thresh;
     A->twin_version = A->version;
+    A->twin_failed = false;
     KT_HIP(hipSetDevice(A->ctx->device));
     return A->twin;
 }
@@ -1107,10 +1133,18 @@ int kt_fun_and_grad_krylov_fun(kt_matrix_t A, int64_t nom, const double* X, cons
         }
     } join{th};
     FunUpdateResult fu = fun_update_impl(A, k, U.data(), B.data(), dfun, tol_df, it);          // :64
+    bool serial = !A2;
     if (A2) {
         th.join();
-        if (terr.code != KT_OK) throw terr;
-    } else {
+        if (terr.code == KT_ERR_ALLOC) {  // the twin's workspace did not fit: serial order
+            (void)hipGetLastError();
+            KT_HIP(hipSetDevice(A->ctx->device));
+            serial = true;
+        } else if (terr.code != KT_OK) {
+            throw terr;
+        }
+    }
+    if (serial) {
         fval = trace_fun_update_impl(A, k, U.data(), B.data(), tol_f, it, fun, nullptr, nullptr);  // :65
     }
     *f = -fval;

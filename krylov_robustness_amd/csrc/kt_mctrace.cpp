@@ -316,7 +316,7 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
                 F.quad_cols(Y.col(0), ld, nm, qm.data());
                 for (int c = sh.rank, t = 0; c < mb; c += sh.world, ++t) qv[c] = qm[t];
             }
-            if (sh.allreduce(qv.data(), mb, sh.user) != 0) fail(KT_ERR_ARG, "mc_trace: all-reduce callback failed");
+            if (sh.allreduce(qv.data(), mb, sh.user) != 0) fail(KT_ERR_CALLBACK, "mc_trace: all-reduce callback failed");
             for (double v : qv) gsum += v;
         } else {
             gsum = F.trace_quad(Z.col(0), ld, mb);

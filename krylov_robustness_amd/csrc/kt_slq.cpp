@@ -137,8 +137,10 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     if (lane && !ctx->aux_stream[lane - 1])
         KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[lane - 1], hipStreamNonBlocking));
     hipStream_t st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
-    // KT_KY_BPC: row-group workgroups per CU of the pass (default 4)
-    static const int bpc = getenv("KT_KY_BPC") ? std::max(1, atoi(getenv("KT_KY_BPC"))) : 4;
+    // KT_KY_BPC: row-group workgroups per CU of the pass (default 4), read per
+    // sweep like KT_SLQ_LANES
+    const char* bpc_env = getenv("KT_KY_BPC");
+    const int bpc = bpc_env ? std::max(1, std::min(16, atoi(bpc_env))) : 4;
     const int grid = spmm_grid(n, P, ctx->num_cu * bpc);
     const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
     const int grid1 = grid + lblocks;

@@ -62,28 +62,50 @@ def allgather_concat(x, counts, group=None):
     return np.concatenate([p[:int(c)].cpu().numpy() for p, c in zip(parts, counts)])
 
 
-def reduce_callback(group=None):
+def reduce_callback(group=None, fail_on_rank=None):
     """A kt_reduce_fn (include/krylov_trace.h) that sums the buffer over the
     torch.distributed group: device tensors on RCCL ("nccl"), CPU tensors
-    on gloo.  Keep the returned object alive for the duration of the call."""
-    import ctypes as C
+    on gloo.  Keep the returned object alive for the duration of the call.
+
+    The buffer travels with one extra element, the rank's local error flag:
+    a rank whose own part fails (reading the buffer, moving it to the
+    device) still joins the collective with that flag set, so every rank
+    sees the failure in the same round and returns 1 (the library call then
+    fails with KT_ERR_CALLBACK everywhere) instead of the other ranks
+    waiting in all_reduce until the process group times out.  Test hook:
+    `fail_on_rank` makes that rank's local part fail."""
     import numpy as np
     import torch
     import torch.distributed as dist
     from . import _lib
 
     def _cb(buf, count, user):
+        k = int(count)
         try:
-            arr = np.ctypeslib.as_array(buf, shape=(int(count),))
             backend = dist.get_backend(group)
             dev = (torch.device("cuda", torch.cuda.current_device()) if backend == "nccl"
                    else torch.device("cpu"))
-            t = torch.from_numpy(arr.copy()).to(dev)
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-            arr[:] = t.cpu().numpy()
-            return 0
-        except Exception:  # reported to the caller as a kt status
+        except Exception:  # no usable process group: nothing to join
             return 1
+        arr = None
+        try:
+            if fail_on_rank is not None and dist.get_rank(group) == fail_on_rank:
+                raise RuntimeError("injected reduce failure")
+            arr = np.ctypeslib.as_array(buf, shape=(k,))
+            t = torch.from_numpy(np.append(arr, 0.0)).to(dev)
+        except Exception:
+            arr = None
+            t = torch.zeros(k + 1, dtype=torch.float64, device=dev)
+            t[k] = 1.0  # local failure flag
+        try:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+            out = t.cpu().numpy()
+        except Exception:
+            return 1
+        if out[k] != 0.0 or arr is None:
+            return 1
+        arr[:] = out[:k]
+        return 0
 
     return _lib.REDUCE_FN(_cb)
 

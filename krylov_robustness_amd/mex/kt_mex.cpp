@@ -130,10 +130,11 @@ int fun_arg(const mxArray* h, int dflt, bool generic = false) {
 mxArray* scalar(double v) { return mxCreateDoubleScalar(v); }
 
 // kt_scalar_fn over a MATLAB handle: y = feval(h, x) on a count x 1 column.
-// Runs inside the library call, so a failure is only recorded (NaN result)
-// and raised after the call returns: no MATLAB error unwinds library frames.
+// Runs inside the library call, so a failure is only recorded and returned
+// as a non-zero status (the library then aborts with KT_ERR_CALLBACK); the
+// MATLAB error is raised after the call returns, so none unwinds library frames.
 bool g_feval_failed = false;
-void feval_scalar_fn(const double* x, double* y, int64_t count, void* user) {
+int feval_scalar_fn(const double* x, double* y, int64_t count, void* user) {
     mxArray* h = static_cast<mxArray*>(user);
     mxArray* in = mxCreateDoubleMatrix((mwSize)count, 1, mxREAL);
     memcpy(mxGetDoubles(in), x, sizeof(double) * (size_t)count);
@@ -149,6 +150,7 @@ void feval_scalar_fn(const double* x, double* y, int64_t count, void* user) {
     }
     mxDestroyArray(in);
     if (out) mxDestroyArray(out);
+    return ok ? 0 : 1;
 }
 
 // ---- mc_trace with a function-handle Afun --------------------------------
@@ -375,12 +377,12 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
               "trace_fun_update");
     else {  // any elementwise handle: sum(fun(d1) - fun(d2)) with fun evaluated by MATLAB (:88)
         g_feval_failed = false;
-        check(kt_trace_fun_update_fn(A, (int64_t)mxGetN(U), mxGetDoubles(U), mxGetDoubles(B),
-                                     scalar_or(nrhs, prhs, 3, 1e-12), (int)scalar_or(nrhs, prhs, 4, 0),
-                                     feval_scalar_fn, const_cast<mxArray*>(fh), &xm, &iter, &lucky),
-              "trace_fun_update");
+        const int st = kt_trace_fun_update_fn(A, (int64_t)mxGetN(U), mxGetDoubles(U), mxGetDoubles(B),
+                                              scalar_or(nrhs, prhs, 3, 1e-12), (int)scalar_or(nrhs, prhs, 4, 0),
+                                              feval_scalar_fn, const_cast<mxArray*>(fh), &xm, &iter, &lucky);
         if (g_feval_failed)
             mexErrMsgIdAndTxt("krylov_hip:fun", "fun must map a real double vector elementwise");
+        check(st, "trace_fun_update");
     }
     {  // warnings stay warnings (trace_fun_update.m:119-130)
         const int it_arg = (int)scalar_or(nrhs, prhs, 4, 0);

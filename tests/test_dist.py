@@ -158,3 +158,42 @@ def test_gloo_world2_reduce_callback():
         p.join(timeout=60)
     assert st == 0
     assert vals == [1.5 * c + 0.25 for c in range(10)]
+
+
+def _reduce_fail_worker(rank, world, port, out):
+    """One rank's local part of the reduce fails (test hook): it still joins
+    the collective with its error flag set, so EVERY rank returns 1 in the
+    same round (no rank is left waiting in all_reduce)."""
+    import ctypes as C
+    import torch.distributed as dist
+    from krylov_robustness_amd.dist import reduce_callback
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cb = reduce_callback(fail_on_rank=1)
+    buf = (C.c_double * 10)(*[float(rank)] * 10)
+    st = cb(buf, 10, None)
+    ok = reduce_callback()  # the group is still usable afterwards
+    buf2 = (C.c_double * 3)(*[1.0] * 3)
+    st2 = ok(buf2, 3, None)
+    out.put((rank, st, list(buf), st2, list(buf2)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_reduce_callback_failure_reaches_every_rank():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reduce_fail_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, st, buf, st2, buf2 in res:
+        assert st == 1                      # failed on both ranks
+        assert buf == [float(rank)] * 10    # the buffer is left untouched
+        assert st2 == 0 and buf2 == [2.0] * 3

@@ -90,6 +90,36 @@ def test_trace_fun_update_generic_handle(kra, gpu_ctx, values):
     assert xd == pytest.approx(ko.exact_trace_update(Ad, Ud, B, f), rel=1e-11)
 
 
+def test_trace_fun_update_failing_handle_raises(kra, gpu_ctx, values):
+    """A handle that raises (or returns the wrong shape) aborts the call: the
+    exception reaches the caller instead of a zero-filled f(d) being summed
+    into Xm = 0 (kt_scalar_fn status -> KT_ERR_CALLBACK).  Lanczos path
+    (rome) and dense shortcut (denmark); the context stays usable after."""
+    B = -np.array([[0.0, 1.0], [1.0, 0.0]])
+
+    class Boom(RuntimeError):
+        pass
+
+    def bad(x):
+        raise Boom("user fun failed")
+
+    def wrong_shape(x):
+        return np.zeros(x.size + 1)
+
+    for name in ["rome", "denmark"]:
+        A = load_graph(name)
+        D = kra.DeviceMatrix(A, gpu_ctx)
+        n = A.shape[0]
+        U = np.zeros((n, 2)); U[3, 0] = 1; U[7, 1] = 1
+        with pytest.raises(Boom):
+            kra.trace_fun_update(D, U, B, 1e-12, min(100, n), fun=bad, ctx=gpu_ctx)
+        with pytest.raises(ValueError):
+            kra.trace_fun_update(D, U, B, 1e-12, min(100, n), fun=wrong_shape, ctx=gpu_ctx)
+        xm, _, _ = kra.trace_fun_update(D, U, B, 1e-12, min(100, n), fun=lambda x: np.exp(x),
+                                        ctx=gpu_ctx)
+        assert xm == pytest.approx(ko.exact_trace_update(A, U, B, "exp"), rel=1e-8, abs=1e-10)
+
+
 def test_trace_fun_update_rank6_sinh(kra, gpu_ctx):
     A = load_graph("india")
     n = A.shape[0]
@@ -218,6 +248,29 @@ def test_fun_and_grad_fun_after_edge_edit(kra, gpu_ctx):
     assert kra.normest(D, 1e-2, ctx=gpu_ctx) == kra.normest(kra.DeviceMatrix(A1, gpu_ctx), 1e-2, ctx=gpu_ctx)
     assert kra.normest(D, 1e-2, ctx=gpu_ctx) == pytest.approx(ko.normest(A1, 1e-2), rel=1e-9)
     np.testing.assert_allclose(g1, g2, rtol=1e-12, atol=1e-14)
+
+
+def test_fun_and_grad_fun_twin_unavailable_falls_back(kra, gpu_ctx, monkeypatch):
+    """When the twin copy cannot be built (KT_TWIN_FAULT=1 injects the
+    allocation failure a full HBM would give), fun_and_grad_krylov_fun runs
+    fun_update and trace_fun_update in the serial order on the one copy --
+    the same objective and gradient, no error (the twin is an optimisation)."""
+    A = load_graph("india")
+    Om = edges(A, 5, offset=100)
+    rng = np.random.default_rng(11)
+    X = rng.uniform(-0.5, 1.0, 5)
+    dfA = rng.normal(size=5)
+    tol = 1e-6 * np.sinh(ko.normest(A, 1e-2))
+    f0, g0 = kra.fun_and_grad_krylov_fun(X, kra.DeviceMatrix(A, gpu_ctx), Om, "sinh", "cosh", dfA, tol,
+                                         100, ctx=gpu_ctx)
+    monkeypatch.setenv("KT_TWIN_FAULT", "1")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    f1, g1 = kra.fun_and_grad_krylov_fun(X, D, Om, "sinh", "cosh", dfA, tol, 100, ctx=gpu_ctx)
+    assert f1 == f0
+    np.testing.assert_array_equal(g1, g0)
+    monkeypatch.delenv("KT_TWIN_FAULT")
+    f2, _ = kra.fun_and_grad_krylov_fun(X, D, Om, "sinh", "cosh", dfA, tol, 100, ctx=gpu_ctx)
+    assert f2 == f0  # not retried for the same matrix version; still the same value
 
 
 def test_trace_fun_update_leaf_candidates(kra, gpu_ctx):
