@@ -14,7 +14,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkrylov_hip.so")
+# KT_LIB: another build of the same library (tools' A/B of compile-time variants)
+LIB_PATH = os.environ.get("KT_LIB") or os.path.join(_HERE, "libkrylov_hip.so")
 
 
 class KrylovLibraryError(RuntimeError):

@@ -93,6 +93,7 @@ enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_START = 2, PROF_NSLOTS = 3 };
 // run on two streams.
 struct SweepBufs {
     DevBuf X0, X1, Y, partial, coef, scales, k2s, trec;
+    DevBuf tick;  // arrival tickets of the fused coefficient step (zeroed when allocated)
 };
 
 struct Workspace {

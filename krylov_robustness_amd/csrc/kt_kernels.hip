@@ -61,6 +61,14 @@ template <int P> using Geo = GeoW<P, (P >= 2) ? 2 : 1>;
 #define KT_K1_VW 4
 #endif
 template <int P> using GeoK1 = GeoW<P, (P >= 16) ? (KT_K1_VW < P ? KT_K1_VW : P) : (P >= 2) ? 2 : 1>;
+// y-form passes (start + step): 16 B per lane, 8 lanes per 128-B probe row.
+// 72 VGPRs = 3 workgroups of 512 per CU vs 118 VGPRs = 2 with 32 B per lane:
+// +1.4 % evals/s with two sweep lanes (profiles/r02_ab_occupancy.txt); 4 per
+// CU (64 VGPRs) is 10 % slower -- more rows in flight thrash the L2.
+#ifndef KT_KY_VW
+#define KT_KY_VW 2
+#endif
+template <int P> using GeoKY = GeoW<P, (P >= 16) ? (KT_KY_VW < P ? KT_KY_VW : P) : (P >= 2) ? 2 : 1>;
 // block SpMM lane width (doubles per lane) from P = 16 on
 #ifndef KT_BLK_VW
 #define KT_BLK_VW 2
@@ -418,6 +426,163 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
     }
 }
 
+// One probe's coefficient step from the pass's three sums d0 = X.t,
+// d1 = X.Out, d2 = Out.Out (shared by k_ycoef and the fused pass tail).
+__device__ __forceinline__ void ycoef_probe(int p, int P, double d0, double d1, double d2, int start,
+                                            int last, double s0, double* __restrict__ ys,
+                                            double* __restrict__ t_alpha, double* __restrict__ t_up,
+                                            double* __restrict__ t_low, double* __restrict__ guard) {
+    double an, bn, bnext_sq, ny2, g = 1.0;
+    if (start) {
+        an = d1 * s0;  // v_0 . y_0 with v_0 = s0 z
+        ny2 = d2;
+        bn = 0.0;      // beta_0
+        bnext_sq = ny2 - an * an;
+        ys[1 * P + p] = 0.0;
+        ys[2 * P + p] = 0.0;
+        ys[4 * P + p] = 0.0;
+        guard[p] = 1.0;
+    } else {
+        const double aj = ys[0 * P + p], bj = ys[1 * P + p], am1 = ys[2 * P + p];
+        const double nyj = ys[3 * P + p], ydj = ys[4 * P + p], b1 = ys[5 * P + p];
+        g = guard[p];
+        const double b1sq = b1 * b1;
+        an = (d0 - 2.0 * aj * nyj - 2.0 * bj * ydj + aj * aj * aj + 2.0 * aj * bj * bj + bj * bj * am1) /
+             b1sq;
+        ny2 = d2;
+        bn = b1;
+        bnext_sq = ny2 - an * an - b1sq;
+        ys[1 * P + p] = b1;
+        ys[2 * P + p] = aj;
+        ys[4 * P + p] = d1;
+    }
+    const double bnext = sqrt(fmax(bnext_sq, 0.0));
+    ys[0 * P + p] = an;
+    ys[3 * P + p] = ny2;
+    ys[5 * P + p] = bnext;
+    t_alpha[p] = an;
+    t_up[p] = bn;
+    t_low[p] = bnext;
+    if (!last) {
+        const double ratio = bnext_sq / ny2;
+        guard[p] = (ratio < g || !(ratio == ratio)) ? ratio : g;  // NaN sticks
+    }
+    const bool ok = bnext > 0.0 && bnext < INFINITY;
+    const double inv = ok ? 1.0 / bnext : 0.0;
+    ys[6 * P + p] = inv;
+    ys[7 * P + p] = an * inv;
+    ys[8 * P + p] = bn * inv;
+}
+
+// ---------------------------------------------------------------------------
+// Fused coefficient step (the default y-form path): the pass's workgroups
+// hand their 3P partial sums to the pass's LAST arriving workgroup, which
+// runs k_ycoef's recurrence itself -- no separate launch, so the next pass
+// of the sweep is not queued behind another lane's workgroups for CU slots
+// (26 us per k_ycoef under two lanes vs 4.5 us alone, profiles/r02_timeline).
+// Two levels keep the serial tail short: workgroups of a group of
+// kTickGroup consecutive ids -> the group's last arriver sums the group's
+// slabs in id order; group sums -> the last group reducer sums them in group
+// order.  Fixed orders: bitwise reproducible whatever the arrival order.
+// Hand-off (cdna_hip_programming.md Guideline 16, counter form with
+// write-through slabs): slab stores sc1 -> every storing wave drains vmcnt
+// -> barrier -> one lane takes a relaxed agent-scope ticket; the last
+// arriver acquires (agent) before loading.  No workgroup ever waits for
+// another (no spin), so residency cannot deadlock it.  Tickets are zeroed
+// once at allocation and reset by their reducer for the next launch.
+// ---------------------------------------------------------------------------
+constexpr int kTickGroup = 32;
+typedef __attribute__((address_space(1))) unsigned int kt_gu32;
+typedef __attribute__((address_space(1))) unsigned long long kt_gu64;
+
+struct YFuse {
+    double* slab;   // [grid][3P] per-workgroup sums
+    double* gpart;  // [groups][3P] per-group sums
+    int* tick;      // [groups + 1] arrival tickets
+    double* ys;
+    double *t_alpha, *t_up, *t_low, *guard;
+    int start, last;
+    double s0;
+};
+
+__device__ __forceinline__ void st_wt(double* p, double v) {  // write-through (sc1) 8-B store
+    __hip_atomic_store((kt_gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int P, int BLOCK>
+__device__ __forceinline__ void fused_ycoef_tail(double (*red)[3][P], const YFuse& f) {
+    constexpr int WAVES = BLOCK / 64, NS = 3 * P;
+    __shared__ int s_last;
+    __shared__ double s_sum[NS];
+    const int tid = threadIdx.x, b = blockIdx.x, nblk = gridDim.x;
+    const int g = b / kTickGroup, g0 = g * kTickGroup;
+    const int gn = (nblk - g0 < kTickGroup) ? nblk - g0 : kTickGroup;
+    const int ngroups = (nblk + kTickGroup - 1) / kTickGroup;
+    for (int t = tid; t < NS; t += BLOCK) {
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) v += red[w][t / P][t % P];
+        st_wt(f.slab + (int64_t)b * NS + t, v);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add((kt_gu32*)(f.tick + g), 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (int)old == gn - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // group reducer: the group's slabs in id order
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = tid; t < NS; t += BLOCK) {
+        const double* col = f.slab + (int64_t)g0 * NS + t;
+        double s = 0.0;
+        for (int i0 = 0; i0 < gn; i0 += 8) {  // 8 loads in flight, added in id order
+            double x[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = i0 + i < gn ? col[(int64_t)(i0 + i) * NS] : 0.0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s += x[i];
+        }
+        st_wt(f.gpart + (int64_t)g * NS + t, s);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __hip_atomic_store((kt_gu32*)(f.tick + g), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned old = __hip_atomic_fetch_add((kt_gu32*)(f.tick + ngroups), 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (int)old == ngroups - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // final reducer: group sums in group order, then the recurrence
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = tid; t < NS; t += BLOCK) {
+        double s = 0.0;
+        for (int gg = 0; gg < ngroups; gg += 8) {
+            double x[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) x[i] = gg + i < ngroups ? f.gpart[(int64_t)(gg + i) * NS + t] : 0.0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s += x[i];
+        }
+        s_sum[t] = s;
+    }
+    __syncthreads();
+    if (tid == 0)
+        __hip_atomic_store((kt_gu32*)(f.tick + ngroups), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int p = tid; p < P; p += BLOCK)
+        ycoef_probe(p, P, s_sum[p], s_sum[P + p], s_sum[2 * P + p], f.start, f.last, f.s0, f.ys,
+                    f.t_alpha, f.t_up, f.t_low, f.guard);
+}
+
 // ---------------------------------------------------------------------------
 // KY: the A-image ("y-form") probe Lanczos step -- the whole step in ONE
 // streaming pass (no K2).  With y_j = A v_j the three-term recurrence
@@ -434,9 +599,9 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
 // nullptr (the last pass of a sweep): only X.t is formed -- Yold is not read
 // and nothing is stored.
 // ---------------------------------------------------------------------------
-template <int P, int FLAGS, class G = Geo<P>>
-__device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s, const double* cg,
-                                               const double* ca, const double* cb, bool has_old,
+template <int P, int FLAGS, class G = Geo<P>, class C = const double*>
+__device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s, C cg,
+                                               C ca, C cb, bool has_old,
                                                const double* __restrict__ X,
                                                const double* __restrict__ Yold,
                                                double* __restrict__ Out, double* d0, double* d1,
@@ -520,8 +685,8 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos_start(
     const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
     int n, const uint32_t* __restrict__ S, double s0, double* __restrict__ Out,
     double* __restrict__ partial, const int* __restrict__ long_rows, int n_long, int long_thresh,
-    int long_blocks) {
-    using G = GeoK1<P>;
+    int long_blocks, YFuse fz) {
+    using G = GeoKY<P>;
     using V = VecT<G::VEC>;
     constexpr int WAVES = BLOCK / 64;
     constexpr int W = (P + 31) / 32;
@@ -597,6 +762,10 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos_start(
         }
     }
     __syncthreads();
+    if (fz.tick) {  // fused coefficient step (default)
+        fused_ycoef_tail<P, BLOCK>(red, fz);
+        return;
+    }
     for (int t = threadIdx.x; t < 3 * P; t += BLOCK) {
         const int q = t / P, p = t % P;
         double v = 0.0;
@@ -606,13 +775,26 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos_start(
     }
 }
 
+// KT_KY_WPE: minimum waves per SIMD the y-form pass is compiled for (register
+// budget: 8 -> <= 64 VGPRs = 4 workgroups of 512 per CU; 0 = compiler's choice)
+#ifndef KT_KY_WPE
+#define KT_KY_WPE 0
+#endif
+#ifndef KT_KY_CF_LDS
+#define KT_KY_CF_LDS 0
+#endif
+#if KT_KY_WPE > 0
+#define KT_KY_BOUNDS(B) __launch_bounds__(B, KT_KY_WPE)
+#else
+#define KT_KY_BOUNDS(B) __launch_bounds__(B)
+#endif
 template <int P, int BLOCK, int FLAGS>
-__global__ __launch_bounds__(BLOCK) void k_spmm_lanczos(
+__global__ KT_KY_BOUNDS(BLOCK) void k_spmm_lanczos(
     const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
     int n, const double* __restrict__ X, const double* __restrict__ Yold, double* __restrict__ Out,
     const double* __restrict__ coef, double* __restrict__ partial,
-    const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks) {
-    using G = GeoK1<P>;
+    const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks, YFuse fz) {
+    using G = GeoKY<P>;
     constexpr int WAVES = BLOCK / 64;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -624,14 +806,27 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos(
     __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         Out, 0, (FLAGS & KF_SC1) ? (int)((int64_t)n * P * 8) : 0, 0x00020000);
 
-    double cg[G::VEC], ca[G::VEC], cb[G::VEC], d0[G::VEC], d1[G::VEC], d2[G::VEC];
+    double d0[G::VEC], d1[G::VEC], d2[G::VEC];
+#pragma unroll
+    for (int e = 0; e < G::VEC; ++e) d0[e] = d1[e] = d2[e] = 0.0;
+#if KT_KY_CF_LDS
+    // (g, a, b) read from LDS per row instead of 3 x VEC registers per lane
+    // (volatile: the compiler must not hoist them back into registers)
+    __shared__ double s_cf[3 * P];
+    for (int t = threadIdx.x; t < 3 * P; t += BLOCK) s_cf[t] = coef[t];
+    __syncthreads();
+    const volatile double* cg = s_cf + p0;
+    const volatile double* ca = s_cf + P + p0;
+    const volatile double* cb = s_cf + 2 * P + p0;
+#else
+    double cg[G::VEC], ca[G::VEC], cb[G::VEC];
 #pragma unroll
     for (int e = 0; e < G::VEC; ++e) {
         cg[e] = coef[p0 + e];
         ca[e] = coef[P + p0 + e];
         cb[e] = coef[2 * P + p0 + e];
-        d0[e] = d1[e] = d2[e] = 0.0;
     }
+#endif
 
     if ((int)blockIdx.x < long_blocks) {
         for (int li = blockIdx.x * WAVES + wave; li < n_long; li += long_blocks * WAVES) {
@@ -647,7 +842,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos(
 #pragma unroll
                 for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
             if (grp == 0)
-                row_epilogue_y<P, FLAGS, G>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2,
+                row_epilogue_y<P, FLAGS, G, decltype(cg)>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2,
                                            orsrc);
         }
     } else {
@@ -661,7 +856,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos(
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
             gather_row<P, FLAGS, G>(beg, end, 1, p0, col, val, X, s);
-            row_epilogue_y<P, FLAGS, G>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2,
+            row_epilogue_y<P, FLAGS, G, decltype(cg)>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2,
                                            orsrc);
         }
     }
@@ -684,6 +879,10 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos(
         }
     }
     __syncthreads();
+    if (fz.tick) {  // fused coefficient step (default)
+        fused_ycoef_tail<P, BLOCK>(red, fz);
+        return;
+    }
     for (int t = threadIdx.x; t < 3 * P; t += BLOCK) {  // slot t = q * P + p
         const int q = t / P, p = t % P;
         double v = 0.0;
@@ -1004,61 +1203,12 @@ __global__ __launch_bounds__(192) void k_ycoef(const double* __restrict__ partia
                                                double* __restrict__ guard) {
     const int p = blockIdx.x;
     const int q = threadIdx.x >> 6;
-    // the recurrence state is loaded before the slab reduction so that its
-    // round trip overlaps the reduction's
-    double aj = 0.0, bj = 0.0, am1 = 0.0, nyj = 0.0, ydj = 0.0, b1 = 0.0, g = 1.0;
-    if (threadIdx.x == 0 && !start) {
-        aj = ys[0 * P + p];
-        bj = ys[1 * P + p];
-        am1 = ys[2 * P + p];
-        nyj = ys[3 * P + p];
-        ydj = ys[4 * P + p];
-        b1 = ys[5 * P + p];
-        g = guard[p];
-    }
     const double r = wave_reduce_slot(partial, nblk, q * P + p);
     __shared__ double d[3];
     if ((threadIdx.x & 63) == 0) d[q] = r;
     __syncthreads();
     if (threadIdx.x != 0) return;
-    double an, bn, bnext_sq, ny2;
-    if (start) {
-        an = d[1] * s0;  // v_0 . y_0 with v_0 = s0 z
-        ny2 = d[2];
-        bn = 0.0;        // beta_0
-        bnext_sq = ny2 - an * an;
-        ys[1 * P + p] = 0.0;
-        ys[2 * P + p] = 0.0;
-        ys[4 * P + p] = 0.0;
-        g = 1.0;
-        guard[p] = 1.0;
-    } else {
-        const double b1sq = b1 * b1;
-        an = (d[0] - 2.0 * aj * nyj - 2.0 * bj * ydj + aj * aj * aj + 2.0 * aj * bj * bj +
-              bj * bj * am1) / b1sq;
-        ny2 = d[2];
-        bn = b1;
-        bnext_sq = ny2 - an * an - b1sq;
-        ys[1 * P + p] = b1;
-        ys[2 * P + p] = aj;
-        ys[4 * P + p] = d[1];
-    }
-    const double bnext = sqrt(fmax(bnext_sq, 0.0));
-    ys[0 * P + p] = an;
-    ys[3 * P + p] = ny2;
-    ys[5 * P + p] = bnext;
-    t_alpha[p] = an;
-    t_up[p] = bn;
-    t_low[p] = bnext;
-    if (!last) {
-        const double ratio = bnext_sq / ny2;
-        guard[p] = (ratio < g || !(ratio == ratio)) ? ratio : g;  // NaN sticks
-    }
-    const bool ok = bnext > 0.0 && bnext < INFINITY;
-    const double inv = ok ? 1.0 / bnext : 0.0;
-    ys[6 * P + p] = inv;
-    ys[7 * P + p] = an * inv;
-    ys[8 * P + p] = bn * inv;
+    ycoef_probe(p, P, d[0], d[1], d[2], start, last, s0, ys, t_alpha, t_up, t_low, guard);
 }
 
 // ---------------------------------------------------------------------------
@@ -1577,16 +1727,26 @@ hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, doub
     });
 }
 
+static YFuse to_fuse(const YFuseArgs* a) {
+    YFuse f{};
+    if (a) f = YFuse{a->slab, a->gpart, a->tick, a->ys, a->t_alpha, a->t_up, a->t_low, a->guard,
+                     a->start, a->last, a->s0};
+    return f;
+}
+
+int fuse_groups(int grid) { return (grid + kTickGroup - 1) / kTickGroup; }
+
 hipError_t launch_spmm_lanczos(int P, int flags, int grid, const int* rp, const int* ci,
                                const double* va, int n, const double* X, const double* Yold,
                                double* Out, const double* coef, double* partial,
                                const int* long_rows, int n_long, int long_thresh, int long_blocks,
-                               hipStream_t st) {
+                               hipStream_t st, const YFuseArgs* fuse) {
+    const YFuse fz = to_fuse(fuse);
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
 #define KT_KY(F)                                                                                   \
     k_spmm_lanczos<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, X, Yold, Out, coef, partial, \
-                                                           long_rows, n_long, long_thresh, long_blocks)
+                                                           long_rows, n_long, long_thresh, long_blocks, fz)
         switch (flags & (KF_UNIT | KF_NTY | KF_SC1)) {
         case 0: KT_KY(0); break;
         case KF_UNIT: KT_KY(KF_UNIT); break;
@@ -1614,13 +1774,15 @@ hipError_t launch_rademacher_signs(int P, int n, uint64_t seed, int64_t probe_ba
 hipError_t launch_spmm_lanczos_start(int P, int flags, int grid, const int* rp, const int* ci,
                                      const double* va, int n, const uint32_t* S, double s0,
                                      double* Out, double* partial, const int* long_rows, int n_long,
-                                     int long_thresh, int long_blocks, hipStream_t st) {
+                                     int long_thresh, int long_blocks, hipStream_t st,
+                                     const YFuseArgs* fuse) {
+    const YFuse fz = to_fuse(fuse);
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
 #define KT_KS(F)                                                                                 \
     k_spmm_lanczos_start<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, S, s0, Out, partial, \
                                                                  long_rows, n_long, long_thresh,  \
-                                                                 long_blocks)
+                                                                 long_blocks, fz)
         switch (flags & (KF_UNIT | KF_NTY | KF_SC1)) {
         case 0: KT_KS(0); break;
         case KF_UNIT: KT_KS(KF_UNIT); break;

@@ -44,19 +44,33 @@ hipError_t launch_update(int P, int grid, int n, const double* y, double* uprev,
                          bool nt = false);
 hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, double* scale_next,
                        double* t_low, hipStream_t st);
-// y-form probe Lanczos (one pass per step) and its per-probe coefficients;
-// Yold == nullptr selects start mode
+// y-form probe Lanczos (one pass per step) and its per-probe coefficients.
+// With `fuse` the pass's last arriving workgroup runs the coefficient step
+// itself (k_ycoef's recurrence; slab [grid][3P], gpart [fuse_groups(grid)][3P],
+// tick [fuse_groups(grid) + 1] zeroed once); without, it writes slot-major
+// partials for launch_ycoef.
+struct YFuseArgs {
+    double* slab;
+    double* gpart;
+    int* tick;
+    double* ys;
+    double *t_alpha, *t_up, *t_low, *guard;
+    int start, last;
+    double s0;
+};
+int fuse_groups(int grid);
 hipError_t launch_spmm_lanczos(int P, int flags, int grid, const int* rp, const int* ci,
                                const double* va, int n, const double* X, const double* Yold,
                                double* Out, const double* coef, double* partial,
                                const int* long_rows, int n_long, int long_thresh, int long_blocks,
-                               hipStream_t st);
+                               hipStream_t st, const YFuseArgs* fuse = nullptr);
 hipError_t launch_rademacher_signs(int P, int n, uint64_t seed, int64_t probe_base,
                                   const int* perm, uint32_t* S, hipStream_t st);
 hipError_t launch_spmm_lanczos_start(int P, int flags, int grid, const int* rp, const int* ci,
                                      const double* va, int n, const uint32_t* S, double s0,
                                      double* Out, double* partial, const int* long_rows, int n_long,
-                                     int long_thresh, int long_blocks, hipStream_t st);
+                                     int long_thresh, int long_blocks, hipStream_t st,
+                                     const YFuseArgs* fuse = nullptr);
 hipError_t launch_ycoef(int P, const double* partial, int nblk, int start, int last, double s0,
                         double* ys, double* t_alpha, double* t_up, double* t_low, double* guard,
                         hipStream_t st);

@@ -149,7 +149,16 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     w.X0.ensure(blk_bytes);
     w.X1.ensure(blk_bytes);
     w.Y.ensure(blk_bytes);
-    w.partial.ensure(sizeof(double) * (size_t)3 * grid1 * P);
+    // KT_KY_FUSED=1: the pass's last arriving workgroup runs the coefficient
+    // step instead of a k_ycoef launch per step (read per sweep).  Measured
+    // neutral with two lanes (+-0.3 %) and 2 % slower with one
+    // (profiles/r02_ab_fused.txt): its serial hand-off tail costs what the
+    // launch saved, so the separate launch stays the default.
+    const char* fe = getenv("KT_KY_FUSED");
+    const bool fused = fe && fe[0] == '1';
+    const int ngroups = fuse_groups(grid1);
+    // slabs [grid1][3P] + group sums [ngroups][3P] (fused) or slot-major [3P][grid1]
+    w.partial.ensure(sizeof(double) * (size_t)3 * P * (grid1 + ngroups));
     w.coef.ensure(sizeof(double) * 9 * P);
     const size_t rec = (size_t)3 * m * P + P;
     w.trec.ensure(sizeof(double) * rec);
@@ -158,6 +167,22 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     double* trec = w.trec.as<double>();
     double* guard = trec + (size_t)3 * m * P;
     auto rec_at = [&](int row, int j) { return trec + (size_t)(row * m + j) * P; };
+    const size_t tick_bytes = ((sizeof(int) * (size_t)(ngroups + 1) + 15) / 16) * 16;
+    if (w.tick.bytes < tick_bytes) {  // every reducer resets its ticket: zero once
+        w.tick.ensure(tick_bytes);
+        KT_HIP(hipMemsetAsync(w.tick.ptr, 0, w.tick.bytes, st));
+    }
+    YFuseArgs fz{part, part + (size_t)3 * P * grid1, w.tick.as<int>(), ys, nullptr, nullptr, nullptr,
+                 guard, 0, 0, 0.0};
+    auto fuse_at = [&](int j, int start, int last, double s) {
+        fz.t_alpha = rec_at(0, j);
+        fz.t_up = rec_at(1, j);
+        fz.t_low = rec_at(2, j);
+        fz.start = start;
+        fz.last = last;
+        fz.s0 = s;
+        return fused ? &fz : nullptr;
+    };
     int flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
     if (blk_bytes >= ((size_t)1 << 31)) flags &= ~16;  // sc1 buffer stores take 32-bit offsets
     const double s0 = 1.0 / std::sqrt((double)n);  // v_0 = z / ||z||, ||z||^2 = n
@@ -171,19 +196,22 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     double* Ot = w.X0.as<double>();  // y_{j+1}
     prof_begin(ctx, PROF_START, st);
     KT_HIP(launch_spmm_lanczos_start(P, flags, grid1, M.rowptr, M.col, M.val, n, Z, s0, Xc, part,
-                                     M.long_rows, M.n_long, A->long_thresh, lblocks, st));
+                                     M.long_rows, M.n_long, A->long_thresh, lblocks, st,
+                                     fuse_at(0, 1, m == 1, s0)));
     prof_end(ctx, PROF_START, st);
-    KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, s0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0),
-                        guard, st));
+    if (!fused)
+        KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, s0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0),
+                            guard, st));
     for (int j = 0; j + 1 < m; ++j) {
         prof_begin(ctx, PROF_SPMM, st);
         const bool last = j + 2 == m;  // y_{m} is never used: alpha_{m-1} needs only X.t
         KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
                                    last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long,
-                                   A->long_thresh, lblocks, st));
+                                   A->long_thresh, lblocks, st, fuse_at(j + 1, 0, last, 0.0)));
         prof_end(ctx, PROF_SPMM, st);
-        KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1),
-                            rec_at(2, j + 1), guard, st));
+        if (!fused)
+            KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1),
+                                rec_at(2, j + 1), guard, st));
         Yo = Xc;  // y_{j+1} overwrites y_{j-1} from the next pass on
         Xc = Ot;
         Ot = Yo;
