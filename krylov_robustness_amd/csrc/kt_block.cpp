@@ -36,12 +36,69 @@ static void rb(rocblas_status s, const char* what) {
         fail(KT_ERR_HIP, std::string(what) + ": " + rocblas_status_to_string(s));
 }
 
-void DevMat::alloc(kt_context_s* ctx, int64_t n_, int ld_) {
+void* ScratchPool::take(size_t want, size_t* got) {
+    size_t best = free.size();
+    for (size_t i = 0; i < free.size(); ++i)
+        if (free[i].first >= want && free[i].first <= 4 * want &&
+            (best == free.size() || free[i].first < free[best].first))
+            best = i;
+    if (best < free.size()) {
+        void* p = free[best].second;
+        *got = free[best].first;
+        free.erase(free.begin() + (std::ptrdiff_t)best);
+        return p;
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess && !free.empty()) {  // HBM full: give the idle blocks back, retry
+        (void)hipGetLastError();
+        clear();
+        e = hipMalloc(&p, want);
+    }
+    if (e != hipSuccess) fail(KT_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+    held += want;
+    *got = want;
+    return p;
+}
+
+void ScratchPool::give(void* p, size_t bytes) {
+    if (!p) return;
+    free.push_back({bytes, p});
+    if (free.size() > 64) {  // bound the list: drop the smallest idle block
+        size_t s = 0;
+        for (size_t i = 1; i < free.size(); ++i)
+            if (free[i].first < free[s].first) s = i;
+        (void)hipFree(free[s].second);
+        held -= free[s].first;
+        free.erase(free.begin() + (std::ptrdiff_t)s);
+    }
+}
+
+void ScratchPool::clear() {
+    for (auto& f : free) {
+        (void)hipFree(f.second);
+        held -= f.first;
+    }
+    free.clear();
+}
+
+void DevMat::alloc(kt_context_s* c, int64_t n_, int ld_) {
     n = n_;
     ld = ld_;
-    buf.ensure(sizeof(double) * (size_t)std::max<int64_t>(n, 1) * ld);
-    KT_HIP(hipMemsetAsync(buf.ptr, 0, sizeof(double) * (size_t)std::max<int64_t>(n, 1) * ld,
-                          ctx->stream));
+    const size_t want = sizeof(double) * (size_t)std::max<int64_t>(n, 1) * (size_t)std::max(ld, 1);
+    if (!ptr || ctx != c || bytes < want) {
+        release();
+        ctx = c;
+        ptr = ctx->pool.take(want, &bytes);
+    }
+    KT_HIP(hipMemsetAsync(ptr, 0, want, ctx->stream));
+}
+
+void DevMat::release() {
+    if (ptr && ctx) ctx->pool.give(ptr, bytes);
+    ptr = nullptr;
+    bytes = 0;
+    ctx = nullptr;
 }
 
 // KT_PINNED_STAGING=0: gram / combine / the thin QR move their small blocks

@@ -18,13 +18,42 @@ int pow2_at_least(int b);
 rocblas_handle blas(kt_context_s* ctx);
 
 // Row-major device array n x ld (zero-initialised).
+// n x ld row-major device block, zeroed by alloc; the storage comes from and
+// returns to the context's ScratchPool (no hipMalloc / hipFree per call).
 struct DevMat {
-    DevBuf buf;
+    kt_context_s* ctx = nullptr;
+    void* ptr = nullptr;
+    size_t bytes = 0;
     int64_t n = 0;
     int ld = 0;
+    DevMat() = default;
+    DevMat(const DevMat&) = delete;
+    DevMat& operator=(const DevMat&) = delete;
+    DevMat(DevMat&& o) noexcept { steal(o); }
+    DevMat& operator=(DevMat&& o) noexcept {
+        if (this != &o) {
+            release();
+            steal(o);
+        }
+        return *this;
+    }
+    ~DevMat() { release(); }
     void alloc(kt_context_s* ctx, int64_t n_, int ld_);
-    double* col(int c) { return buf.as<double>() + c; }
-    const double* col(int c) const { return static_cast<const double*>(buf.ptr) + c; }
+    void release();
+    double* col(int c) { return static_cast<double*>(ptr) + c; }
+    const double* col(int c) const { return static_cast<const double*>(ptr) + c; }
+
+  private:
+    void steal(DevMat& o) {
+        ctx = o.ctx;
+        ptr = o.ptr;
+        bytes = o.bytes;
+        n = o.n;
+        ld = o.ld;
+        o.ctx = nullptr;
+        o.ptr = nullptr;
+        o.bytes = 0;
+    }
 };
 
 // G (host, px x py column-major) = X[:, 0:px]' Y[:, 0:py]   (synchronises)

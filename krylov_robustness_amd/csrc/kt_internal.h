@@ -56,6 +56,23 @@ struct DevBuf {
     }
 };
 
+// Device scratch blocks recycled per context (behind DevMat, kt_block.h):
+// hipFree synchronises the whole device, so block-Krylov calls that allocate
+// their bases per call stalled the host at every return (config 1's expmv
+// composition: 85 us gaps before each re-allocation's fill, tools/gaps.py).
+// Blocks return to the context's free list and are reused by later calls on
+// the same stream (stream order makes the reuse safe); freed at context
+// destruction.
+struct ScratchPool {
+    std::vector<std::pair<size_t, void*>> free;  // (bytes, ptr), reusable now
+    size_t held = 0;                             // bytes owned (free + in use)
+    // a block of >= want bytes (best fit within 4x, else a new allocation)
+    void* take(size_t want, size_t* got);
+    void give(void* p, size_t bytes);
+    void clear();
+    ~ScratchPool() { clear(); }
+};
+
 struct PinnedBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
@@ -137,6 +154,7 @@ struct kt_context_s {
     void* blas = nullptr;  // rocblas_handle, created on first block-Krylov use
     kt::ProfSlot prof[kt::PROF_NSLOTS];
     kt::Workspace ws;
+    kt::ScratchPool pool;  // DevMat scratch (kt_block.h)
 };
 
 namespace kt {

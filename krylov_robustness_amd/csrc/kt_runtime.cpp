@@ -281,6 +281,7 @@ int kt_context_destroy(kt_context_t ctx) {
     w.small.release(); w.small2.release(); w.qrtmp.release();
     w.eigA.release(); w.eigW.release(); w.eigInfo.release();
     w.hist.release(); w.norm_part.release();
+    ctx->pool.clear();
     if (ctx->blas) rocblas_destroy_handle(static_cast<rocblas_handle>(ctx->blas));
     if (w.comb_ev) (void)hipEventDestroy(w.comb_ev);
     w.host_trec.release();
