@@ -295,8 +295,11 @@ int kt_context_destroy(kt_context_t ctx) {
 int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr, const int64_t* rowind,
                          const double* vals, int check_symmetric, kt_matrix_t* out) {
     KT_GUARD_BEGIN
-    if (!ctx || !out || !colptr || (!rowind && n > 0)) fail(KT_ERR_ARG, "NULL argument");
+    // the arrays are validated before the context is touched (a malformed
+    // CSC never reaches the device, and the checks run without a GPU)
+    if (!out || !colptr || (!rowind && n > 0)) fail(KT_ERR_ARG, "NULL argument");
     if (n < 0) fail(KT_ERR_ARG, "negative dimension");
+    if (colptr[0] != 0) fail(KT_ERR_ARG, "column pointers must start at 0 (jc[0] == 0)");
     const int64_t nnz = colptr[n];
     if (n >= (int64_t(1) << 31) || nnz >= (int64_t(1) << 31))
         fail(KT_ERR_UNSUPPORTED, "n and nnz must be < 2^31 (int32 device indices)");
@@ -304,6 +307,7 @@ int kt_matrix_create_csc(kt_context_t ctx, int64_t n, const int64_t* colptr, con
         if (colptr[j + 1] < colptr[j]) fail(KT_ERR_ARG, "column pointers not monotone");
     for (int64_t k = 0; k < nnz; ++k)
         if (rowind[k] < 0 || rowind[k] >= n) fail(KT_ERR_ARG, "row index out of range");
+    if (!ctx) fail(KT_ERR_ARG, "NULL context");
 
     auto* A = new kt_matrix_s();
     A->ctx = ctx;

@@ -45,6 +45,30 @@ def test_abi_version_and_null_arguments():
     assert lib.kt_context_destroy(None) == _lib.KT_OK
 
 
+def test_matrix_create_validates_csc_before_the_device():
+    """Malformed MATLAB CSC arrays are rejected on the host, before any
+    device work (no GPU needed): jc[0] != 0, non-monotone jc, row indices out
+    of [0, n), negative n; a valid CSC then only fails on the NULL context."""
+    from krylov_robustness_amd import _lib
+    lib = _lib.load()
+    h = C.c_void_p()
+    i64 = lambda a: (C.c_int64 * len(a))(*a)  # noqa: E731
+    one = (C.c_double * 4)(1, 1, 1, 1)
+    cases = [
+        (2, [-1, 1, 2], [1, 0], b"start at 0"),
+        (2, [0, 2, 1], [1, 0], b"monotone"),
+        (2, [0, 1, 2], [1, 2], b"out of range"),
+        (2, [0, 1, 2], [-1, 0], b"out of range"),
+        (-1, [0], [], b"negative"),
+    ]
+    for n, jc, ir, msg in cases:
+        st = lib.kt_matrix_create_csc(None, n, i64(jc), i64(ir or [0]), one, 0, C.byref(h))
+        assert st == _lib.KT_ERR_ARG, (jc, ir)
+        assert msg in lib.kt_last_error(), (jc, ir, lib.kt_last_error())
+    st = lib.kt_matrix_create_csc(None, 2, i64([0, 1, 2]), i64([1, 0]), one, 0, C.byref(h))
+    assert st == _lib.KT_ERR_ARG and b"NULL context" in lib.kt_last_error()
+
+
 def test_no_gpu_fails_loudly():
     """With no device the library reports an error instead of computing on CPU."""
     import krylov_robustness_amd as kra
