@@ -275,6 +275,11 @@ int kt_eigs_leading(kt_matrix_t A, double tol, int maxit, double* lambda, double
 int kt_profile_enable(kt_context_t ctx, int enable);
 int kt_profile_read(kt_context_t ctx, int kernel, int64_t* launches, double* total_ms);
 int kt_profile_reset(kt_context_t ctx);
+/* Wall time during which at least one launch of `kernel` was in flight (the
+ * union of the launches' event intervals, on whichever sweep-lane stream
+ * each ran): with several lanes overlapping, summed per-launch durations
+ * count shared time twice; this does not. */
+int kt_profile_busy(kt_context_t ctx, int kernel, double* busy_ms);
 
 /* Hot-path statistics.  stat 0: kt_slq_trace sweeps whose y-form probe
  * Lanczos tripped the cancellation guard (a lucky breakdown, or a beta^2

@@ -98,6 +98,7 @@ SIGNATURES = [
     ("kt_profile_enable", C.c_int, [_ctx_p, C.c_int]),
     ("kt_profile_read", C.c_int, [_ctx_p, C.c_int, _i64p, _dp]),
     ("kt_profile_reset", C.c_int, [_ctx_p]),
+    ("kt_profile_busy", C.c_int, [_ctx_p, C.c_int, _dp]),
     ("kt_context_stat", C.c_int, [_ctx_p, C.c_int, _i64p]),
 ]
 

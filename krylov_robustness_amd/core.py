@@ -56,6 +56,13 @@ class Context:
         _lib.check(_lib.load().kt_profile_read(self._h, kernel, C.byref(n), C.byref(ms)))
         return int(n.value), float(ms.value)
 
+    def profile_busy(self, kernel: int) -> float:
+        """Milliseconds during which at least one profiled launch of `kernel`
+        was in flight (union over the sweep lanes' streams)."""
+        ms = C.c_double()
+        _lib.check(_lib.load().kt_profile_busy(self._h, kernel, C.byref(ms)))
+        return float(ms.value)
+
     def yform_redone(self) -> int:
         """Sweeps of the y-form hot path recomputed by the explicit CGS2 sweep
         (cancellation guard / lucky breakdown), since context creation."""

@@ -102,6 +102,7 @@ struct ProfSlot {
     size_t used = 0;             // events used (2 per launch)
     int64_t launches = 0;
     double total_ms = 0.0;
+    double busy_ms = 0.0;  // union of the launches' intervals
 };
 
 enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_START = 2, PROF_NSLOTS = 3 };

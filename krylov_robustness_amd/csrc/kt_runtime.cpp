@@ -41,12 +41,28 @@ void prof_end(kt_context_s* ctx, int slot, hipStream_t st) {
 void prof_collect(kt_context_s* ctx) {
     for (int k = 0; k < PROF_NSLOTS; ++k) {
         ProfSlot& s = ctx->prof[k];
+        std::vector<std::pair<double, double>> iv;  // relative to the slot's first event
         for (size_t i = 0; i + 1 < s.used; i += 2) {
-            float ms = 0.f;
+            float ms = 0.f, a = 0.f, b = 0.f;
             KT_HIP(hipEventElapsedTime(&ms, s.ev[i], s.ev[i + 1]));
+            KT_HIP(hipEventElapsedTime(&a, s.ev[0], s.ev[i]));
+            KT_HIP(hipEventElapsedTime(&b, s.ev[0], s.ev[i + 1]));
+            iv.push_back({a, b});
             s.total_ms += ms;
             s.launches += 1;
         }
+        std::sort(iv.begin(), iv.end());
+        double cs = 0.0, ce = -1.0;
+        for (auto& x : iv) {  // union of the intervals
+            if (x.first > ce) {
+                if (ce > cs) s.busy_ms += ce - cs;
+                cs = x.first;
+                ce = x.second;
+            } else if (x.second > ce) {
+                ce = x.second;
+            }
+        }
+        if (ce > cs) s.busy_ms += ce - cs;
         s.used = 0;
     }
 }
@@ -418,7 +434,14 @@ int kt_context_stat(kt_context_t ctx, int stat, int64_t* value) {
 int kt_profile_reset(kt_context_t ctx) {
     KT_GUARD_BEGIN
     if (!ctx) fail(KT_ERR_ARG, "ctx is NULL");
-    for (auto& s : ctx->prof) { s.launches = 0; s.total_ms = 0.0; s.used = 0; }
+    for (auto& s : ctx->prof) { s.launches = 0; s.total_ms = 0.0; s.busy_ms = 0.0; s.used = 0; }
+    KT_GUARD_END
+}
+
+int kt_profile_busy(kt_context_t ctx, int kernel, double* busy_ms) {
+    KT_GUARD_BEGIN
+    if (!ctx || !busy_ms || kernel < 0 || kernel >= PROF_NSLOTS) fail(KT_ERR_ARG, "bad profile query");
+    *busy_ms = ctx->prof[kernel].busy_ms;
     KT_GUARD_END
 }
 

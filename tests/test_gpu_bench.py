@@ -39,6 +39,12 @@ def test_bench_single_process_line():
     assert roof["bound"] == "hbm" and roof["unit"] == "GB/s" and roof["peak"] == 8000.0
     assert roof["frac"] == pytest.approx(roof["achieved"] / roof["peak"], rel=1e-3)
     assert roof["avg_launch_us"] > 0
+    # the timed-region duration per launch is the union of the launches'
+    # intervals over the lanes: no longer than the mean per-launch event time,
+    # and the union no longer than the timed wall time
+    assert roof["avg_launch_us"] <= roof["timed_region_avg_launch_us_overlapped"] * 1.001
+    assert roof["timed_region_busy_ms"] <= d["steps"] * d["ms_per_step"] * 1.01
+    assert roof["isolated_pass"]["avg_launch_us"] > 0 and roof["isolated_pass"]["launches"] > 0
     cpu = d["cpu_baseline"]
     assert cpu["kind"] == "port" and cpu["value"] > 0 and cpu["cores"] >= 1
     assert d["yform_redone_sweeps"] == 0

@@ -45,7 +45,7 @@ static int access_line(Cache* c, int64_t line) {
 // lines, stream hits, csr lines, csr hits.
 void simulate(int n, const int64_t* rowptr, const int32_t* col, const int32_t* order,
               const int64_t* xcd_off, int nxcd, int rowbytes, int l2_bytes, int inflight,
-              int64_t* out) {
+              int64_t* out, int stream_bypass) {
     memset(out, 0, sizeof(int64_t) * 6);
     const int64_t lines_per_row = (rowbytes + 127) / 128;
     const int64_t tbl = (int64_t)n * lines_per_row;  // line ids: table [0,tbl), yold [tbl,2tbl), out [2tbl,3tbl), csr above
@@ -79,6 +79,7 @@ void simulate(int n, const int64_t* rowptr, const int32_t* col, const int32_t* o
                 if (slot_k[s] < 0) {  // own row, yold row, output row
                     for (int64_t l = 0; l < lines_per_row; ++l) {
                         out[2] += 3;
+                        if (stream_bypass & 1) continue;  // streams do not allocate in L2
                         out[3] += access_line(&c, r * lines_per_row + l);
                         out[3] += access_line(&c, tbl + r * lines_per_row + l);
                         out[3] += access_line(&c, 2 * tbl + r * lines_per_row + l);
@@ -88,7 +89,7 @@ void simulate(int n, const int64_t* rowptr, const int32_t* col, const int32_t* o
                 const int64_t k = slot_k[s];
                 if (k < rowptr[r + 1]) {
                     out[4]++;
-                    out[5] += access_line(&c, csr_base + k / 32);
+                    if (!(stream_bypass & 2)) out[5] += access_line(&c, csr_base + k / 32);
                     const int64_t cc = col[k];
                     for (int64_t l = 0; l < lines_per_row; ++l) {
                         out[0]++;

@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(HERE, "..", ".."))
 def load():
     lib = C.CDLL(os.path.join(HERE, "libl2sim.so"))
     lib.simulate.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
-                             C.c_int, C.c_int, C.c_void_p]
+                             C.c_int, C.c_int, C.c_void_p, C.c_int]
     return lib
 
 
@@ -30,14 +30,14 @@ def hub_relabel(A):
     return B
 
 
-def run(lib, A, order, xoff, P=16, inflight=2048, l2=4 << 20):
+def run(lib, A, order, xoff, P=16, inflight=2048, l2=4 << 20, bypass=0):
     out = np.zeros(6, dtype=np.int64)
     rp = np.ascontiguousarray(A.indptr, dtype=np.int64)
     col = np.ascontiguousarray(A.indices, dtype=np.int32)
     order = np.ascontiguousarray(order, dtype=np.int32)
     xoff = np.ascontiguousarray(xoff, dtype=np.int64)
     lib.simulate(A.shape[0], rp.ctypes.data, col.ctypes.data, order.ctypes.data, xoff.ctypes.data,
-                 len(xoff) - 1, 8 * P, l2, inflight, out.ctypes.data)
+                 len(xoff) - 1, 8 * P, l2, inflight, out.ctypes.data, bypass)
     g, gh, s, sh, c, ch = [int(v) for v in out]
     miss_lines = (g - gh) + (s - sh) + (c - ch) / 1.0
     return {"gather_hit": gh / g, "stream_hit": sh / s, "miss_GB": miss_lines * 128 / 1e9,
@@ -79,6 +79,7 @@ def main():
     ap.add_argument("--nnz", type=int, default=10_000_000)
     ap.add_argument("--inflight", type=int, default=2048)
     ap.add_argument("--schedules", default="baseline")
+    ap.add_argument("--bypass", type=int, default=0, help="1: row streams skip L2, 2: CSR skips L2, 3: both")
     args = ap.parse_args()
     from krylov_robustness_amd import graphs
     t0 = time.time()
@@ -91,7 +92,7 @@ def main():
         t0 = time.time()
         order, xoff = baseline_schedule(A) if name == "baseline" else getattr(schedules, name)(A)
         assert np.array_equal(np.sort(order), np.arange(A.shape[0]))
-        r = run(lib, A, order, xoff, inflight=args.inflight)
+        r = run(lib, A, order, xoff, inflight=args.inflight, bypass=args.bypass)
         loads = [int(A.indptr[order[xoff[k]:xoff[k + 1]] + 1].sum() - A.indptr[order[xoff[k]:xoff[k + 1]]].sum())
                  for k in range(8)]
         print(f"{name:24s} gather hit {r['gather_hit']:.3f}  stream hit {r['stream_hit']:.3f}  "

@@ -14,18 +14,34 @@ def main(trace_csv, bench_json, out_json):
     rows = [r for r in csv.DictReader(open(trace_csv)) if f"kt::{kname}," in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]  # us
-    iso = roof["launches"]
+    iso = (roof.get("isolated_pass") or {}).get("launches", roof["launches"])
     timed = b["steps"] * (b["config"]["probes_per_eval"] // b["config"]["probes_per_sweep"]) * \
         (b["config"]["lanczos_m"] - 1)
     t_iso, t_timed = dur[-iso:], dur[-iso - timed:-iso]
+    # union of the timed region's launch intervals (lane overlap counted once)
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows[-iso - timed:-iso])
+    union, cs, ce = 0, None, None
+    for a, e in iv:
+        if ce is None or a > ce:
+            if ce is not None:
+                union += ce - cs
+            cs, ce = a, e
+        else:
+            ce = max(ce, e)
+    union += ce - cs
     out = {
         "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py (default command)",
         "kernel": kname,
         "bench_value": b["value"],
         "launches_total": len(dur),
         "isolated_pass": {"launches": len(t_iso), "rocprof_avg_us": round(sum(t_iso) / len(t_iso), 2),
-                          "bench_avg_launch_us": roof["avg_launch_us"]},
+                          "bench_avg_launch_us": (roof.get("isolated_pass") or {}).get(
+                              "avg_launch_us", roof["avg_launch_us"])},
         "timed_region": {"launches": len(t_timed),
+                         "rocprof_union_busy_ms": round(union / 1e6, 3),
+                         "bench_timed_region_busy_ms": roof.get("timed_region_busy_ms"),
+                         "rocprof_union_us_per_launch": round(union / 1e3 / len(t_timed), 2),
+                         "bench_avg_launch_us": roof["avg_launch_us"],
                          "rocprof_avg_us": round(sum(t_timed) / len(t_timed), 2),
                          "bench_timed_region_avg_launch_us_overlapped":
                              roof["timed_region_avg_launch_us_overlapped"],
