@@ -30,6 +30,7 @@ namespace kt {
 namespace {
 
 constexpr int kMaxPairs = 256;  // candidates per device batch (512 columns)
+constexpr int64_t kFusedMaxN = 16384;  // the fused one-workgroup-per-candidate path up to this n
 
 // Per-candidate Lanczos state: the 2x2 blocks lanczos_krylov.m:88,90 writes
 // into H at step b (column-major): D = h(cur), P = h(prev), R = qr's R.
@@ -92,8 +93,55 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
         acc += std::chrono::duration<double, std::milli>(t - t0).count();
         t0 = t;
     };
-    const int CP = cols <= 64 ? pow2_at_least(cols) : (cols + 127) / 128 * 128;
     Workspace& ws = ctx->ws;
+    // Small graphs: one workgroup per candidate runs the whole
+    // trace_fun_update in ONE launch (k_pair_fused), no per-step grid-wide
+    // hand-offs.  KT_PAIRS_FUSED=0 keeps the batched steps below; larger n
+    // keeps them too (one workgroup per candidate would sweep too many rows).
+    const char* fz = getenv("KT_PAIRS_FUSED");
+    const bool fused = !(fz && fz[0] == '0') && n <= kFusedMaxN && pair_fused_lds_bytes(it) <= 150 * 1024 &&
+                       getenv("KT_PAIRS_HOST") == nullptr;
+    if (fused) {
+        const DevCSR& M = natural_csr(A);
+        const CsrView V{M.rowptr, M.col, M.val, (int)n, M.long_rows, M.n_long, A->long_thresh,
+                        kSplitThresh, M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split};
+        ws.pair_blk[0].ensure(sizeof(double) * 6 * (size_t)std::max<int64_t>(n, 1) * C);
+        ws.pair_idx.ensure(sizeof(int) * 2 * (size_t)C);
+        ws.pair_state.ensure(sizeof(double) * 8 * (size_t)C);
+        const int nnmax = 2 * it;
+        int64_t big_stride = 0;
+        double* big = nullptr;
+        const char* de = getenv("KT_PAIRS_DENSE_EIG");  // the dense solver needs global scratch past 2j = 56
+        if (de && de[0] == '1' && nnmax > 56) {  // G, T, d/e, eigenvalues per candidate
+            big_stride = 2 * (int64_t)nnmax * nnmax + 6 * (int64_t)nnmax;
+            ws.pair_scratch.ensure(sizeof(double) * (size_t)C * big_stride);
+            big = ws.pair_scratch.as<double>();
+        }
+        std::vector<int> idx(2 * (size_t)C);
+        for (int c = 0; c < C; ++c) {
+            idx[c] = (int)ei[c];
+            idx[C + c] = (int)ej[c];
+        }
+        KT_HIP(hipMemcpyAsync(ws.pair_idx.ptr, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice,
+                              ctx->stream));
+        KT_HIP(launch_pair_fused(C, (int)n, V, A->unit_values, ws.pair_idx.as<int>(), ws.pair_idx.as<int>() + C,
+                                 B, it, fun, tol, ws.pair_blk[0].as<double>(), big, big_stride,
+                                 ws.pair_state.as<double>(), ctx->stream));
+        std::vector<double> sv((size_t)C * 8);
+        KT_HIP(hipMemcpyAsync(sv.data(), ws.pair_state.ptr, sizeof(double) * sv.size(), hipMemcpyDeviceToHost,
+                              ctx->stream));
+        KT_HIP(hipStreamSynchronize(ctx->stream));
+        lap(t_gpu);
+        for (int c = 0; c < C; ++c) {
+            if (sv[(size_t)8 * c + 3] < 0) fail(KT_ERR_HIP, "pair_fused: eigen scratch missing");
+            Xm[c] = sv[(size_t)8 * c + 2];
+            if (iter) iter[c] = (int)sv[(size_t)8 * c + 3];
+            if (lucky) lucky[c] = sv[(size_t)8 * c + 4] != 0.0 ? 1 : 0;
+        }
+        if (timing) fprintf(stderr, "[kt pairs] fused C=%d n=%lld %.3f ms\n", C, (long long)n, t_gpu);
+        return;
+    }
+    const int CP = cols <= 64 ? pow2_at_least(cols) : (cols + 127) / 128 * 128;
     const size_t blk_bytes = sizeof(double) * (size_t)std::max<int64_t>(n, 1) * CP;
     double* S[3];
     for (int t = 0; t < 3; ++t) {
@@ -161,7 +209,8 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
         const int64_t sstride = 2 * (int64_t)nnmax * nnmax + 3 * (int64_t)nnmax;
         ws.pair_hist.ensure(sizeof(double) * (size_t)it * C * 11);
         ws.pair_state.ensure(sizeof(double) * (size_t)C * 8 + sizeof(double) * 4 * (size_t)C);
-        ws.pair_scratch.ensure(sizeof(double) * (size_t)C * sstride);
+        const char* dense_eig = getenv("KT_PAIRS_DENSE_EIG");  // only the dense solver uses the scratch
+        if (dense_eig && dense_eig[0] == '1') ws.pair_scratch.ensure(sizeof(double) * (size_t)C * sstride);
         ws.pair_active.ensure(sizeof(int) * 2);
         ws.pair_active_host.ensure(sizeof(int) * 2);
         double* hist = ws.pair_hist.as<double>();

@@ -24,6 +24,9 @@
 // completions match MATLAB's qr(w, 0).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "kt_launch.h"
 
 namespace kt {
@@ -753,6 +756,689 @@ __global__ __launch_bounds__(128 * W) void k_pair_eig_wave(int C, int j, int it,
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fused candidate runs (default for small n): ONE workgroup per candidate runs
+// its whole trace_fun_update (krylov_miobi.m:99 -> trace_fun_update.m:53-125)
+// in one launch -- the qr(U) start, then per Lanczos step the SpMM
+// (lanczos_krylov.m:81), the five CGS2 / Householder sweeps of
+// launch_pairs_orth (:109-115, :90) with workgroup reductions in a fixed
+// order, the step's record, both projected eigenproblems in LDS (wave
+// Householder + Sturm multisection, as k_pair_eig_wave) and the lag-2 stop.
+// No grid-wide hand-off per step: the batched path needed ~10 dependent
+// launches per step over all candidates.  The candidate's vectors live in
+// its own slice of `vec` ([C][3][n][2], L2-resident for small n).
+// ---------------------------------------------------------------------------
+#ifndef KT_FUSED_THREADS
+#define KT_FUSED_THREADS 512
+#endif
+constexpr int kFusedThreads = KT_FUSED_THREADS;
+constexpr int kFusedWaves = kFusedThreads / 64;
+constexpr int kFusedMaxNN = 56;  // 2j at which the eigenproblems leave LDS
+
+// fixed-order workgroup sum of NV per-thread values; every thread gets them
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&acc)[NV], double* red /* [kFusedWaves][NV] */) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = wave_sum64(acc[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) red[wave * NV + k] = acc[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kFusedWaves; ++w) s += red[w * NV + k];
+        acc[k] = s;
+    }
+    __syncthreads();  // red is reused by the next reduction
+}
+
+struct FusedCSR {
+    const int* rp;
+    const int* ci;
+    const double* va;
+    const int* long_rows;
+    int n_long, long_thresh, unit;
+};
+
+// W = A V (n x 2): short rows one thread each, long rows one wave each
+__device__ void fused_spmm(int n, const FusedCSR& M, const double* __restrict__ V, double* __restrict__ W) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int r = tid; r < n; r += kFusedThreads) {
+        const int b = M.rp[r], e = M.rp[r + 1];
+        if (e - b > M.long_thresh) continue;
+        double s0 = 0.0, s1 = 0.0;
+        for (int k0 = b; k0 < e; k0 += 4) {  // 4 gathers in flight, added in order
+            int c[4];
+            double a[4];
+            double2 v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool ok = k0 + q < e;
+                c[q] = ok ? M.ci[k0 + q] : 0;
+                a[q] = ok ? (M.unit ? 1.0 : M.va[k0 + q]) : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const double2*>(V + 2 * (int64_t)c[q]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (k0 + q < e) {
+                    s0 = fma(a[q], v[q].x, s0);
+                    s1 = fma(a[q], v[q].y, s1);
+                }
+        }
+        *reinterpret_cast<double2*>(W + 2 * (int64_t)r) = make_double2(s0, s1);
+    }
+    for (int li = wave; li < M.n_long; li += kFusedWaves) {
+        const int r = M.long_rows[li];
+        const int b = M.rp[r], e = M.rp[r + 1];
+        double s0 = 0.0, s1 = 0.0;
+        for (int k = b + lane; k < e; k += 64) {
+            const int c = M.ci[k];
+            const double a = M.unit ? 1.0 : M.va[k];
+            const double2 v = *reinterpret_cast<const double2*>(V + 2 * (int64_t)c);
+            s0 = fma(a, v.x, s0);
+            s1 = fma(a, v.y, s1);
+        }
+        s0 = wave_sum64(s0);
+        s1 = wave_sum64(s1);
+        if (lane == 0) *reinterpret_cast<double2*>(W + 2 * (int64_t)r) = make_double2(s0, s1);
+    }
+}
+
+// The CGS2 + thin Householder QR of W against the window [P C]
+// (launch_pairs_orth's sweeps A-E on one candidate).  P == nullptr: the
+// first step (window of one block, p = 0); C == nullptr: qr(U) of the start
+// (sweep C0, no projection).  W is overwritten by Q; rec[0..10] = (g1 + g2
+// [8], beta1, R12, beta2).  Ends with a workgroup barrier.
+__device__ void fused_orth(int n, const double* __restrict__ P, const double* __restrict__ Cv,
+                           double* __restrict__ W, double* cf, double* red, double* rec) {
+    const int tid = threadIdx.x;
+    if (Cv) {
+        for (int ph = 0; ph < 2; ++ph) {  // sweep A (dots) then B (update + dots)
+            double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            double g[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) g[k] = ph ? cf[CF_G1 + k] : 0.0;
+            constexpr int U = 4;  // rows per round: their loads issue together (row order kept)
+            for (int r0 = tid; r0 < n; r0 += U * kFusedThreads) {
+                double2 w[U], u[U], p[U];
+#pragma unroll
+                for (int q = 0; q < U; ++q) {
+                    const int r = r0 + q * kFusedThreads;
+                    const bool ok = r < n;
+                    w[q] = ok ? *reinterpret_cast<const double2*>(W + 2 * (int64_t)r) : make_double2(0.0, 0.0);
+                    u[q] = ok ? *reinterpret_cast<const double2*>(Cv + 2 * (int64_t)r) : make_double2(0.0, 0.0);
+                    p[q] = (ok && P) ? *reinterpret_cast<const double2*>(P + 2 * (int64_t)r) : make_double2(0.0, 0.0);
+                }
+#pragma unroll
+                for (int q = 0; q < U; ++q) {
+                    const int r = r0 + q * kFusedThreads;
+                    if (ph) {
+                        w[q].x -= p[q].x * g[0] + p[q].y * g[1] + u[q].x * g[2] + u[q].y * g[3];
+                        w[q].y -= p[q].x * g[4] + p[q].y * g[5] + u[q].x * g[6] + u[q].y * g[7];
+                        if (r < n) *reinterpret_cast<double2*>(W + 2 * (int64_t)r) = w[q];
+                    }
+                    acc[0] += p[q].x * w[q].x; acc[1] += p[q].y * w[q].x; acc[2] += u[q].x * w[q].x; acc[3] += u[q].y * w[q].x;
+                    acc[4] += p[q].x * w[q].y; acc[5] += p[q].y * w[q].y; acc[6] += u[q].x * w[q].y; acc[7] += u[q].y * w[q].y;
+                }
+            }
+            block_sum<8>(acc, red);
+            if (tid == 0)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) cf[(ph ? CF_G2 : CF_G1) + k] = acc[k];
+            __syncthreads();
+        }
+    } else if (tid == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) cf[CF_G1 + k] = 0.0;
+    }
+    {  // sweep C (C0 without the projection): s1 = |w0(2:n)|^2, ab = w0(2:n)' w1(2:n)
+        double acc[2] = {0.0, 0.0};
+        double g[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = Cv ? cf[CF_G2 + k] : 0.0;
+        constexpr int U = 4;
+        for (int r0 = tid; r0 < n; r0 += U * kFusedThreads) {
+            double2 w[U], u[U], p[U];
+#pragma unroll
+            for (int q = 0; q < U; ++q) {
+                const int r = r0 + q * kFusedThreads;
+                const bool ok = r < n;
+                w[q] = ok ? *reinterpret_cast<const double2*>(W + 2 * (int64_t)r) : make_double2(0.0, 0.0);
+                u[q] = (ok && Cv) ? *reinterpret_cast<const double2*>(Cv + 2 * (int64_t)r) : make_double2(0.0, 0.0);
+                p[q] = (ok && Cv && P) ? *reinterpret_cast<const double2*>(P + 2 * (int64_t)r) : make_double2(0.0, 0.0);
+            }
+#pragma unroll
+            for (int q = 0; q < U; ++q) {
+                const int r = r0 + q * kFusedThreads;
+                if (Cv) {
+                    w[q].x -= p[q].x * g[0] + p[q].y * g[1] + u[q].x * g[2] + u[q].y * g[3];
+                    w[q].y -= p[q].x * g[4] + p[q].y * g[5] + u[q].x * g[6] + u[q].y * g[7];
+                    if (r < n) *reinterpret_cast<double2*>(W + 2 * (int64_t)r) = w[q];
+                }
+                if (r >= 1 && r < n) {
+                    acc[0] += w[q].x * w[q].x;
+                    acc[1] += w[q].x * w[q].y;
+                }
+            }
+        }
+        block_sum<2>(acc, red);  // its barrier also publishes W's updated rows 0, 1
+        if (tid == 0) {
+            const double2 w0 = *reinterpret_cast<const double2*>(W), w1 = *reinterpret_cast<const double2*>(W + 2);
+            double beta1, tau1, scal1;
+            larfg(w0.x, acc[0], beta1, tau1, scal1);
+            const double t = w0.y + scal1 * acc[1];  // v1' w(:,2)
+            cf[CF_SCAL1] = scal1;
+            cf[CF_TAU1] = tau1;
+            cf[CF_KAPPA] = tau1 * t * scal1;
+            cf[CF_BETA1] = beta1;
+            cf[CF_R12] = w0.y - tau1 * t;
+            cf[CF_V11] = w1.x * scal1;
+        }
+        __syncthreads();
+    }
+    {  // sweep D: z = w1 - kappa w0;  s2 = |z(3:n)|^2, dz = w0(3:n)' z(3:n)
+        double acc[2] = {0.0, 0.0};
+        const double kappa = cf[CF_KAPPA];
+        for (int r = tid; r < n; r += kFusedThreads) {
+            if (r < 2) continue;
+            const double2 w = *reinterpret_cast<const double2*>(W + 2 * (int64_t)r);
+            const double z = w.y - kappa * w.x;
+            acc[0] += z * z;
+            acc[1] += w.x * z;
+        }
+        block_sum<2>(acc, red);
+        if (tid == 0) {
+            const double2 w1 = *reinterpret_cast<const double2*>(W + 2);
+            const double z1 = w1.y - cf[CF_KAPPA] * w1.x;
+            double beta2, tau2, scal2;
+            larfg(z1, acc[0], beta2, tau2, scal2);
+            const double v11 = cf[CF_V11];
+            const double d = v11 + cf[CF_SCAL1] * scal2 * acc[1];  // v1' v2
+            cf[CF_SCAL2] = scal2;
+            cf[CF_TAU2] = tau2;
+            cf[CF_K2] = cf[CF_TAU1] * (v11 - tau2 * d);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) rec[k] = cf[CF_G1 + k] + cf[CF_G2 + k];
+            rec[8] = cf[CF_BETA1];
+            rec[9] = cf[CF_R12];
+            rec[10] = beta2;
+        }
+        __syncthreads();
+    }
+    {  // sweep E: W <- [q1 q2] = dorg2r(H1, H2)
+        const double tau1 = cf[CF_TAU1], tau2 = cf[CF_TAU2], scal1 = cf[CF_SCAL1], scal2 = cf[CF_SCAL2];
+        const double k2 = cf[CF_K2], kappa = cf[CF_KAPPA], v11 = cf[CF_V11];
+        for (int r = tid; r < n; r += kFusedThreads) {
+            const double2 w = *reinterpret_cast<const double2*>(W + 2 * (int64_t)r);
+            double v1, v2;
+            if (r == 0) {
+                v1 = 1.0;
+                v2 = 0.0;
+            } else if (r == 1) {
+                v1 = v11;
+                v2 = 1.0;
+            } else {
+                v1 = w.x * scal1;
+                v2 = (w.y - kappa * w.x) * scal2;
+            }
+            double2 q;
+            q.x = (r == 0 ? 1.0 : 0.0) - tau1 * v1;
+            q.y = (r == 1 ? 1.0 : 0.0) - tau2 * v2 - k2 * v1;
+            *reinterpret_cast<double2*>(W + 2 * (int64_t)r) = q;
+        }
+        __syncthreads();
+    }
+}
+
+// Both projections of step j (trace_fun_update.m:71-89) from the records in
+// LDS; returns Xm to every thread.  nn = 2j <= kFusedMaxNN: in LDS, wave 0-3
+// on the updated projection T, waves 4-7 on G (wave 0 / 4 tridiagonalise,
+// then 4 waves multisect each); larger nn: one thread per projection on the
+// global scratch `big` (dev_sym_eigvals).
+__device__ double fused_xm(int j, int fun, const double* rec /* [j][11] LDS */, const double* cm,
+                           double* sm, double* big) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nn = 2 * j;
+    const bool lds = nn <= kFusedMaxNN;
+    double* G = lds ? sm : big;
+    double* T = G + nn * nn;
+    double* de = T + nn * nn;   // per projection: d (nn), e (nn)
+    double* ev = de + 4 * nn;   // eigenvalues: eig(T) (nn), eig(G) (nn)
+    for (int t = tid; t < nn * nn; t += kFusedThreads) G[t] = 0.0;
+    __syncthreads();
+    for (int b = tid; b < j; b += kFusedThreads) {  // row-major G[r * nn + col]
+        const double* h = rec + 11 * b;
+        G[(2 * b) * nn + 2 * b] = h[2];
+        G[(2 * b + 1) * nn + 2 * b] = h[3];
+        G[(2 * b) * nn + 2 * b + 1] = h[6];
+        G[(2 * b + 1) * nn + 2 * b + 1] = h[7];
+        if (b >= 1) {
+            G[(2 * b - 2) * nn + 2 * b] = h[0];
+            G[(2 * b - 1) * nn + 2 * b] = h[1];
+            G[(2 * b - 2) * nn + 2 * b + 1] = h[4];
+            G[(2 * b - 1) * nn + 2 * b + 1] = h[5];
+        }
+        if (b + 1 < j) {
+            G[(2 * b + 2) * nn + 2 * b] = h[8];
+            G[(2 * b + 2) * nn + 2 * b + 1] = h[9];
+            G[(2 * b + 3) * nn + 2 * b + 1] = h[10];
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < nn * nn; t += kFusedThreads) T[t] = G[t];
+    __syncthreads();
+    if (tid == 0) {  // Cm column-major 2x2
+        T[0] += cm[0];
+        T[nn] += cm[1];
+        T[1] += cm[2];
+        T[nn + 1] += cm[3];
+    }
+    __syncthreads();
+    for (int t = tid; t < nn * nn; t += kFusedThreads) {  // (X + X') / 2   :78-81
+        const int r = t / nn, q = t % nn;
+        if (q < r) {
+            const double g = 0.5 * (G[r * nn + q] + G[q * nn + r]);
+            const double x = 0.5 * (T[r * nn + q] + T[q * nn + r]);
+            G[r * nn + q] = G[q * nn + r] = g;
+            T[r * nn + q] = T[q * nn + r] = x;
+        }
+    }
+    __syncthreads();
+    if (lds) {
+        constexpr int W = kFusedWaves / 2;
+        const int mat = wave / W, wv = wave % W;  // mat 0: T, 1: G
+        if (wv == 0) {
+            double dl, el;
+            wave_tridiag(nn, mat == 0 ? T : G, dl, el);
+            if (lane < nn) {
+                de[mat * 2 * nn + lane] = dl;
+                de[mat * 2 * nn + nn + lane] = el;
+            }
+        }
+        __syncthreads();
+        const double dreg = lane < nn ? de[mat * 2 * nn + lane] : 0.0;
+        const double ereg = lane < nn ? de[mat * 2 * nn + nn + lane] : 0.0;
+        const int per = (nn + W - 1) / W;
+        const int k0 = wv * per;
+        const int ne = min(per, nn - k0);
+        if (ne > 0) {  // wave-uniform
+            const double lam = wave_multisect<4>(nn, dreg, ereg, k0, ne);
+            const int g = 64 / ne;
+            if (lane % g == 0 && lane / g < ne) ev[mat * nn + k0 + lane / g] = lam;
+        }
+    } else if (lane == 0 && wave < 2) {  // row-major storage is its own transpose (symmetric)
+        dev_sym_eigvals(nn, wave == 0 ? T : G, ev + wave * nn, de + wave * 2 * nn);
+    }
+    __syncthreads();
+    double term = 0.0;  // :85-89 (k-th smallest of each)
+    if (wave == 0)
+        for (int i = lane; i < nn; i += 64)
+            term += (fun == 0) ? exp(ev[i]) * (1.0 - exp(ev[nn + i] - ev[i]))
+                               : dev_fscalar(fun, ev[i]) - dev_fscalar(fun, ev[nn + i]);
+    term = wave_sum64(term);
+    __shared__ double s_xm;
+    if (tid == 0) s_xm = term;
+    __syncthreads();
+    const double xm = s_xm;
+    __syncthreads();
+    return xm;
+}
+
+// ---- eigenvalues of the symmetrised block-tridiagonal projection by block
+// Sturm counts.  Gm (trace_fun_update.m:71-81) is block tridiagonal with 2x2
+// blocks: diagonal blocks M_k (symmetric) and couplings U_k = M(blk k, blk
+// k+1).  For a shift x the block LDL' of M - xI,
+//   D_0 = M_0 - xI,   D_{k+1} = M_{k+1} - xI - U_k' D_k^{-1} U_k,
+// has the inertia of M - xI (Sylvester), so #eig(M) < x = sum over k of the
+// negative eigenvalues of the 2x2 D_k: an O(j) count, no tridiagonalisation.
+// A near-singular D_k is evaluated at x + eps (see block_count_ms).  Checked
+// on the CPU against eigvalsh on every India candidate's projections
+// (tools/blk_sturm_check.py): eigenvalues within 4e-15 of the spectral radius.  The blocks are the exact (X + X')/2 entries the dense path
+// forms, so both solve the same matrix.
+struct Blk2 {
+    double a, b, c;        // M_k = [a b; b c]
+    double u0, u1, u2, u3;  // U_k = [u0 u1; u2 u3] (row-major), k < j-1
+};
+
+// MS shifts at once: MS independent LDL' chains share each block's loads
+// (latency hiding); 1/det by rcp + one Newton step (full precision)
+template <int MS>
+__device__ __forceinline__ void block_count_ms(int j, const Blk2* __restrict__ B, const double (&x)[MS],
+                                               double pivmin, double eps, int (&cnt)[MS]) {
+    double a[MS], b[MS], c[MS];
+    {
+        const Blk2 m = B[0];
+#pragma unroll
+        for (int s = 0; s < MS; ++s) {
+            a[s] = m.a - x[s];
+            b[s] = m.b;
+            c[s] = m.c - x[s];
+            cnt[s] = 0;
+        }
+    }
+    for (int k = 0;; ++k) {
+        double det[MS];
+#pragma unroll
+        for (int s = 0; s < MS; ++s) {
+            det[s] = fma(a[s], c[s], -b[s] * b[s]);
+            if (fabs(det[s]) < pivmin) {
+                // near-singular D_k: evaluate this block at x + eps -- the 2x2
+                // analogue of dstebz's q = -pivmin.  Perturbing det alone fails
+                // for D_k = 0 (zero adjugate: e.g. a zero leading block with the
+                // shift at exactly 0).  eps^2 = 100 pivmin keeps det above
+                // pivmin; |U|^2 / eps stays below 1e153 (no overflow next block).
+                a[s] -= eps;
+                c[s] -= eps;
+                det[s] = fma(a[s], c[s], -b[s] * b[s]);
+                if (fabs(det[s]) < pivmin) det[s] = -pivmin;
+            }
+            cnt[s] += det[s] < 0.0 ? 1 : (a[s] < 0.0 ? 2 : 0);
+        }
+        if (k + 1 >= j) break;
+        const Blk2 q = B[k];  // U_k
+        const Blk2 nx = B[k + 1];
+#pragma unroll
+        for (int s = 0; s < MS; ++s) {
+            double r = __builtin_amdgcn_rcp(det[s]);
+            r = fma(fma(-det[s], r, 1.0), r, r);
+            const double i00 = c[s] * r, i01 = -b[s] * r, i11 = a[s] * r;
+            // t = D^{-1} U, S = U' t
+            const double t00 = i00 * q.u0 + i01 * q.u2, t01 = i00 * q.u1 + i01 * q.u3;
+            const double t10 = i01 * q.u0 + i11 * q.u2, t11 = i01 * q.u1 + i11 * q.u3;
+            const double s00 = q.u0 * t00 + q.u2 * t10;
+            const double s01 = q.u0 * t01 + q.u2 * t11;
+            const double s11 = q.u1 * t01 + q.u3 * t11;
+            a[s] = nx.a - x[s] - s00;
+            b[s] = nx.b - s01;
+            c[s] = nx.c - x[s] - s11;
+        }
+    }
+}
+
+// Eigenvalues k0 .. k0+ne-1 (ascending) of the block matrix by one wave:
+// g = 64 / ne lanes per eigenvalue, MS interleaved shifts each per round;
+// bracket to 2 ulp of the spectral radius (as wave_multisect).
+template <int MS>
+__device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne) {
+    const int lane = threadIdx.x & 63;
+    const int nn = 2 * j;
+    double lo = INFINITY, hi = -INFINITY, smax = 0.0;
+    for (int r = lane; r < nn; r += 64) {  // Gershgorin over the rows
+        const int k = r >> 1, s = r & 1;
+        const Blk2& m = B[k];
+        const double d = s ? m.c : m.a;
+        double off = fabs(m.b);
+        if (k + 1 < j) off += s ? fabs(m.u2) + fabs(m.u3) : fabs(m.u0) + fabs(m.u1);  // U_k row s
+        if (k >= 1) {  // U_{k-1}' row s = column s of U_{k-1}
+            const Blk2& p = B[k - 1];
+            off += s ? fabs(p.u1) + fabs(p.u3) : fabs(p.u0) + fabs(p.u2);
+        }
+        lo = fmin(lo, d - off);
+        hi = fmax(hi, d + off);
+        smax = fmax(smax, fmax(fabs(d), off));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = fmin(lo, __shfl_xor(lo, o, 64));
+        hi = fmax(hi, __shfl_xor(hi, o, 64));
+        smax = fmax(smax, __shfl_xor(smax, o, 64));
+    }
+    const double span = fmax(hi - lo, 1e-300);
+    lo -= 2.2e-16 * span + 1e-300;
+    hi += 2.2e-16 * span + 1e-300;
+    const double sc = fmax(1.0, smax);
+    const double pivmin = 2.2250738585072014e-308 * sc * sc * sc * sc;
+    const double eps = 10.0 * sqrt(pivmin);
+    const double atol = 4.4e-16 * fmax(fabs(lo), fabs(hi)) + 1e-300;
+    const int g = 64 / ne;
+    const int kl = lane / g, sub = lane % g;
+    const int k = k0 + kl;
+    const int M = g * MS;
+    double a = lo, b = hi;
+    const bool live = kl < ne;
+    bool done = !live;
+    for (int round = 0; round < 64; ++round) {
+        if (!done && !(b - a > atol)) done = true;
+        if (__ballot(!done) == 0ull) break;
+        const double h = (b - a) / (double)(M + 1);
+        int mine = M;
+        if (!done) {
+            double xs[MS];
+            int cnt[MS];
+#pragma unroll
+            for (int s2 = 0; s2 < MS; ++s2) xs[s2] = a + h * (double)(sub * MS + s2 + 1);
+            block_count_ms<MS>(j, B, xs, pivmin, eps, cnt);
+#pragma unroll
+            for (int s2 = MS - 1; s2 >= 0; --s2)
+                if (cnt[s2] > k) mine = sub * MS + s2;
+        }
+        int first = mine;
+        for (int o = 1; o < g; ++o) first = min(first, __shfl(mine, kl * g + (sub + o) % g, 64));
+        if (!done) {
+            const double na = first == 0 ? a : a + h * (double)first;
+            const double nb = first == M ? b : fmin(b, a + h * (double)(first + 1));
+            if (!(na > a || nb < b)) {
+                done = true;
+            } else {
+                a = na;
+                b = nb;
+            }
+        }
+    }
+    return 0.5 * (a + b);
+}
+
+// Xm of step j from the records by block Sturm multisection (any j: the
+// blocks take 7 doubles each).  Waves 0..W-1 solve the updated projection
+// T, waves W..2W-1 the plain one G.
+__device__ double fused_xm_blk(int j, int fun, const double* rec /* [j][11] */, const double* cm,
+                               Blk2* blk /* [2][j] LDS */, double* ev /* [2][2j] LDS */) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nn = 2 * j;
+    for (int t = tid; t < 2 * j; t += kFusedThreads) {
+        const int mat = t / j, k = t % j;  // mat 0: T = G + Cm, 1: G
+        const double* h = rec + 11 * k;
+        Blk2 m;
+        double d00 = h[2], d10 = h[3], d01 = h[6], d11 = h[7];
+        if (mat == 0 && k == 0) {  // T(0:1, 0:1) += Cm (column-major)
+            d00 += cm[0];
+            d10 += cm[1];
+            d01 += cm[2];
+            d11 += cm[3];
+        }
+        m.a = d00;
+        m.b = 0.5 * (d10 + d01);  // (X + X')/2, lower + upper as the dense path adds them
+        m.c = d11;
+        if (k + 1 < j) {  // coupling to block k+1: lower block from record k, upper from record k+1
+            const double* h1 = rec + 11 * (k + 1);
+            m.u0 = 0.5 * (h[8] + h1[0]);
+            m.u1 = 0.5 * (0.0 + h1[4]);
+            m.u2 = 0.5 * (h[9] + h1[1]);
+            m.u3 = 0.5 * (h[10] + h1[5]);
+        } else {
+            m.u0 = m.u1 = m.u2 = m.u3 = 0.0;
+        }
+        blk[mat * j + k] = m;
+    }
+    __syncthreads();
+    constexpr int W = kFusedWaves / 2;
+    const int mat = wave / W, wv = wave % W;
+    const int per = (nn + W - 1) / W;
+    const int k0 = wv * per;
+    const int ne = min(per, nn - k0);
+    for (int e0 = 0; e0 < ne; e0 += 64) {  // more than 64 eigenvalues per wave: 64 at a time
+        const int cnt = min(64, ne - e0);
+        const double lam = wave_multisect_blk<4>(j, blk + mat * j, k0 + e0, cnt);
+        const int g = 64 / cnt;
+        if (lane % g == 0 && lane / g < cnt) ev[mat * nn + k0 + e0 + lane / g] = lam;
+    }
+    __syncthreads();
+    double term = 0.0;  // :85-89 (k-th smallest of each)
+    if (wave == 0)
+        for (int i = lane; i < nn; i += 64)
+            term += (fun == 0) ? exp(ev[i]) * (1.0 - exp(ev[nn + i] - ev[i]))
+                               : dev_fscalar(fun, ev[i]) - dev_fscalar(fun, ev[nn + i]);
+    term = wave_sum64(term);
+    __shared__ double s_xm2;
+    if (tid == 0) s_xm2 = term;
+    __syncthreads();
+    const double xm = s_xm2;
+    __syncthreads();
+    return xm;
+}
+
+__global__ __launch_bounds__(kFusedThreads) void k_pair_fused(
+    int C, int n, FusedCSR M, const int* __restrict__ ii, const int* __restrict__ jj, double b00,
+    double b10, double b01, double b11, int it, int fun, double tol, double* __restrict__ vec,
+    double* __restrict__ big, int64_t big_stride, double* __restrict__ state, int blk_eig) {
+    extern __shared__ double sm[];  // eig workspace (2 nn^2 + 6 nn) | records [it][11]
+    __shared__ double red[kFusedWaves * 8];  // block_sum scratch
+    __shared__ double cf[CF_NCOEF];
+    __shared__ double rec0[11];
+    __shared__ double cm[4];
+    const int c = blockIdx.x, tid = threadIdx.x;
+    const int64_t vn = 2 * (int64_t)n;
+    double* V[3] = {vec + 3 * vn * c, vec + 3 * vn * c + vn, vec + 3 * vn * c + 2 * vn};
+    double* eigsm = sm;
+    const size_t eigw = blk_eig ? (size_t)18 * it
+                                : (size_t)2 * kFusedMaxNN * kFusedMaxNN + 6 * kFusedMaxNN;
+    double* rec = sm + eigw;  // [it][11]
+    // [V, ~] = qr(U, 0), U = [e_i e_j]   (lanczos_krylov.m:48; krylov_miobi.m:82-84)
+    for (int64_t t = tid; t < vn; t += kFusedThreads) V[0][t] = 0.0;
+    __syncthreads();
+    if (tid == 0) {
+        V[0][2 * (int64_t)ii[c]] = 1.0;
+        V[0][2 * (int64_t)jj[c] + 1] = 1.0;
+    }
+    __syncthreads();
+    fused_orth(n, nullptr, nullptr, V[0], cf, red, rec0);
+    if (tid == 0) {  // Cm = R B R'  (trace_fun_update.m:65-66; V1' U = R for unit selectors)
+        const double R00 = rec0[8], R01 = rec0[9], R11 = rec0[10];  // R = [R00 R01; 0 R11]
+        const double RB00 = R00 * b00 + R01 * b10, RB01 = R00 * b01 + R01 * b11;
+        const double RB10 = R11 * b10, RB11 = R11 * b11;
+        cm[0] = RB00 * R00 + RB01 * R01;  // column-major (0,0)
+        cm[1] = RB10 * R00 + RB11 * R01;  // (1,0)
+        cm[2] = RB01 * R11;               // (0,1)
+        cm[3] = RB11 * R11;               // (1,1)
+    }
+    __syncthreads();
+    int prev = -1, cur = 0, w = 1;
+    double x0 = 0.0, x1 = 0.0, xm = 0.0;
+    int iter = it, lucky = 0;
+    double* mybig = big ? big + big_stride * c : nullptr;
+    for (int j = 1; j <= it; ++j) {
+        fused_spmm(n, M, V[cur], V[w]);  // w = A * w   (lanczos_krylov.m:81)
+        __syncthreads();
+        fused_orth(n, prev >= 0 ? V[prev] : nullptr, V[cur], V[w], cf, red, rec + 11 * (j - 1));
+        if (!blk_eig && 2 * j > kFusedMaxNN && !mybig) {  // no global scratch: cannot continue (host checks)
+            iter = -j;
+            break;
+        }
+#ifdef KT_FUSED_NOEIG  // diagnostic build: vector work only (never stops early)
+        xm = (double)j;
+        (void)eigsm;
+#else
+        if (blk_eig)
+            xm = fused_xm_blk(j, fun, rec, cm, reinterpret_cast<Blk2*>(eigsm), eigsm + 14 * (size_t)it);
+        else
+            xm = fused_xm(j, fun, rec, cm, eigsm, mybig);
+#endif
+        const double* hj = rec + 11 * (j - 1);
+        lucky = sqrt(hj[8] * hj[8] + hj[9] * hj[9] + hj[10] * hj[10]) < 1e-8;  // :91-93
+        bool stop = false;
+        if (j <= 2) {  // :104-118, lag d = 2
+            if (j == 1) x0 = xm;
+            else x1 = xm;
+        } else if (fabs(xm - x0) < tol) {
+            stop = true;
+        } else {
+            x0 = x1;
+            x1 = xm;
+        }
+        if (stop || lucky || j == it) {
+            iter = j;
+            break;
+        }
+        const int freed = prev >= 0 ? prev : 3 - cur - w;
+        prev = cur;
+        cur = w;
+        w = freed;
+    }
+    if (tid == 0) {
+        double* st = state + (int64_t)c * PS_N;
+        st[PS_XM] = xm;
+        st[PS_ITER] = iter;
+        st[PS_LUCKY] = lucky ? 1.0 : 0.0;
+        st[PS_DONE] = 1.0;
+    }
+}
+
+// dynamic LDS: the eigen workspace (dense: 2 nn^2 + 6 nn at nn <= 56; block
+// Sturm: 2 j Blk2 + 4 j eigenvalues) followed by the records [it][11]
+// Batched path's per-step eigenproblems by block Sturm counts (any 2j; one
+// workgroup per candidate): the records of candidate c come from hist
+// [step][C][11]; same Xm, lag-2 stop and lucky test as k_pair_eig_wave.
+__global__ __launch_bounds__(kFusedThreads) void k_pair_eig_blk(int C, int j, int it, int fun, double tol,
+                                                               const double* __restrict__ hist,
+                                                               const double* __restrict__ Cm,
+                                                               double* __restrict__ state) {
+    extern __shared__ double sm[];  // records [j][11] | blocks [2][j] Blk2 | eigenvalues [2][2j]
+    const int c = blockIdx.x, tid = threadIdx.x;
+    double* st = state + (int64_t)c * PS_N;
+    if (st[PS_DONE] != 0.0) return;  // uniform over the workgroup
+    double* rec = sm;
+    Blk2* blk = reinterpret_cast<Blk2*>(sm + 11 * (size_t)j);
+    double* ev = sm + 11 * (size_t)j + 14 * (size_t)j;
+    __shared__ double cm[4];
+    for (int t = tid; t < 11 * j; t += kFusedThreads) rec[t] = hist[((int64_t)(t / 11) * C + c) * 11 + t % 11];
+    if (tid < 4) cm[tid] = Cm[(int64_t)c * 4 + tid];
+    __syncthreads();
+    const double xm = fused_xm_blk(j, fun, rec, cm, blk, ev);
+    if (tid == 0) {
+        const double* hj = rec + 11 * (j - 1);
+        const bool lucky = sqrt(hj[8] * hj[8] + hj[9] * hj[9] + hj[10] * hj[10]) < 1e-8;
+        st[PS_XM] = xm;
+        st[PS_LUCKY] = lucky ? 1.0 : 0.0;
+        bool stop = false;
+        if (j <= 2) {
+            st[PS_X0 + j - 1] = xm;
+        } else if (fabs(xm - st[PS_X0]) < tol) {
+            stop = true;
+        } else {
+            st[PS_X0] = st[PS_X1];
+            st[PS_X1] = xm;
+        }
+        if (stop || lucky || j == it) {
+            st[PS_DONE] = 1.0;
+            st[PS_ITER] = j;
+        }
+    }
+}
+
+size_t pair_fused_lds_bytes(int it) {
+    const size_t dense = (size_t)2 * kFusedMaxNN * kFusedMaxNN + 6 * kFusedMaxNN;
+    const size_t blk = (size_t)14 * it + 4 * (size_t)it;
+    return sizeof(double) * (std::max(dense, blk) + 11 * (size_t)it);
+}
+
+hipError_t launch_pair_fused(int C, int n, const CsrView& A, bool unit, const int* ii, const int* jj,
+                             const double* B, int it, int fun, double tol, double* vec, double* big,
+                             int64_t big_stride, double* state, hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    const FusedCSR M{A.rp, A.ci, A.va, A.long_rows, A.n_long, A.long_thresh, unit ? 1 : 0};
+    // KT_PAIRS_DENSE_EIG=1: the dense tridiagonalisation + multisection in LDS
+    // (and the one-thread solver past 2j = 56) instead of block Sturm counts
+    const char* de = getenv("KT_PAIRS_DENSE_EIG");
+    const int blk_eig = !(de && de[0] == '1');
+    k_pair_fused<<<C, kFusedThreads, pair_fused_lds_bytes(it), st>>>(
+        C, n, M, ii, jj, B[0], B[1], B[2], B[3], it, fun, tol, vec, big, big_stride, state, blk_eig);
+    return hipGetLastError();
+}
+
 // active[0] = number of candidates not done
 __global__ void k_pair_active(int C, const double* __restrict__ state, int* __restrict__ active) {
     __shared__ int red[256];
@@ -770,7 +1456,11 @@ __global__ void k_pair_active(int C, const double* __restrict__ state, int* __re
 hipError_t launch_pair_eig(int C, int j, int it, int fun, double tol, const double* hist,
                            const double* Cm, double* scratch, int64_t sstride, double* state,
                            int* active, hipStream_t st) {
-    if (2 * j <= 56) {  // 2 nn^2 + 6 nn doubles <= 52 KB of LDS
+    const char* de = getenv("KT_PAIRS_DENSE_EIG");
+    if (!(de && de[0] == '1')) {  // block Sturm counts: no LDS limit, no one-thread fallback
+        const size_t lds = sizeof(double) * (11 * (size_t)j + 14 * (size_t)j + 4 * (size_t)j);
+        k_pair_eig_blk<<<C, kFusedThreads, lds, st>>>(C, j, it, fun, tol, hist, Cm, state);
+    } else if (2 * j <= 56) {  // 2 nn^2 + 6 nn doubles <= 52 KB of LDS
         const size_t lds = sizeof(double) * (2 * (size_t)(2 * j) * (2 * j) + 6 * (size_t)(2 * j));
         // W = 1, MS = 4 measured fastest (profiles/r01_greedy_eig_variants.txt):
         // the Sturm rounds are VALU-issue-bound, more waves per SIMD only

@@ -180,3 +180,78 @@ def test_pairs_device_and_host_eig_agree(kra, gpu_ctx, monkeypatch):
     np.testing.assert_allclose(x_dev, x_host, rtol=1e-11, atol=1e-13)
     np.testing.assert_array_equal(it_dev, it_host)
     np.testing.assert_array_equal(l_dev, l_host)
+
+
+@pytest.mark.parametrize("tol,it", [(1e-10, 100), (1e-30, 40)])
+def test_pairs_fused_matches_batched(kra, gpu_ctx, monkeypatch, tol, it):
+    """One workgroup per candidate running its whole trace_fun_update in one
+    launch (k_pair_fused, the default for n <= 16384) gives the batched
+    per-step path's scores (KT_PAIRS_FUSED=0): the same CGS2 / Householder
+    arithmetic with workgroup instead of grid reductions, eigenvalues by
+    block Sturm counts instead of tridiagonalisation + Sturm.  Both deliver
+    eigenvalues to O(eps ||T||); Xm = sum exp(l1)(1 - exp(l2 - l1)) over 2j
+    terms turns that into ~1e-12 absolute, i.e. up to 1e-10 relative at
+    |Xm| ~ 0.1 -- and the same iteration counts and lucky flags.  tol = 1e-30 drives candidates
+    past 2j = 56, where the projected eigenproblems leave LDS for the
+    global-scratch solver; there the lag-2 test can only fire on bitwise
+    equal iterates and late lucky breakdowns sit at the 1e-8 threshold, so
+    WHEN a candidate stops is rounding-dependent -- scores still agree."""
+    A, c = _india(kra)
+    E = kra.find_top_edges(A, c, 64, "min")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    x_f, it_f, l_f = kra.trace_fun_update_pairs(D, E, BREAK, tol, it, ctx=gpu_ctx)
+    monkeypatch.setenv("KT_PAIRS_FUSED", "0")
+    monkeypatch.setenv("KT_PAIRS_DENSE_EIG", "1")  # the batched path with the dense LDS solver
+    x_b, it_b, l_b = kra.trace_fun_update_pairs(D, E, BREAK, tol, it, ctx=gpu_ctx)
+    np.testing.assert_allclose(x_f, x_b, rtol=1e-10, atol=1e-12)
+    if tol < 1e-20:
+        assert (it_f > 28).sum() > len(E) // 2  # the global-scratch eigen path ran
+    else:
+        np.testing.assert_array_equal(it_f, it_b)
+        np.testing.assert_array_equal(l_f, l_b)
+
+
+def test_pairs_fused_hub_rows_and_weights(kra, gpu_ctx, monkeypatch):
+    """Fused path on a weighted scale-free graph with rows longer than 64
+    (wave-per-row SpMM branch), vs the batched path and single calls."""
+    from krylov_robustness_amd import graphs
+    A = graphs.chung_lu(3000, 24000, seed=11)
+    rng = np.random.default_rng(2)
+    A = sp.triu(A, 1)
+    A.data = rng.uniform(0.2, 1.0, A.nnz)
+    A = (A + A.T).tocsr()
+    assert np.diff(A.indptr).max() > 64
+    c = kra.compute_centrality(A)
+    E = kra.find_top_edges(A, c, 40, "min")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    # the reference's stopping tolerance (test_unweighted_break.m:74): an
+    # absolute 1e-10 would sit at the rounding noise of |Xm| ~ 10-100 here
+    tol = 1e-6 * np.exp(kra.normest(D, 1e-2, ctx=gpu_ctx))
+    x_f, it_f, _ = kra.trace_fun_update_pairs(D, E, BREAK, tol, 100, ctx=gpu_ctx)
+    monkeypatch.setenv("KT_PAIRS_FUSED", "0")
+    monkeypatch.setenv("KT_PAIRS_DENSE_EIG", "1")
+    x_b, it_b, _ = kra.trace_fun_update_pairs(D, E, BREAK, tol, 100, ctx=gpu_ctx)
+    np.testing.assert_allclose(x_f, x_b, rtol=1e-10, atol=1e-12)
+    np.testing.assert_array_equal(it_f, it_b)
+    for h in (0, 17, 39):
+        x1, i1, _ = kra.trace_fun_update(D, _U(A.shape[0], *E[h]), BREAK, tol, 100, ctx=gpu_ctx)
+        assert x_f[h] == pytest.approx(x1, rel=1e-9, abs=1e-12)
+        assert it_f[h] == i1
+
+
+def test_pairs_batched_block_sturm_eig(kra, gpu_ctx, monkeypatch):
+    """The batched per-step path (KT_PAIRS_FUSED=0, used above n = 16384)
+    with its eigenproblems by block Sturm counts (k_pair_eig_blk, default)
+    vs the dense LDS solver (KT_PAIRS_DENSE_EIG=1): same scores (1e-10, the
+    eigen accuracy argument of test_pairs_fused_matches_batched), same
+    iteration counts and lucky flags."""
+    A, c = _india(kra)
+    E = kra.find_top_edges(A, c, 48, "min")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    monkeypatch.setenv("KT_PAIRS_FUSED", "0")
+    x_s, it_s, l_s = kra.trace_fun_update_pairs(D, E, BREAK, 1e-10, 100, ctx=gpu_ctx)
+    monkeypatch.setenv("KT_PAIRS_DENSE_EIG", "1")
+    x_d, it_d, l_d = kra.trace_fun_update_pairs(D, E, BREAK, 1e-10, 100, ctx=gpu_ctx)
+    np.testing.assert_allclose(x_s, x_d, rtol=1e-10, atol=1e-12)
+    np.testing.assert_array_equal(it_s, it_d)
+    np.testing.assert_array_equal(l_s, l_d)
