@@ -909,8 +909,8 @@ static void gradient(kt_matrix_s* A, FunUpdateResult& fu, int64_t nom, const dou
 // workspace): the caller then runs the serial order, which needs no second
 // copy, instead of failing.  A failed build is not retried until A changes.
 kt_matrix_s* twin_of(kt_matrix_s* A) {
-    static const bool off = getenv("KT_TWIN") && getenv("KT_TWIN")[0] == '0';
-    if (off) return nullptr;
+    const char* tw = getenv("KT_TWIN");  // read per call (A/B within one process)
+    if (tw && tw[0] == '0') return nullptr;
     if (A->twin && A->twin_version == A->version) return A->twin;
     if (A->twin_failed && A->twin_failed_version == A->version) return nullptr;
     if (A->twin) {

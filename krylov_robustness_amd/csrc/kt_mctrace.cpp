@@ -11,7 +11,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <thread>
 
+#include "kt_krylov.h"
 #include "kt_launch.h"
 #include "kt_slq.h"
 
@@ -276,7 +278,7 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
     const int K = (maxit + 3 * mb - 1) / (3 * mb);  // :41 ceil(maxit/30)
     double tr = 0.0, tr_old = 0.0, tr_new = 0.0, res = 1.0;
     std::vector<DevMat> Qs;
-    DevMat S, G, Z, Y;
+    DevMat S, G, Z, Y, Zg2;
     int it = 0;
     for (it = 1; it <= K; ++it) {
         const int64_t base = (int64_t)(it - 1) * 2 * mb;
@@ -298,15 +300,49 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
         // tr += trace(Q' Afun_it(Q)) = sum quadforms of P_1..P_{it-1} Q          :46
         copy_cols(ctx, n, Y.col(0), ld, Z.col(0), ld, mb);
         for (int q = (int)Qs.size() - 1; q >= 0; --q) project(ctx, n, Qs[q].col(0), ld, mb, Z.col(0), mb);
-        tr += F.trace_quad(Z.col(0), ld, mb);
+        const bool split = !(sh.world > 1 && F.kind != AFUN_EXPMV);  // the G term is local
+        kt_matrix_s* A2 = split ? twin_of(A) : nullptr;
+        if (!A2) tr += F.trace_quad(Z.col(0), ld, mb);
         Qs.emplace_back();                                                         // :47-48
         Qs.back().alloc(ctx, n, ld);
         copy_cols(ctx, n, Y.col(0), ld, Qs.back().col(0), ld, mb);
         // tr_new = tr + trace(G' Afun_{it+1}(G)) / m                              :49
-        copy_cols(ctx, n, G.col(0), ld, Z.col(0), ld, mb);
-        for (int q = (int)Qs.size() - 1; q >= 0; --q) project(ctx, n, Qs[q].col(0), ld, mb, Z.col(0), mb);
+        DevMat& Zg = A2 ? Zg2 : Z;
+        if (A2) Zg.alloc(ctx, n, ld);
+        copy_cols(ctx, n, G.col(0), ld, Zg.col(0), ld, mb);
+        for (int q = (int)Qs.size() - 1; q >= 0; --q) project(ctx, n, Qs[q].col(0), ld, mb, Zg.col(0), mb);
         double gsum = 0.0;
-        if (sh.world > 1 && F.kind != AFUN_EXPMV) {
+        if (A2) {
+            // The two quadratures of the round are independent Afun calls:
+            // the G term runs on the matrix's twin (own stream, workspace and
+            // device copy; kt_krylov.cpp twin_of) on a second host thread
+            // while the Q term runs here -- same kernels on the same data,
+            // so the sums are bit-identical to the serial order.
+            KT_HIP(hipStreamSynchronize(ctx->stream));  // Z and Zg are ready for both streams
+            Status gerr{KT_OK, ""};
+            std::thread th([&] {
+                try {
+                    KT_HIP(hipSetDevice(A2->ctx->device));
+                    AfunDev F2{A2, F.kind, F.fun, F.m};
+                    gsum = F2.trace_quad(Zg.col(0), ld, mb);
+                    KT_HIP(hipStreamSynchronize(A2->ctx->stream));
+                } catch (const Status& e) {
+                    gerr = e;
+                } catch (...) {
+                    gerr = Status{KT_ERR_HIP, "mc_trace: G term on the twin failed"};
+                }
+            });
+            double qsum = 0.0;
+            try {
+                qsum = F.trace_quad(Z.col(0), ld, mb);
+            } catch (...) {
+                th.join();
+                throw;
+            }
+            th.join();
+            if (gerr.code != KT_OK) throw gerr;
+            tr += qsum;
+        } else if (sh.world > 1 && F.kind != AFUN_EXPMV) {
             std::vector<double> qv(mb, 0.0), qm;
             int nm = 0;
             for (int c = sh.rank; c < mb; c += sh.world) copy_cols(ctx, n, Z.col(c), ld, Y.col(nm++), ld, 1);

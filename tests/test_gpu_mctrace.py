@@ -90,3 +90,26 @@ def test_trace_exp_lanczos_config1(kra, gpu_ctx, values):
     assert tr == pytest.approx(values["oregon_A6"]["exact_tr_exp"], rel=1e-3)
     full = kra.trace_exp(D, method="lanczos", m=20, seed=0, ctx=gpu_ctx)   # tol 1e-4, maxit 1000
     assert full == pytest.approx(values["oregon_A6"]["exact_tr_exp"], rel=1e-4)
+
+
+@pytest.mark.parametrize("afun", ["expmv", "lanczos", "matrix"])
+def test_mc_trace_twin_split_is_bit_identical(kra, gpu_ctx, monkeypatch, afun):
+    """Each round's two quadratures (trace(Q' Afun Q) and trace(G' Afun G),
+    mc_trace.m:46,49) run concurrently, the G term on the matrix's twin
+    context: the same kernels on the same data as the serial order
+    (KT_TWIN=0), so tr, res and the round count are bit-identical."""
+    A = load_graph("oregon_A0")
+    args = dict(n=A.shape[0], tol=1e-4, maxit=150, isAreal=1, seed=3, m=20)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    if afun == "matrix":
+        par = kra.mc_trace(D, ctx=gpu_ctx, **args)
+    else:
+        par = kra.mc_trace(afun, A=D, ctx=gpu_ctx, **args)
+    monkeypatch.setenv("KT_TWIN", "0")
+    D2 = kra.DeviceMatrix(A, gpu_ctx)
+    if afun == "matrix":
+        ser = kra.mc_trace(D2, ctx=gpu_ctx, **args)
+    else:
+        ser = kra.mc_trace(afun, A=D2, ctx=gpu_ctx, **args)
+    assert par == ser
+    assert par[2] > 1  # several rounds (nested deflation) were run
