@@ -1259,6 +1259,67 @@ __global__ __launch_bounds__(256) void k_inf_norm(int n, int nc, const double* _
     if (threadIdx.x == 0) partial[blockIdx.x] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
 }
 
+// normest1 (t = 1, normAm.m:25): statistics of Y = B^m X for the host's
+// iteration -- per-block sum |Y| and S_prev . S, with S = mysign(Y)
+// (sign(0) = +1) written for the transposed product.  The sign dot is a sum
+// of +-1 terms, exact in fp64.
+__global__ __launch_bounds__(256) void k_normest1_y(int n, const double* __restrict__ Y,
+                                                   const double* __restrict__ Sprev,
+                                                   double* __restrict__ S,
+                                                   double* __restrict__ partial) {
+    double a = 0.0, d = 0.0;
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+        const double y = Y[r];
+        const double s = y < 0.0 ? -1.0 : 1.0;
+        a += fabs(y);
+        d = fma(Sprev[r], s, d);
+        S[r] = s;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        d += __shfl_xor(d, o, 64);
+    }
+    __shared__ double red[2][4];
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = a;
+        red[1][threadIdx.x >> 6] = d;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        partial[blockIdx.x] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+        partial[gridDim.x + blockIdx.x] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    }
+}
+
+// per-block max |Z| and the smallest row index attaining it (normest1's
+// h = abs(Z) and its ordering for t = 1)
+__device__ __forceinline__ void absmax_merge(double& v, int& i, double v2, int i2) {
+    if (v2 > v || (v2 == v && i2 < i)) {
+        v = v2;
+        i = i2;
+    }
+}
+__global__ __launch_bounds__(256) void k_absmax_idx(int n, const double* __restrict__ Z,
+                                                    double* __restrict__ pval, int* __restrict__ pidx) {
+    double v = -1.0;
+    int i = 0x7fffffff;
+    for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x)
+        absmax_merge(v, i, fabs(Z[r]), r);
+    for (int o = 32; o > 0; o >>= 1) absmax_merge(v, i, __shfl_xor(v, o, 64), __shfl_xor(i, o, 64));
+    __shared__ double sv[4];
+    __shared__ int si[4];
+    if ((threadIdx.x & 63) == 0) {
+        sv[threadIdx.x >> 6] = v;
+        si[threadIdx.x >> 6] = i;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) absmax_merge(v, i, sv[w], si[w]);
+        pval[blockIdx.x] = v;
+        pidx[blockIdx.x] = i;
+    }
+}
+
 __global__ void k_fill(double* __restrict__ x, int count, double v) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < count) x[t] = v;
@@ -1902,6 +1963,22 @@ hipError_t launch_gather_elems(int64_t count, const double* D, const int64_t* of
                                hipStream_t st) {
     if (count <= 0) return hipSuccess;
     k_gather_elems<<<stream_grid(count), 256, 0, st>>>(count, D, off, out);
+    return hipGetLastError();
+}
+
+int normest1_blocks(int n) {
+    const int b = (n + 255) / 256;
+    return b < 1 ? 1 : (b > 1024 ? 1024 : b);
+}
+
+hipError_t launch_normest1_y(int n, const double* Y, const double* Sprev, double* S, double* partial,
+                             hipStream_t st) {
+    k_normest1_y<<<normest1_blocks(n), 256, 0, st>>>(n, Y, Sprev, S, partial);
+    return hipGetLastError();
+}
+
+hipError_t launch_absmax_idx(int n, const double* Z, double* pval, int* pidx, hipStream_t st) {
+    k_absmax_idx<<<normest1_blocks(n), 256, 0, st>>>(n, Z, pval, pidx);
     return hipGetLastError();
 }
 

@@ -93,6 +93,13 @@ hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int
 hipError_t launch_axpby(int n, int nc, double a, const double* X, int ldx, double b, double* Y,
                         int ldy, hipStream_t st);
 int inf_norm_blocks();
+// normest1 (t = 1) reductions, normest1_blocks(n) partials each: sum |Y| in
+// partial[0, nb), S_prev . S in partial[nb, 2 nb), S = mysign(Y); per-block
+// max |Z| and its smallest index
+int normest1_blocks(int n);
+hipError_t launch_normest1_y(int n, const double* Y, const double* Sprev, double* S, double* partial,
+                             hipStream_t st);
+hipError_t launch_absmax_idx(int n, const double* Z, double* pval, int* pidx, hipStream_t st);
 // batched greedy candidates (kt_pairs.hip)
 hipError_t launch_pair_select(int C, const int* ii, const int* jj, double* X, int ld,
                               hipStream_t st);

@@ -51,11 +51,18 @@ static const double kTheta[100] = {
 
 enum { AFUN_MATRIX = 0, AFUN_LANCZOS = 1, AFUN_EXPMV = 2 };
 
-// normAm.m: ||A^m||_1 for A >= 0 (exact: e = A'^m ones, c = ||e||_inf), for
+// B = A - mu I (expmv.m:33-36 shift; A symmetric, so B' = B): y = B x on one
+// column, as the SpMV of A followed by y -= mu x.
+static void shifted_spmv(kt_matrix_s* A, double mu, const double* x, double* y) {
+    spmm(A, x, 1, y, 1, 1);
+    if (mu != 0.0) KT_HIP(launch_axpby((int)A->n, 1, -mu, x, 1, 1.0, y, 1, A->ctx->stream));
+}
+
+// normAm.m: ||A^m||_1 for A - mu I >= 0 (exact: e = A'^m ones, c = ||e||_inf), for
 // every m = 2..mmax at once: select_taylor_degree.m:48-53 asks for
 // m = p + 1, p = 1..p_max, each from ones -- the same vectors A^m ones, so
 // one chain of mmax SpMVs gives them all (one host round trip).
-static std::vector<double> normAm_chain(kt_matrix_s* A, int mmax) {
+static std::vector<double> normAm_chain(kt_matrix_s* A, double mu, int mmax) {
     kt_context_s* ctx = A->ctx;
     const int64_t n = A->n;
     const int nb = inf_norm_blocks();
@@ -65,8 +72,8 @@ static std::vector<double> normAm_chain(kt_matrix_s* A, int mmax) {
     DevBuf& part = ctx->ws.norm_part;
     part.ensure(sizeof(double) * (size_t)nb * (mmax + 1));
     KT_HIP(launch_fill(e.col(0), (int)n, 1.0, ctx->stream));
-    for (int j = 1; j <= mmax; ++j) {  // A symmetric: A' = A
-        spmm(A, e.col(0), 1, t.col(0), 1, 1);
+    for (int j = 1; j <= mmax; ++j) {  // B' e = B e
+        shifted_spmv(A, mu, e.col(0), t.col(0));
         copy_cols(ctx, n, t.col(0), 1, e.col(0), 1, 1);
         KT_HIP(launch_inf_norm((int)n, 1, e.col(0), 1, part.as<double>() + (size_t)j * nb, ctx->stream));
     }
@@ -78,6 +85,111 @@ static std::vector<double> normAm_chain(kt_matrix_s* A, int mmax) {
     for (int j = 1; j <= mmax; ++j)
         c[j] = *std::max_element(h.begin() + (size_t)j * nb, h.begin() + (size_t)(j + 1) * nb);
     return c;
+}
+
+// normAm.m:25-26 for a matrix with negative entries: [c,~,~,it] =
+// normest1(@afun_power, t = 1), the Higham-Tisseur estimator (Algorithm 2.4)
+// of ||C^m||_1, C = t (A - mu I), with one column -- deterministic: start
+// ones/n, then unit vectors e_ind at the largest |Z| (smallest index on
+// ties), stop on no improvement, parallel signs, a repeated best index or
+// after itmax = 5 (oracle/krylov_oracle.py normest1_t1).  C is symmetric,
+// so the transposed products are the same chain.  Products and reductions
+// run on the device; the host reads 2-3 partial vectors per iteration.
+// Returns {c, mv = it(2) * m}.
+static std::pair<double, int> normest1_power(kt_matrix_s* A, double mu, double t, int m) {
+    kt_context_s* ctx = A->ctx;
+    hipStream_t st = ctx->stream;
+    const int64_t n = A->n;
+    DevMat X, Y, T, S0, S1;
+    X.alloc(ctx, n, 1);
+    Y.alloc(ctx, n, 1);
+    T.alloc(ctx, n, 1);
+    S0.alloc(ctx, n, 1);  // S_old (zero before the first sign vector)
+    S1.alloc(ctx, n, 1);
+    auto apply = [&](const double* in, double* out) {  // out = C^m in (in kept)
+        const double* src = in;
+        for (int i = 0; i < m; ++i) {
+            double* dst = (i % 2 == m % 2) ? T.col(0) : out;  // the last product lands in out
+            shifted_spmv(A, mu, src, dst);
+            if (t != 1.0) KT_HIP(launch_axpby((int)n, 1, t, dst, 1, 0.0, dst, 1, st));
+            src = dst;
+        }
+    };
+    auto unit = [&](double* x, int64_t i) {
+        static const double one = 1.0;
+        KT_HIP(hipMemsetAsync(x, 0, sizeof(double) * (size_t)n, st));
+        KT_HIP(hipMemcpyAsync(x + i, &one, sizeof(double), hipMemcpyHostToDevice, st));
+    };
+    const int nb = normest1_blocks((int)n);
+    DevBuf& part = ctx->ws.norm_part;
+    part.ensure(std::max(sizeof(double) * 2 * nb, (sizeof(double) + sizeof(int)) * nb));
+    std::vector<double> hp(2 * nb);
+    std::vector<int> hi(nb);
+    if (n <= 4) {  // exact: the identity's columns (normest1's small-n branch)
+        double est = 0.0;
+        std::vector<double> y(n);
+        for (int64_t j = 0; j < n; ++j) {
+            unit(X.col(0), j);
+            apply(X.col(0), Y.col(0));
+            KT_HIP(hipMemcpyAsync(y.data(), Y.col(0), sizeof(double) * n, hipMemcpyDeviceToHost, st));
+            KT_HIP(hipStreamSynchronize(st));
+            double s = 0.0;
+            for (double v : y) s += std::fabs(v);
+            est = std::max(est, s);
+        }
+        return {est, 0};
+    }
+    KT_HIP(launch_fill(X.col(0), (int)n, 1.0 / (double)n, st));
+    double* S = S1.col(0);
+    double* S_old = S0.col(0);
+    const int itmax = 5;
+    double est = 0.0, est_old = 0.0;
+    int64_t ind = -1, ind_best = -1;
+    int k = 1, it2 = 0;
+    while (true) {
+        apply(X.col(0), Y.col(0));                                       // (1) Y = C^m X
+        KT_HIP(launch_normest1_y((int)n, Y.col(0), S_old, S, part.as<double>(), st));
+        KT_HIP(hipMemcpyAsync(hp.data(), part.ptr, sizeof(double) * 2 * nb, hipMemcpyDeviceToHost, st));
+        KT_HIP(hipStreamSynchronize(st));
+        double ssum = 0.0, dot = 0.0;
+        for (int b = 0; b < nb; ++b) {
+            ssum += hp[b];
+            dot += hp[nb + b];
+        }
+        est = ssum;
+        if ((est > est_old || k == 2) && k >= 2) ind_best = ind;
+        if (k >= 2 && est <= est_old) {                                  // (2)
+            est = est_old;
+            break;
+        }
+        est_old = est;
+        if (k > itmax) break;
+        if (std::fabs(dot) == (double)n) break;                          // (3) S parallel to S_old
+        apply(S, Y.col(0));                                              // (4) Z = C^m S (into Y)
+        ++it2;
+        double* pv = part.as<double>();
+        int* pi = reinterpret_cast<int*>(pv + nb);
+        KT_HIP(launch_absmax_idx((int)n, Y.col(0), pv, pi, st));
+        double zbest = 0.0;
+        KT_HIP(hipMemcpyAsync(hp.data(), pv, sizeof(double) * nb, hipMemcpyDeviceToHost, st));
+        KT_HIP(hipMemcpyAsync(hi.data(), pi, sizeof(int) * nb, hipMemcpyDeviceToHost, st));
+        if (k >= 2)
+            KT_HIP(hipMemcpyAsync(&zbest, Y.col(0) + ind_best, sizeof(double), hipMemcpyDeviceToHost, st));
+        KT_HIP(hipStreamSynchronize(st));
+        double hmax = -1.0;
+        int imax = 0x7fffffff;
+        for (int b = 0; b < nb; ++b)
+            if (hp[b] > hmax || (hp[b] == hmax && hi[b] < imax)) {
+                hmax = hp[b];
+                imax = hi[b];
+            }
+        if (k >= 2 && hmax == std::fabs(zbest)) break;                   // (5)
+        ind = imax;
+        unit(X.col(0), ind);                                             // X = e_ind
+        std::swap(S, S_old);
+        ++k;
+    }
+    return {est, it2 * m};
 }
 
 struct Expmv {
@@ -92,12 +204,10 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
     hipStream_t st = ctx->stream;
     Expmv r;
     // shift: mu = trace(A)/n   (:31-36)
-    double trA = 0.0, minv = 0.0;
+    double trA = 0.0;
     for (int64_t i = 0; i < n; ++i)
-        for (int64_t k = A->h_rowptr[i]; k < A->h_rowptr[i + 1]; ++k) {
+        for (int64_t k = A->h_rowptr[i]; k < A->h_rowptr[i + 1]; ++k)
             if (A->h_col[k] == i) trA += A->h_val[k];
-            minv = std::min(minv, A->h_val[k]);
-        }
     const double mu = n ? trA / (double)n : 0.0;
     // select_taylor_degree(t*(A - mu I), b)   (:41; select_taylor_degree.m:16-68)
     const int m_max = 55, p_max = 8;
@@ -115,14 +225,32 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
     if (normA <= 4.0 * kTheta[m_max - 1] * p_max * (p_max + 3) / ((double)m_max * nc)) {
         std::fill(alpha.begin(), alpha.end(), normA);  // unA = 1
     } else {
-        if (mu != 0.0 || minv < 0.0)
-            fail(KT_ERR_UNSUPPORTED, "expmv: normest1 branch of normAm.m (A - mu I not >= 0) is not built");
+        // normAm.m:17 isequal(A, abs(A)) on t (A - mu I): every stored entry
+        // and every diagonal (absent ones are -mu) times t is >= 0
+        bool nonneg = true;
+        for (int64_t i = 0; i < n && nonneg; ++i) {
+            bool has = false;
+            for (int64_t k = A->h_rowptr[i]; k < A->h_rowptr[i + 1]; ++k) {
+                const bool dg = A->h_col[k] == i;
+                has |= dg;
+                if (t * (A->h_val[k] - (dg ? mu : 0.0)) < 0.0) nonneg = false;
+            }
+            if (!has && t * -mu < 0.0) nonneg = false;
+        }
         std::vector<double> eta(p_max);
-        const std::vector<double> nAm = normAm_chain(A, p_max + 1);
-        for (int p = 1; p <= p_max; ++p) {
-            const double c = nAm[p + 1] * std::pow(std::fabs(t), p + 1);
-            r.mv += p + 1;  // as normAm.m counts them (one chain per m)
-            eta[p - 1] = std::pow(c, 1.0 / (p + 1));
+        if (nonneg) {
+            const std::vector<double> nAm = normAm_chain(A, mu, p_max + 1);
+            for (int p = 1; p <= p_max; ++p) {
+                const double c = nAm[p + 1] * std::pow(std::fabs(t), p + 1);
+                r.mv += p + 1;  // as normAm.m counts them (one chain per m)
+                eta[p - 1] = std::pow(c, 1.0 / (p + 1));
+            }
+        } else {
+            for (int p = 1; p <= p_max; ++p) {  // :25-26 normest1, mv = it(2) * m
+                const std::pair<double, int> cm = normest1_power(A, mu, t, p + 1);
+                r.mv += cm.second;
+                eta[p - 1] = std::pow(cm.first, 1.0 / (p + 1));
+            }
         }
         for (int p = 1; p < p_max; ++p) alpha[p - 1] = std::max(eta[p - 1], eta[p]);
     }

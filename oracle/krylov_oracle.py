@@ -503,6 +503,66 @@ def theta_taylor():
     return _THETA
 
 
+def _mysign(y):
+    """normest1's mysign: sign with sign(0) = +1."""
+    s = np.sign(y)
+    s[s == 0] = 1.0
+    return s
+
+
+def normest1_t1(matvec, rmatvec, n):
+    """[est, ~, ~, it] = normest1(afun, t = 1) -- the block 1-norm estimator
+    of Higham & Tisseur (SIAM J. Matrix Anal. Appl. 21(4), 2000, Algorithm
+    2.4) that normAm.m:25 calls with ONE column, so no random start columns
+    and no column de-duplication are involved: the iteration is
+    deterministic.  MATLAB's normest1 itself is a closed built-in (not in the
+    reference); this restates the published algorithm, with
+    ties in the ordering of h broken towards the smallest index.  Returns
+    (est, it1, it2) -- it2 = the number of transposed products, which
+    normAm.m:26 turns into mv = it(2) * t * m.
+      n <= 4: the exact norm from the identity's columns (no iteration)."""
+    if n <= 4:
+        Y = np.column_stack([matvec(e) for e in np.eye(n)])
+        return float(np.abs(Y).sum(axis=0).max()), 1, 0
+    X = np.ones(n) / n                                    # X = ones(n,t)/n
+    itmax = 5
+    est_old = 0.0
+    ind = -1                                              # index of the unit vector X
+    ind_best = -1
+    S = np.zeros(n)
+    k = 1
+    it1 = it2 = 0
+    est = 0.0
+    while True:
+        Y = matvec(X)                                     # (1) Y = A X
+        it1 += 1
+        est = float(np.abs(Y).sum())
+        if est > est_old or k == 2:
+            if k >= 2:
+                ind_best = ind
+        if k >= 2 and est <= est_old:                     # (2) no improvement
+            est = est_old
+            break
+        est_old = est
+        S_old = S
+        if k > itmax:
+            break
+        S = _mysign(Y)                                    # (3)
+        if abs(float(S_old @ S)) == n:                    # S parallel to S_old
+            break
+        Z = rmatvec(S)                                    # (4) Z = A' S
+        it2 += 1
+        h = np.abs(Z)
+        hmax = float(h.max())
+        if k >= 2 and hmax == h[ind_best]:                # (5)
+            break
+        ind = int(np.argmax(h))                           # first index of the maximum
+        X = np.zeros(n)                                   # X = e_ind
+        X[ind] = 1.0
+        k += 1
+    return est, it1, it2
+
+
 def normAm(A, m):
     """normAm.m:1-52."""
     n = A.shape[0]
@@ -512,10 +572,8 @@ def normAm(A, m):
         for _ in range(m):
             e = A.T @ e
         return float(np.max(np.abs(e))), m
-    # :25-26 normest1(@afun_power, t=1): SciPy's onenormest is the same
-    # Higham-Tisseur block 1-norm estimator (published algorithm).
-    from scipy.sparse.linalg import LinearOperator, onenormest
 
+    # :25-26 [c,v,w,it] = normest1(@afun_power, t = 1); mv = it(2)*t*m
     def mv(x):
         for _ in range(m):
             x = A @ x
@@ -525,9 +583,8 @@ def normAm(A, m):
         for _ in range(m):
             x = A.T @ x
         return x
-    op = LinearOperator((n, n), matvec=mv, rmatvec=rmv, dtype=np.float64)
-    c = onenormest(op, t=1)
-    return float(c), 2 * m
+    c, _, it2 = normest1_t1(mv, rmv, n)
+    return float(c), it2 * m
 
 
 def select_taylor_degree(A, b, m_max=55, p_max=8, shift=False, force_estm=False):

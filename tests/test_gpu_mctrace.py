@@ -113,3 +113,29 @@ def test_mc_trace_twin_split_is_bit_identical(kra, gpu_ctx, monkeypatch, afun):
         ser = kra.mc_trace(afun, A=D2, ctx=gpu_ctx, **args)
     assert par == ser
     assert par[2] > 1  # several rounds (nested deflation) were run
+
+
+@pytest.mark.parametrize("kind", ["loops", "signed"])
+def test_expmv_normest1_branch_matches_oracle(kra, gpu_ctx, kind):
+    """normAm.m:25-26: t (A - mu I) with negative entries (self loops after the
+    shift, or signed weights) -> normest1 (t = 1) on the device (products and
+    reductions on the device, the Higham-Tisseur iteration on the host); the
+    same s, m, mv as the oracle's restatement and F to 1e-11."""
+    from test_normest1 import looped, signed_graph
+    A = looped(load_graph("oregon_A0")) if kind == "loops" else 4.0 * signed_graph(300, seed=5)
+    b = np.random.default_rng(1).normal(size=(A.shape[0], 3))
+    F, s, m, mv = kra.expmv(1.0, kra.DeviceMatrix(A, gpu_ctx), b, ctx=gpu_ctx)
+    Fo, so, mo, mvo = ko.expmv(1.0, A, b)
+    assert (s, m, mv) == (so, mo, mvo)
+    np.testing.assert_allclose(F, Fo, rtol=1e-11, atol=1e-13 * np.abs(Fo).max())
+
+
+def test_trace_exp_with_self_loops(kra, gpu_ctx):
+    """trace_exp.m on a graph with self loops (expmv's shift mu != 0 and the
+    normest1 branch): the oracle's estimate to 1e-9, the exact trace to 1e-4."""
+    from test_normest1 import looped
+    A = looped(load_graph("oregon_A0"))
+    tr = kra.trace_exp(kra.DeviceMatrix(A, gpu_ctx), method="expmv", seed=1, ctx=gpu_ctx)
+    assert tr == pytest.approx(ko.trace_exp(A, seed=1), rel=1e-9)
+    exact = float(np.exp(np.linalg.eigvalsh(A.toarray())).sum())
+    assert tr == pytest.approx(exact, rel=1e-4)
