@@ -1159,9 +1159,73 @@ __device__ __forceinline__ void block_count_ms(int j, const Blk2* __restrict__ B
     }
 }
 
+// One shift with the derivative, for Newton on det(M - xI): cnt = #eig < x
+// (as block_count_ms) and S = d/dx log|det(M - xI)| = sum_k tr(D_k^{-1} D_k'),
+// with D_0' = -I, D_{k+1}' = -I + T_k' D_k' T_k, T_k = D_k^{-1} U_k.  The
+// Newton step on the characteristic polynomial is x - 1/S.
+__device__ __forceinline__ void block_count_newton(int j, const Blk2* __restrict__ B, double x,
+                                                   double pivmin, double eps, int& cnt, double& S) {
+    const Blk2 m0 = B[0];
+    double a = m0.a - x, b = m0.b, c = m0.c - x;
+    double p = -1.0, q = 0.0, r = -1.0;  // D_k'
+    cnt = 0;
+    S = 0.0;
+    for (int k = 0;; ++k) {
+        double det = fma(a, c, -b * b);
+        if (fabs(det) < pivmin) {  // as block_count_ms
+            a -= eps;
+            c -= eps;
+            det = fma(a, c, -b * b);
+            if (fabs(det) < pivmin) det = -pivmin;
+        }
+        cnt += det < 0.0 ? 1 : (a < 0.0 ? 2 : 0);
+        double rr = __builtin_amdgcn_rcp(det);
+        rr = fma(fma(-det, rr, 1.0), rr, rr);
+        const double i00 = c * rr, i01 = -b * rr, i11 = a * rr;
+        S = fma(i00, p, fma(2.0 * i01, q, fma(i11, r, S)));
+        if (k + 1 >= j) break;
+        const Blk2 u = B[k];
+        const Blk2 nx = B[k + 1];
+        const double t00 = i00 * u.u0 + i01 * u.u2, t01 = i00 * u.u1 + i01 * u.u3;
+        const double t10 = i01 * u.u0 + i11 * u.u2, t11 = i01 * u.u1 + i11 * u.u3;
+        const double s00 = u.u0 * t00 + u.u2 * t10;
+        const double s01 = u.u0 * t01 + u.u2 * t11;
+        const double s11 = u.u1 * t01 + u.u3 * t11;
+        const double e00 = p * t00 + q * t10, e01 = p * t01 + q * t11;
+        const double e10 = q * t00 + r * t10, e11 = q * t01 + r * t11;
+        p = -1.0 + t00 * e00 + t10 * e10;
+        q = t00 * e01 + t10 * e11;
+        r = -1.0 + t01 * e01 + t11 * e11;
+        a = nx.a - x - s00;
+        b = nx.b - s01;
+        c = nx.c - x - s11;
+    }
+}
+
+// lanes per eigenvalue when one wave solves ne of them: a power of two, so a
+// group's lanes are an aligned xor-butterfly range
+__device__ __forceinline__ int group_lanes(int ne) {
+    int g = 64;
+    while (g > 1 && g * ne > 64) g >>= 1;
+    return g;
+}
+
+#ifndef KT_BLK_NEWTON
+#define KT_BLK_NEWTON 1
+#endif
+
 // Eigenvalues k0 .. k0+ne-1 (ascending) of the block matrix by one wave:
-// g = 64 / ne lanes per eigenvalue, MS interleaved shifts each per round;
-// bracket to 2 ulp of the spectral radius (as wave_multisect).
+// g = group_lanes(ne) lanes per eigenvalue.  Multisection (MS interleaved
+// shifts per lane, g*MS + 1 parts per round) brackets each eigenvalue; once
+// every bracket is span/4096 wide a safeguarded Newton iteration
+// on det(M - xI) (block_count_newton; a step leaving the count bracket is a
+// bisection) converges in ~4 steps, and is accepted once its step is below
+// 64 atol AND the counts at x -+ 8 atol bracket lambda_k (certified to
+// 8 atol = 3.5e-15 of the spectral radius).  Lanes whose Newton run is not
+// certified (~1 % on the greedy projections, tests/test_block_sturm.py)
+// continue the multisection to 2 ulp of the spectral radius (as before:
+// KT_BLK_NEWTON=0 builds that alone).  Returns lambda_{k0 + lane / g} in
+// every lane of group lane / g < ne.
 template <int MS>
 __device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne) {
     const int lane = threadIdx.x & 63;
@@ -1194,16 +1258,14 @@ __device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne) {
     const double pivmin = 2.2250738585072014e-308 * sc * sc * sc * sc;
     const double eps = 10.0 * sqrt(pivmin);
     const double atol = 4.4e-16 * fmax(fabs(lo), fabs(hi)) + 1e-300;
-    const int g = 64 / ne;
+    const int g = group_lanes(ne);
     const int kl = lane / g, sub = lane % g;
     const int k = k0 + kl;
     const int M = g * MS;
     double a = lo, b = hi;
     const bool live = kl < ne;
     bool done = !live;
-    for (int round = 0; round < 64; ++round) {
-        if (!done && !(b - a > atol)) done = true;
-        if (__ballot(!done) == 0ull) break;
+    auto ms_round = [&]() {
         const double h = (b - a) / (double)(M + 1);
         int mine = M;
         if (!done) {
@@ -1216,8 +1278,8 @@ __device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne) {
             for (int s2 = MS - 1; s2 >= 0; --s2)
                 if (cnt[s2] > k) mine = sub * MS + s2;
         }
-        int first = mine;
-        for (int o = 1; o < g; ++o) first = min(first, __shfl(mine, kl * g + (sub + o) % g, 64));
+        int first = mine;  // group minimum (aligned butterfly)
+        for (int o = 1; o < g; o <<= 1) first = min(first, __shfl_xor(first, o, 64));
         if (!done) {
             const double na = first == 0 ? a : a + h * (double)first;
             const double nb = first == M ? b : fmin(b, a + h * (double)(first + 1));
@@ -1228,6 +1290,61 @@ __device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne) {
                 b = nb;
             }
         }
+    };
+    int round = 0;
+#if KT_BLK_NEWTON
+    // Newton pays where a wave holds <= 16 eigenvalues (g >= 4): with more, one
+    // uncertified lane in the wave sends all of them back to the multisection
+    // (measured: 2j = 80 at 4 waves per projection is 10 % slower with it)
+    if (g >= 4) {
+    // multisection until every bracket is within span / 4096 (2 rounds at
+    // g = 16, 4 at g = 2), where Newton converges in ~4 steps
+    const double narrow = (hi - lo) * (1.0 / 4096.0);
+    for (; round < 64; ++round) {
+        if (!done && !(b - a > atol)) done = true;
+        if (__ballot(!done && b - a > narrow) == 0ull) break;
+        ms_round();
+    }
+    bool newton = !done, conv = false;
+    double x = 0.5 * (a + b);
+    for (int it = 0; it < 8; ++it) {
+        if (__ballot(newton && !conv) == 0ull) break;
+        if (newton && !conv) {
+            int cnt;
+            double S;
+            block_count_newton(j, B, x, pivmin, eps, cnt, S);
+            if (cnt > k) b = x;
+            else a = x;
+            const double xn = x - 1.0 / S;  // S = 0 or inf: xn is not finite / = x
+            const bool inb = xn >= a && xn <= b;
+            if (fabs(xn - x) <= 64.0 * atol || !(b - a > atol)) {
+                conv = true;
+                if (inb) x = xn;
+            } else {
+                x = inb ? xn : 0.5 * (a + b);
+            }
+        }
+    }
+    if (__ballot(newton && conv) != 0ull) {  // certify: #eig < x - 8 atol <= k < #eig < x + 8 atol
+        int cnt[2] = {0, 0};
+        if (newton && conv) {
+            const double xs[2] = {x - 8.0 * atol, x + 8.0 * atol};
+            block_count_ms<2>(j, B, xs, pivmin, eps, cnt);
+            if (cnt[0] <= k && cnt[1] > k) {
+                done = true;
+                a = b = x;
+            } else {  // keep the tighter count bracket for the multisection
+                if (cnt[0] <= k) a = fmax(a, xs[0]);
+                if (cnt[1] > k) b = fmin(b, xs[1]);
+            }
+        }
+    }
+    }
+#endif
+    for (; round < 64; ++round) {
+        if (!done && !(b - a > atol)) done = true;
+        if (__ballot(!done) == 0ull) break;
+        ms_round();
     }
     return 0.5 * (a + b);
 }
@@ -1273,7 +1390,7 @@ __device__ double fused_xm_blk(int j, int fun, const double* rec /* [j][11] */, 
     for (int e0 = 0; e0 < ne; e0 += 64) {  // more than 64 eigenvalues per wave: 64 at a time
         const int cnt = min(64, ne - e0);
         const double lam = wave_multisect_blk<4>(j, blk + mat * j, k0 + e0, cnt);
-        const int g = 64 / cnt;
+        const int g = group_lanes(cnt);
         if (lane % g == 0 && lane / g < cnt) ev[mat * nn + k0 + e0 + lane / g] = lam;
     }
     __syncthreads();
