@@ -124,7 +124,7 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
         }
         KT_HIP(hipMemcpyAsync(ws.pair_idx.ptr, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice,
                               ctx->stream));
-        KT_HIP(launch_pair_fused(C, (int)n, V, A->unit_values, ws.pair_idx.as<int>(), ws.pair_idx.as<int>() + C,
+        KT_HIP(launch_pair_fused(C, (int)n, (int64_t)A->h_rowptr[n], V, A->unit_values, ws.pair_idx.as<int>(), ws.pair_idx.as<int>() + C,
                                  B, it, fun, tol, ws.pair_blk[0].as<double>(), big, big_stride,
                                  ws.pair_state.as<double>(), ctx->stream));
         std::vector<double> sv((size_t)C * 8);

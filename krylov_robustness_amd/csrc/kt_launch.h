@@ -36,9 +36,9 @@ constexpr int kMedThresh = 16;     // expmv terms: rows longer than this get a w
 // k_pair_fused); vec: C x 3 x n x 2 doubles; big: C x big_stride doubles of
 // eigen scratch, needed only when 2 it > 56 (else may be null); state: C x 8.
 size_t pair_fused_lds_bytes(int it);
-hipError_t launch_pair_fused(int C, int n, const CsrView& A, bool unit, const int* ii, const int* jj,
-                             const double* B, int it, int fun, double tol, double* vec, double* big,
-                             int64_t big_stride, double* state, hipStream_t st);
+hipError_t launch_pair_fused(int C, int n, int64_t nnz, const CsrView& A, bool unit, const int* ii,
+                             const int* jj, const double* B, int it, int fun, double tol, double* vec,
+                             double* big, int64_t big_stride, double* state, hipStream_t st);
 hipError_t launch_spmm_block(int P, int flags, int grid, const CsrView& M, const double* X, int ldx,
                              double* Y, int ldy, int long_blocks, int chunk_blocks, double* ck_part,
                              hipStream_t st, int slices = 1, const int* skip = nullptr);

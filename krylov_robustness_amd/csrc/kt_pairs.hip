@@ -775,6 +775,26 @@ constexpr int kFusedThreads = KT_FUSED_THREADS;
 constexpr int kFusedWaves = kFusedThreads / 64;
 constexpr int kFusedMaxNN = 56;  // 2j at which the eigenproblems leave LDS
 
+// KT_FUSED_PROF builds (diagnostic, tools/fused_phases.sh): thread 0 of
+// candidate 0 accumulates the 100 MHz wall clock per phase of the fused run
+// and prints the totals at its end.  Slots: 0 start, 1 SpMM, 2-6 sweeps A-E,
+// 7 eigenvalues, 8 stop test; slot 15 holds the last timestamp.
+#ifdef KT_FUSED_PROF
+__shared__ unsigned long long g_fprof[16];  // LDS: the marks add no global-memory stalls
+#define FPROF(k)                                                          \
+    do {                                                                  \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                        \
+            const unsigned long long t_ = wall_clock64();                 \
+            g_fprof[k] += t_ - g_fprof[15];                               \
+            g_fprof[15] = t_;                                             \
+        }                                                                 \
+    } while (0)
+#else
+#define FPROF(k) \
+    do {         \
+    } while (0)
+#endif
+
 // fixed-order workgroup sum of NV per-thread values; every thread gets them
 template <int NV>
 __device__ __forceinline__ void block_sum(double (&acc)[NV], double* red /* [kFusedWaves][NV] */) {
@@ -890,6 +910,7 @@ __device__ void fused_orth(int n, const double* __restrict__ P, const double* __
 #pragma unroll
                 for (int k = 0; k < 8; ++k) cf[(ph ? CF_G2 : CF_G1) + k] = acc[k];
             __syncthreads();
+            FPROF(2 + ph);
         }
     } else if (tid == 0) {
 #pragma unroll
@@ -939,6 +960,7 @@ __device__ void fused_orth(int n, const double* __restrict__ P, const double* __
             cf[CF_V11] = w1.x * scal1;
         }
         __syncthreads();
+        FPROF(4);
     }
     {  // sweep D: z = w1 - kappa w0;  s2 = |z(3:n)|^2, dz = w0(3:n)' z(3:n)
         double acc[2] = {0.0, 0.0};
@@ -968,6 +990,7 @@ __device__ void fused_orth(int n, const double* __restrict__ P, const double* __
             rec[10] = beta2;
         }
         __syncthreads();
+        FPROF(5);
     }
     {  // sweep E: W <- [q1 q2] = dorg2r(H1, H2)
         const double tau1 = cf[CF_TAU1], tau2 = cf[CF_TAU2], scal1 = cf[CF_SCAL1], scal2 = cf[CF_SCAL2];
@@ -991,6 +1014,7 @@ __device__ void fused_orth(int n, const double* __restrict__ P, const double* __
             *reinterpret_cast<double2*>(W + 2 * (int64_t)r) = q;
         }
         __syncthreads();
+        FPROF(6);
     }
 }
 
@@ -1108,15 +1132,17 @@ struct Blk2 {
 // (latency hiding); 1/det by rcp + one Newton step (full precision)
 template <int MS>
 __device__ __forceinline__ void block_count_ms(int j, const Blk2* __restrict__ B, const double (&x)[MS],
-                                               double pivmin, double eps, int (&cnt)[MS]) {
+                                               double pivmin, double eps, int (&cnt)[MS],
+                                               const double* m0 = nullptr) {
     double a[MS], b[MS], c[MS];
     {
         const Blk2 m = B[0];
+        const double ma = m0 ? m0[0] : m.a, mb = m0 ? m0[1] : m.b, mc = m0 ? m0[2] : m.c;
 #pragma unroll
         for (int s = 0; s < MS; ++s) {
-            a[s] = m.a - x[s];
-            b[s] = m.b;
-            c[s] = m.c - x[s];
+            a[s] = ma - x[s];
+            b[s] = mb;
+            c[s] = mc - x[s];
             cnt[s] = 0;
         }
     }
@@ -1164,9 +1190,10 @@ __device__ __forceinline__ void block_count_ms(int j, const Blk2* __restrict__ B
 // with D_0' = -I, D_{k+1}' = -I + T_k' D_k' T_k, T_k = D_k^{-1} U_k.  The
 // Newton step on the characteristic polynomial is x - 1/S.
 __device__ __forceinline__ void block_count_newton(int j, const Blk2* __restrict__ B, double x,
-                                                   double pivmin, double eps, int& cnt, double& S) {
-    const Blk2 m0 = B[0];
-    double a = m0.a - x, b = m0.b, c = m0.c - x;
+                                                   double pivmin, double eps, int& cnt, double& S,
+                                                   const double* m0 = nullptr) {
+    const Blk2 b0 = B[0];
+    double a = (m0 ? m0[0] : b0.a) - x, b = m0 ? m0[1] : b0.b, c = (m0 ? m0[2] : b0.c) - x;
     double p = -1.0, q = 0.0, r = -1.0;  // D_k'
     cnt = 0;
     S = 0.0;
@@ -1226,16 +1253,18 @@ __device__ __forceinline__ int group_lanes(int ne) {
 // continue the multisection to 2 ulp of the spectral radius (as before:
 // KT_BLK_NEWTON=0 builds that alone).  Returns lambda_{k0 + lane / g} in
 // every lane of group lane / g < ne.
+// m0 (optional): (a, b, c) of the first diagonal block in place of B[0]'s --
+// the updated projection T differs from G only there (T = G + Cm)
 template <int MS>
-__device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne) {
+__device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne, const double* m0 = nullptr) {
     const int lane = threadIdx.x & 63;
     const int nn = 2 * j;
     double lo = INFINITY, hi = -INFINITY, smax = 0.0;
     for (int r = lane; r < nn; r += 64) {  // Gershgorin over the rows
         const int k = r >> 1, s = r & 1;
         const Blk2& m = B[k];
-        const double d = s ? m.c : m.a;
-        double off = fabs(m.b);
+        const double d = (k == 0 && m0) ? m0[s ? 2 : 0] : (s ? m.c : m.a);
+        double off = fabs((k == 0 && m0) ? m0[1] : m.b);
         if (k + 1 < j) off += s ? fabs(m.u2) + fabs(m.u3) : fabs(m.u0) + fabs(m.u1);  // U_k row s
         if (k >= 1) {  // U_{k-1}' row s = column s of U_{k-1}
             const Blk2& p = B[k - 1];
@@ -1273,7 +1302,7 @@ __device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne) {
             int cnt[MS];
 #pragma unroll
             for (int s2 = 0; s2 < MS; ++s2) xs[s2] = a + h * (double)(sub * MS + s2 + 1);
-            block_count_ms<MS>(j, B, xs, pivmin, eps, cnt);
+            block_count_ms<MS>(j, B, xs, pivmin, eps, cnt, m0);
 #pragma unroll
             for (int s2 = MS - 1; s2 >= 0; --s2)
                 if (cnt[s2] > k) mine = sub * MS + s2;
@@ -1312,7 +1341,7 @@ __device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne) {
         if (newton && !conv) {
             int cnt;
             double S;
-            block_count_newton(j, B, x, pivmin, eps, cnt, S);
+            block_count_newton(j, B, x, pivmin, eps, cnt, S, m0);
             if (cnt > k) b = x;
             else a = x;
             const double xn = x - 1.0 / S;  // S = 0 or inf: xn is not finite / = x
@@ -1329,7 +1358,7 @@ __device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne) {
         int cnt[2] = {0, 0};
         if (newton && conv) {
             const double xs[2] = {x - 8.0 * atol, x + 8.0 * atol};
-            block_count_ms<2>(j, B, xs, pivmin, eps, cnt);
+            block_count_ms<2>(j, B, xs, pivmin, eps, cnt, m0);
             if (cnt[0] <= k && cnt[1] > k) {
                 done = true;
                 a = b = x;
@@ -1424,6 +1453,12 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_fused(
     const size_t eigw = blk_eig ? (size_t)18 * it
                                 : (size_t)2 * kFusedMaxNN * kFusedMaxNN + 6 * kFusedMaxNN;
     double* rec = sm + eigw;  // [it][11]
+#ifdef KT_FUSED_PROF
+    if (c == 0 && tid == 0) {
+        for (int k = 0; k < 15; ++k) g_fprof[k] = 0;
+        g_fprof[15] = wall_clock64();
+    }
+#endif
     // [V, ~] = qr(U, 0), U = [e_i e_j]   (lanczos_krylov.m:48; krylov_miobi.m:82-84)
     for (int64_t t = tid; t < vn; t += kFusedThreads) V[0][t] = 0.0;
     __syncthreads();
@@ -1443,6 +1478,12 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_fused(
         cm[3] = RB11 * R11;               // (1,1)
     }
     __syncthreads();
+#ifdef KT_FUSED_PROF
+    if (c == 0 && tid == 0) {  // the start's sweeps count as slot 0
+        for (int k = 1; k < 15; ++k) g_fprof[0] += g_fprof[k], g_fprof[k] = 0;
+    }
+#endif
+    FPROF(0);
     int prev = -1, cur = 0, w = 1;
     double x0 = 0.0, x1 = 0.0, xm = 0.0;
     int iter = it, lucky = 0;
@@ -1450,6 +1491,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_fused(
     for (int j = 1; j <= it; ++j) {
         fused_spmm(n, M, V[cur], V[w]);  // w = A * w   (lanczos_krylov.m:81)
         __syncthreads();
+        FPROF(1);
         fused_orth(n, prev >= 0 ? V[prev] : nullptr, V[cur], V[w], cf, red, rec + 11 * (j - 1));
         if (!blk_eig && 2 * j > kFusedMaxNN && !mybig) {  // no global scratch: cannot continue (host checks)
             iter = -j;
@@ -1464,6 +1506,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_fused(
         else
             xm = fused_xm(j, fun, rec, cm, eigsm, mybig);
 #endif
+        FPROF(7);
         const double* hj = rec + 11 * (j - 1);
         lucky = sqrt(hj[8] * hj[8] + hj[9] * hj[9] + hj[10] * hj[10]) < 1e-8;  // :91-93
         bool stop = false;
@@ -1484,7 +1527,14 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_fused(
         prev = cur;
         cur = w;
         w = freed;
+        FPROF(8);
     }
+#ifdef KT_FUSED_PROF
+    if (c == 0 && tid == 0)
+        printf("fused_prof n=%d it=%d iter=%d start=%llu spmm=%llu A=%llu B=%llu C=%llu D=%llu E=%llu eig=%llu stop=%llu (x10ns)\n",
+               n, it, iter, g_fprof[0], g_fprof[1], g_fprof[2], g_fprof[3], g_fprof[4], g_fprof[5], g_fprof[6],
+               g_fprof[7], g_fprof[8]);
+#endif
     if (tid == 0) {
         double* st = state + (int64_t)c * PS_N;
         st[PS_XM] = xm;
@@ -1542,15 +1592,482 @@ size_t pair_fused_lds_bytes(int it) {
     return sizeof(double) * (std::max(dense, blk) + 11 * (size_t)it);
 }
 
-hipError_t launch_pair_fused(int C, int n, const CsrView& A, bool unit, const int* ii, const int* jj,
-                             const double* B, int it, int fun, double tol, double* vec, double* big,
-                             int64_t big_stride, double* state, hipStream_t st) {
+// ---------------------------------------------------------------------------
+// Register-resident candidate runs (n <= 8 * kFusedThreads): the same
+// trace_fun_update as k_pair_fused, but thread t OWNS rows t + q T (q < R,
+// T = kFusedThreads) of the candidate's three blocks -- the window P, C and
+// the new block W -- in registers for the whole run.  Only the gathered block
+// (C, for the next SpMM) and the CSR live in LDS.  So no sweep touches global
+// memory: the CGS2 / Householder sweeps are register arithmetic between
+// workgroup reductions, and the SpMM gathers from LDS.  Every sum is formed in
+// k_pair_fused's order (a thread's rows in q order, waves in id order; long
+// rows lane-strided + wave_sum64); the two kernels agree to rounding (the
+// compiler contracts a few products into FMAs differently).
+// ---------------------------------------------------------------------------
+constexpr int kRegLongCap = 256;  // long rows (degree > long_thresh) handled by whole waves
+
+// fixed-order workgroup sum, one barrier: `red` alternates between two halves
+// (a wave cannot run two reductions ahead of a slower one: each has a barrier)
+template <int NV>
+__device__ __forceinline__ void block_sum1(double (&acc)[NV], double* red /* [2][kFusedWaves][8] */, int& par) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double* rb = red + par * kFusedWaves * 8;
+    par ^= 1;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = wave_sum64(acc[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) rb[wave * 8 + k] = acc[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kFusedWaves; ++w) s += rb[w * 8 + k];
+        acc[k] = s;
+    }
+}
+
+struct RegRec {  // the step's QR quantities, identical in every thread
+    double g[16];  // g1 (8), g2 (8)
+    double beta1, r12, beta2;
+};
+
+// CGS2 against the window [P C] (has_win) + thin Householder QR of the owned
+// rows of W; W <- Q, also written over the LDS gather block X (C's rows are
+// held in registers, read from X before the SpMM).  (fused_orth's sweeps A-E, same arithmetic
+// and order.)
+template <int R>
+__device__ __forceinline__ void reg_orth(int n, bool has_p, bool has_win, const double2 (&P)[R],
+                                         const double2 (&Cv)[R], double2 (&W)[R], double* X, double* red,
+                                         double* bc, int& par, RegRec& o) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o.g[k] = 0.0;
+    if (has_win) {
+#pragma unroll
+        for (int ph = 0; ph < 2; ++ph) {  // sweep A (dots), B (update + dots)
+            double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const int r = tid + q * kFusedThreads;
+                const double2 p = has_p ? P[q] : make_double2(0.0, 0.0);
+                const double2 u = Cv[q];
+                double2 w = W[q];
+                if (ph) {
+                    const double* g = o.g;
+                    w.x -= p.x * g[0] + p.y * g[1] + u.x * g[2] + u.y * g[3];
+                    w.y -= p.x * g[4] + p.y * g[5] + u.x * g[6] + u.y * g[7];
+                    if (r < n) W[q] = w;
+                }
+                if (r < n) {
+                    acc[0] += p.x * w.x; acc[1] += p.y * w.x; acc[2] += u.x * w.x; acc[3] += u.y * w.x;
+                    acc[4] += p.x * w.y; acc[5] += p.y * w.y; acc[6] += u.x * w.y; acc[7] += u.y * w.y;
+                }
+            }
+            block_sum1<8>(acc, red, par);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o.g[8 * ph + k] = acc[k];
+            FPROF(2 + ph);
+        }
+    }
+    // sweep C: w -= [p c] g2;  s1 = |w0(2:n)|^2, ab = w0(2:n)' w1(2:n); rows 0, 1 broadcast
+    double acc2[2] = {0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int r = tid + q * kFusedThreads;
+        double2 w = W[q];
+        if (has_win) {
+            const double2 p = has_p ? P[q] : make_double2(0.0, 0.0);
+            const double2 u = Cv[q];
+            const double* g = o.g + 8;
+            w.x -= p.x * g[0] + p.y * g[1] + u.x * g[2] + u.y * g[3];
+            w.y -= p.x * g[4] + p.y * g[5] + u.x * g[6] + u.y * g[7];
+            if (r < n) W[q] = w;
+        }
+        if (r >= 1 && r < n) {
+            acc2[0] += w.x * w.x;
+            acc2[1] += w.x * w.y;
+        }
+    }
+    if (tid < 2) {  // rows 0 and 1 are owned by threads 0 and 1 (q = 0)
+        bc[2 * tid] = W[0].x;
+        bc[2 * tid + 1] = W[0].y;
+    }
+    block_sum1<2>(acc2, red, par);
+    const double w0x = bc[0], w0y = bc[1], w1x = bc[2], w1y = bc[3];
+    double beta1, tau1, scal1;
+    larfg(w0x, acc2[0], beta1, tau1, scal1);
+    const double t = w0y + scal1 * acc2[1];  // v1' w(:,2)
+    const double kappa = tau1 * t * scal1;
+    const double r12 = w0y - tau1 * t;
+    const double v11 = w1x * scal1;
+    FPROF(4);
+    // sweep D: z = w1 - kappa w0;  s2 = |z(3:n)|^2, dz = w0(3:n)' z(3:n)
+    double acc3[2] = {0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int r = tid + q * kFusedThreads;
+        if (r >= 2 && r < n) {
+            const double z = W[q].y - kappa * W[q].x;
+            acc3[0] += z * z;
+            acc3[1] += W[q].x * z;
+        }
+    }
+    block_sum1<2>(acc3, red, par);
+    const double z1 = w1y - kappa * w1x;
+    double beta2, tau2, scal2;
+    larfg(z1, acc3[0], beta2, tau2, scal2);
+    const double d = v11 + scal1 * scal2 * acc3[1];  // v1' v2
+    const double k2 = tau1 * (v11 - tau2 * d);
+    o.beta1 = beta1;
+    o.r12 = r12;
+    o.beta2 = beta2;
+    FPROF(5);
+    // sweep E: W <- [q1 q2] = dorg2r(H1, H2), into the gather block
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int r = tid + q * kFusedThreads;
+        if (r < n) {
+            const double2 w = W[q];
+            double v1, v2;
+            if (r == 0) {
+                v1 = 1.0;
+                v2 = 0.0;
+            } else if (r == 1) {
+                v1 = v11;
+                v2 = 1.0;
+            } else {
+                v1 = w.x * scal1;
+                v2 = (w.y - kappa * w.x) * scal2;
+            }
+            double2 qq;
+            qq.x = (r == 0 ? 1.0 : 0.0) - tau1 * v1;
+            qq.y = (r == 1 ? 1.0 : 0.0) - tau2 * v2 - k2 * v1;
+            *reinterpret_cast<double2*>(X + 2 * r) = qq;
+        }
+    }
+}
+
+// The register kernel's LDS (bytes, in this order; doubles first):
+//   X [n][2] (gather block C) | G blocks [it] Blk2
+//   | ev [2][2 it] | (has_long) wl [kRegLongCap][2] | (csr >= 2) val [nnz]
+//   | (has_long) slot [n] int | (csr >= 1) rp [n+1] int, ci [nnz] u16
+struct RegLds {
+    size_t x, gblk, ev, wl, va, slot, rp, ci, total;
+};
+__host__ __device__ inline RegLds reg_lds_layout(int n, int64_t nnz, int it, bool has_long, int csr) {
+    RegLds L;
+    size_t o = 0;
+    L.x = o;
+    o += sizeof(double) * 2 * (size_t)n;
+    L.gblk = o;
+    o += sizeof(Blk2) * (size_t)it;
+    L.ev = o;
+    o += sizeof(double) * 4 * (size_t)it;
+    L.wl = o;
+    if (has_long) o += sizeof(double) * 2 * kRegLongCap;
+    L.va = o;
+    if (csr >= 2) o += sizeof(double) * (size_t)nnz;
+    L.slot = o;
+    if (has_long) o += sizeof(int) * (size_t)n;
+    L.rp = o;
+    if (csr >= 1) o += sizeof(int) * ((size_t)n + 1);
+    L.ci = o;
+    if (csr >= 1) o += sizeof(unsigned short) * (size_t)nnz;
+    L.total = o;
+    return L;
+}
+
+// Xm of step j from the persistent G blocks (T = G but for T's first
+// diagonal block t0): fused_xm_blk's arithmetic without rebuilding the
+// blocks every step.  Waves 0..W-1 solve T, W..2W-1 G.
+__device__ double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nn = 2 * j;
+    constexpr int W = kFusedWaves / 2;
+    const int mat = wave / W, wv = wave % W;
+    const int per = (nn + W - 1) / W;
+    const int k0 = wv * per;
+    const int ne = min(per, nn - k0);
+    for (int e0 = 0; e0 < ne; e0 += 64) {
+        const int cnt = min(64, ne - e0);
+        const double lam = wave_multisect_blk<4>(j, gblk, k0 + e0, cnt, mat == 0 ? t0 : nullptr);
+        const int g = group_lanes(cnt);
+        if (lane % g == 0 && lane / g < cnt) ev[mat * nn + k0 + e0 + lane / g] = lam;
+    }
+    __syncthreads();
+    double term = 0.0;  // trace_fun_update.m:85-89 (k-th smallest of each)
+    if (wave == 0)
+        for (int i = lane; i < nn; i += 64)
+            term += (fun == 0) ? exp(ev[i]) * (1.0 - exp(ev[nn + i] - ev[i]))
+                               : dev_fscalar(fun, ev[i]) - dev_fscalar(fun, ev[nn + i]);
+    term = wave_sum64(term);
+    __shared__ double s_xm3;
+    if (tid == 0) s_xm3 = term;
+    __syncthreads();
+    const double xm = s_xm3;
+    __syncthreads();
+    return xm;
+}
+
+// CSR: 0 = CSR in global memory, 1 = row pointers + u16 columns in LDS, 2 = and
+// the weights.  A template argument, so every CSR access has a known address
+// space (a pointer chosen at run time between LDS and global memory compiles
+// to flat loads).
+template <int R, int CSR>
+__global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nnz, FusedCSR M,
+                                                            const int* __restrict__ ii, const int* __restrict__ jj,
+                                                            double b00, double b10, double b01, double b11,
+                                                            int it, int fun, double tol,
+                                                            double* __restrict__ state) {
+    extern __shared__ double sm[];
+    __shared__ double red[2 * kFusedWaves * 8];
+    __shared__ double bc[4];
+    __shared__ double t0[3];     // T's first diagonal block (a, b, c): G's + Cm
+    __shared__ double cm[4];     // Cm = R B R' (column-major)
+    __shared__ double lastr[3];  // the previous record's R (beta1, r12, beta2)
+    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nl = min(M.n_long, kRegLongCap);
+    const RegLds L = reg_lds_layout(n, nnz, it, nl > 0, CSR);
+    char* base = reinterpret_cast<char*>(sm);
+    double* X = reinterpret_cast<double*>(base + L.x);
+    Blk2* gblk = reinterpret_cast<Blk2*>(base + L.gblk);
+    double* ev = reinterpret_cast<double*>(base + L.ev);
+    double* wl = reinterpret_cast<double*>(base + L.wl);
+    int* slot = reinterpret_cast<int*>(base + L.slot);
+    int* lrp = reinterpret_cast<int*>(base + L.rp);
+    unsigned short* lci = reinterpret_cast<unsigned short*>(base + L.ci);
+    double* lva = reinterpret_cast<double*>(base + L.va);
+    // the CSR (shared by every candidate, L2-resident) copied once into LDS
+    if (CSR >= 1) {
+        for (int t = tid; t <= n; t += kFusedThreads) lrp[t] = M.rp[t];
+        for (int t = tid; t < nnz; t += kFusedThreads) lci[t] = (unsigned short)M.ci[t];
+    }
+    if (CSR >= 2)
+        for (int t = tid; t < nnz; t += kFusedThreads) lva[t] = M.va[t];
+    const int* rp = CSR >= 1 ? lrp : M.rp;
+    const double* va = CSR >= 2 ? lva : M.va;
+    auto col = [&](int k) -> int { return CSR >= 1 ? (int)lci[k] : M.ci[k]; };
+#ifdef KT_FUSED_PROF
+    const unsigned long long clk0 = clock64(), wclk0 = wall_clock64();
+    if (c == 0 && tid == 0) {
+        for (int k = 0; k < 15; ++k) g_fprof[k] = 0;
+        g_fprof[15] = wall_clock64();
+    }
+#endif
+    // long rows handled by waves: slot[r] = position in the wave list, -1 for
+    // rows their owner sums
+    if (nl > 0) {
+        for (int t = tid; t < n; t += kFusedThreads) slot[t] = -1;
+        __syncthreads();
+        for (int li = tid; li < nl; li += kFusedThreads) slot[M.long_rows[li]] = li;
+    }
+    __syncthreads();
+    double2 P[R], Cv[R], W[R];
+    // [V, ~] = qr(U, 0), U = [e_i e_j]   (lanczos_krylov.m:48; krylov_miobi.m:82-84)
+    const int ri = ii[c], rj = jj[c];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+        const int r = tid + q * kFusedThreads;
+        P[q] = Cv[q] = make_double2(0.0, 0.0);
+        W[q] = make_double2(r == ri ? 1.0 : 0.0, r == rj ? 1.0 : 0.0);
+    }
+    int par = 0;
+    RegRec o;
+    reg_orth<R>(n, false, false, P, Cv, W, X, red, bc, par, o);
+    if (tid == 0) {  // Cm = R B R'  (trace_fun_update.m:65-66; V1' U = R for unit selectors)
+        const double R00 = o.beta1, R01 = o.r12, R11 = o.beta2;
+        const double RB00 = R00 * b00 + R01 * b10, RB01 = R00 * b01 + R01 * b11;
+        const double RB10 = R11 * b10, RB11 = R11 * b11;
+        cm[0] = RB00 * R00 + RB01 * R01;
+        cm[1] = RB10 * R00 + RB11 * R01;
+        cm[2] = RB01 * R11;
+        cm[3] = RB11 * R11;
+    }
+    __syncthreads();  // X = V_1
+#ifdef KT_FUSED_PROF
+    if (c == 0 && tid == 0)
+        for (int k = 1; k < 15; ++k) g_fprof[0] += g_fprof[k], g_fprof[k] = 0;
+#endif
+    FPROF(0);
+    double x0 = 0.0, x1 = 0.0, xm = 0.0;
+    int iter = it, lucky = 0;
+    for (int j = 1; j <= it; ++j) {
+        // W = A C   (lanczos_krylov.m:81): short rows by their owner, gathers from LDS
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int r = tid + q * kFusedThreads;
+            Cv[q] = r < n ? *reinterpret_cast<const double2*>(X + 2 * r) : make_double2(0.0, 0.0);
+            double s0 = 0.0, s1 = 0.0;
+            if (r < n && (nl == 0 || slot[r] < 0)) {
+                const int rb = rp[r], re = rp[r + 1];
+                for (int k0 = rb; k0 < re; k0 += 4) {
+                    int cc[4];
+                    double a[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool ok = k0 + u < re;
+                        cc[u] = ok ? col(k0 + u) : 0;
+                        a[u] = ok ? (M.unit ? 1.0 : va[k0 + u]) : 0.0;
+                    }
+                    double2 v[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const double2*>(X + 2 * cc[u]);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (k0 + u < re) {
+                            s0 = fma(a[u], v[u].x, s0);
+                            s1 = fma(a[u], v[u].y, s1);
+                        }
+                }
+            }
+            W[q] = make_double2(s0, s1);
+        }
+        for (int li = wave; li < nl; li += kFusedWaves) {
+            const int r = M.long_rows[li];
+            const int b = rp[r], e = rp[r + 1];
+            double s0 = 0.0, s1 = 0.0;
+            for (int k = b + lane; k < e; k += 64) {
+                const int cc = col(k);
+                const double a = M.unit ? 1.0 : va[k];
+                const double2 v = *reinterpret_cast<const double2*>(X + 2 * cc);
+                s0 = fma(a, v.x, s0);
+                s1 = fma(a, v.y, s1);
+            }
+            s0 = wave_sum64(s0);
+            s1 = wave_sum64(s1);
+            if (lane == 0) {
+                wl[2 * li] = s0;
+                wl[2 * li + 1] = s1;
+            }
+        }
+        if (nl > 0) {
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const int r = tid + q * kFusedThreads;
+                const int ls = r < n ? slot[r] : -1;
+                if (ls >= 0) W[q] = make_double2(wl[2 * ls], wl[2 * ls + 1]);
+            }
+        }
+        FPROF(1);
+        // X is overwritten by Q in sweep E: every SpMM read is behind the sweeps' barriers
+        reg_orth<R>(n, j > 1, true, P, Cv, W, X, red, bc, par, o);
+#pragma unroll
+        for (int q = 0; q < R; ++q) P[q] = Cv[q];  // the next step's window block
+        if (tid == 0) {  // step j's blocks (fused_xm_blk's entries, appended)
+            double h[11];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h[k] = o.g[k] + o.g[8 + k];
+            h[8] = o.beta1;
+            h[9] = o.r12;
+            h[10] = o.beta2;
+            const int k = j - 1;
+            Blk2 m;
+            m.a = h[2];
+            m.b = 0.5 * (h[3] + h[6]);
+            m.c = h[7];
+            m.u0 = m.u1 = m.u2 = m.u3 = 0.0;
+            gblk[k] = m;
+            if (k == 0) {  // T(0:1, 0:1) += Cm (column-major)
+                t0[0] = h[2] + cm[0];
+                t0[1] = 0.5 * ((h[3] + cm[1]) + (h[6] + cm[2]));
+                t0[2] = h[7] + cm[3];
+            } else {  // coupling of block k-1 to k: lower block R_{k-1}, upper block from record k
+                Blk2& p = gblk[k - 1];
+                p.u0 = 0.5 * (lastr[0] + h[0]);
+                p.u1 = 0.5 * (0.0 + h[4]);
+                p.u2 = 0.5 * (lastr[1] + h[1]);
+                p.u3 = 0.5 * (lastr[2] + h[5]);
+            }
+            lastr[0] = h[8];
+            lastr[1] = h[9];
+            lastr[2] = h[10];
+        }
+        __syncthreads();  // X = V_{j+1}, blocks of step j visible
+        FPROF(6);
+#ifdef KT_FUSED_NOEIG
+        xm = (double)j;
+#else
+        xm = reg_xm_blk(j, fun, gblk, t0, ev);
+#endif
+        FPROF(7);
+        lucky = sqrt(o.beta1 * o.beta1 + o.r12 * o.r12 + o.beta2 * o.beta2) < 1e-8;  // :91-93
+#ifdef KT_FUSED_NOEIG
+        lucky = 0;  // diagnostic builds run exactly `it` steps
+#endif
+        bool stop = false;
+        if (j <= 2) {  // :104-118, lag d = 2
+            if (j == 1) x0 = xm;
+            else x1 = xm;
+        } else if (fabs(xm - x0) < tol) {
+            stop = true;
+        } else {
+            x0 = x1;
+            x1 = xm;
+        }
+        FPROF(8);
+        if (stop || lucky || j == it) {
+            iter = j;
+            break;
+        }
+    }
+#ifdef KT_FUSED_PROF
+    if (c == 0 && tid == 0)
+        printf("reg_prof n=%d it=%d iter=%d start=%llu spmm=%llu A=%llu B=%llu C=%llu D=%llu E=%llu eig=%llu stop=%llu (x10ns) shader_MHz=%.0f\n",
+               n, it, iter, g_fprof[0], g_fprof[1], g_fprof[2], g_fprof[3], g_fprof[4], g_fprof[5], g_fprof[6],
+               g_fprof[7], g_fprof[8], 100.0 * (double)(clock64() - clk0) / (double)(wall_clock64() - wclk0));
+#endif
+    if (tid == 0) {
+        double* st = state + (int64_t)c * PS_N;
+        st[PS_XM] = xm;
+        st[PS_ITER] = iter;
+        st[PS_LUCKY] = lucky ? 1.0 : 0.0;
+        st[PS_DONE] = 1.0;
+    }
+}
+
+hipError_t launch_pair_fused(int C, int n, int64_t nnz, const CsrView& A, bool unit, const int* ii,
+                             const int* jj, const double* B, int it, int fun, double tol, double* vec,
+                             double* big, int64_t big_stride, double* state, hipStream_t st) {
     if (C <= 0) return hipSuccess;
     const FusedCSR M{A.rp, A.ci, A.va, A.long_rows, A.n_long, A.long_thresh, unit ? 1 : 0};
     // KT_PAIRS_DENSE_EIG=1: the dense tridiagonalisation + multisection in LDS
     // (and the one-thread solver past 2j = 56) instead of block Sturm counts
     const char* de = getenv("KT_PAIRS_DENSE_EIG");
     const int blk_eig = !(de && de[0] == '1');
+    // register-resident runs (k_pair_reg) up to 8 rows per thread; KT_PAIRS_REG=0 keeps k_pair_fused.
+    // LDS: the gather block and the eigen workspace, then as much of the CSR as
+    // fits (row pointers + u16 columns, then the weights).
+    const char* rg = getenv("KT_PAIRS_REG");
+    constexpr size_t kLdsMax = 160 * 1024 - 2048;  // static __shared__ of the kernel
+    const bool has_long = std::min(A.n_long, kRegLongCap) > 0;
+    if (blk_eig && !(rg && rg[0] == '0') && n >= 2 && n <= 8 * kFusedThreads && nnz < (int64_t)1 << 31 &&
+        reg_lds_layout(n, nnz, it, has_long, 0).total <= kLdsMax) {
+        int csr = 0;
+        for (int cand = unit ? 1 : 2; cand >= 1; --cand)
+            if (reg_lds_layout(n, nnz, it, has_long, cand).total <= kLdsMax) {
+                csr = cand;
+                break;
+            }
+        const size_t lds = reg_lds_layout(n, nnz, it, has_long, csr).total;
+        const int rows = (n + kFusedThreads - 1) / kFusedThreads;
+        const int rr = rows <= 2 ? 2 : rows <= 4 ? 4 : 8;
+#define KT_REG_LAUNCH(RR, CC)                                                                                  \
+    k_pair_reg<RR, CC><<<C, kFusedThreads, lds, st>>>(C, n, (int)nnz, M, ii, jj, B[0], B[1], B[2], B[3], it, fun, \
+                                                      tol, state)
+#define KT_REG_CSR(RR)                       \
+    if (csr == 0) KT_REG_LAUNCH(RR, 0);      \
+    else if (csr == 1) KT_REG_LAUNCH(RR, 1); \
+    else KT_REG_LAUNCH(RR, 2)
+        if (rr == 2) { KT_REG_CSR(2); }
+        else if (rr == 4) { KT_REG_CSR(4); }
+        else { KT_REG_CSR(8); }
+#undef KT_REG_CSR
+#undef KT_REG_LAUNCH
+        return hipGetLastError();
+    }
     k_pair_fused<<<C, kFusedThreads, pair_fused_lds_bytes(it), st>>>(
         C, n, M, ii, jj, B[0], B[1], B[2], B[3], it, fun, tol, vec, big, big_stride, state, blk_eig);
     return hipGetLastError();
