@@ -221,6 +221,18 @@ int kt_krylov_miobi(kt_matrix_t A, int k, int64_t nE, const int64_t* ei, const i
                     double tol, int it, int make, double rescale, int64_t* sel_i, int64_t* sel_j,
                     double* rob, int64_t* nsel);
 
+/* The step loop of greedy_krylov.m:64-93 once its search space is ranked
+ * (find_top_edges / find_top_missing_edges, greedy_krylov.m:82): ntop >= k
+ * ranked pairs ti/tj (0-based).  Step s runs krylov_miobi(A, 1, E, tol, it,
+ * ...) on E = the first Q remaining pairs (one selection, A edited in place,
+ * :89) and drops the selected pair from the ranking (first match, :84-86).
+ * sel_i/sel_j (capacity k, nullable) receive the chosen edges, rob the summed
+ * variation (:90), nsel their count.  Replaces the per-step host round trips
+ * of calling kt_krylov_miobi k times; same results. */
+int kt_greedy_krylov_steps(kt_matrix_t A, int k, int64_t Q, int64_t ntop, const int64_t* ti,
+                           const int64_t* tj, double tol, int it, int make, double rescale, int64_t* sel_i,
+                           int64_t* sel_j, double* rob, int64_t* nsel);
+
 /* A(i,j) = A(j,i) = value for each pair (value 0 removes the entry, as MATLAB
  * sparse assignment does); device copies are refreshed. */
 int kt_matrix_set_pairs(kt_matrix_t A, int64_t count, const int64_t* ei, const int64_t* ej,

@@ -85,6 +85,8 @@ SIGNATURES = [
                                             C.c_double, C.c_int, C.c_int, _dp, _ip, _ip]),
     ("kt_krylov_miobi", C.c_int, [_mat_p, C.c_int, C.c_int64, _i64p, _i64p, C.c_double, C.c_int,
                                   C.c_int, C.c_double, _i64p, _i64p, _dp, _i64p]),
+    ("kt_greedy_krylov_steps", C.c_int, [_mat_p, C.c_int, C.c_int64, C.c_int64, _i64p, _i64p, C.c_double,
+                                         C.c_int, C.c_int, C.c_double, _i64p, _i64p, _dp, _i64p]),
     ("kt_matrix_set_pairs", C.c_int, [_mat_p, C.c_int64, _i64p, _i64p, C.c_double]),
     ("kt_matrix_export_csc", C.c_int, [_mat_p, _i64p, _i64p, _dp]),
     ("kt_function_multiple_entries", C.c_int, [_mat_p, C.c_int64, _i64p, _i64p, C.c_int, C.c_double,

@@ -503,6 +503,54 @@ int kt_matrix_export_csc(kt_matrix_t A, int64_t* colptr, int64_t* rowind, double
     KT_GUARD_END
 }
 
+}  // extern "C"
+
+namespace kt {
+namespace {
+
+// One selection of krylov_miobi.m:70-135 over the candidates Ei/Ej[0, m):
+// score them all (:76-99), take the first extreme (:112-124, strict
+// comparison), edit A in place (:129-135).  Returns the chosen index.
+int64_t miobi_select(kt_matrix_s* A, std::vector<int64_t>& Ei, std::vector<int64_t>& Ej, int64_t m,
+                     const double* B, double sg, double tol, int it, int make, std::vector<double>& xm,
+                     double* value) {
+    static const bool timing = getenv("KT_PAIRS_TIMING") != nullptr;
+    using clk = std::chrono::steady_clock;
+    xm.assign(m, 0.0);
+    const auto t0 = clk::now();
+    trace_fun_update_pairs(A, m, Ei.data(), Ej.data(), B, sg, tol, it, KT_FUN_EXP, xm.data(), nullptr,
+                           nullptr);
+    const auto t1 = clk::now();
+    int64_t best = -1;
+    double bv = make ? -INFINITY : INFINITY;
+    for (int64_t h = 0; h < m; ++h)
+        if (make ? xm[h] > bv : xm[h] < bv) {
+            bv = xm[h];
+            best = h;
+        }
+    if (best < 0) fail(KT_ERR_ARG, "KRYLOV_MIOBI:: no finite candidate score");
+    const int64_t ci = Ei[best], cj = Ej[best];
+    set_pairs(A, 1, &ci, &cj, make ? 1.0 : 0.0);
+    if (timing)
+        fprintf(stderr, "[kt miobi] score %.3f ms  select+edit %.3f ms\n",
+                std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                std::chrono::duration<double, std::milli>(clk::now() - t1).count());
+    *value = bv;
+    return best;
+}
+
+void miobi_checks(kt_matrix_s* A, int k, int make, int& it) {
+    require_symmetric(A, "KRYLOV_MIOBI:: Adjacency matrix should be symmetric");  // :26-28
+    if (it <= 0) it = (int)std::min<int64_t>(100, A->n);                        // :32-34
+    if (!make && A->nnz < 2 * (int64_t)k)                                       // :63-65
+        fail(KT_ERR_ARG, "KRYLOV_MIOBI:: edges to be removed are more than edges in the network");
+}
+
+}  // namespace
+}  // namespace kt
+
+extern "C" {
+
 int kt_krylov_miobi(kt_matrix_t A, int k, int64_t nE, const int64_t* ei, const int64_t* ej,
                     double tol, int it, int make, double rescale, int64_t* sel_i, int64_t* sel_j,
                     double* rob, int64_t* nsel) {
@@ -510,10 +558,7 @@ int kt_krylov_miobi(kt_matrix_t A, int k, int64_t nE, const int64_t* ei, const i
     if (!A || !rob || !nsel || (nE > 0 && (!ei || !ej))) fail(KT_ERR_ARG, "NULL argument");
     if (k < 0 || nE < 0) fail(KT_ERR_ARG, "negative k or candidate count");
     KT_HIP(hipSetDevice(A->ctx->device));
-    require_symmetric(A, "KRYLOV_MIOBI:: Adjacency matrix should be symmetric");  // :26-28
-    if (it <= 0) it = (int)std::min<int64_t>(100, A->n);                        // :32-34
-    if (!make && A->nnz < 2 * (int64_t)k)                                       // :63-65
-        fail(KT_ERR_ARG, "KRYLOV_MIOBI:: edges to be removed are more than edges in the network");
+    miobi_checks(A, k, make, it);
     const double sg = make ? 1.0 : -1.0;
     const double B[4] = {0.0, sg / rescale, sg / rescale, 0.0};  // :78-84
     std::vector<int64_t> Ei(ei, ei + nE), Ej(ej, ej + nE);
@@ -521,35 +566,53 @@ int kt_krylov_miobi(kt_matrix_t A, int k, int64_t nE, const int64_t* ei, const i
     double total = 0.0;
     int64_t done = 0;
     const int64_t steps = std::min<int64_t>(k, nE);
-    static const bool timing = getenv("KT_PAIRS_TIMING") != nullptr;
-    using clk = std::chrono::steady_clock;
     for (int64_t s = 0; s < steps; ++s) {  // :70
-        const int64_t m = (int64_t)Ei.size();
-        xm.assign(m, 0.0);
-        const auto t0 = clk::now();
-        trace_fun_update_pairs(A, m, Ei.data(), Ej.data(), B, sg, tol, it, KT_FUN_EXP, xm.data(),
-                               nullptr, nullptr);  // :76-99
-        const auto t1 = clk::now();
-        int64_t best = -1;  // :112-124 (strict comparison: first extreme wins)
-        double bv = make ? -INFINITY : INFINITY;
-        for (int64_t h = 0; h < m; ++h)
-            if (make ? xm[h] > bv : xm[h] < bv) {
-                bv = xm[h];
-                best = h;
-            }
-        if (best < 0) fail(KT_ERR_ARG, "KRYLOV_MIOBI:: no finite candidate score");
-        const int64_t ci = Ei[best], cj = Ej[best];
+        double bv;
+        const int64_t best = miobi_select(A, Ei, Ej, (int64_t)Ei.size(), B, sg, tol, it, make, xm, &bv);
+        if (sel_i) sel_i[done] = Ei[best];
+        if (sel_j) sel_j[done] = Ej[best];
         Ei.erase(Ei.begin() + best);  // :127
         Ej.erase(Ej.begin() + best);
-        set_pairs(A, 1, &ci, &cj, make ? 1.0 : 0.0);  // :129-135
-        if (timing)
-            fprintf(stderr, "[kt miobi] step %lld score %.3f ms  select+edit %.3f ms\n", (long long)s,
-                    std::chrono::duration<double, std::milli>(t1 - t0).count(),
-                    std::chrono::duration<double, std::milli>(clk::now() - t1).count());
+        total += bv;
+        ++done;
+    }
+    *rob = total;
+    *nsel = done;
+    KT_GUARD_END
+}
+
+int kt_greedy_krylov_steps(kt_matrix_t A, int k, int64_t Q, int64_t ntop, const int64_t* ti,
+                           const int64_t* tj, double tol, int it, int make, double rescale, int64_t* sel_i,
+                           int64_t* sel_j, double* rob, int64_t* nsel) {
+    KT_GUARD_BEGIN
+    if (!A || !rob || !nsel || (ntop > 0 && (!ti || !tj))) fail(KT_ERR_ARG, "NULL argument");
+    if (k < 0 || Q < 1 || ntop < k) fail(KT_ERR_ARG, "greedy steps: need k >= 0, Q >= 1 and ntop >= k");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    const double sg = make ? 1.0 : -1.0;
+    const double B[4] = {0.0, sg / rescale, sg / rescale, 0.0};  // krylov_miobi.m:78-84
+    std::vector<int64_t> Ti(ti, ti + ntop), Tj(tj, tj + ntop);
+    std::vector<double> xm;
+    double total = 0.0;
+    int64_t done = 0;
+    for (int s = 0; s < k; ++s) {  // greedy_krylov.m:80-93
+        int itc = it;
+        miobi_checks(A, 1, make, itc);  // krylov_miobi(A, 1, E, ...) checks its A each call
+        std::vector<int64_t> Ei(Ti.begin(), Ti.begin() + std::min<int64_t>(Q, (int64_t)Ti.size()));
+        std::vector<int64_t> Ej(Tj.begin(), Tj.begin() + (int64_t)Ei.size());
+        double bv;
+        const int64_t best = miobi_select(A, Ei, Ej, (int64_t)Ei.size(), B, sg, tol, itc, make, xm, &bv);
+        const int64_t ci = Ei[best], cj = Ej[best];
         if (sel_i) sel_i[done] = ci;
         if (sel_j) sel_j[done] = cj;
         total += bv;
         ++done;
+        // drop the selected pair from the ranking (greedy_krylov.m:84-86: first match)
+        for (size_t h = 0; h < Ti.size(); ++h)
+            if (Ti[h] == ci && Tj[h] == cj) {
+                Ti.erase(Ti.begin() + h);
+                Tj.erase(Tj.begin() + h);
+                break;
+            }
     }
     *rob = total;
     *nsel = done;

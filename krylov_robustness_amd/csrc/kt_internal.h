@@ -175,10 +175,11 @@ struct DevCSR {
     int *ck_beg = nullptr, *ck_end = nullptr, *sp_rows = nullptr, *sp_first = nullptr;
     int n_chunks = 0, n_split = 0;
     bool built = false;
-    // allocation sizes in elements: a rebuild after edge edits (greedy) reuses
-    // the buffers instead of a hipFree / hipMalloc round trip
-    size_t cap_rp = 0, cap_col = 0, cap_val = 0, cap_lr = 0, cap_perm = 0, cap_med = 0;
-    size_t cap_ckb = 0, cap_cke = 0, cap_spr = 0, cap_spf = 0;
+    // every array above is a slice of one device allocation; a rebuild after
+    // edge edits (greedy) reuses it instead of a hipFree / hipMalloc round trip
+    char* blob = nullptr;
+    size_t blob_bytes = 0;
+    PinnedBuf stage;  // host staging of a (re)build: one async upload, one sync
     void release();
     void invalidate() { built = false; }  // contents stale, buffers kept
 };

@@ -68,35 +68,14 @@ void prof_collect(kt_context_s* ctx) {
 }
 
 void DevCSR::release() {
-    if (rowptr) (void)hipFree(rowptr);
-    if (col) (void)hipFree(col);
-    if (val) (void)hipFree(val);
-    if (long_rows) (void)hipFree(long_rows);
-    if (perm) (void)hipFree(perm);
-    for (int* q : {ck_beg, ck_end, sp_rows, sp_first})
-        if (q) (void)hipFree(q);
+    if (blob) (void)hipFree(blob);
+    blob = nullptr;
+    blob_bytes = 0;
+    rowptr = col = long_rows = perm = med_rows = nullptr;
     ck_beg = ck_end = sp_rows = sp_first = nullptr;
-    n_chunks = n_split = 0;
-    cap_ckb = cap_cke = cap_spr = cap_spf = 0;
-    if (med_rows) (void)hipFree(med_rows);
-    med_rows = nullptr;
-    n_med = 0;
-    cap_med = 0;
-    rowptr = col = long_rows = perm = nullptr;
     val = nullptr;
-    n_long = 0;
+    n_long = n_med = n_chunks = n_split = 0;
     built = false;
-    cap_rp = cap_col = cap_val = cap_lr = cap_perm = 0;
-}
-
-template <class T>
-static void ensure_dev(T*& p, size_t& cap, size_t want) {
-    if (want <= cap && p) return;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-    KT_HIP(hipMalloc(&p, sizeof(T) * want));
-    cap = want;
 }
 
 void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out) {
@@ -133,53 +112,75 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
         const int32_t d = rp32[r + 1] - rp32[r];
         if (d > kMedThresh && d <= A->long_thresh) mr.push_back((int32_t)r);
     }
-    // buffers may be reused: nothing of this context may still read them
+    // hub-row chunk table (block SpMM)
+    std::vector<int32_t> ckb, cke, spr, spf(1, 0);
+    for (int32_t r : lr) {  // heaviest first
+        const int32_t b = rp32[r], e = rp32[r + 1];
+        if (e - b <= kSplitThresh) continue;
+        spr.push_back(r);
+        for (int32_t k = b; k < e; k += kChunkNnz) {
+            ckb.push_back(k);
+            cke.push_back(std::min(e, k + kChunkNnz));
+        }
+        spf.push_back((int32_t)ckb.size());
+    }
+    // One device allocation holds every array (256-B aligned slices), filled
+    // by ONE async copy out of a pinned staging buffer and one stream sync:
+    // greedy rebuilds the natural copy after every edge edit, and a pageable
+    // hipMemcpy per array stages and syncs each time.
+    struct Seg {
+        void** dst;
+        const void* src;
+        size_t bytes;
+    };
+    std::vector<Seg> segs;
+    auto add = [&](auto*& dst, const void* src, size_t bytes) {
+        segs.push_back({reinterpret_cast<void**>(&dst), src, bytes});
+    };
+    add(out.rowptr, rp32.data(), sizeof(int) * (n + 1));
+    add(out.col, c32.data(), sizeof(int) * c32.size());
+    add(out.val, v64.data(), sizeof(double) * v64.size());
+    add(out.long_rows, lr.data(), sizeof(int) * lr.size());
+    add(out.med_rows, mr.data(), sizeof(int) * mr.size());
+    if (!spr.empty()) {
+        add(out.ck_beg, ckb.data(), sizeof(int) * ckb.size());
+        add(out.ck_end, cke.data(), sizeof(int) * cke.size());
+        add(out.sp_rows, spr.data(), sizeof(int) * spr.size());
+        add(out.sp_first, spf.data(), sizeof(int) * spf.size());
+    }
+    if (!ident) add(out.perm, new2old.data(), sizeof(int) * n);
+    auto slice = [](size_t b) { return (std::max<size_t>(b, 16) + 255) & ~(size_t)255; };
+    size_t total = 0;
+    for (const Seg& g : segs) total += slice(g.bytes);
+    // buffers may be reused: nothing of this context may still read them, and
+    // the previous build's copy out of the staging buffer is done
     KT_HIP(hipStreamSynchronize(A->ctx->stream));
     for (hipStream_t st : A->ctx->aux_stream)
         if (st) KT_HIP(hipStreamSynchronize(st));
     try {
-        ensure_dev(out.rowptr, out.cap_rp, (size_t)n + 1);
-        ensure_dev(out.col, out.cap_col, c32.size());
-        ensure_dev(out.val, out.cap_val, v64.size());
-        ensure_dev(out.long_rows, out.cap_lr, std::max<size_t>(lr.size(), 1));
-        KT_HIP(hipMemcpy(out.rowptr, rp32.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice));
-        KT_HIP(hipMemcpy(out.col, c32.data(), sizeof(int) * c32.size(), hipMemcpyHostToDevice));
-        KT_HIP(hipMemcpy(out.val, v64.data(), sizeof(double) * v64.size(), hipMemcpyHostToDevice));
-        if (!lr.empty())
-            KT_HIP(hipMemcpy(out.long_rows, lr.data(), sizeof(int) * lr.size(), hipMemcpyHostToDevice));
-        out.n_long = (int)lr.size();
-        ensure_dev(out.med_rows, out.cap_med, std::max<size_t>(mr.size(), 1));
-        if (!mr.empty())
-            KT_HIP(hipMemcpy(out.med_rows, mr.data(), sizeof(int) * mr.size(), hipMemcpyHostToDevice));
-        out.n_med = (int)mr.size();
-        // hub-row chunk table (block SpMM)
-        std::vector<int32_t> ckb, cke, spr, spf(1, 0);
-        for (int32_t r : lr) {  // heaviest first
-            const int32_t b = rp32[r], e = rp32[r + 1];
-            if (e - b <= kSplitThresh) continue;
-            spr.push_back(r);
-            for (int32_t k = b; k < e; k += kChunkNnz) {
-                ckb.push_back(k);
-                cke.push_back(std::min(e, k + kChunkNnz));
-            }
-            spf.push_back((int32_t)ckb.size());
+        if (total > out.blob_bytes || !out.blob) {
+            if (out.blob) (void)hipFree(out.blob);
+            out.blob = nullptr;
+            out.blob_bytes = 0;
+            KT_HIP(hipMalloc(&out.blob, total));
+            out.blob_bytes = total;
         }
+        out.stage.ensure(total);
+        char* h = out.stage.as<char>();
+        size_t off = 0;
+        out.ck_beg = out.ck_end = out.sp_rows = out.sp_first = nullptr;
+        out.perm = nullptr;
+        for (const Seg& g : segs) {
+            if (g.bytes) std::memcpy(h + off, g.src, g.bytes);
+            *g.dst = out.blob + off;
+            off += slice(g.bytes);
+        }
+        KT_HIP(hipMemcpyAsync(out.blob, h, total, hipMemcpyHostToDevice, A->ctx->stream));
+        KT_HIP(hipStreamSynchronize(A->ctx->stream));
+        out.n_long = (int)lr.size();
+        out.n_med = (int)mr.size();
         out.n_split = (int)spr.size();
         out.n_chunks = (int)ckb.size();
-        if (out.n_split) {
-            ensure_dev(out.ck_beg, out.cap_ckb, ckb.size());
-            ensure_dev(out.ck_end, out.cap_cke, cke.size());
-            ensure_dev(out.sp_rows, out.cap_spr, spr.size());
-            ensure_dev(out.sp_first, out.cap_spf, spf.size());
-            KT_HIP(hipMemcpy(out.ck_beg, ckb.data(), sizeof(int) * ckb.size(), hipMemcpyHostToDevice));
-            KT_HIP(hipMemcpy(out.ck_end, cke.data(), sizeof(int) * cke.size(), hipMemcpyHostToDevice));
-            KT_HIP(hipMemcpy(out.sp_rows, spr.data(), sizeof(int) * spr.size(), hipMemcpyHostToDevice));
-            KT_HIP(hipMemcpy(out.sp_first, spf.data(), sizeof(int) * spf.size(), hipMemcpyHostToDevice));
-        }
-        if (!ident) {
-            ensure_dev(out.perm, out.cap_perm, (size_t)std::max<int64_t>(n, 1));
-            if (n) KT_HIP(hipMemcpy(out.perm, new2old.data(), sizeof(int) * n, hipMemcpyHostToDevice));
-        }
     } catch (...) {
         out.release();
         throw;

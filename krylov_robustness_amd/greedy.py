@@ -269,15 +269,29 @@ def greedy_krylov(A, k, Q=0, centrality=None, order="mult", tol=1e-12, it=None, 
         raise _lib.KrylovError(_lib.KT_ERR_ARG, "GREEDY_KRYLOV:: edges to be removed are more than edges in the network")
     if centrality is None:
         centrality = compute_centrality(D, "eig", ctx=ctx)
+    top = (find_top_missing_edges(S, centrality, Q + k, order) if miobi == "make"
+           else find_top_edges(S, centrality, Q + k, order))  # :82 (first step)
+    if len(top) >= int(k) > 0:
+        # the step loop in the library (kt_greedy_krylov_steps): krylov_miobi(A, 1,
+        # top(1:Q)) per step, the selected pair dropped from the ranking (:84-89)
+        T = np.asarray(top, dtype=np.int64).reshape(-1, 2)
+        ti, pi = _i64(T[:, 0] - 1)
+        tj, pj = _i64(T[:, 1] - 1)
+        si = np.zeros(int(k), dtype=np.int64)
+        sj = np.zeros(int(k), dtype=np.int64)
+        rb = C.c_double()
+        ns = C.c_int64()
+        _lib.check(_lib.load().kt_greedy_krylov_steps(
+            D.handle, int(k), int(Q), len(T), pi, pj, float(tol), int(it or 0), 1 if miobi == "make" else 0,
+            float(rescale), si.ctypes.data_as(C.POINTER(C.c_int64)), sj.ctypes.data_as(C.POINTER(C.c_int64)),
+            C.byref(rb), C.byref(ns)))
+        m = int(ns.value)
+        return np.stack([si[:m] + 1, sj[:m] + 1], axis=1), float(rb.value), D
     edges = np.zeros((0, 2), dtype=np.int64)
     rob = 0.0
-    top = None
     last = None
     for j in range(int(k)):  # :64-93
-        if j == 0:
-            top = (find_top_missing_edges(S, centrality, Q + k, order) if miobi == "make"
-                   else find_top_edges(S, centrality, Q + k, order))
-        else:  # drop the previously selected edge from the search space
+        if j > 0:  # drop the previously selected edge from the search space
             hit = np.flatnonzero(np.all(top == last, axis=1))
             if len(hit):
                 top = np.delete(top, hit[0], axis=0)

@@ -142,6 +142,33 @@ def test_greedy_krylov_config5_slice(kra, gpu_ctx):
     assert (abs(D2.to_scipy() - sp.csc_matrix(Ao)) > 0).nnz == 0
 
 
+@pytest.mark.parametrize("miobi", ["break", "make"])
+def test_greedy_step_loop_matches_per_step_miobi(kra, gpu_ctx, miobi):
+    """The library's step loop (kt_greedy_krylov_steps) equals greedy_krylov.m's
+    loop written with one krylov_miobi(A, 1, top(1:Q)) call per step and the
+    selected pair dropped from the ranking (:80-93): same edges, bit-equal
+    variation (same kernels in the same order), same A_new."""
+    A, c = _india(kra)
+    k, Q = 5, 40
+    tol = 1e-6 * np.exp(1.3)
+    D1 = kra.DeviceMatrix(A, gpu_ctx)
+    e1, r1, D1 = kra.greedy_krylov(D1, k, Q, c, "min", tol, 100, np.inf, 0, miobi, ctx=gpu_ctx)
+    S = A.tocsr()
+    top = (kra.find_top_missing_edges(S, c, Q + k, "min") if miobi == "make"
+           else kra.find_top_edges(S, c, Q + k, "min"))
+    D2 = kra.DeviceMatrix(A, gpu_ctx)
+    edges, rob = [], 0.0
+    for _ in range(k):
+        e, r, D2 = kra.krylov_miobi(D2, 1, top[:Q], tol, 100, np.inf, 0, miobi, ctx=gpu_ctx)
+        edges.append(e[0])
+        rob += r
+        hit = np.flatnonzero(np.all(top == e[0], axis=1))
+        top = np.delete(top, hit[0], axis=0)
+    np.testing.assert_array_equal(e1, np.array(edges))
+    assert r1 == rob
+    assert (abs(D1.to_scipy() - D2.to_scipy()) > 0).nnz == 0
+
+
 def test_krylov_miobi_sharded_world1(kra, gpu_ctx):
     """The sharded greedy step through a 1-rank gloo group on
     the device gives krylov_miobi's edges, variation and A_new."""
