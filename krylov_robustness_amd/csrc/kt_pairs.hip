@@ -1130,14 +1130,16 @@ struct Blk2 {
 
 // MS shifts at once: MS independent LDL' chains share each block's loads
 // (latency hiding); 1/det by rcp + one Newton step (full precision)
-template <int MS>
+// HAS_M0: (a, b, c) of the first diagonal block come from m0 instead of B[0]
+// (a compile-time switch, so the callers without an override keep their code)
+template <int MS, bool HAS_M0 = false>
 __device__ __forceinline__ void block_count_ms(int j, const Blk2* __restrict__ B, const double (&x)[MS],
                                                double pivmin, double eps, int (&cnt)[MS],
                                                const double* m0 = nullptr) {
     double a[MS], b[MS], c[MS];
     {
         const Blk2 m = B[0];
-        const double ma = m0 ? m0[0] : m.a, mb = m0 ? m0[1] : m.b, mc = m0 ? m0[2] : m.c;
+        const double ma = HAS_M0 ? m0[0] : m.a, mb = HAS_M0 ? m0[1] : m.b, mc = HAS_M0 ? m0[2] : m.c;
 #pragma unroll
         for (int s = 0; s < MS; ++s) {
             a[s] = ma - x[s];
@@ -1189,11 +1191,12 @@ __device__ __forceinline__ void block_count_ms(int j, const Blk2* __restrict__ B
 // (as block_count_ms) and S = d/dx log|det(M - xI)| = sum_k tr(D_k^{-1} D_k'),
 // with D_0' = -I, D_{k+1}' = -I + T_k' D_k' T_k, T_k = D_k^{-1} U_k.  The
 // Newton step on the characteristic polynomial is x - 1/S.
+template <bool HAS_M0 = false>
 __device__ __forceinline__ void block_count_newton(int j, const Blk2* __restrict__ B, double x,
                                                    double pivmin, double eps, int& cnt, double& S,
                                                    const double* m0 = nullptr) {
     const Blk2 b0 = B[0];
-    double a = (m0 ? m0[0] : b0.a) - x, b = m0 ? m0[1] : b0.b, c = (m0 ? m0[2] : b0.c) - x;
+    double a = (HAS_M0 ? m0[0] : b0.a) - x, b = HAS_M0 ? m0[1] : b0.b, c = (HAS_M0 ? m0[2] : b0.c) - x;
     double p = -1.0, q = 0.0, r = -1.0;  // D_k'
     cnt = 0;
     S = 0.0;
@@ -1255,16 +1258,16 @@ __device__ __forceinline__ int group_lanes(int ne) {
 // every lane of group lane / g < ne.
 // m0 (optional): (a, b, c) of the first diagonal block in place of B[0]'s --
 // the updated projection T differs from G only there (T = G + Cm)
-template <int MS>
-__device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne, const double* m0 = nullptr) {
+template <int MS, bool HAS_M0 = false>
+__device__ __forceinline__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne, const double* m0 = nullptr) {
     const int lane = threadIdx.x & 63;
     const int nn = 2 * j;
     double lo = INFINITY, hi = -INFINITY, smax = 0.0;
     for (int r = lane; r < nn; r += 64) {  // Gershgorin over the rows
         const int k = r >> 1, s = r & 1;
         const Blk2& m = B[k];
-        const double d = (k == 0 && m0) ? m0[s ? 2 : 0] : (s ? m.c : m.a);
-        double off = fabs((k == 0 && m0) ? m0[1] : m.b);
+        const double d = (HAS_M0 && k == 0) ? m0[s ? 2 : 0] : (s ? m.c : m.a);
+        double off = fabs((HAS_M0 && k == 0) ? m0[1] : m.b);
         if (k + 1 < j) off += s ? fabs(m.u2) + fabs(m.u3) : fabs(m.u0) + fabs(m.u1);  // U_k row s
         if (k >= 1) {  // U_{k-1}' row s = column s of U_{k-1}
             const Blk2& p = B[k - 1];
@@ -1302,7 +1305,7 @@ __device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne, const
             int cnt[MS];
 #pragma unroll
             for (int s2 = 0; s2 < MS; ++s2) xs[s2] = a + h * (double)(sub * MS + s2 + 1);
-            block_count_ms<MS>(j, B, xs, pivmin, eps, cnt, m0);
+            block_count_ms<MS, HAS_M0>(j, B, xs, pivmin, eps, cnt, m0);
 #pragma unroll
             for (int s2 = MS - 1; s2 >= 0; --s2)
                 if (cnt[s2] > k) mine = sub * MS + s2;
@@ -1341,7 +1344,7 @@ __device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne, const
         if (newton && !conv) {
             int cnt;
             double S;
-            block_count_newton(j, B, x, pivmin, eps, cnt, S, m0);
+            block_count_newton<HAS_M0>(j, B, x, pivmin, eps, cnt, S, m0);
             if (cnt > k) b = x;
             else a = x;
             const double xn = x - 1.0 / S;  // S = 0 or inf: xn is not finite / = x
@@ -1358,7 +1361,7 @@ __device__ double wave_multisect_blk(int j, const Blk2* B, int k0, int ne, const
         int cnt[2] = {0, 0};
         if (newton && conv) {
             const double xs[2] = {x - 8.0 * atol, x + 8.0 * atol};
-            block_count_ms<2>(j, B, xs, pivmin, eps, cnt, m0);
+            block_count_ms<2, HAS_M0>(j, B, xs, pivmin, eps, cnt, m0);
             if (cnt[0] <= k && cnt[1] > k) {
                 done = true;
                 a = b = x;
@@ -1792,7 +1795,8 @@ __device__ double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0,
     const int ne = min(per, nn - k0);
     for (int e0 = 0; e0 < ne; e0 += 64) {
         const int cnt = min(64, ne - e0);
-        const double lam = wave_multisect_blk<4>(j, gblk, k0 + e0, cnt, mat == 0 ? t0 : nullptr);
+        const double lam = mat == 0 ? wave_multisect_blk<4, true>(j, gblk, k0 + e0, cnt, t0)
+                                    : wave_multisect_blk<4, false>(j, gblk, k0 + e0, cnt);
         const int g = group_lanes(cnt);
         if (lane % g == 0 && lane / g < cnt) ev[mat * nn + k0 + e0 + lane / g] = lam;
     }
