@@ -153,5 +153,20 @@ hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_
                              int ld, double mu, double coef,
                              double tol, int k, const double* bin, double* bout, double* F,
                              const double* pin, double* pout, void* state, hipStream_t st);
+// the whole expmv call (s stages x up to m terms, stop tests, f = eta f) in
+// ONE persistent launch of `grid` workgroups (capped so all are resident);
+// b0 / F hold the input block, b1 is scratch (n x ld each, zero padded);
+// part: 4 * grid doubles; bar: expmv_run_bar_bytes() (zeroed by the launch).
+// After the stream is synchronised, copy bar to the host and
+// expmv_run_read() gives the terms executed and 1 = completed (2 = a grid
+// barrier timed out).
+size_t expmv_run_bar_bytes();
+// sc1: the handed-off blocks are stored and loaded sc1, no fences at the barriers
+hipError_t launch_expmv_run(int P, bool unit, bool sc1, int grid, int num_cu, const CsrView& M,
+                            const int* med_rows, int n_med, int nc, int ld, double mu, double t, double tol,
+                            double eta, int s, int m, double* b0, double* b1, double* F, double* part,
+                            void* bar, hipStream_t st, unsigned long long* prof = nullptr);
+int expmv_prof_epochs();  // prof: [grid][expmv_prof_epochs()][2] wall clocks (100 MHz)
+int expmv_run_read(const void* bar_host, int* mv);
 
 }  // namespace kt

@@ -10,6 +10,7 @@
 // [10,20) of the build's counter RNG (oracle/krylov_oracle.py:mc_trace).
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <thread>
 
@@ -295,6 +296,94 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
     void* state = ctx->ws.expmv_state.ptr;
     KT_HIP(hipMemsetAsync(state, 0, expmv_state_bytes(), st));
     const int P = pow2_at_least(std::max(nc, 1));
+    const char* persist = std::getenv("KT_EXPMV_PERSIST");
+    if (P <= 32 && ld >= P && !std::getenv("KT_EXPMV_UNFUSED") && persist && persist[0] == '1') {
+        // KT_EXPMV_PERSIST=1: the whole call in ONE launch (k_expmv_run):
+        // stages, terms, stop tests and f = eta f, a grid barrier per term
+        // instead of a launch; the same per-row arithmetic as the per-term
+        // launches below (bit-identical).  Measured slower on config 1
+        // (25 vs 18.5 ms): the barrier is cheap (1.5 us, sc1 form) but a
+        // term's virtual blocks are chains of dependent loads (median 8.8 us,
+        // hub rows 14.7 us per term), which the per-term grid runs in
+        // parallel (profiles/r02_expmv_persistent.txt).
+        const DevCSR& M = natural_csr(A);
+        const CsrView V{M.rowptr, M.col, M.val, (int)n, M.long_rows, M.n_long, A->long_thresh,
+                        kSplitThresh, M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split};
+        const int nvb = expmv_step_blocks((int)n, P, M.n_long, M.n_med);
+        int grid = std::min(nvb, ctx->num_cu);
+        if (const char* g = std::getenv("KT_EXPMV_GRID")) grid = std::max(1, std::atoi(g));
+        ctx->ws.norm_part.ensure(sizeof(double) * 4 * (size_t)std::max(grid, 1));
+        ctx->ws.expmv_state.ensure(std::max(expmv_state_bytes(), expmv_run_bar_bytes()));
+        // KT_EXPMV_PROF=1 (diagnostic): wall clocks at every barrier's entry
+        // and exit per workgroup, summarised on stderr
+        const char* pf = std::getenv("KT_EXPMV_PROF");
+        const bool prof = pf && pf[0] == '1';
+        const int pe = expmv_prof_epochs();
+        DevBuf pbuf;
+        if (prof) {
+            pbuf.ensure(sizeof(unsigned long long) * 2 * (size_t)pe * grid);
+            KT_HIP(hipMemsetAsync(pbuf.ptr, 0, sizeof(unsigned long long) * 2 * (size_t)pe * grid, st));
+        }
+        const char* sc1e = std::getenv("KT_EXPMV_SC1");
+        const bool sc1 = !(sc1e && sc1e[0] == '0');
+        KT_HIP(launch_expmv_run(P, A->unit_values, sc1, grid, ctx->num_cu, V, M.med_rows, M.n_med, nc, ld, mu, t,
+                                tol, eta, r.s, r.m, b.col(0), Ab.col(0), F, ctx->ws.norm_part.as<double>(),
+                                ctx->ws.expmv_state.ptr, st,
+                                prof ? static_cast<unsigned long long*>(pbuf.ptr) : nullptr));
+        std::vector<char> hb(expmv_run_bar_bytes());
+        KT_HIP(hipMemcpyAsync(hb.data(), ctx->ws.expmv_state.ptr, hb.size(), hipMemcpyDeviceToHost, st));
+        KT_HIP(hipStreamSynchronize(st));
+        int terms = 0;
+        if (expmv_run_read(hb.data(), &terms) != 1)
+            fail(KT_ERR_HIP, "expmv: a grid barrier of the persistent Taylor launch timed out");
+        if (prof) {
+            std::vector<unsigned long long> h(2 * (size_t)pe * grid);
+            KT_HIP(hipMemcpy(h.data(), pbuf.ptr, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+            // per epoch: work = max over workgroups of (enter_e - exit_{e-1}),
+            // barrier = max exit_e - max enter_e (the last arrival to the last release)
+            double work = 0, bar = 0, skew = 0;
+            int ne = 0;
+            for (int e = 1; e < pe; ++e) {
+                unsigned long long me = 0, mx = 0, mn = ~0ull, w = 0;
+                bool any = false;
+                for (int g2 = 0; g2 < grid; ++g2) {
+                    const unsigned long long en = h[((size_t)g2 * pe + e) * 2], ex = h[((size_t)g2 * pe + e) * 2 + 1];
+                    const unsigned long long px = h[((size_t)g2 * pe + e - 1) * 2 + 1];
+                    if (!en || !ex || !px) continue;
+                    any = true;
+                    me = std::max(me, en);
+                    mn = std::min(mn, ex);
+                    mx = std::max(mx, ex);
+                    w = std::max(w, en - px);
+                }
+                if (!any) break;
+                ++ne;
+                work += (double)w;
+                bar += (double)(mx - me);
+                skew += (double)(mx - mn);
+            }
+            if (ne) {
+                std::fprintf(stderr, "[expmv prof] grid %d epochs %d: work %.2f us, last-arrival->last-exit %.2f us, exit skew %.2f us per epoch\n",
+                             grid, ne, work / ne / 100.0, bar / ne / 100.0, skew / ne / 100.0);
+                // per workgroup: mean work over the epochs (enter_e - exit_{e-1})
+                std::vector<std::pair<double, int>> wg(grid);
+                for (int g2 = 0; g2 < grid; ++g2) {
+                    double s = 0;
+                    for (int e = 1; e <= ne; ++e)
+                        s += (double)(h[((size_t)g2 * pe + e) * 2] - h[((size_t)g2 * pe + e - 1) * 2 + 1]);
+                    wg[g2] = {s / ne / 100.0, g2};
+                }
+                std::sort(wg.begin(), wg.end());
+                std::fprintf(stderr, "[expmv prof]   per-wg work: min %.2f median %.2f max %.2f us; top:", wg[0].first,
+                             wg[grid / 2].first, wg[grid - 1].first);
+                for (int q = grid - 1; q >= std::max(0, grid - 6); --q)
+                    std::fprintf(stderr, " wg%d %.2f", wg[q].second, wg[q].first);
+                std::fprintf(stderr, " (long rows %d, med rows %d, vblocks %d)\n", M.n_long, M.n_med, nvb);
+            }
+        }
+        r.mv += terms;
+        return r;
+    }
     if (P <= 32 && ld >= P && !std::getenv("KT_EXPMV_UNFUSED")) {
         // One launch per term (k_expmv_step: the previous term's stop test,
         // SpMM, update, norm partials); b and the partials ping-pong.

@@ -50,6 +50,36 @@ def test_expmv_wide_block_and_unfused_form(kra, gpu_ctx, monkeypatch):
     np.testing.assert_allclose(Fu, Ff, rtol=1e-13, atol=1e-15 * np.abs(Ff).max())
 
 
+@pytest.mark.parametrize("name,loops", [("oregon_A6", False), ("oregon_A0", True), ("anaheim", False)])
+def test_expmv_persistent_launch_is_bit_identical(kra, gpu_ctx, monkeypatch, name, loops):
+    """KT_EXPMV_PERSIST=1: the whole expmv call as ONE persistent launch
+    (k_expmv_run: a grid barrier per Taylor term, the stop test inside the
+    launch) runs the per-term kernel's row arithmetic: F, s, m and mv equal
+    the per-term launches (the default) bit for bit -- in both barrier forms
+    (sc1 hand-off without fences, and plain stores + agent release/acquire,
+    KT_EXPMV_SC1=0), for the default grid, a grid of one workgroup (every
+    virtual block on one workgroup) and a grid of 7 (a partial XCD group);
+    self loops exercise mu != 0."""
+    from test_normest1 import looped
+    A = load_graph(name)
+    if loops:
+        A = looped(A)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    b = np.random.default_rng(5).normal(size=(A.shape[0], 10))
+    ref = kra.expmv(1.0, D, b, ctx=gpu_ctx)
+    Fo, *ro = ko.expmv(1.0, A, b)
+    assert tuple(ref[1:]) == tuple(ro)
+    np.testing.assert_allclose(ref[0], Fo, rtol=1e-11, atol=1e-13 * np.abs(Fo).max())
+    monkeypatch.setenv("KT_EXPMV_PERSIST", "1")
+    for sc1, grid in (("1", None), ("0", None), ("1", "1"), ("1", "7"), ("0", "7")):
+        monkeypatch.setenv("KT_EXPMV_SC1", sc1)
+        if grid:
+            monkeypatch.setenv("KT_EXPMV_GRID", grid)
+        out = kra.expmv(1.0, D, b, ctx=gpu_ctx)
+        assert tuple(out[1:]) == tuple(ref[1:])
+        np.testing.assert_array_equal(out[0], ref[0])
+
+
 def test_lanczos_fmv_matches_oracle(kra, gpu_ctx):
     A = load_graph("rome")
     X = np.random.default_rng(2).normal(size=(A.shape[0], 4))
