@@ -29,6 +29,11 @@ int slq_auto_block(int64_t n, int64_t nprobes) {
     int P = 128;
     while (P > 8 && (double)n * 8.0 * P > 160.0e6) P >>= 1;
     while (P > 1 && P / 2 >= nprobes) P >>= 1;
+    // at least two sweeps, so the two sweep lanes overlap one sweep's small
+    // coefficient launches and pass tails with the other's pass: config 2
+    // (n = 100k, 128 probes) 150 evals/s at one P = 128 sweep, 168 at two
+    // P = 64 sweeps (profiles/r02_er100k_sweep.txt)
+    while (P > 16 && nprobes < 2 * P) P >>= 1;
     return P;
 }
 
