@@ -1785,7 +1785,17 @@ __host__ __device__ inline RegLds reg_lds_layout(int n, int64_t nnz, int it, boo
 // Xm of step j from the persistent G blocks (T = G but for T's first
 // diagonal block t0): fused_xm_blk's arithmetic without rebuilding the
 // blocks every step.  Waves 0..W-1 solve T, W..2W-1 G.
-__device__ double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev) {
+// Inlined into k_pair_reg (KT_REG_XM_INLINE=0 builds it as a called function:
+// each call then saves callee-saved registers to scratch)
+#ifndef KT_REG_XM_INLINE
+#define KT_REG_XM_INLINE 1
+#endif
+#if KT_REG_XM_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nn = 2 * j;
     constexpr int W = kFusedWaves / 2;
