@@ -1,5 +1,6 @@
 // kt_block.cpp -- tall-skinny device block operations (rocBLAS dgemm for the
 // plain GEMM shapes, the HIP SpMM kernel for A*X) and CholQR.
+#include <cstdlib>
 #include <cstring>
 
 #include "kt_block.h"
@@ -416,20 +417,39 @@ void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std
     double* taus = sums + BP;
     double* Md = taus + BP;
     KT_HIP(hipMemsetAsync(V, 0, sizeof(double) * (size_t)n * BP, ctx->stream));
-    KT_HIP(launch_ts_reflectors((int)n, bs, BP, W, ld, V, pivot, sums, ws.ts_part.as<double>(), taus,
-                                ctx->num_cu, ctx->stream));
+    // the reflector sweep: two launches per column; KT_TSQR_PERSIST=1 runs it as
+    // one persistent launch (k_ts_qr, bit-identical) where the row blocks fit
+    // LDS -- measured slower (config 3 fun_and_grad 17.9 vs 17.0 ms: two grid
+    // barriers per column cost more than the two launches, profiles/r02_tsqr_persistent.txt)
+    const char* pe = std::getenv("KT_TSQR_PERSIST");
+    const int pgrid = (pe && pe[0] == '1') ? ts_qr_grid((int)n, BP, ctx->num_cu) : 0;
+    if (pgrid > 0) {
+        ws.ts_pub.ensure(sizeof(double) * ts_qr_pub_doubles((int)n, BP, ctx->num_cu));
+        ws.ts_bar.ensure(ts_qr_bar_bytes());
+        KT_HIP(launch_ts_qr((int)n, bs, BP, ctx->num_cu, W, ld, V, ws.ts_pub.as<double>(), taus, ws.ts_bar.ptr,
+                            ctx->stream));
+    } else {
+        KT_HIP(launch_ts_reflectors((int)n, bs, BP, W, ld, V, pivot, sums, ws.ts_part.as<double>(), taus,
+                                    ctx->num_cu, ctx->stream));
+    }
     // R's rows, V's top block and the taus come back through pinned staging
     // (asynchronous); gram's synchronisation covers them
-    ws.pin_qr.ensure(sizeof(double) * ((size_t)bs * bs + (size_t)bs * BP + bs));
+    ws.pin_qr.ensure(sizeof(double) * ((size_t)bs * bs + (size_t)bs * BP + bs + 1));
     double* ptop = ws.pin_qr.as<double>();
     double* pV1 = ptop + (size_t)bs * bs;
     double* ptau = pV1 + (size_t)bs * BP;
+    unsigned* ptmo = reinterpret_cast<unsigned*>(ptau + bs);
+    *ptmo = 0;
+    if (pgrid > 0)
+        KT_HIP(hipMemcpyAsync(ptmo, static_cast<char*>(ws.ts_bar.ptr) + ts_qr_tmo_offset(), sizeof(unsigned),
+                              hipMemcpyDeviceToHost, ctx->stream));
     KT_HIP(hipMemcpy2DAsync(ptop, sizeof(double) * bs, W, sizeof(double) * ld, sizeof(double) * bs, (size_t)bs,
                             hipMemcpyDeviceToHost, ctx->stream));
     KT_HIP(hipMemcpyAsync(pV1, V, sizeof(double) * (size_t)bs * BP, hipMemcpyDeviceToHost, ctx->stream));
     KT_HIP(hipMemcpyAsync(ptau, taus, sizeof(double) * bs, hipMemcpyDeviceToHost, ctx->stream));
     std::vector<double> G;  // V' V (bs x bs), gram synchronises the stream
     gram(ctx, n, V, BP, bs, V, BP, bs, G);
+    if (*ptmo) fail(KT_ERR_HIP, "thin QR: a grid barrier of the persistent reflector sweep timed out");
     const std::vector<double> top(ptop, ptop + (size_t)bs * bs), V1(pV1, pV1 + (size_t)bs * BP),
         tau(ptau, ptau + bs);
     for (int i = 0; i < bs; ++i)

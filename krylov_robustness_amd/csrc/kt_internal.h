@@ -135,6 +135,7 @@ struct Workspace {
     DevBuf pair_hist, pair_state, pair_scratch, pair_active;  // device-mode candidate state
     PinnedBuf pair_active_host;
     DevBuf ts_V, ts_part, ts_small;  // tall-skinny Householder QR (kt_tsqr.hip)
+    DevBuf ts_pub, ts_bar;           // its persistent form (k_ts_qr): hand-off slots, barrier words
 };
 
 }  // namespace kt

@@ -119,6 +119,17 @@ int ts_nrb(int n, int num_cu);
 hipError_t launch_ts_reflectors(int n, int bs, int BP, double* W, int ld, double* V, double* pivot,
                                 double* sums, double* part, double* taus, int num_cu,
                                 hipStream_t st);
+// the reflector sweep as one persistent launch (k_ts_qr), bit-identical to
+// launch_ts_reflectors: ts_qr_grid > 0 when it applies; pub:
+// ts_qr_pub_doubles doubles; bar: ts_qr_bar_bytes() (zeroed by the launch);
+// the unsigned at bar + ts_qr_tmo_offset() is nonzero after the launch if a
+// grid barrier timed out
+size_t ts_qr_bar_bytes();
+size_t ts_qr_tmo_offset();
+int ts_qr_grid(int n, int BP, int num_cu);
+size_t ts_qr_pub_doubles(int n, int BP, int num_cu);
+hipError_t launch_ts_qr(int n, int bs, int BP, int num_cu, double* W, int ld, double* V, double* pub,
+                        double* taus, void* bar, hipStream_t st);
 hipError_t launch_ts_formq(int n, int bs, int BP, const double* V, const double* M, double* W,
                            int ld, hipStream_t st);
 hipError_t launch_sum_slabs(int count, int S, const double* part, double* G, hipStream_t st);
