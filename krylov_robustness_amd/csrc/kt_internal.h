@@ -210,6 +210,14 @@ struct kt_matrix_s {
     bool normest_ok = false;
     uint64_t normest_version = 0;
     double normest_tol = 0.0, normest_val = 0.0;
+    // last expmv shift + Taylor degree selection (kt_mctrace.cpp expmv_device):
+    // a function of A, t and the block width only (expmv.m:31-68), so calls on
+    // the same A (every mc_trace round of trace_exp) reuse it; valid for
+    // `expmv_sel_version`
+    bool expmv_sel_ok = false;
+    uint64_t expmv_sel_version = 0;
+    double expmv_sel_t = 0.0, expmv_sel_mu = 0.0;
+    int expmv_sel_nc = 0, expmv_sel_s = 1, expmv_sel_m = 0, expmv_sel_mv = 0;
     // twin: a second context (own stream + workspace) holding another device
     // copy of this matrix, built on first use, so that two independent Krylov
     // runs of one call overlap (fun_and_grad_krylov_fun.m:64-65)
