@@ -1511,14 +1511,23 @@ __device__ __forceinline__ void expmv_row_update(int row, int p0, const double* 
 // <= kMedThresh per row group (8 deep).
 // bin / bout and pin / pout ping-pong between terms; columns nc..P-1 of the
 // blocks stay zero so the P-wide gathers read finite values.
+// waves per block of the per-term expmv kernel (a row longer than long_thresh
+// is one block's, its gather chain degree / (16 WAVES) deep).  8 waves were
+// measured slower than 4 on config 1 (trace_exp 18.1 vs 16.1 ms,
+// profiles/r02_expmv_waves.txt): the hub chains are not the term's limit.
+#ifndef KT_EXPMV_WAVES
+#define KT_EXPMV_WAVES 4
+#endif
+constexpr int kExpmvWaves = KT_EXPMV_WAVES;
+
 template <int P, int FLAGS>
-__global__ __launch_bounds__(256) void k_expmv_step(
+__global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
     const int* __restrict__ rp, const int* __restrict__ ci, const double* __restrict__ va, int n,
     const int* __restrict__ long_rows, int n_long, const int* __restrict__ med_rows, int n_med,
     int nc, int ld, double mu, double coef, double tol, int k, const double* __restrict__ bin,
     double* __restrict__ bout, double* __restrict__ F, const double* __restrict__ pin,
     double* __restrict__ pout, ExpmvState* st) {
-    constexpr int WAVES = 4;
+    constexpr int WAVES = kExpmvWaves, THREADS = 64 * WAVES;
     using G = GeoW<P, (P >= 2) ? 2 : 1>;                          // short rows
     using GL = GeoW<P, (P >= 4) ? 4 : (P >= 2) ? 2 : 1>;          // medium / long rows
     __shared__ double red[2][WAVES];
@@ -1535,7 +1544,7 @@ __global__ __launch_bounds__(256) void k_expmv_step(
     double pb[4], pf[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int i = (int)threadIdx.x + u * 256;
+        const int i = (int)threadIdx.x + u * THREADS;
         const bool ok = k > 1 && i < nb;
         pb[u] = ok ? pin[i] : 0.0;
         pf[u] = ok ? pin[nb + i] : 0.0;
@@ -1590,7 +1599,7 @@ __global__ __launch_bounds__(256) void k_expmv_step(
         mb = fmax(mb, pb[u]);
         mf = fmax(mf, pf[u]);
     }
-    for (int i = (int)threadIdx.x + 1024; k > 1 && i < nb; i += 256) {  // grids above 1024 blocks
+    for (int i = (int)threadIdx.x + 4 * THREADS; k > 1 && i < nb; i += THREADS) {  // grids above 4 THREADS blocks
         mb = fmax(mb, pin[i]);
         mf = fmax(mf, pin[nb + i]);
     }
@@ -1606,8 +1615,12 @@ __global__ __launch_bounds__(256) void k_expmv_step(
     if (threadIdx.x == 0) decide = act;
     __syncthreads();
     if (threadIdx.x == 0 && act && k > 1) {
-        const double c2 = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
-        const double nf = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+        double c2 = red[0][0], nf = red[1][0];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) {
+            c2 = fmax(c2, red[0][w]);
+            nf = fmax(nf, red[1][w]);
+        }
         if (c1 + c2 <= tol * nf) {
             st->active = 0;
             decide = 0;
@@ -1631,7 +1644,12 @@ __global__ __launch_bounds__(256) void k_expmv_step(
         if (kind == 2 && wave == 0 && grpL == 0) {
 #pragma unroll
             for (int e = 0; e < GL::VEC; ++e)
-                sl[e] = lred[0][p0L + e] + lred[1][p0L + e] + lred[2][p0L + e] + lred[3][p0L + e];
+            {
+                double t = lred[0][p0L + e];
+#pragma unroll
+                for (int w = 1; w < WAVES; ++w) t += lred[w][p0L + e];
+                sl[e] = t;
+            }
             mine = true;
         }
         if (mine) expmv_row_update<GL::VEC>(row, p0L, sl, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
@@ -1655,8 +1673,14 @@ __global__ __launch_bounds__(256) void k_expmv_step(
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        pout[blockIdx.x] = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
-        pout[gridDim.x + blockIdx.x] = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
+        double x = red[0][0], y = red[1][0];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) {
+            x = fmax(x, red[0][w]);
+            y = fmax(y, red[1][w]);
+        }
+        pout[blockIdx.x] = x;
+        pout[gridDim.x + blockIdx.x] = y;
     }
 }
 
@@ -2280,9 +2304,10 @@ hipError_t launch_expmv_check(int n, const double* partial, double tol, void* st
 
 size_t expmv_state_bytes() { return sizeof(ExpmvState); }
 
-int expmv_step_blocks(int n, int P, int n_long, int n_med) {
+int expmv_step_blocks(int n, int P, int n_long, int n_med, int waves) {
+    if (waves <= 0) waves = kExpmvWaves;
     const int gpw = (P >= 2) ? 64 / (P / 2) : 64;
-    return n_long + (n_med + 3) / 4 + (n + 4 * gpw - 1) / (4 * gpw);
+    return n_long + (n_med + waves - 1) / waves + (n + waves * gpw - 1) / (waves * gpw);
 }
 
 hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_rows, int n_med, int nc,
@@ -2293,11 +2318,11 @@ hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_
     ExpmvState* s = static_cast<ExpmvState*>(state);
 #define KT_EXPMV_STEP(PP)                                                                          \
     if (unit)                                                                                      \
-        k_expmv_step<PP, KF_UNIT><<<grid, 256, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long,  \
+        k_expmv_step<PP, KF_UNIT><<<grid, 64 * kExpmvWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long,  \
                                                         med_rows, n_med, nc, ld, mu, coef, tol, k,    \
                                                         bin, bout, F, pin, pout, s);                 \
     else                                                                                           \
-        k_expmv_step<PP, 0><<<grid, 256, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long,        \
+        k_expmv_step<PP, 0><<<grid, 64 * kExpmvWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long,        \
                                                   med_rows, n_med, nc, ld, mu, coef, tol, k, bin,    \
                                                   bout, F, pin, pout, s);
     switch (P) {
@@ -2328,7 +2353,7 @@ hipError_t launch_expmv_run(int P, bool unit, bool sc1, int grid, int num_cu, co
                             double eta, int s, int m, double* b0, double* b1, double* F, double* part,
                             void* bar, hipStream_t st, unsigned long long* prof) {
     ExpmvRunArgs a{M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long, med_rows, n_med, nc, ld, mu, t, tol, eta,
-                   s, m, expmv_step_blocks(M.n, P, M.n_long, n_med), b0, b1, F, part,
+                   s, m, expmv_step_blocks(M.n, P, M.n_long, n_med, 4), b0, b1, F, part,
                    static_cast<ExpmvBar*>(bar), prof};
     hipError_t e = hipMemsetAsync(bar, 0, sizeof(ExpmvBar), st);
     if (e != hipSuccess) return e;

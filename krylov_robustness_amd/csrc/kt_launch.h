@@ -159,7 +159,8 @@ hipError_t launch_expmv_check(int n, const double* partial, double tol, void* st
 // one fused launch per Taylor term k (P = pow2 >= nc, P <= 32, ld >= P): the
 // check of term k-1 (from pin), SpMM of the natural-order CSR (M), update,
 // norm partials of term k into pout (each 2 * expmv_step_blocks doubles)
-int expmv_step_blocks(int n, int P, int n_long, int n_med);
+// waves: per block (0: the per-term kernel's; the persistent form uses 4)
+int expmv_step_blocks(int n, int P, int n_long, int n_med, int waves = 0);
 hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_rows, int n_med, int nc,
                              int ld, double mu, double coef,
                              double tol, int k, const double* bin, double* bout, double* F,

@@ -330,7 +330,7 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
         const DevCSR& M = natural_csr(A);
         const CsrView V{M.rowptr, M.col, M.val, (int)n, M.long_rows, M.n_long, A->long_thresh,
                         kSplitThresh, M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split};
-        const int nvb = expmv_step_blocks((int)n, P, M.n_long, M.n_med);
+        const int nvb = expmv_step_blocks((int)n, P, M.n_long, M.n_med, 4);  // the persistent form's virtual blocks
         int grid = std::min(nvb, ctx->num_cu);
         if (const char* g = std::getenv("KT_EXPMV_GRID")) grid = std::max(1, std::atoi(g));
         ctx->ws.norm_part.ensure(sizeof(double) * 4 * (size_t)std::max(grid, 1));

@@ -55,7 +55,7 @@ def test_expmv_persistent_launch_is_bit_identical(kra, gpu_ctx, monkeypatch, nam
     """KT_EXPMV_PERSIST=1: the whole expmv call as ONE persistent launch
     (k_expmv_run: a grid barrier per Taylor term, the stop test inside the
     launch) runs the per-term kernel's row arithmetic: F, s, m and mv equal
-    the per-term launches (the default) bit for bit -- in both barrier forms
+    the per-term launches (the default, 4-wave blocks) bit for bit -- in both barrier forms
     (sc1 hand-off without fences, and plain stores + agent release/acquire,
     KT_EXPMV_SC1=0), for the default grid, a grid of one workgroup (every
     virtual block on one workgroup) and a grid of 7 (a partial XCD group);
