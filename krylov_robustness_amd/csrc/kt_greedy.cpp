@@ -102,7 +102,7 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
     const bool fused = !(fz && fz[0] == '0') && n <= kFusedMaxN && pair_fused_lds_bytes(it) <= 150 * 1024 &&
                        getenv("KT_PAIRS_HOST") == nullptr;
     if (fused) {
-        const DevCSR& M = natural_csr(A);
+        const DevCSR& M = natural_csr_ordered(A);  // every reader below is on ctx->stream
         const CsrView V{M.rowptr, M.col, M.val, (int)n, M.long_rows, M.n_long, A->long_thresh,
                         kSplitThresh, M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split};
         ws.pair_blk[0].ensure(sizeof(double) * 6 * (size_t)std::max<int64_t>(n, 1) * C);
@@ -117,19 +117,23 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
             ws.pair_scratch.ensure(sizeof(double) * (size_t)C * big_stride);
             big = ws.pair_scratch.as<double>();
         }
-        std::vector<int> idx(2 * (size_t)C);
+        // candidate indices up and states down through pinned staging (a
+        // pageable copy is staged synchronously by the runtime)
+        ws.pair_host[0].ensure(std::max(sizeof(int) * 2 * (size_t)C, sizeof(double) * 8 * (size_t)C));
+        int* idx = ws.pair_host[0].as<int>();
         for (int c = 0; c < C; ++c) {
             idx[c] = (int)ei[c];
             idx[C + c] = (int)ej[c];
         }
-        KT_HIP(hipMemcpyAsync(ws.pair_idx.ptr, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice,
+        KT_HIP(hipMemcpyAsync(ws.pair_idx.ptr, idx, sizeof(int) * 2 * (size_t)C, hipMemcpyHostToDevice,
                               ctx->stream));
         KT_HIP(launch_pair_fused(C, (int)n, (int64_t)A->h_rowptr[n], V, A->unit_values, ws.pair_idx.as<int>(), ws.pair_idx.as<int>() + C,
                                  B, it, fun, tol, ws.pair_blk[0].as<double>(), big, big_stride,
                                  ws.pair_state.as<double>(), ctx->stream));
-        std::vector<double> sv((size_t)C * 8);
-        KT_HIP(hipMemcpyAsync(sv.data(), ws.pair_state.ptr, sizeof(double) * sv.size(), hipMemcpyDeviceToHost,
-                              ctx->stream));
+        ws.pair_host[1].ensure(sizeof(double) * 8 * (size_t)C);
+        const double* sv = ws.pair_host[1].as<double>();
+        KT_HIP(hipMemcpyAsync(ws.pair_host[1].ptr, ws.pair_state.ptr, sizeof(double) * 8 * (size_t)C,
+                              hipMemcpyDeviceToHost, ctx->stream));
         KT_HIP(hipStreamSynchronize(ctx->stream));
         lap(t_gpu);
         for (int c = 0; c < C; ++c) {
@@ -413,7 +417,14 @@ void trace_fun_update_pairs(kt_matrix_s* A, int64_t nC, const int64_t* ei, const
 static void run_pairs_range(kt_matrix_s* A, const std::vector<int64_t>& pairs, size_t p0, size_t p1,
                             const int64_t* ei, const int64_t* ej, const double* B, double tol, int it,
                             int fun, double* Xm, int* iter, int* lucky) {
-    (void)natural_csr(A);
+    {
+        static const bool timing = getenv("KT_PAIRS_TIMING") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
+        (void)natural_csr_ordered(A);  // candidate kernels run on ctx->stream (side-stream work waits on its events)
+        if (timing)
+            fprintf(stderr, "[kt pairs] natural CSR %.3f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
     for (size_t b0 = p0; b0 < p1; b0 += kMaxPairs) {
         const int C = (int)std::min<size_t>(kMaxPairs, p1 - b0);
         std::vector<int64_t> bi(C), bj(C);
@@ -539,6 +550,118 @@ int64_t miobi_select(kt_matrix_s* A, std::vector<int64_t>& Ei, std::vector<int64
     return best;
 }
 
+// greedy_krylov's k selection steps with the loop on the device (break
+// mode, the register-resident candidate kernel): per step one k_pair_reg
+// launch on the first min(Q, |T|) ranked pairs and one k_greedy_edit launch
+// (argmin, ranking update, the edge deleted into the other CSR buffer), all
+// queued without a host round trip; the host replays the selected edits on
+// its copy at the end.  Same candidates, same kernel, same CSR contents as
+// the host loop, so the same scores and edges.  false: not applicable (the
+// caller runs the host loop).  KT_GREEDY_DEVICE=0 disables it.
+bool greedy_steps_device(kt_matrix_s* A, int k, int64_t Q, const std::vector<int64_t>& Ti,
+                         const std::vector<int64_t>& Tj, const double* B, double tol, int it, int64_t* sel_i,
+                         int64_t* sel_j, double* rob, int64_t* nsel) {
+    const char* ge = getenv("KT_GREEDY_DEVICE");
+    if (ge && ge[0] == '0') return false;
+    const int64_t n = A->n, ntop = (int64_t)Ti.size();
+    const char* fz = getenv("KT_PAIRS_FUSED");
+    if (k <= 0 || n <= 130 || ntop > 4096 || ntop < k || Q > kMaxPairs || (fz && fz[0] == '0') ||
+        getenv("KT_PAIRS_HOST") || n > kFusedMaxN || pair_fused_lds_bytes(it) > 150 * 1024)
+        return false;
+    for (int64_t h = 0; h < ntop; ++h)
+        if (Ti[h] == Tj[h] || Ti[h] < 0 || Ti[h] >= n || Tj[h] < 0 || Tj[h] >= n) return false;
+    if (A->nnz - 2 * (int64_t)(k - 1) < 2) return false;  // krylov_miobi.m:63-65 would fire: host loop
+    kt_context_s* ctx = A->ctx;
+    hipStream_t st = ctx->stream;
+    const DevCSR& M0 = natural_csr(A);
+    const int64_t nnz0 = A->nnz;
+    if (!pair_reg_applies((int)n, nnz0, it, M0.n_long, A->unit_values)) return false;
+    const int nl0 = std::max(M0.n_long, 1);
+    // device state: two CSR sets {rp, ci, va, lr, dyn}, the ranking, the picks
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t set_bytes = al(sizeof(int) * (n + 1)) + al(sizeof(int) * nnz0) + al(sizeof(double) * nnz0) +
+                             al(sizeof(int) * nl0) + al(sizeof(int) * 2);
+    const size_t tail = al(sizeof(int) * ntop) * 2 + al(sizeof(int) * 2 * k) + al(sizeof(double) * k);
+    Workspace& ws = ctx->ws;
+    ws.pair_scratch.ensure(2 * set_bytes + tail);
+    char* base = ws.pair_scratch.as<char>();
+    struct Set {
+        int *rp, *ci, *lr, *dyn;
+        double* va;
+    } S[2];
+    for (int t = 0; t < 2; ++t) {
+        char* p = base + t * set_bytes;
+        S[t].rp = reinterpret_cast<int*>(p);
+        p += al(sizeof(int) * (n + 1));
+        S[t].ci = reinterpret_cast<int*>(p);
+        p += al(sizeof(int) * nnz0);
+        S[t].va = reinterpret_cast<double*>(p);
+        p += al(sizeof(double) * nnz0);
+        S[t].lr = reinterpret_cast<int*>(p);
+        p += al(sizeof(int) * nl0);
+        S[t].dyn = reinterpret_cast<int*>(p);
+    }
+    char* p = base + 2 * set_bytes;
+    int* dTi = reinterpret_cast<int*>(p);
+    p += al(sizeof(int) * ntop);
+    int* dTj = reinterpret_cast<int*>(p);
+    p += al(sizeof(int) * ntop);
+    int* dsel = reinterpret_cast<int*>(p);
+    p += al(sizeof(int) * 2 * k);
+    double* dselv = reinterpret_cast<double*>(p);
+    ws.pair_state.ensure(sizeof(double) * 8 * (size_t)kMaxPairs);
+    // staging: ranking + dyn up, picks down (pinned)
+    ws.pair_host[0].ensure(sizeof(int) * (2 * (size_t)ntop + 2));
+    int* h = ws.pair_host[0].as<int>();
+    for (int64_t t = 0; t < ntop; ++t) {
+        h[t] = (int)Ti[t];
+        h[ntop + t] = (int)Tj[t];
+    }
+    h[2 * ntop] = (int)nnz0;
+    h[2 * ntop + 1] = M0.n_long;
+    KT_HIP(hipMemcpyAsync(dTi, h, sizeof(int) * ntop, hipMemcpyHostToDevice, st));
+    KT_HIP(hipMemcpyAsync(dTj, h + ntop, sizeof(int) * ntop, hipMemcpyHostToDevice, st));
+    KT_HIP(hipMemcpyAsync(S[0].dyn, h + 2 * ntop, sizeof(int) * 2, hipMemcpyHostToDevice, st));
+    KT_HIP(hipMemcpyAsync(S[0].rp, M0.rowptr, sizeof(int) * (n + 1), hipMemcpyDeviceToDevice, st));
+    KT_HIP(hipMemcpyAsync(S[0].ci, M0.col, sizeof(int) * nnz0, hipMemcpyDeviceToDevice, st));
+    KT_HIP(hipMemcpyAsync(S[0].va, M0.val, sizeof(double) * nnz0, hipMemcpyDeviceToDevice, st));
+    if (M0.n_long > 0)
+        KT_HIP(hipMemcpyAsync(S[0].lr, M0.long_rows, sizeof(int) * M0.n_long, hipMemcpyDeviceToDevice, st));
+    double* state = ws.pair_state.as<double>();
+    for (int s = 0; s < k; ++s) {
+        const int C = (int)std::min<int64_t>(Q, ntop - s);
+        const Set& cur = S[s & 1];
+        const Set& nxt = S[(s & 1) ^ 1];
+        const CsrView V{cur.rp, cur.ci, cur.va, (int)n, cur.lr, M0.n_long, A->long_thresh, kSplitThresh,
+                        nullptr, nullptr, 0, nullptr, nullptr, 0};
+        KT_HIP(launch_pair_reg_dyn(C, (int)n, nnz0, V, A->unit_values, dTi, dTj, B, it, KT_FUN_EXP, tol, state,
+                                   cur.dyn, st));
+        KT_HIP(launch_greedy_edit(C, state, dTi, dTj, (int)(ntop - s), (int)n, A->long_thresh, cur.rp, cur.ci,
+                                  cur.va, cur.lr, cur.dyn, nxt.rp, nxt.ci, nxt.va, nxt.lr, nxt.dyn, s, dsel, dselv,
+                                  st));
+    }
+    ws.pair_host[1].ensure(sizeof(int) * 2 * (size_t)k + sizeof(double) * (size_t)k);
+    double* hv = ws.pair_host[1].as<double>();
+    int* hs = reinterpret_cast<int*>(hv + k);
+    KT_HIP(hipMemcpyAsync(hv, dselv, sizeof(double) * k, hipMemcpyDeviceToHost, st));
+    KT_HIP(hipMemcpyAsync(hs, dsel, sizeof(int) * 2 * k, hipMemcpyDeviceToHost, st));
+    KT_HIP(hipStreamSynchronize(st));
+    std::vector<int64_t> ei(k), ej(k);
+    double total = 0.0;
+    for (int s = 0; s < k; ++s) {
+        if (hs[2 * s] < 0) fail(KT_ERR_ARG, "KRYLOV_MIOBI:: no finite candidate score");
+        ei[s] = hs[2 * s];
+        ej[s] = hs[2 * s + 1];
+        if (sel_i) sel_i[s] = ei[s];
+        if (sel_j) sel_j[s] = ej[s];
+        total += hv[s];
+    }
+    set_pairs(A, k, ei.data(), ej.data(), 0.0);  // the host copy (and a current twin) take the same edits
+    *rob = total;
+    *nsel = k;
+    return true;
+}
+
 void miobi_checks(kt_matrix_s* A, int k, int make, int& it) {
     require_symmetric(A, "KRYLOV_MIOBI:: Adjacency matrix should be symmetric");  // :26-28
     if (it <= 0) it = (int)std::min<int64_t>(100, A->n);                        // :32-34
@@ -591,6 +714,11 @@ int kt_greedy_krylov_steps(kt_matrix_t A, int k, int64_t Q, int64_t ntop, const 
     const double sg = make ? 1.0 : -1.0;
     const double B[4] = {0.0, sg / rescale, sg / rescale, 0.0};  // krylov_miobi.m:78-84
     std::vector<int64_t> Ti(ti, ti + ntop), Tj(tj, tj + ntop);
+    if (!make && k > 0) {
+        int itc = it;
+        miobi_checks(A, 1, make, itc);
+        if (greedy_steps_device(A, k, Q, Ti, Tj, B, tol, itc, sel_i, sel_j, rob, nsel)) return KT_OK;
+    }
     std::vector<double> xm;
     double total = 0.0;
     int64_t done = 0;

@@ -231,8 +231,10 @@ struct kt_matrix_s {
 namespace kt {
 
 // build one device CSR of A with rows in the order new2old (identity if empty)
-void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out);
+// sync = false: the upload is only stream-ordered (see natural_csr_ordered)
+void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out, bool sync = true);
 const DevCSR& natural_csr(kt_matrix_s* A);
+const DevCSR& natural_csr_ordered(kt_matrix_s* A);
 void refresh_device(kt_matrix_s* A);
 const DevCSR& hub_csr(kt_matrix_s* A);
 

@@ -39,6 +39,17 @@ size_t pair_fused_lds_bytes(int it);
 hipError_t launch_pair_fused(int C, int n, int64_t nnz, const CsrView& A, bool unit, const int* ii,
                              const int* jj, const double* B, int it, int fun, double tol, double* vec,
                              double* big, int64_t big_stride, double* state, hipStream_t st);
+// device-resident greedy steps (kt_greedy.cpp): k_pair_reg with the CSR's
+// {nnz, n_long} read from dyn (the LDS sized for nnz_max), and one step's
+// selection + ranking update + edge deletion into the other CSR buffer
+bool pair_reg_applies(int n, int64_t nnz, int it, int n_long, bool unit);
+hipError_t launch_pair_reg_dyn(int C, int n, int64_t nnz_max, const CsrView& A, bool unit, const int* ii,
+                               const int* jj, const double* B, int it, int fun, double tol, double* state,
+                               const int* dyn, hipStream_t st);
+hipError_t launch_greedy_edit(int C, const double* state, int* Ti, int* Tj, int nT, int n, int long_thresh,
+                              const int* rp, const int* ci, const double* va, const int* lr, const int* dyn,
+                              int* rp2, int* ci2, double* va2, int* lr2, int* dyn2, int step, int* sel,
+                              double* selv, hipStream_t st);
 hipError_t launch_spmm_block(int P, int flags, int grid, const CsrView& M, const double* X, int ldx,
                              double* Y, int ldy, int long_blocks, int chunk_blocks, double* ck_part,
                              hipStream_t st, int slices = 1, const int* skip = nullptr);

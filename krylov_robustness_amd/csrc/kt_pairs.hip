@@ -1830,11 +1830,12 @@ double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev
 // space (a pointer chosen at run time between LDS and global memory compiles
 // to flat loads).
 template <int R, int CSR>
-__global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nnz, FusedCSR M,
+__global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nnz_host, FusedCSR M,
                                                             const int* __restrict__ ii, const int* __restrict__ jj,
                                                             double b00, double b10, double b01, double b11,
                                                             int it, int fun, double tol,
-                                                            double* __restrict__ state) {
+                                                            double* __restrict__ state,
+                                                            const int* __restrict__ dyn = nullptr) {
     extern __shared__ double sm[];
     __shared__ double red[2 * kFusedWaves * 8];
     __shared__ double bc[4];
@@ -1842,7 +1843,11 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
     __shared__ double cm[4];     // Cm = R B R' (column-major)
     __shared__ double lastr[3];  // the previous record's R (beta1, r12, beta2)
     const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nl = min(M.n_long, kRegLongCap);
+    // dyn (device-resident greedy loop): {nnz, n_long} of the current CSR,
+    // written by the previous step's k_greedy_edit; the LDS was sized for the
+    // first step's (larger) matrix
+    const int nnz = dyn ? dyn[0] : nnz_host;
+    const int nl = min(dyn ? dyn[1] : M.n_long, kRegLongCap);
     const RegLds L = reg_lds_layout(n, nnz, it, nl > 0, CSR);
     char* base = reinterpret_cast<char*>(sm);
     double* X = reinterpret_cast<double*>(base + L.x);
@@ -2040,6 +2045,173 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
         st[PS_LUCKY] = lucky ? 1.0 : 0.0;
         st[PS_DONE] = 1.0;
     }
+}
+
+// One greedy step's bookkeeping on the device (greedy_krylov.m:80-93 with
+// krylov_miobi(A, 1, E, ...), break mode): the candidate with the smallest
+// score (the first on ties, as the host loop), its pair dropped from the
+// ranking (greedy_krylov.m:84-86), and A with that edge deleted from both
+// triangles (krylov_miobi.m:129-135) written to the other CSR buffer -- row
+// order and the surviving long rows' order kept, so the next candidate launch
+// computes exactly what it computes after the host edit.  One workgroup.
+__global__ __launch_bounds__(1024) void k_greedy_edit(int C, const double* __restrict__ state, int* __restrict__ Ti,
+                                                     int* __restrict__ Tj, int nT, int n, int long_thresh,
+                                                     const int* __restrict__ rp, const int* __restrict__ ci,
+                                                     const double* __restrict__ va, const int* __restrict__ lr,
+                                                     const int* __restrict__ dyn, int* __restrict__ rp2,
+                                                     int* __restrict__ ci2, double* __restrict__ va2,
+                                                     int* __restrict__ lr2, int* __restrict__ dyn2, int step,
+                                                     int* __restrict__ sel, double* __restrict__ selv) {
+    __shared__ double wv[16];
+    __shared__ int wi[16];
+    __shared__ int s_best, s_ci, s_cj, s_k1, s_k2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double v = INFINITY;
+    int idx = 0x7fffffff;
+    for (int c = tid; c < C; c += 1024) {
+        const double x = state[(int64_t)c * PS_N + PS_XM];
+        if (x < v) {  // ascending c per thread: the first minimum; NaN never wins (as xm < bv)
+            v = x;
+            idx = c;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(v, o, 64);
+        const int oi = __shfl_xor(idx, o, 64);
+        if (ov < v || (ov == v && oi < idx)) {
+            v = ov;
+            idx = oi;
+        }
+    }
+    if (lane == 0) {
+        wv[wave] = v;
+        wi[wave] = idx;
+    }
+    __syncthreads();
+    if (tid == 0) {  // (v, idx) hold wave 0's minimum
+        for (int w = 1; w < 16; ++w)
+            if (wv[w] < v || (wv[w] == v && wi[w] < idx)) {
+                v = wv[w];
+                idx = wi[w];
+            }
+        const bool ok = idx < C;
+        s_best = ok ? idx : -1;
+        s_ci = ok ? Ti[idx] : -1;
+        s_cj = ok ? Tj[idx] : -1;
+        sel[2 * step] = s_ci;
+        sel[2 * step + 1] = s_cj;
+        selv[step] = v;
+        // the entries (ci, cj) and (cj, ci): binary search in their sorted rows
+        int k1 = -1, k2 = -1;
+        if (ok) {
+            auto find = [&](int r, int c) {
+                int lo = rp[r], hi = rp[r + 1];
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (ci[mid] < c) lo = mid + 1;
+                    else hi = mid;
+                }
+                return (lo < rp[r + 1] && ci[lo] == c) ? lo : -1;
+            };
+            k1 = find(s_ci, s_cj);
+            if (s_cj != s_ci) k2 = find(s_cj, s_ci);
+        }
+        s_k1 = k1;
+        s_k2 = k2;
+    }
+    __syncthreads();
+    const int best = s_best, r1 = s_ci, r2 = s_cj, k1 = s_k1, k2 = s_k2;
+    const int nnz = dyn[0];
+    // ranking: drop entry `best` (read all, barrier, write shifted)
+    int tv[4], tw[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int t = best + 1 + tid + u * 1024;
+        tv[u] = (best >= 0 && t < nT) ? Ti[t] : 0;
+        tw[u] = (best >= 0 && t < nT) ? Tj[t] : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int t = best + 1 + tid + u * 1024;
+        if (best >= 0 && t < nT) {
+            Ti[t - 1] = tv[u];
+            Tj[t - 1] = tw[u];
+        }
+    }
+    // the CSR without positions k1, k2 (into the other buffer)
+    for (int t = tid; t < nnz; t += 1024) {
+        if (t == k1 || t == k2) continue;
+        const int d = t - (k1 >= 0 && t > k1) - (k2 >= 0 && t > k2);
+        ci2[d] = ci[t];
+        va2[d] = va[t];
+    }
+    for (int r = tid; r <= n; r += 1024)
+        rp2[r] = rp[r] - (k1 >= 0 && r > r1) - (k2 >= 0 && r > r2);
+    __syncthreads();
+    if (tid == 0) {  // long rows that stay long, in their order
+        int m = 0;
+        for (int l = 0; l < dyn[1]; ++l) {
+            const int r = lr[l];
+            if (rp2[r + 1] - rp2[r] > long_thresh) lr2[m++] = r;
+        }
+        dyn2[0] = nnz - (k1 >= 0) - (k2 >= 0);
+        dyn2[1] = m;
+    }
+}
+
+bool pair_reg_applies(int n, int64_t nnz, int it, int n_long, bool unit) {
+    const char* de = getenv("KT_PAIRS_DENSE_EIG");
+    const char* rg = getenv("KT_PAIRS_REG");
+    constexpr size_t kLdsMax = 160 * 1024 - 2048;
+    const bool has_long = std::min(n_long, kRegLongCap) > 0;
+    (void)unit;
+    return !(de && de[0] == '1') && !(rg && rg[0] == '0') && n >= 2 && n <= 8 * kFusedThreads &&
+           nnz < (int64_t)1 << 31 && reg_lds_layout(n, nnz, it, has_long, 0).total <= kLdsMax;
+}
+
+// k_pair_reg on candidates ii/jj (device) with the CSR's nnz / n_long read
+// from dyn; nnz_max / has_long_max size the LDS (the first step's matrix)
+hipError_t launch_pair_reg_dyn(int C, int n, int64_t nnz_max, const CsrView& A, bool unit, const int* ii,
+                               const int* jj, const double* B, int it, int fun, double tol, double* state,
+                               const int* dyn, hipStream_t st) {
+    if (C <= 0) return hipSuccess;
+    const FusedCSR M{A.rp, A.ci, A.va, A.long_rows, A.n_long, A.long_thresh, unit ? 1 : 0};
+    constexpr size_t kLdsMax = 160 * 1024 - 2048;
+    const bool has_long = std::min(A.n_long, kRegLongCap) > 0;
+    int csr = 0;
+    for (int cand = unit ? 1 : 2; cand >= 1; --cand)
+        if (reg_lds_layout(n, nnz_max, it, has_long, cand).total <= kLdsMax) {
+            csr = cand;
+            break;
+        }
+    const size_t lds = reg_lds_layout(n, nnz_max, it, has_long, csr).total;
+    const int rows = (n + kFusedThreads - 1) / kFusedThreads;
+    const int rr = rows <= 2 ? 2 : rows <= 4 ? 4 : 8;
+#define KT_REG_LAUNCH(RR, CC)                                                                                  \
+    k_pair_reg<RR, CC><<<C, kFusedThreads, lds, st>>>(C, n, (int)nnz_max, M, ii, jj, B[0], B[1], B[2], B[3], it, \
+                                                      fun, tol, state, dyn)
+#define KT_REG_CSR(RR)                       \
+    if (csr == 0) KT_REG_LAUNCH(RR, 0);      \
+    else if (csr == 1) KT_REG_LAUNCH(RR, 1); \
+    else KT_REG_LAUNCH(RR, 2)
+    if (rr == 2) { KT_REG_CSR(2); }
+    else if (rr == 4) { KT_REG_CSR(4); }
+    else { KT_REG_CSR(8); }
+#undef KT_REG_CSR
+#undef KT_REG_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_greedy_edit(int C, const double* state, int* Ti, int* Tj, int nT, int n, int long_thresh,
+                              const int* rp, const int* ci, const double* va, const int* lr, const int* dyn,
+                              int* rp2, int* ci2, double* va2, int* lr2, int* dyn2, int step, int* sel,
+                              double* selv, hipStream_t st) {
+    if (nT > 4 * 1024) return hipErrorInvalidValue;
+    k_greedy_edit<<<1, 1024, 0, st>>>(C, state, Ti, Tj, nT, n, long_thresh, rp, ci, va, lr, dyn, rp2, ci2, va2,
+                                      lr2, dyn2, step, sel, selv);
+    return hipGetLastError();
 }
 
 hipError_t launch_pair_fused(int C, int n, int64_t nnz, const CsrView& A, bool unit, const int* ii,

@@ -78,7 +78,7 @@ void DevCSR::release() {
     built = false;
 }
 
-void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out) {
+void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out, bool sync) {
     const int64_t n = A->n, nnz = A->nnz;
     const bool ident = new2old.empty();
     auto orig = [&](int64_t r) -> int64_t { return ident ? r : new2old[r]; };
@@ -92,8 +92,19 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
     std::vector<std::pair<int32_t, double>> tmp;
     for (int64_t r = 0; r < n; ++r) {
         const int64_t o = orig(r);
+        const int64_t kb = A->h_rowptr[o], ke = A->h_rowptr[o + 1];
+        if (ident) {  // natural order: copy a row that is already sorted (the usual
+                      // case -- MATLAB CSC and set_entry keep rows sorted)
+            bool sorted = true;
+            for (int64_t k = kb + 1; k < ke && sorted; ++k) sorted = A->h_col[k - 1] < A->h_col[k];
+            if (sorted) {
+                std::copy(A->h_col.begin() + kb, A->h_col.begin() + ke, c32.begin() + rp32[r]);
+                std::copy(A->h_val.begin() + kb, A->h_val.begin() + ke, v64.begin() + rp32[r]);
+                continue;
+            }
+        }
         tmp.clear();
-        for (int64_t k = A->h_rowptr[o]; k < A->h_rowptr[o + 1]; ++k)
+        for (int64_t k = kb; k < ke; ++k)
             tmp.push_back({ident ? A->h_col[k] : A->old2new[A->h_col[k]], A->h_val[k]});
         std::sort(tmp.begin(), tmp.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
         for (size_t t = 0; t < tmp.size(); ++t) {
@@ -176,7 +187,10 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out)
             off += slice(g.bytes);
         }
         KT_HIP(hipMemcpyAsync(out.blob, h, total, hipMemcpyHostToDevice, A->ctx->stream));
-        KT_HIP(hipStreamSynchronize(A->ctx->stream));
+        // the copy is ordered before later work on the context's stream; other
+        // streams may read the arrays, so the default waits for it (the
+        // staging buffer is not rewritten before the next build's sync above)
+        if (sync) KT_HIP(hipStreamSynchronize(A->ctx->stream));
         out.n_long = (int)lr.size();
         out.n_med = (int)mr.size();
         out.n_split = (int)spr.size();
@@ -220,6 +234,14 @@ const DevCSR& hub_csr(kt_matrix_s* A) {
 
 const DevCSR& natural_csr(kt_matrix_s* A) {
     if (!A->nat.built) build_csr(A, std::vector<int32_t>(), A->nat);
+    return A->nat;
+}
+
+// the same, without waiting for the upload: for callers whose every reader of
+// the arrays is ordered after the context's stream (the greedy candidate
+// paths, which rebuild the copy after every edge edit)
+const DevCSR& natural_csr_ordered(kt_matrix_s* A) {
+    if (!A->nat.built) build_csr(A, std::vector<int32_t>(), A->nat, false);
     return A->nat;
 }
 

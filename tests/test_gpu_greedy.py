@@ -334,3 +334,20 @@ def test_pairs_batched_block_sturm_eig(kra, gpu_ctx, monkeypatch):
     np.testing.assert_allclose(x_s, x_d, rtol=1e-10, atol=1e-12)
     np.testing.assert_array_equal(it_s, it_d)
     np.testing.assert_array_equal(l_s, l_d)
+
+
+def test_greedy_device_loop_matches_host_loop(kra, gpu_ctx, monkeypatch):
+    """Break mode queues the k greedy steps on the device (k_pair_reg + the
+    k_greedy_edit selection / ranking / edge deletion per step, no host round
+    trip); KT_GREEDY_DEVICE=0 runs the host loop.  Same edges, bit-equal
+    variation, the same A_new -- over 12 steps of the config-5 settings."""
+    A, c = _india(kra)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    tol = kra.default_greedy_tol(D, ctx=gpu_ctx)
+    e1, r1, D1 = kra.greedy_krylov(D, 12, 250, c, "min", tol, 100, np.inf, 0, "break", ctx=gpu_ctx)
+    monkeypatch.setenv("KT_GREEDY_DEVICE", "0")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    e2, r2, D2 = kra.greedy_krylov(D, 12, 250, c, "min", tol, 100, np.inf, 0, "break", ctx=gpu_ctx)
+    np.testing.assert_array_equal(e1, e2)
+    assert r1 == r2
+    assert (abs(D1.to_scipy() - D2.to_scipy()) > 0).nnz == 0
