@@ -114,8 +114,36 @@ struct SweepBufs {
     DevBuf tick;  // arrival tickets of the fused coefficient step (zeroed when allocated)
 };
 
+// one host int the device may store to at system scope (fine-grained,
+// coherent pinned memory): read by the host without a stream sync
+struct HostFlag {
+    int* host = nullptr;
+    int* dev = nullptr;
+    HostFlag() = default;
+    HostFlag(const HostFlag&) = delete;
+    HostFlag& operator=(const HostFlag&) = delete;
+    ~HostFlag() {
+        if (host) (void)hipHostFree(host);
+    }
+    void ensure() {
+        if (host) return;
+        void* p = nullptr;
+        hipError_t e = hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped);
+        if (e != hipSuccess) fail(KT_ERR_ALLOC, std::string("hipHostMalloc(coherent): ") + hipGetErrorString(e));
+        void* d = nullptr;
+        e = hipHostGetDevicePointer(&d, p, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(p);
+            fail(KT_ERR_HIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
+        }
+        host = static_cast<int*>(p);
+        dev = static_cast<int*>(d);
+    }
+};
+
 struct Workspace {
     SweepBufs sweep[4];
+    HostFlag expmv_stop;  // the stage a k_expmv_step launch found stopped (expmv_device)
     DevBuf small, small2, qrtmp, eigA, eigW, eigInfo;  // block-Krylov scratch
     DevBuf expm;                                       // batched device expm (6 x batch x n^2)
     DevBuf ck_part;                                    // block SpMM hub-row chunk partials

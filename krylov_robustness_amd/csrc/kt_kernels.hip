@@ -1526,7 +1526,7 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
     const int* __restrict__ long_rows, int n_long, const int* __restrict__ med_rows, int n_med,
     int nc, int ld, double mu, double coef, double tol, int k, const double* __restrict__ bin,
     double* __restrict__ bout, double* __restrict__ F, const double* __restrict__ pin,
-    double* __restrict__ pout, ExpmvState* st) {
+    double* __restrict__ pout, ExpmvState* st, int* hflag, int stage) {
     constexpr int WAVES = kExpmvWaves, THREADS = 64 * WAVES;
     using G = GeoW<P, (P >= 2) ? 2 : 1>;                          // short rows
     using GL = GeoW<P, (P >= 4) ? 4 : (P >= 2) ? 2 : 1>;          // medium / long rows
@@ -1624,6 +1624,10 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
         if (c1 + c2 <= tol * nf) {
             st->active = 0;
             decide = 0;
+            // tell the host (pinned, coherent): the rest of this stage's terms
+            // are no-ops, it may stop queueing them
+            if (hflag && blockIdx.x == 0)
+                __hip_atomic_store(hflag, stage, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         } else {
             st->c1s[k & 1] = c2;
         }
@@ -2313,18 +2317,18 @@ int expmv_step_blocks(int n, int P, int n_long, int n_med, int waves) {
 hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_rows, int n_med, int nc,
                              int ld, double mu, double coef, double tol, int k, const double* bin,
                              double* bout, double* F, const double* pin, double* pout, void* state,
-                             hipStream_t st) {
+                             hipStream_t st, int* hflag, int stage) {
     const int grid = expmv_step_blocks(M.n, P, M.n_long, n_med);
     ExpmvState* s = static_cast<ExpmvState*>(state);
 #define KT_EXPMV_STEP(PP)                                                                          \
     if (unit)                                                                                      \
         k_expmv_step<PP, KF_UNIT><<<grid, 64 * kExpmvWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long,  \
                                                         med_rows, n_med, nc, ld, mu, coef, tol, k,    \
-                                                        bin, bout, F, pin, pout, s);                 \
+                                                        bin, bout, F, pin, pout, s, hflag, stage);   \
     else                                                                                           \
         k_expmv_step<PP, 0><<<grid, 64 * kExpmvWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long,        \
                                                   med_rows, n_med, nc, ld, mu, coef, tol, k, bin,    \
-                                                  bout, F, pin, pout, s);
+                                                  bout, F, pin, pout, s, hflag, stage);
     switch (P) {
     case 1: KT_EXPMV_STEP(1) break;
     case 2: KT_EXPMV_STEP(2) break;

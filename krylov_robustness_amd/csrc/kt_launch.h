@@ -175,7 +175,8 @@ int expmv_step_blocks(int n, int P, int n_long, int n_med, int waves = 0);
 hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_rows, int n_med, int nc,
                              int ld, double mu, double coef,
                              double tol, int k, const double* bin, double* bout, double* F,
-                             const double* pin, double* pout, void* state, hipStream_t st);
+                             const double* pin, double* pout, void* state, hipStream_t st,
+                             int* hflag = nullptr, int stage = 0);
 // the whole expmv call (s stages x up to m terms, stop tests, f = eta f) in
 // ONE persistent launch of `grid` workgroups (capped so all are resident);
 // b0 / F hold the input block, b1 is scratch (n x ld each, zero padded);

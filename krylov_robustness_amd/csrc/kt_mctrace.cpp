@@ -414,15 +414,29 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
         const int nbs = expmv_step_blocks((int)n, P, M.n_long, M.n_med);
         ctx->ws.norm_part.ensure(sizeof(double) * std::max(2 * nb, 4 * nbs));
         part = ctx->ws.norm_part.as<double>();
+        // The launch that finds a stage's stop test satisfied also stores the
+        // stage index into a coherent host flag; the host, which queues terms
+        // only slightly ahead of the device here, stops queueing that stage's
+        // remaining (no-op) terms once it sees it.  KT_EXPMV_STOPFLAG=0 queues
+        // all s * m terms.
+        const char* sf = std::getenv("KT_EXPMV_STOPFLAG");
+        const bool use_flag = !(sf && sf[0] == '0');
+        int* hflag = nullptr;
+        if (use_flag) {
+            ctx->ws.expmv_stop.ensure();
+            __atomic_store_n(ctx->ws.expmv_stop.host, -1, __ATOMIC_RELEASE);
+            hflag = ctx->ws.expmv_stop.dev;
+        }
         for (int i = 0; i < r.s; ++i) {
             KT_HIP(launch_inf_norm((int)n, nc, b.col(0), ld, part, st));   // c1 = norm(b, inf)
             KT_HIP(launch_expmv_begin(part, nb, state, st));
             double* cur = b.col(0);
             double* nxt = Ab.col(0);
             for (int k = 1; k <= r.m; ++k) {
+                if (use_flag && k > 2 && __atomic_load_n(ctx->ws.expmv_stop.host, __ATOMIC_ACQUIRE) >= i) break;
                 KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu, t / ((double)r.s * k), tol, k, cur,
                                          nxt, F, part + (size_t)((k - 1) & 1) * 2 * nbs,
-                                         part + (size_t)(k & 1) * 2 * nbs, state, st));
+                                         part + (size_t)(k & 1) * 2 * nbs, state, st, hflag, i));
                 std::swap(cur, nxt);
             }
             KT_HIP(launch_axpby((int)n, nc, eta, F, ld, 0.0, F, ld, st));  // f = eta f

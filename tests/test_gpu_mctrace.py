@@ -80,6 +80,24 @@ def test_expmv_persistent_launch_is_bit_identical(kra, gpu_ctx, monkeypatch, nam
         np.testing.assert_array_equal(out[0], ref[0])
 
 
+def test_expmv_host_stop_flag_is_exact(kra, gpu_ctx, monkeypatch):
+    """The per-term launches stop being queued once the launch that found a
+    stage's stop test satisfied has told the host (coherent host flag): the
+    skipped launches were no-ops, so F, s, m, mv equal queueing all s * m
+    terms (KT_EXPMV_STOPFLAG=0), bit for bit; trace_exp likewise."""
+    A = load_graph("oregon_A6")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    b = np.random.default_rng(9).normal(size=(A.shape[0], 10))
+    f1 = kra.expmv(1.0, D, b, ctx=gpu_ctx)
+    t1 = kra.trace_exp(D, method="expmv", seed=2, ctx=gpu_ctx)
+    monkeypatch.setenv("KT_EXPMV_STOPFLAG", "0")
+    f0 = kra.expmv(1.0, D, b, ctx=gpu_ctx)
+    t0 = kra.trace_exp(D, method="expmv", seed=2, ctx=gpu_ctx)
+    assert tuple(f1[1:]) == tuple(f0[1:])
+    np.testing.assert_array_equal(f1[0], f0[0])
+    assert t1 == t0
+
+
 def test_lanczos_fmv_matches_oracle(kra, gpu_ctx):
     A = load_graph("rome")
     X = np.random.default_rng(2).normal(size=(A.shape[0], 4))
