@@ -5,8 +5,10 @@
 // implicit-shift QL that rotates only the first row of the eigenvector matrix
 // (Golub-Welsch), giving theta_k and tau_k = (Q e1)_k for the quadrature
 //   e1' f(T) e1 = sum_k tau_k^2 f(theta_k).
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 
 #include "kt_internal.h"
 
@@ -251,8 +253,160 @@ static void tql2(int n, double* d, double* e, double* z /* nullable */) {
     }
 }
 
+// Eigenvalues only, larger n: Householder tridiagonalisation from the left
+// on the lower triangle of the column-major copy -- every inner loop runs
+// down a contiguous column (symmetric matrix-vector product and rank-2
+// update), where tred2's walk along rows strides by n.  Golub & Van Loan's
+// house(): P x = mu e1, so the subdiagonal is mu.  Output in tql2's layout
+// (e[i] couples i-1 and i, e[0] unused).
+template <int>
+static inline __attribute__((always_inline)) void tridiag_lower_cols(int n, double* __restrict__ a, double* __restrict__ d,
+                                                                     double* __restrict__ e, double* __restrict__ v,
+                                                                     double* __restrict__ p) {
+    for (int k = 0; k + 2 < n; ++k) {
+        const int m = n - k - 1;
+        double* x = a + (k + 1) + (size_t)k * n;  // A(k+1:n, k)
+        double sigma = 0.0;
+        for (int i = 1; i < m; ++i) sigma += x[i] * x[i];
+        d[k] = a[k + (size_t)k * n];
+        const double alpha = x[0];
+        if (sigma == 0.0) {  // already reduced in this column
+            e[k + 1] = alpha;
+            continue;
+        }
+        const double mu = std::sqrt(alpha * alpha + sigma);
+        const double v0 = alpha <= 0.0 ? alpha - mu : -sigma / (alpha + mu);
+        const double tau = 2.0 * v0 * v0 / (sigma + v0 * v0);
+        const double iv0 = 1.0 / v0;
+        v[0] = 1.0;
+        for (int i = 1; i < m; ++i) v[i] = x[i] * iv0;
+        e[k + 1] = mu;
+        double* __restrict__ B = a + (k + 1) + (size_t)(k + 1) * n;  // trailing block, lower triangle valid
+        // p = tau B v (B symmetric, lower triangle stored)
+        for (int i = 0; i < m; ++i) p[i] = 0.0;
+        for (int j = 0; j < m; ++j) {
+            const double* __restrict__ col = B + (size_t)j * n;
+            const double vj = v[j];
+            double s0 = col[j] * vj, s1 = 0.0, s2 = 0.0, s3 = 0.0;  // 4 partial sums: vectorisable
+            int i = j + 1;
+            for (; i + 3 < m; i += 4) {
+                p[i] += col[i] * vj;
+                p[i + 1] += col[i + 1] * vj;
+                p[i + 2] += col[i + 2] * vj;
+                p[i + 3] += col[i + 3] * vj;
+                s0 += col[i] * v[i];
+                s1 += col[i + 1] * v[i + 1];
+                s2 += col[i + 2] * v[i + 2];
+                s3 += col[i + 3] * v[i + 3];
+            }
+            for (; i < m; ++i) {
+                p[i] += col[i] * vj;
+                s0 += col[i] * v[i];
+            }
+            p[j] += (s0 + s1) + (s2 + s3);
+        }
+        double pv = 0.0;
+        for (int i = 0; i < m; ++i) {
+            p[i] *= tau;
+            pv += p[i] * v[i];
+        }
+        const double K = 0.5 * tau * pv;
+        for (int i = 0; i < m; ++i) p[i] -= K * v[i];  // w
+        // B -= v w' + w v' (lower triangle)
+        for (int j = 0; j < m; ++j) {
+            double* __restrict__ col = B + (size_t)j * n;
+            const double vj = v[j], wj = p[j];
+            for (int i = j; i < m; ++i) col[i] -= v[i] * wj + p[i] * vj;
+        }
+    }
+    if (n >= 2) {
+        d[n - 2] = a[(n - 2) + (size_t)(n - 2) * n];
+        e[n - 1] = a[(n - 1) + (size_t)(n - 2) * n];
+    }
+    d[n - 1] = a[(n - 1) + (size_t)(n - 1) * n];
+    e[0] = 0.0;
+}
+
+__attribute__((target("avx2,fma"))) static void tridiag_lower_cols_avx2(int n, double* a, double* d, double* e,
+                                                                        double* v, double* p) {
+    tridiag_lower_cols<1>(n, a, d, e, v, p);
+}
+static void tridiag_lower_cols_base(int n, double* a, double* d, double* e, double* v, double* p) {
+    tridiag_lower_cols<0>(n, a, d, e, v, p);
+}
+
+// tql2 without eigenvectors for the column path: the rotations' radii by
+// sqrt(f^2 + g^2) instead of hypot (a libm call per rotation), rescaled when
+// the squares could leave the double range
+static void tql_values(int n, double* d, double* e) {
+    for (int i = 1; i < n; ++i) e[i - 1] = e[i];
+    e[n - 1] = 0.0;
+    auto rad = [](double f, double g) {
+        const double af = std::fabs(f), ag = std::fabs(g);
+        const double mx = af > ag ? af : ag;
+        if (mx > 1e150 || (mx < 1e-150 && mx > 0.0)) return std::hypot(f, g);
+        return std::sqrt(f * f + g * g);
+    };
+    for (int l = 0; l < n; ++l) {
+        int iter = 0;
+        for (;;) {
+            int m = l;
+            for (; m < n - 1; ++m) {
+                const double dd = std::fabs(d[m]) + std::fabs(d[m + 1]);
+                if (std::fabs(e[m]) <= DBL_EPSILON * dd) break;
+            }
+            if (m == l || iter++ == 200) break;
+            double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+            double r = rad(g, 1.0);
+            g = d[m] - d[l] + e[l] / (g + std::copysign(r, g));
+            double s = 1.0, c = 1.0, p = 0.0;
+            bool deflated = false;
+            for (int i = m - 1; i >= l; --i) {
+                const double f = s * e[i];
+                const double b = c * e[i];
+                r = rad(f, g);
+                e[i + 1] = r;
+                if (r == 0.0) {
+                    d[i + 1] -= p;
+                    e[m] = 0.0;
+                    deflated = true;
+                    break;
+                }
+                s = f / r;
+                c = g / r;
+                g = d[i + 1] - p;
+                r = (d[i] - g) * s + 2.0 * c * b;
+                p = s * r;
+                d[i + 1] = g + p;
+                g = c * r - b;
+            }
+            if (deflated) continue;
+            d[l] -= p;
+            e[l] = g;
+            e[m] = 0.0;
+        }
+    }
+    std::sort(d, d + n);
+}
+
+// values-only problems from this size take tridiag_lower_cols (smaller ones,
+// e.g. the greedy candidates' 2j x 2j projections, keep tred2 bit for bit)
+constexpr int kColTridiagMinN = 96;
+
 void sym_eig_host(int n, const double* A, double* w, double* V /* nullable */) {
     if (n <= 0) return;
+    static const bool col_ok = [] {
+        const char* c = std::getenv("KT_EIG_COLTRIDIAG");
+        return !(c && c[0] == '0');
+    }();
+    if (!V && col_ok && n >= kColTridiagMinN) {
+        std::vector<double> a(A, A + (size_t)n * n), e(n), v(n), p(n);
+        static const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
+        if (avx2) tridiag_lower_cols_avx2(n, a.data(), w, e.data(), v.data(), p.data());
+        else tridiag_lower_cols_base(n, a.data(), w, e.data(), v.data(), p.data());
+        tql_values(n, w, e.data());
+        return;
+    }
     std::vector<double> a(A, A + (size_t)n * n), e(n);
     tred2(n, a.data(), w, e.data(), V != nullptr);
     tql2(n, w, e.data(), V ? a.data() : nullptr);

@@ -48,3 +48,34 @@ def test_host_eig_block_tridiagonal():
             A[2*b:2*b+2, 2*b+2:2*b+4] = R.T
     w, _ = _eig(A, False)
     np.testing.assert_allclose(np.sort(w), np.linalg.eigvalsh(A), atol=1e-13)
+
+
+@pytest.mark.parametrize("n", [96, 150, 225, 320])
+def test_host_eig_values_column_tridiagonalisation(n, monkeypatch):
+    """Values-only problems from n = 96 on take the column-oriented
+    tridiagonalisation (tridiag_lower_cols, contiguous inner loops): the
+    eigenvalues of dense, 25x25-block-tridiagonal (config 3's Lanczos
+    projections) and rank-deficient / partly reduced matrices equal LAPACK's
+    to rounding."""
+    rng = np.random.default_rng(n)
+    M = rng.normal(size=(n, n))
+    cases = [(M + M.T) / 2]
+    bs = 25
+    B = np.zeros((n, n))
+    for b0 in range(0, n, bs):
+        D = rng.normal(size=(min(bs, n - b0),) * 2)
+        B[b0:b0 + bs, b0:b0 + bs] = D + D.T
+        if b0 + bs < n:
+            R = np.triu(rng.normal(size=(bs, min(bs, n - b0 - bs))))
+            B[b0 + bs:b0 + 2 * bs, b0:b0 + bs] = R.T
+            B[b0:b0 + bs, b0 + bs:b0 + 2 * bs] = R
+    cases.append(B)
+    Z = (M + M.T) / 2
+    Z[:, 3] = 0.0
+    Z[3, :] = 0.0                                   # a zero row/column (sigma = 0 in step 3)
+    T = np.diag(rng.normal(size=n)) + np.diag(rng.normal(size=n - 1), 1) + np.diag(rng.normal(size=n - 1), -1)
+    cases += [Z, T]                                 # an already tridiagonal matrix
+    for A in cases:
+        w, _ = _eig(A, False)
+        ref = np.linalg.eigvalsh(A)
+        np.testing.assert_allclose(np.sort(w), ref, atol=2e-13 * max(1, np.abs(ref).max()))
