@@ -96,6 +96,13 @@ def test_slq_full_size_config2_properties(kra, gpu_ctx):
     np.testing.assert_allclose(q16, q128, rtol=1e-10)
     _, q_ref = slq_ref.slq_trace(A, 4, 30, seed=0)
     np.testing.assert_allclose(q128[:4], q_ref, rtol=RTOL)
+    # the plan: the largest P whose block fits ~160 MB, halved until a call has
+    # at least two sweeps (two sweep lanes overlap); the default equals P = 64
+    assert kra.slq_plan(D, 128, ctx=gpu_ctx) == 64
+    assert kra.slq_plan(D, 1024, ctx=gpu_ctx) == 128
+    assert kra.slq_plan(D, 20, ctx=gpu_ctx) == 16
+    _, _, qd = kra.slq_quadforms(D, 128, 30, seed=0, ctx=gpu_ctx)
+    np.testing.assert_allclose(qd, q128, rtol=1e-10)
 
 
 @pytest.mark.parametrize("block", [4, 16, 128])
