@@ -168,15 +168,24 @@ static std::vector<std::vector<double>> expm_device_batch(kt_context_s* ctx, int
         KT_HIP(launch_poly4(n, 1.0, U, c[4 * k], c[4 * k + 1], X1, c[4 * k + 2], X2, c[4 * k + 3], X3, T, st,
                             nb));
     }
-    for (int q = 0;; ++q) {  // squarings of the matrices with s > q (a prefix)
+    // squarings of the matrices with s > q (a prefix), ping-ponging between T
+    // and U: matrix k's result ends in T for even s_k, in U for odd
+    double* buf2[2] = {T, U};
+    for (int q = 0;; ++q) {
         int cnt = 0;
         while (cnt < nb && sv[ord[cnt]] > q) ++cnt;
         if (cnt == 0) break;
-        mm(T, T, U, cnt);
-        KT_HIP(hipMemcpyAsync(T, U, sizeof(double) * nn * cnt, hipMemcpyDeviceToDevice, st));
+        mm(buf2[q & 1], buf2[q & 1], buf2[(q + 1) & 1], cnt);
     }
     std::vector<double> Fh(bn);
-    KT_HIP(hipMemcpyAsync(Fh.data(), T, sizeof(double) * bn, hipMemcpyDeviceToHost, st));
+    for (int k = 0; k < nb;) {  // one read-back per run of equal parity
+        const int par = sv[ord[k]] & 1;
+        int e = k + 1;
+        while (e < nb && (sv[ord[e]] & 1) == par) ++e;
+        KT_HIP(hipMemcpyAsync(Fh.data() + k * nn, buf2[par] + k * nn, sizeof(double) * nn * (e - k),
+                              hipMemcpyDeviceToHost, st));
+        k = e;
+    }
     KT_HIP(hipStreamSynchronize(st));
     std::vector<std::vector<double>> out(nb);
     for (int k = 0; k < nb; ++k) out[ord[k]].assign(Fh.begin() + k * nn, Fh.begin() + (k + 1) * nn);
