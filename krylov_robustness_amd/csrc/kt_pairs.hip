@@ -1243,6 +1243,13 @@ __device__ __forceinline__ int group_lanes(int ne) {
 #ifndef KT_BLK_NEWTON
 #define KT_BLK_NEWTON 1
 #endif
+// shifts per lane per multisection round.  The eigenvalue phase is bound by
+// FP64 issue (a wave64 FMA takes 4 cycles; 2 waves per SIMD), not latency, so
+// fewer shifts with more rounds does less work: 1 beats 4 by 4 % end to end
+// on config 5 (profiles/r02_greedy_blk_ms.txt)
+#ifndef KT_BLK_MS
+#define KT_BLK_MS 1
+#endif
 
 // Eigenvalues k0 .. k0+ne-1 (ascending) of the block matrix by one wave:
 // g = group_lanes(ne) lanes per eigenvalue.  Multisection (MS interleaved
@@ -1329,8 +1336,9 @@ __device__ __forceinline__ double wave_multisect_blk(int j, const Blk2* B, int k
     // uncertified lane in the wave sends all of them back to the multisection
     // (measured: 2j = 80 at 4 waves per projection is 10 % slower with it)
     if (g >= 4) {
-    // multisection until every bracket is within span / 4096 (2 rounds at
-    // g = 16, 4 at g = 2), where Newton converges in ~4 steps
+    // multisection until every bracket is within span / 4096 (ceil(12 /
+    // log2(g MS + 1)) rounds: 3 at g = 16, MS = 1), where Newton converges in
+    // ~4 steps
     const double narrow = (hi - lo) * (1.0 / 4096.0);
     for (; round < 64; ++round) {
         if (!done && !(b - a > atol)) done = true;
@@ -1421,7 +1429,7 @@ __device__ double fused_xm_blk(int j, int fun, const double* rec /* [j][11] */, 
     const int ne = min(per, nn - k0);
     for (int e0 = 0; e0 < ne; e0 += 64) {  // more than 64 eigenvalues per wave: 64 at a time
         const int cnt = min(64, ne - e0);
-        const double lam = wave_multisect_blk<4>(j, blk + mat * j, k0 + e0, cnt);
+        const double lam = wave_multisect_blk<KT_BLK_MS>(j, blk + mat * j, k0 + e0, cnt);
         const int g = group_lanes(cnt);
         if (lane % g == 0 && lane / g < cnt) ev[mat * nn + k0 + e0 + lane / g] = lam;
     }
@@ -1805,8 +1813,8 @@ double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev
     const int ne = min(per, nn - k0);
     for (int e0 = 0; e0 < ne; e0 += 64) {
         const int cnt = min(64, ne - e0);
-        const double lam = mat == 0 ? wave_multisect_blk<4, true>(j, gblk, k0 + e0, cnt, t0)
-                                    : wave_multisect_blk<4, false>(j, gblk, k0 + e0, cnt);
+        const double lam = mat == 0 ? wave_multisect_blk<KT_BLK_MS, true>(j, gblk, k0 + e0, cnt, t0)
+                                    : wave_multisect_blk<KT_BLK_MS, false>(j, gblk, k0 + e0, cnt);
         const int g = group_lanes(cnt);
         if (lane % g == 0 && lane / g < cnt) ev[mat * nn + k0 + e0 + lane / g] = lam;
     }
