@@ -1250,6 +1250,20 @@ __device__ __forceinline__ int group_lanes(int ne) {
 #ifndef KT_BLK_MS
 #define KT_BLK_MS 1
 #endif
+// Waves per projection for the per-step eigenvalues (both the fused and the
+// register kernel, so they solve identically): KT_XM_WAVES_SMALL while each
+// wave still holds <= 16 eigenvalues (g >= 4 lanes each: the Newton path),
+// else half the workgroup.  Fewer waves issue fewer FP64 operations in total;
+// the others wait at the barrier (2 waves: config 5 -2-3 %,
+// profiles/r02_greedy_xm_waves.txt)
+#ifndef KT_XM_WAVES_SMALL
+#define KT_XM_WAVES_SMALL 2
+#endif
+__device__ __forceinline__ int xm_waves(int nn) {
+    constexpr int half = kFusedWaves / 2;
+    constexpr int small = KT_XM_WAVES_SMALL < half ? KT_XM_WAVES_SMALL : half;
+    return nn <= 16 * small ? small : half;
+}
 
 // Eigenvalues k0 .. k0+ne-1 (ascending) of the block matrix by one wave:
 // g = group_lanes(ne) lanes per eigenvalue.  Multisection (MS interleaved
@@ -1422,11 +1436,11 @@ __device__ double fused_xm_blk(int j, int fun, const double* rec /* [j][11] */, 
         blk[mat * j + k] = m;
     }
     __syncthreads();
-    constexpr int W = kFusedWaves / 2;
+    const int W = xm_waves(nn);  // waves per projection; the rest wait at the barrier
     const int mat = wave / W, wv = wave % W;
     const int per = (nn + W - 1) / W;
     const int k0 = wv * per;
-    const int ne = min(per, nn - k0);
+    const int ne = mat < 2 ? min(per, nn - k0) : 0;
     for (int e0 = 0; e0 < ne; e0 += 64) {  // more than 64 eigenvalues per wave: 64 at a time
         const int cnt = min(64, ne - e0);
         const double lam = wave_multisect_blk<KT_BLK_MS>(j, blk + mat * j, k0 + e0, cnt);
@@ -1806,11 +1820,11 @@ __device__ __noinline__
 double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nn = 2 * j;
-    constexpr int W = kFusedWaves / 2;
+    const int W = xm_waves(nn);  // waves per projection; the rest wait at the barrier
     const int mat = wave / W, wv = wave % W;
     const int per = (nn + W - 1) / W;
     const int k0 = wv * per;
-    const int ne = min(per, nn - k0);
+    const int ne = mat < 2 ? min(per, nn - k0) : 0;
     for (int e0 = 0; e0 < ne; e0 += 64) {
         const int cnt = min(64, ne - e0);
         const double lam = mat == 0 ? wave_multisect_blk<KT_BLK_MS, true>(j, gblk, k0 + e0, cnt, t0)
