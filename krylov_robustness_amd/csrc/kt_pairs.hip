@@ -1247,6 +1247,15 @@ __device__ __forceinline__ int group_lanes(int ne) {
 // FP64 issue (a wave64 FMA takes 4 cycles; 2 waves per SIMD), not latency, so
 // fewer shifts with more rounds does less work: 1 beats 4 by 4 % end to end
 // on config 5 (profiles/r02_greedy_blk_ms.txt)
+// Newton's last step is taken and the run ends once the step is below
+// KT_BLK_NEWTON_ACCEPT atol (2^20 atol ~ 5e-10 of the spectral radius: the
+// step's quadratic error is far below atol), then certified by the counts
+// at x -+ 8 atol as before -- a lane that fails goes on bisecting.  One
+// Newton count fewer per eigenvalue than at 64 atol: config 5 -1 %
+// (profiles/r02_greedy_newton_accept.txt)
+#ifndef KT_BLK_NEWTON_ACCEPT
+#define KT_BLK_NEWTON_ACCEPT 1048576
+#endif
 #ifndef KT_BLK_MS
 #define KT_BLK_MS 1
 #endif
@@ -1271,7 +1280,7 @@ __device__ __forceinline__ int xm_waves(int nn) {
 // every bracket is span/4096 wide a safeguarded Newton iteration
 // on det(M - xI) (block_count_newton; a step leaving the count bracket is a
 // bisection) converges in ~4 steps, and is accepted once its step is below
-// 64 atol AND the counts at x -+ 8 atol bracket lambda_k (certified to
+// KT_BLK_NEWTON_ACCEPT atol AND the counts at x -+ 8 atol bracket lambda_k (certified to
 // 8 atol = 3.5e-15 of the spectral radius).  Lanes whose Newton run is not
 // certified (~1 % on the greedy projections, tests/test_block_sturm.py)
 // continue the multisection to 2 ulp of the spectral radius (as before:
@@ -1371,7 +1380,7 @@ __device__ __forceinline__ double wave_multisect_blk(int j, const Blk2* B, int k
             else a = x;
             const double xn = x - 1.0 / S;  // S = 0 or inf: xn is not finite / = x
             const bool inb = xn >= a && xn <= b;
-            if (fabs(xn - x) <= 64.0 * atol || !(b - a > atol)) {
+            if (fabs(xn - x) <= (double)KT_BLK_NEWTON_ACCEPT * atol || !(b - a > atol)) {
                 conv = true;
                 if (inb) x = xn;
             } else {
