@@ -1243,10 +1243,6 @@ __device__ __forceinline__ int group_lanes(int ne) {
 #ifndef KT_BLK_NEWTON
 #define KT_BLK_NEWTON 1
 #endif
-// shifts per lane per multisection round.  The eigenvalue phase is bound by
-// FP64 issue (a wave64 FMA takes 4 cycles; 2 waves per SIMD), not latency, so
-// fewer shifts with more rounds does less work: 1 beats 4 by 4 % end to end
-// on config 5 (profiles/r02_greedy_blk_ms.txt)
 // Newton's last step is taken and the run ends once the step is below
 // KT_BLK_NEWTON_ACCEPT atol (2^20 atol ~ 5e-10 of the spectral radius: the
 // step's quadratic error is far below atol), then certified by the counts
@@ -1256,6 +1252,10 @@ __device__ __forceinline__ int group_lanes(int ne) {
 #ifndef KT_BLK_NEWTON_ACCEPT
 #define KT_BLK_NEWTON_ACCEPT 1048576
 #endif
+// shifts per lane per multisection round.  The eigenvalue phase is bound by
+// FP64 issue (a wave64 FMA takes 4 cycles; 2 waves per SIMD), not latency, so
+// fewer shifts with more rounds does less work: 1 beats 4 by 4 % end to end
+// on config 5 (profiles/r02_greedy_blk_ms.txt)
 #ifndef KT_BLK_MS
 #define KT_BLK_MS 1
 #endif
