@@ -20,6 +20,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -36,8 +38,11 @@ def parse():
     ap.add_argument("--nprobes", type=int, default=None)
     ap.add_argument("--m", "--lanczos-m", dest="m", type=int, default=30)
     ap.add_argument("--block", type=int, default=0, help="probes per SpMM sweep (0 = auto)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="CPU-baseline time budget (rank 0, N=1 only); 0 disables")
+    ap.add_argument("--cpu-seconds", type=float, default=30.0,
+                    help="CPU-baseline time budget (rank 0, N=1 only; stops earlier once half an "
+                         "evaluation's probes are done); 0 disables")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline OpenMP threads (0 = every CPU this process may use)")
     ap.add_argument("--lanes", type=int, default=0,
                     help="probe sweeps in flight on separate HIP streams (KT_SLQ_LANES, 1..4; "
                          "0 = the library default: 2 for the y-form pass, 3 for the explicit sweep)")
@@ -60,20 +65,55 @@ def make_graph(config):
         "erdos_renyi n=100k nnz~1M (BASELINE configs[1])"
 
 
-def cpu_baseline(A, m, budget_s, nprobes_eval):
+def cpu_share():
+    """CPUs this process may actually use: the affinity mask, capped by the
+    cgroup CPU quota when one is set (cgroup v2 cpu.max, v1 cfs_quota_us).
+    Returns (cpus, detail)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as f:
+                txt = f.read().strip()
+        except OSError:
+            continue
+        if parse is not None:
+            q, per = (parse(txt) + ["100000"])[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+        else:
+            q = int(txt)
+            if q > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    quota = q / int(f.read().strip())
+        break
+    cpus = aff if quota is None else max(1, min(aff, int(math.floor(quota + 1e-9))))
+    return cpus, {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "host_cpus": os.cpu_count(),
+                  "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(A, m, budget_s, nprobes_eval, threads=0):
     """Time the C restatement (oracle/slq_ref.c, OpenMP over probes) on a
-    bounded sample of the same workload; extrapolate to evals/s."""
+    bounded sample of the same workload (at least half an evaluation's probes
+    unless the time budget runs out first); extrapolate to evals/s.  Threads:
+    every CPU the process may use (cpu_share) unless given."""
     from oracle import slq_ref
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    share, detail = cpu_share()
+    threads = int(threads) or share
     slq_ref.load()
     done = 0
     t0 = time.perf_counter()
     batch = threads
+    target = max(1, nprobes_eval // 2)
     while True:
         slq_ref.slq_trace(A, batch, m, seed=12345, probe_offset=done, nthreads=threads)
         done += batch
         el = time.perf_counter() - t0
-        if el >= budget_s or done >= nprobes_eval:
+        if el >= budget_s or done >= target:
             break
     probes_per_s = done / el
     model = None
@@ -83,9 +123,10 @@ def cpu_baseline(A, m, budget_s, nprobes_eval):
     except OSError:
         pass
     return {"value": probes_per_s / nprobes_eval, "unit": "evals/s", "cores": threads,
-            "kind": "port", "cpu_model": model, "host_cpus": os.cpu_count(),
+            "kind": "port", "cpu_model": model, **detail,
             "sample": f"{done} of the {nprobes_eval} probes of one evaluation (m={m}) in "
-                      f"{el:.1f} s with {threads} OpenMP threads, extrapolated"}
+                      f"{el:.1f} s with {threads} OpenMP threads (every CPU this process may use: "
+                      f"affinity mask capped by the cgroup quota), extrapolated"}
 
 
 def _kernel_template_args(name):
@@ -137,7 +178,11 @@ def main():
     rank, world, local_rank = kdist.env_rank()
     if os.environ.get("KT_BENCH_ONE_DEVICE") == "1":  # rehearsal: every rank on GPU 0
         local_rank = 0
-    if world > 1:
+    # a process group whenever torchrun launched us -- at world 1 too, so the
+    # RCCL init and the all-reduce run inside the process that holds
+    # libkrylov_hip.so's streams exactly as at N > 1
+    use_pg = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    if use_pg:
         torch.cuda.set_device(local_rank)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world,
@@ -160,11 +205,11 @@ def main():
 
     def step(seed):
         s1, s2, _ = kra.slq_quadforms(D, cnt, m, seed=seed, probe_offset=off, block=P, ctx=ctx)
-        s1, s2 = kdist.allreduce_sums([s1, s2], device=coll_dev)
-        return s1 / N, s2
+        s1, s2 = kdist.allreduce_sums([s1, s2], device=coll_dev, force=use_pg)
+        return s1, s2
 
     def barrier():
-        if world > 1:
+        if use_pg:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
@@ -175,14 +220,19 @@ def main():
         ctx.profile(True)
     barrier()
     t0 = time.perf_counter()
-    tr = None
+    sums = None
     for s in range(args.steps):
-        tr, _ = step(s)
+        sums = step(s)
     barrier()
     el = time.perf_counter() - t0
     if not args.no_profile:
         ctx.profile(False)
-    el_max = kdist.allreduce_max(el, device=coll_dev)
+    el_max = kdist.allreduce_max(el, device=coll_dev, force=use_pg)
+    # plain Hutchinson over N probes: estimate = mean q, standard error from
+    # the sample variance of the N quadratic forms (sum q, sum q^2)
+    tr = sums[0] / N
+    var = max(sums[1] - N * tr * tr, 0.0) / (N - 1) if N > 1 else float("nan")
+    tr_stderr = math.sqrt(var / N) if N > 1 else None
     k1_overlapped = None
     timed = None
     if not args.no_profile:
@@ -211,9 +261,18 @@ def main():
     # charged the whole step although its K2 streams two of them.
     kbase = "k_spmm_dot" if args.explicit else "k_spmm_lanczos"
     kname = f"{kbase}<{P}"
-    k1_bytes = 12 * nnz + 4 * (n + 1) + 24 * n * P
+    # SURVEY's per-unit figure charges fp64 values + int32 columns (12 B per
+    # nonzero).  A unit-weight matrix (every stored value 1.0, detected when
+    # the device matrix is created) never reads the values: its kernels'
+    # compulsory CSR bytes are 4 B per nonzero, and that is the figure the
+    # roofline fraction uses (the SURVEY figure is kept beside it, labelled).
+    unit = bool(A.nnz) and bool(np.all(A.data == 1.0))
+    per_nnz = 4 if unit else 12
+    k1_bytes_survey = 12 * nnz + 4 * (n + 1) + 24 * n * P
+    k1_bytes = per_nnz * nnz + 4 * (n + 1) + 24 * n * P
     sweeps = math.ceil(cnt / P)
-    b_eval_rank = m * (sweeps * (12 * nnz + 4 * (n + 1)) + 24 * n * cnt)
+    b_eval_rank = m * (sweeps * (per_nnz * nnz + 4 * (n + 1)) + 24 * n * cnt)
+    b_eval_rank_survey = m * (sweeps * (12 * nnz + 4 * (n + 1)) + 24 * n * cnt)
     roof = None
     extra = {}
     if not args.no_profile:
@@ -232,6 +291,11 @@ def main():
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": kname + ">", "avg_launch_us": round(k1_ms * 1e3, 2),
                     "launches": tl, "algorithmic_bytes_per_launch": k1_bytes,
+                    "algorithmic_bytes_basis": ("unit-weight matrix: 4 nnz (int32 columns; values "
+                                                "never read) + 4 (n+1) + 24 n P" if unit else
+                                                "12 nnz + 4 (n+1) + 24 n P"),
+                    "survey_bytes_per_launch": k1_bytes_survey,
+                    "survey_frac": round(k1_bytes_survey / (k1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "measured": "HIP events around every launch of the kernel in the timed region, "
                                 "on each sweep lane's stream; avg_launch_us = union of their intervals "
                                 "(time with >= 1 launch in flight, lane overlap counted once) / launches",
@@ -256,11 +320,15 @@ def main():
     extra["yform_redone_sweeps"] = ctx.yform_redone()
     eval_gbs = b_eval_rank / (ms_per_step * 1e-3) / 1e9
     extra["eval_roofline"] = {"B_eval_bytes_per_rank": b_eval_rank, "achieved_GBs_per_rank":
-                              round(eval_gbs, 1), "frac": round(eval_gbs / HBM_PEAK_GBS, 4)}
+                              round(eval_gbs, 1), "frac": round(eval_gbs / HBM_PEAK_GBS, 4),
+                              "B_eval_bytes_per_rank_survey": b_eval_rank_survey,
+                              "unit_weight_matrix": unit}
+    extra["collective"] = (f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all_reduce of "
+                           f"(sum q, sum q^2) per evaluation" if use_pg else None)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(A, m, args.cpu_seconds, N)
+        cpu = cpu_baseline(A, m, args.cpu_seconds, N, args.cpu_threads)
 
     if rank == 0:
         out = {
@@ -271,10 +339,14 @@ def main():
             "config": {"workload": wl, "n": n, "nnz": nnz, "probes_per_eval": N, "lanczos_m": m,
                        "probes_per_sweep": P, "sweep_lanes": args.lanes, "fun": "exp",
                        "parallelism": f"probes sharded x{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "trace_estimate": tr, **extra,
+            "roofline": roof, "cpu_baseline": cpu, "trace_estimate": tr,
+            "trace_stderr": tr_stderr,
+            "trace_stderr_basis": f"sample standard deviation of the {N} per-probe quadratic "
+                                  f"forms / sqrt({N}) (plain Hutchinson)",
+            **extra,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -164,7 +164,9 @@ typedef int (*kt_reduce_fn)(double* buf, int64_t count, void* user);
  * count = 10) and summed in column order, so every rank returns the same
  * tr / res / it.  KT_AFUN_EXPMV is computed replicated (its Taylor degree is
  * chosen per block, expmv.m:41) and never calls `allreduce`.  Replaces
- * mc_trace.m:1-63 on a multi-GPU node; world = 1 equals kt_mc_trace. */
+ * mc_trace.m:1-63 on a multi-GPU node; world = 1 equals kt_mc_trace (with a
+ * non-NULL `allreduce` the round sums still pass through it, bit-identically;
+ * `allreduce` may be NULL only at world = 1). */
 int kt_mc_trace_sharded(kt_matrix_t A, int afun, int fun, int m, double tol, int maxit,
                         int isAreal, uint64_t seed, int rank, int world, kt_reduce_fn allreduce,
                         void* user, double* tr, double* res, int* it);
@@ -296,7 +298,10 @@ int kt_profile_busy(kt_context_t ctx, int kernel, double* busy_ms);
 /* Hot-path statistics.  stat 0: kt_slq_trace sweeps whose y-form probe
  * Lanczos tripped the cancellation guard (a lucky breakdown, or a beta^2
  * below 1e-4 ||A v||^2) and were recomputed by the explicit CGS2 sweep,
- * counted since context creation. */
+ * counted since context creation.  stat 1: fun_update runs (kt_fun_update,
+ * kt_fun_and_grad_krylov_*) that took the dense fallback of fun_update.m:85-90,
+ * since context creation.  stat 2: the projected size (basis columns) of the
+ * last fun_update run on this context (n when it went dense). */
 int kt_context_stat(kt_context_t ctx, int stat, int64_t* value);
 
 #ifdef __cplusplus

@@ -66,9 +66,18 @@ class Context:
     def yform_redone(self) -> int:
         """Sweeps of the y-form hot path recomputed by the explicit CGS2 sweep
         (cancellation guard / lucky breakdown), since context creation."""
+        return self.stat(0)
+
+    def stat(self, which: int) -> int:
+        """kt_context_stat: 0 y-form sweeps redone, 1 fun_update dense
+        fallbacks, 2 basis columns of the last fun_update."""
         v = C.c_int64()
-        _lib.check(_lib.load().kt_context_stat(self._h, 0, C.byref(v)))
+        _lib.check(_lib.load().kt_context_stat(self._h, int(which), C.byref(v)))
         return int(v.value)
+
+    def fun_update_stats(self):
+        """(dense fallbacks so far, projected size of the last fun_update)."""
+        return self.stat(1), self.stat(2)
 
 
 _default_ctx: Optional[Context] = None

@@ -576,6 +576,11 @@ bool greedy_steps_device(kt_matrix_s* A, int k, int64_t Q, const std::vector<int
     const DevCSR& M0 = natural_csr(A);
     const int64_t nnz0 = A->nnz;
     if (!pair_reg_applies((int)n, nnz0, it, M0.n_long, A->unit_values)) return false;
+    // k_greedy_edit keeps the long-row list in its previous order, a host
+    // rebuild re-sorts it heaviest first; with more long rows than k_pair_reg
+    // hands to whole waves an edit could change which rows those are, and the
+    // device loop would no longer form the host loop's sums: host loop
+    if (M0.n_long > kRegLongCap) return false;
     const int nl0 = std::max(M0.n_long, 1);
     // device state: two CSR sets {rp, ci, va, lr, dyn}, the ranking, the picks
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -646,12 +651,19 @@ bool greedy_steps_device(kt_matrix_s* A, int k, int64_t Q, const std::vector<int
     KT_HIP(hipMemcpyAsync(hv, dselv, sizeof(double) * k, hipMemcpyDeviceToHost, st));
     KT_HIP(hipMemcpyAsync(hs, dsel, sizeof(int) * 2 * k, hipMemcpyDeviceToHost, st));
     KT_HIP(hipStreamSynchronize(st));
-    std::vector<int64_t> ei(k), ej(k);
+    std::vector<int64_t> ei, ej;
+    ei.reserve(k);
+    ej.reserve(k);
     double total = 0.0;
     for (int s = 0; s < k; ++s) {
-        if (hs[2 * s] < 0) fail(KT_ERR_ARG, "KRYLOV_MIOBI:: no finite candidate score");
-        ei[s] = hs[2 * s];
-        ej[s] = hs[2 * s + 1];
+        if (hs[2 * s] < 0) {
+            // the host loop (and the reference) had already deleted the edges
+            // of steps 0..s-1 when step s found no finite score: leave A so
+            if (!ei.empty()) set_pairs(A, (int64_t)ei.size(), ei.data(), ej.data(), 0.0);
+            fail(KT_ERR_ARG, "KRYLOV_MIOBI:: no finite candidate score");
+        }
+        ei.push_back(hs[2 * s]);
+        ej.push_back(hs[2 * s + 1]);
         if (sel_i) sel_i[s] = ei[s];
         if (sel_j) sel_j[s] = ej[s];
         total += hv[s];

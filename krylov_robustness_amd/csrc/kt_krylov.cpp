@@ -766,6 +766,8 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
             res.iter = j;
             res.lucky = Ar.lucky;
             res.dense = true;
+            ctx->fu_dense++;
+            ctx->fu_last_cols = n;
             return res;
         }
         const int nn = Ar.Hr - rk;                                           // :93
@@ -801,6 +803,7 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
     if (j > it) j = it;
     res.iter = j;
     res.lucky = Ar.lucky;
+    ctx->fu_last_cols = res.nx;
     return res;
 }
 
@@ -1147,6 +1150,7 @@ int kt_fun_and_grad_krylov_fun(kt_matrix_t A, int64_t nom, const double* X, cons
         th.join();
         if (terr.code == KT_ERR_ALLOC) {  // the twin's workspace did not fit: serial order
             (void)hipGetLastError();
+            A2->ctx->pool.clear();  // its idle scratch blocks back to the device
             KT_HIP(hipSetDevice(A->ctx->device));
             serial = true;
         } else if (terr.code != KT_OK) {

@@ -42,6 +42,10 @@ hipError_t launch_pair_fused(int C, int n, int64_t nnz, const CsrView& A, bool u
 // device-resident greedy steps (kt_greedy.cpp): k_pair_reg with the CSR's
 // {nnz, n_long} read from dyn (the LDS sized for nnz_max), and one step's
 // selection + ranking update + edge deletion into the other CSR buffer
+// k_pair_reg: the first kRegLongCap long rows (degree > long_thresh, in the
+// CSR's long-row list order) are summed by whole waves, the rest by their
+// owning threads -- so the list order is part of the kernel's arithmetic
+constexpr int kRegLongCap = 256;
 bool pair_reg_applies(int n, int64_t nnz, int it, int n_long, bool unit);
 hipError_t launch_pair_reg_dyn(int C, int n, int64_t nnz_max, const CsrView& A, bool unit, const int* ii,
                                const int* jj, const double* B, int it, int fun, double tol, double* state,

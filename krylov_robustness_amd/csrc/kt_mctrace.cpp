@@ -552,7 +552,11 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
         // tr += trace(Q' Afun_it(Q)) = sum quadforms of P_1..P_{it-1} Q          :46
         copy_cols(ctx, n, Y.col(0), ld, Z.col(0), ld, mb);
         for (int q = (int)Qs.size() - 1; q >= 0; --q) project(ctx, n, Qs[q].col(0), ld, mb, Z.col(0), mb);
-        const bool split = !(sh.world > 1 && F.kind != AFUN_EXPMV);  // the G term is local
+        // G columns dealt over the ranks whenever the caller supplied the
+        // all-reduce (at world 1 too: rank 0 takes every column, the sums
+        // still travel through the collective); expmv stays replicated
+        const bool sharded = sh.allreduce != nullptr && F.kind != AFUN_EXPMV;
+        const bool split = !sharded;  // the G term is local
         kt_matrix_s* A2 = split ? twin_of(A) : nullptr;
         if (!A2) tr += F.trace_quad(Z.col(0), ld, mb);
         Qs.emplace_back();                                                         // :47-48
@@ -592,9 +596,19 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
                 throw;
             }
             th.join();
-            if (gerr.code != KT_OK) throw gerr;
+            if (gerr.code == KT_ERR_ALLOC) {
+                // the twin's workspace did not fit: give its idle blocks back
+                // and run the G term in the serial order on A (as
+                // fun_and_grad_krylov_fun does, kt_krylov.cpp)
+                (void)hipGetLastError();
+                A2->ctx->pool.clear();
+                KT_HIP(hipSetDevice(ctx->device));
+                gsum = F.trace_quad(Zg.col(0), ld, mb);
+            } else if (gerr.code != KT_OK) {
+                throw gerr;
+            }
             tr += qsum;
-        } else if (sh.world > 1 && F.kind != AFUN_EXPMV) {
+        } else if (sharded) {
             std::vector<double> qv(mb, 0.0), qm;
             int nm = 0;
             for (int c = sh.rank; c < mb; c += sh.world) copy_cols(ctx, n, Z.col(c), ld, Y.col(nm++), ld, 1);

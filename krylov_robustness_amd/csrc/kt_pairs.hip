@@ -1638,7 +1638,7 @@ size_t pair_fused_lds_bytes(int it) {
 // rows lane-strided + wave_sum64); the two kernels agree to rounding (the
 // compiler contracts a few products into FMAs differently).
 // ---------------------------------------------------------------------------
-constexpr int kRegLongCap = 256;  // long rows (degree > long_thresh) handled by whole waves
+// kRegLongCap (kt_launch.h): long rows handled by whole waves
 
 // fixed-order workgroup sum, one barrier: `red` alternates between two halves
 // (a wave cannot run two reductions ahead of a slower one: each has a barrier)

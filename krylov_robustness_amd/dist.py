@@ -23,21 +23,31 @@ def env_rank():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def allreduce_sums(vals, device=None):
+def _group_ready(force: bool) -> bool:
+    """Issue the collective?  Always with more than one rank; at world 1 only
+    when `force` is set and a process group exists (exercises RCCL init and
+    the collective inside a process that holds libkrylov_hip.so's streams)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size() > 1 or bool(force)
+
+
+def allreduce_sums(vals, device=None, force: bool = False):
     """Sum a short list of doubles over the default process group."""
     import torch
     import torch.distributed as dist
     t = torch.tensor(list(vals), dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _group_ready(force):
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(x) for x in t.cpu().tolist()]
 
 
-def allreduce_max(val: float, device=None):
+def allreduce_max(val: float, device=None, force: bool = False):
     import torch
     import torch.distributed as dist
     t = torch.tensor([float(val)], dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _group_ready(force):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -111,13 +121,15 @@ def reduce_callback(group=None, fail_on_rank=None):
 
 
 def mc_trace_sharded(Afun, n=None, tol=1e-3, maxit=10, isAreal=0, debug=0, seed=0, fun="exp",
-                     m=30, A=None, rank=None, world=None, allreduce=None, group=None, ctx=None):
+                     m=30, A=None, rank=None, world=None, allreduce=None, group=None, ctx=None,
+                     force=False):
     """[tr, res, it] = mc_trace(...) on `world` GPUs: every
     rank recomputes S, Q and tr(Q' Afun Q) from the shared seed, the G-probe
     columns are dealt round-robin and their quadratic forms summed by one
     all-reduce per round (kt_mc_trace_sharded).  Afun as in core.mc_trace.
     rank / world default to the torch.distributed group; `allreduce` is a
-    _lib.REDUCE_FN (default: reduce_callback(group))."""
+    _lib.REDUCE_FN (default: reduce_callback(group); at world 1 none unless
+    `force`, which routes the round sums through the group's all-reduce)."""
     import ctypes as C
     from . import _lib
     from .core import _dev
@@ -135,7 +147,7 @@ def mc_trace_sharded(Afun, n=None, tol=1e-3, maxit=10, isAreal=0, debug=0, seed=
         D = _dev(Afun, ctx)
     if n is not None and int(n) != D.n:
         raise _lib.KrylovError(_lib.KT_ERR_ARG, "n does not match the matrix")
-    cb = allreduce if allreduce is not None else (reduce_callback(group) if world > 1
+    cb = allreduce if allreduce is not None else (reduce_callback(group) if world > 1 or force
                                                   else _lib.REDUCE_FN(0))
     tr, res, it = C.c_double(), C.c_double(), C.c_int()
     _lib.check(_lib.load().kt_mc_trace_sharded(

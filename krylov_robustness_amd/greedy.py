@@ -264,14 +264,17 @@ def greedy_krylov(A, k, Q=0, centrality=None, order="mult", tol=1e-12, it=None, 
     if (S != S.T).nnz:  # :27-29
         raise _lib.KrylovError(_lib.KT_ERR_NOT_HERMITIAN, "GREEDY_KRYLOV:: Adjacency matrix should be symmetric")
     if not Q:
-        Q = int(np.asarray(S.sum(axis=0)).max())  # :42-44
+        # :42-44 Q = max(sum(A, 1)); top_edges(1:Q, :) indexes floor(Q) rows, so
+        # a weighted graph whose largest weighted degree is below 1 gives Q = 0,
+        # an empty E, and krylov_miobi then scores every edge (krylov_miobi.m:43-46)
+        Q = int(np.floor(np.asarray(S.sum(axis=0)).max()))
     if miobi == "break" and S.nnz < 2 * k:  # :54-56
         raise _lib.KrylovError(_lib.KT_ERR_ARG, "GREEDY_KRYLOV:: edges to be removed are more than edges in the network")
     if centrality is None:
         centrality = compute_centrality(D, "eig", ctx=ctx)
     top = (find_top_missing_edges(S, centrality, Q + k, order) if miobi == "make"
            else find_top_edges(S, centrality, Q + k, order))  # :82 (first step)
-    if len(top) >= int(k) > 0:
+    if len(top) >= int(k) > 0 and int(Q) >= 1:
         # the step loop in the library (kt_greedy_krylov_steps): krylov_miobi(A, 1,
         # top(1:Q)) per step, the selected pair dropped from the ranking (:84-89)
         T = np.asarray(top, dtype=np.int64).reshape(-1, 2)
@@ -293,8 +296,8 @@ def greedy_krylov(A, k, Q=0, centrality=None, order="mult", tol=1e-12, it=None, 
     for j in range(int(k)):  # :64-93
         if j > 0:  # drop the previously selected edge from the search space
             hit = np.flatnonzero(np.all(top == last, axis=1))
-            if len(hit):
-                top = np.delete(top, hit[0], axis=0)
+            # :84-86; with no match [1 : ind-1, ind+1 : n] is empty and so is top_edges
+            top = np.delete(top, hit[0], axis=0) if len(hit) else top[:0]
         E = top[:Q]
         tmp_edges, tmp_rob, D = krylov_miobi(D, 1, E, tol, it, poles, debug, miobi, rescale)
         edges = np.vstack([edges, tmp_edges])

@@ -829,7 +829,14 @@ def exact_trace_update(A, U, B, fun="exp"):
 def krylov_miobi(A, k, E, tol=1e-12, it=None, poles=np.inf, debug=0, miobi="break", rescale=1.0):
     """krylov_miobi.m:1-142 (E 1-based, E(j,1) >= E(j,2); poles unused there too)."""
     A = sp.csr_matrix(A, dtype=np.float64).copy()
-    E = np.asarray(E, dtype=np.int64).copy()
+    if E is None or len(E) == 0:                          # :43-46 [tmp1, tmp2] = find(A), tmp1 >= tmp2
+        C = sp.csc_matrix(A)
+        C.sort_indices()
+        cols = np.repeat(np.arange(C.shape[1]), np.diff(C.indptr))   # find(): column-major
+        rows = C.indices
+        keep = (rows >= cols) & (C.data != 0)
+        E = np.stack([rows[keep], cols[keep]], axis=1) + 1
+    E = np.asarray(E, dtype=np.int64).reshape(-1, 2).copy()
     n = A.shape[0]
     if it is None:
         it = min(100, n)
@@ -917,14 +924,18 @@ def greedy_krylov(A, k, Q, centrality, order="mult", tol=1e-12, it=None, poles=n
     rob = 0.0
     top = None
     tmp_edges = None
+    if not Q:                                             # :42-44 Q = max(sum(A, 1))
+        Q = float(np.asarray(sp.csr_matrix(A).sum(axis=0)).max())
+    Qi = int(np.floor(Q))                                 # 1:Q indexes floor(Q) rows
     for j in range(k):
         if j == 0:
-            top = (find_top_edges(A, centrality, Q + k, order) if miobi == "break"
-                   else find_top_missing_edges_min(A, centrality, Q + k))
+            top = (find_top_edges(A, centrality, Qi + k, order) if miobi == "break"
+                   else find_top_missing_edges_min(A, centrality, Qi + k))
         else:
             hit = [h for h in range(len(top)) if tuple(top[h]) == tuple(tmp_edges[0])]
-            top = np.delete(top, hit[0], axis=0)
-        E = top[:Q]
+            # :84-86 with no match, [1 : ind-1, ind+1 : n] is empty: top_edges empties
+            top = np.delete(top, hit[0], axis=0) if hit else top[:0]
+        E = top[:Qi]
         tmp_edges, tmp_rob, A = krylov_miobi(A, 1, E, tol, it, poles, debug, miobi, rescale)
         edges = np.vstack([edges, tmp_edges])
         rob += tmp_rob

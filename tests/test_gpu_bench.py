@@ -45,9 +45,24 @@ def test_bench_single_process_line():
     assert roof["avg_launch_us"] <= roof["timed_region_avg_launch_us_overlapped"] * 1.001
     assert roof["timed_region_busy_ms"] <= d["steps"] * d["ms_per_step"] * 1.01
     assert roof["isolated_pass"]["avg_launch_us"] > 0 and roof["isolated_pass"]["launches"] > 0
+    # unit-weight graph: the roofline is priced on the bytes the kernel must
+    # move (4 B per nonzero, values never read), SURVEY's 12 B figure beside it
+    n, nnz, P = d["config"]["n"], d["config"]["nnz"], d["config"]["probes_per_sweep"]
+    assert d["eval_roofline"]["unit_weight_matrix"] is True
+    assert roof["algorithmic_bytes_per_launch"] == 4 * nnz + 4 * (n + 1) + 24 * n * P
+    assert roof["survey_bytes_per_launch"] == 12 * nnz + 4 * (n + 1) + 24 * n * P
+    assert roof["survey_frac"] > roof["frac"]
+    # the estimator's standard error from sum q^2
+    assert d["trace_stderr"] is not None and 0 < d["trace_stderr"] < abs(d["trace_estimate"])
     cpu = d["cpu_baseline"]
     assert cpu["kind"] == "port" and cpu["value"] > 0 and cpu["cores"] >= 1
+    # every CPU the process may use: the affinity mask, capped by the cgroup quota
+    sys.path.insert(0, ROOT)
+    import bench
+    assert cpu["cores"] == bench.cpu_share()[0]
+    assert cpu["affinity_cpus"] >= cpu["cores"]
     assert d["yform_redone_sweeps"] == 0
+    assert d["collective"] is None  # single process, no torchrun: no process group
 
 
 def test_bench_two_ranks_one_gpu_gloo():
@@ -62,3 +77,45 @@ def test_bench_two_ranks_one_gpu_gloo():
     d = lines[0]
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "probes sharded x2"
     assert d["cpu_baseline"] is None and d["value"] > 0
+
+
+def test_bench_world1_torchrun_rccl():
+    """torchrun with ONE rank and the nccl (RCCL) backend: the process group is
+    initialised (device_id bound before any library call) and the per-evaluation
+    all-reduce of (sum q, sum q^2) and the max-over-ranks time run through RCCL
+    at world 1 -- RCCL init coexisting with libkrylov_hip.so's streams, the
+    launch the driver uses at N > 1 minus the peers."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", *SMALL, "--dist-backend", "nccl", "--cpu-seconds", "0"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 1 and d["collective"].startswith("RCCL all_reduce")
+    assert d["value"] > 0 and d["roofline"]["avg_launch_us"] > 0
+    # same probes, same estimate as the single-process line (the collective is a sum of one)
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, "--cpu-seconds", "0",
+                         "--no-profile"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r1.returncode == 0, r1.stderr[-2000:]
+    d1 = _json_lines(r1.stdout)[0]
+    assert d["trace_estimate"] == d1["trace_estimate"]
+    assert d["trace_stderr"] == d1["trace_stderr"]
+
+
+def test_mc_trace_sharded_rccl_world1():
+    """kt_mc_trace_sharded with dist.reduce_callback on device tensors over an
+    RCCL group of one rank (tests/rccl_world1_worker.py under torchrun): the
+    G-term sums of every round travel through RCCL's all-reduce, and the
+    estimate, residual and round count are bit-identical to kt_mc_trace."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", "29535",
+           os.path.join(ROOT, "tests", "rccl_world1_worker.py")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_lines(r.stdout)[-1]
+    assert d["backend"] == "nccl" and d["callback_calls"] >= 1
+    assert d["sharded"] == d["single"]

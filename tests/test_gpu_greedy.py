@@ -351,3 +351,44 @@ def test_greedy_device_loop_matches_host_loop(kra, gpu_ctx, monkeypatch):
     np.testing.assert_array_equal(e1, e2)
     assert r1 == r2
     assert (abs(D1.to_scipy() - D2.to_scipy()) > 0).nnz == 0
+
+
+def test_greedy_krylov_weighted_q_below_one_scores_every_edge(kra, gpu_ctx):
+    """greedy_krylov.m:42-44 sets Q = max(sum(A, 1)); on a weighted graph whose
+    largest weighted degree is below 1, top_edges(1:Q, :) (:88) is empty and
+    krylov_miobi.m:43-46 then scores EVERY edge (find(A), E(:,1) >= E(:,2)).
+    The device path takes the per-step host loop there (the library's step
+    loop needs Q >= 1) and must select what the oracle selects."""
+    A = load_graph("austria")                       # n = 149 > 130: Lanczos path
+    A = (A * (0.9 / np.asarray(A.sum(axis=0)).max())).tocsr()
+    assert np.asarray(A.sum(axis=0)).max() < 1
+    c = kra.compute_centrality(A)
+    tol = 1e-10
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    edges, rob, D2 = kra.greedy_krylov(D, 2, 0, c, "min", tol, 60, ctx=gpu_ctx)
+    eo, ro, Ao = ko.greedy_krylov(A, 2, 0, c, "min", tol, 60)
+    np.testing.assert_array_equal(edges, eo)
+    assert rob == pytest.approx(ro, rel=1e-7, abs=1e-12)
+    assert (abs(D2.to_scipy() - sp.csc_matrix(Ao)) > 0).nnz == 0
+
+
+@pytest.mark.parametrize("name", ["hub", "dense"])
+def test_greedy_device_loop_matches_host_loop_long_rows(kra, gpu_ctx, monkeypatch, name):
+    """Device-queued greedy steps vs the host loop on graphs with rows longer
+    than 64: 'hub' (a weighted scale-free graph, a few long rows: the device
+    loop runs, its edits keep the long-row list that k_pair_reg sums by whole
+    waves) and 'dense' (more long rows than k_pair_reg's wave list holds: an
+    edit could change which rows get a wave, so the library runs the host
+    loop).  Same edges, bit-equal variation, the same A_new."""
+    A = _reg_graphs(kra)[name]
+    c = kra.compute_centrality(A)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    tol = kra.default_greedy_tol(D, ctx=gpu_ctx)
+    monkeypatch.setenv("KT_GREEDY_DEVICE", "1")
+    e1, r1, D1 = kra.greedy_krylov(D, 6, 60, c, "min", tol, 100, np.inf, 0, "break", ctx=gpu_ctx)
+    monkeypatch.setenv("KT_GREEDY_DEVICE", "0")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    e2, r2, D2 = kra.greedy_krylov(D, 6, 60, c, "min", tol, 100, np.inf, 0, "break", ctx=gpu_ctx)
+    np.testing.assert_array_equal(e1, e2)
+    assert r1 == r2
+    assert (abs(D1.to_scipy() - D2.to_scipy()) > 0).nnz == 0
