@@ -126,6 +126,13 @@ void gram(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const 
     std::memcpy(G.data(), pb.ptr, sizeof(double) * G.size());
 }
 
+// KT_GEMM_ROCBLAS=1: gram / combine through rocBLAS dgemm (the A/B switch of
+// kt_gemm_ts.hip); read per call
+static bool rocblas_gemm_path() {
+    const char* e = getenv("KT_GEMM_ROCBLAS");
+    return e && e[0] == '1';
+}
+
 const double* gram_device(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* Y,
                           int ldy, int py) {
     DevBuf& d = ctx->ws.small;
@@ -136,6 +143,12 @@ const double* gram_device(kt_context_s* ctx, int64_t n, const double* X, int ldx
     }
     const double one = 1.0, zero = 0.0;
     const int64_t count = (int64_t)px * py;
+    if (!rocblas_gemm_path()) {  // kt_gemm_ts.hip: MFMA row-chunk partials + fixed-order slab sum
+        const int S = gram_ts_chunks(n);
+        d.ensure(sizeof(double) * (size_t)count * (S + 1));
+        KT_HIP(launch_gram_ts(n, X, ldx, px, Y, ldy, py, d.as<double>() + count, d.as<double>(), ctx->stream));
+        return d.as<double>();
+    }
     // column-major views: X is (ldx x n), Y is (ldy x n);  G = X(0:px,:) Y(0:py,:)'.
     // The reduction dimension n is long and the output tiny, so split it over
     // S row chunks (one strided-batched GEMM) and add the S slabs in a fixed
@@ -169,6 +182,10 @@ const double* gram_device(kt_context_s* ctx, int64_t n, const double* X, int ldx
 void combine_device(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* dC, int q,
                     double alpha, double beta, double* Y, int ldy) {
     if (q == 0 || px == 0) return;
+    if (!rocblas_gemm_path()) {
+        KT_HIP(launch_combine_ts(n, X, ldx, px, dC, q, alpha, beta, Y, ldy, ctx->stream));
+        return;
+    }
     // Yc (q x n) = beta Yc + alpha C' (q x px) * Xc (px x n), C on the device
     rb(rocblas_dgemm(blas(ctx), rocblas_operation_transpose, rocblas_operation_none, q,
                      (rocblas_int)n, px, &alpha, dC, px, X, ldx, &beta, Y, ldy),
@@ -208,6 +225,10 @@ void combine(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px,
     KT_HIP(hipEventRecord(ws.comb_ev, ctx->stream));
     ws.comb_pending = true;
     // Yc (q x n) = beta Yc + C' (q x px) * Xc (px x n)
+    if (!rocblas_gemm_path()) {
+        KT_HIP(launch_combine_ts(n, X, ldx, px, d.as<double>(), q, 1.0, beta, Y, ldy, ctx->stream));
+        return;
+    }
     rb(rocblas_dgemm(blas(ctx), rocblas_operation_transpose, rocblas_operation_none, q,
                      (rocblas_int)n, px, &one, d.as<double>(), px, X, ldx, &beta, Y, ldy),
        "rocblas_dgemm(combine)");
@@ -272,6 +293,54 @@ void zero_cols(kt_context_s* ctx, int64_t n, double* X, int ldx, int cols) {
 void upload_rows(kt_matrix_s* A, const double* H, int cols, double* D, int ldd) {
     const int64_t n = A->n;
     if (n == 0 || cols == 0) return;
+    // Mostly-zero blocks (the node selectors U of fun_and_grad_krylov_* and
+    // the greedy candidates, e_i columns) travel as their nonzeros: a zeroed
+    // device block plus one scatter, instead of a host transpose of n x cols
+    // and a pageable copy of it (4.4 MB at n = 21,774, cols = 25).  Column
+    // scans are sequential reads; bail out to the dense path past n*cols/16.
+    {
+        const size_t cap = (size_t)n * cols / 16;
+        std::vector<int64_t> off;
+        std::vector<double> val;
+        bool sparse = true;
+        for (int c = 0; c < cols && sparse; ++c) {
+            const double* col = H + (size_t)c * n;
+            for (int64_t i = 0; i < n; ++i)
+                if (col[i] != 0.0) {
+                    if (off.size() >= cap) {
+                        sparse = false;
+                        break;
+                    }
+                    off.push_back(i * (int64_t)ldd + c);
+                    val.push_back(col[i]);
+                }
+        }
+        if (sparse) {
+            hipStream_t st = A->ctx->stream;
+            KT_HIP(hipMemset2DAsync(D, sizeof(double) * ldd, 0, sizeof(double) * cols, (size_t)n, st));
+            const size_t m = off.size();
+            if (m) {
+                DevBuf& d = A->ctx->ws.qrtmp;
+                const size_t ob = (sizeof(int64_t) * m + 255) / 256 * 256;
+                d.ensure(ob + sizeof(double) * m);
+                PinnedBuf& hp = A->ctx->ws.pin_comb;
+                if (A->ctx->ws.comb_pending) {  // combine()'s last upload out of pin_comb
+                    KT_HIP(hipEventSynchronize(A->ctx->ws.comb_ev));
+                    A->ctx->ws.comb_pending = false;
+                }
+                hp.ensure(ob + sizeof(double) * m);
+                char* h = hp.as<char>();
+                std::memcpy(h, off.data(), sizeof(int64_t) * m);
+                std::memcpy(h + ob, val.data(), sizeof(double) * m);
+                KT_HIP(hipMemcpyAsync(d.ptr, h, ob + sizeof(double) * m, hipMemcpyHostToDevice, st));
+                KT_HIP(launch_scatter_elems((int64_t)m, d.as<int64_t>(),
+                                            reinterpret_cast<double*>(static_cast<char*>(d.ptr) + ob), D, st));
+                // pin_comb is reused by the next upload: wait for this copy
+                KT_HIP(hipStreamSynchronize(st));
+            }
+            return;
+        }
+    }
     std::vector<double> tmp((size_t)n * cols, 0.0);  // compact row-major, device numbering
     for (int c = 0; c < cols; ++c)
         for (int64_t i = 0; i < n; ++i) tmp[(size_t)i * cols + c] = H[(size_t)c * n + i];
@@ -395,6 +464,66 @@ bool cholqr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector
 }  // namespace kt
 
 namespace kt {
+
+// The thin QR of a block-Krylov step (lanczos_krylov.m:48,90,
+// arnoldi_krylov.m:50,99).  When the block is well conditioned the thin QR is
+// unique up to the signs of Q's columns, and every quantity the Krylov
+// drivers return is invariant under those signs (H, Gm, tGm, Cm change by a
+// diagonal +-1 similarity: same eigenvalues, same Um Xm Um', same traces), so
+// CholeskyQR2 -- two Gram / Cholesky / W R^-1 passes, 6 launches and 2 host
+// round trips -- stands in for the 2 bs + 3 launches of the Householder
+// sweep; its Q agrees with Householder's to ~kappa eps.  A block whose first
+// Cholesky fails or whose factor's diagonal spans more than 1e4 (kappa >~
+// 1e4), or whose scale is at a breakdown, takes householder_qr on the
+// untouched W: rank-deficient blocks keep LAPACK's reflectors and tau = 0
+// completions, which decide the reference's continuation.
+// KT_QR_CHOL=0 always takes householder_qr.
+static void apply_rinv(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, const std::vector<double>& R) {
+    std::vector<double> Ri((size_t)bs * bs);
+    tri_upper_inv(R.data(), bs, Ri.data());
+    if (bs <= 32 && !rocblas_gemm_path()) {
+        // in place: k_combine_ts has ONE workgroup per 64 rows when q <= 32,
+        // and it reads all of its rows' X before it writes any Y
+        combine(ctx, n, W, ld, bs, Ri, bs, 0.0, W, ld);
+        return;
+    }
+    DevBuf& t = ctx->ws.qrtmp;  // output must not alias the input
+    t.ensure(sizeof(double) * (size_t)std::max<int64_t>(n, 1) * bs);
+    combine(ctx, n, W, ld, bs, Ri, bs, 0.0, t.as<double>(), bs);
+    copy_cols(ctx, n, t.as<double>(), bs, W, ld, bs);
+}
+
+void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R) {
+    const char* e = std::getenv("KT_QR_CHOL");
+    if ((e && e[0] == '0') || n < 4 * (int64_t)bs || bs < 1) {
+        householder_qr(ctx, n, W, ld, bs, R);
+        return;
+    }
+    std::vector<double> R1;
+    gram(ctx, n, W, ld, bs, W, ld, bs, R1);
+    bool ok = chol_upper(R1.data(), bs);
+    double dmax = 0.0, dmin = HUGE_VAL;
+    for (int k = 0; ok && k < bs; ++k) {
+        dmax = std::max(dmax, R1[k + (size_t)k * bs]);
+        dmin = std::min(dmin, R1[k + (size_t)k * bs]);
+    }
+    if (!ok || !(dmin >= 1e-4 * dmax) || !(dmax > 1e-6)) {
+        householder_qr(ctx, n, W, ld, bs, R);
+        return;
+    }
+    apply_rinv(ctx, n, W, ld, bs, R1);
+    std::vector<double> R2;
+    gram(ctx, n, W, ld, bs, W, ld, bs, R2);
+    R.assign((size_t)bs * bs, 0.0);
+    if (!chol_upper(R2.data(), bs)) {  // not expected after a kappa <= 1e4 first pass
+        householder_qr(ctx, n, W, ld, bs, R2);
+    } else {
+        apply_rinv(ctx, n, W, ld, bs, R2);
+    }
+    matmul(bs, bs, bs, R2.data(), R1.data(), R.data());
+    for (int j = 0; j < bs; ++j)  // R2 R1 is upper triangular; clear rounding below
+        for (int i = j + 1; i < bs; ++i) R[i + (size_t)j * bs] = 0.0;
+}
 
 // Householder thin QR (the factorisation MATLAB's qr(w, 0) uses: LAPACK
 // reflectors, R with dlarfg's signs, Q = H_1 ... H_bs E), on the tall-skinny

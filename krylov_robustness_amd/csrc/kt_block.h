@@ -94,6 +94,8 @@ void download_block(kt_matrix_s* A, const double* D, int ldd, int cols, double* 
 bool cholqr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R);
 // Householder thin QR of W in place (rocSOLVER LQ of W'); R upper, signs as LAPACK.
 void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R);
+// block-Krylov thin QR: CholeskyQR2 where well conditioned, else householder_qr
+void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R);
 
 // small host helpers (column-major)
 void matmul(int m, int k, int n, const double* A, const double* B, double* C);  // C = A B

@@ -184,6 +184,10 @@ struct kt_context_s {
     int ky_flags = 8;   // KT_KY_FLAGS: y-form pass flags (8 = nontemporal store of y_{j+1}, +0.3 %)
     bool yform = true;  // KT_SLQ_YFORM=0: the hot path runs the explicit K1/K2 sweep
     void* blas = nullptr;  // rocblas_handle, created on first block-Krylov use
+    // a second context on the same device (own stream, rocBLAS handle and
+    // workspace) for the projected-matrix work that a block-Krylov run hands
+    // to a worker thread while its next step runs here (kt_krylov.cpp)
+    kt_context_s* helper = nullptr;
     kt::ProfSlot prof[kt::PROF_NSLOTS];
     kt::Workspace ws;
     kt::ScratchPool pool;  // DevMat scratch (kt_block.h)

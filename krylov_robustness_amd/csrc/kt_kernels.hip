@@ -1374,6 +1374,15 @@ __global__ __launch_bounds__(256) void k_gather_elems(int64_t count, const doubl
         out[t] = D[off[t]];
 }
 
+// D[off[t]] = val[t]: the nonzeros of a mostly-zero host block (a node
+// selector U of fun_and_grad_krylov_*) dropped into a zeroed device block
+__global__ __launch_bounds__(256) void k_scatter_elems(int64_t count, const int64_t* __restrict__ off,
+                                                       const double* __restrict__ val, double* __restrict__ D) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count;
+         t += (int64_t)gridDim.x * blockDim.x)
+        D[off[t]] = val[t];
+}
+
 // ---------------------------------------------------------------------------
 // expmv.m:71-92 Taylor loop with its stop test on the device, so the host
 // queues a whole stage without a round trip per term.  State (ExpmvState):
@@ -2408,6 +2417,13 @@ hipError_t launch_gather_elems(int64_t count, const double* D, const int64_t* of
                                hipStream_t st) {
     if (count <= 0) return hipSuccess;
     k_gather_elems<<<stream_grid(count), 256, 0, st>>>(count, D, off, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_elems(int64_t count, const int64_t* off, const double* val, double* D,
+                                hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    k_scatter_elems<<<stream_grid(count), 256, 0, st>>>(count, off, val, D);
     return hipGetLastError();
 }
 

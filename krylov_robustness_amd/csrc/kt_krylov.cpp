@@ -16,7 +16,11 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <exception>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -48,6 +52,23 @@ struct EigTimer {
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         std::lock_guard<std::mutex> lk(g_eig_mu);
         g_eig.ms += ms;
+    }
+};
+
+// KT_FG_TIMING=1: per-step wall-clock phases of fun_update / trace_fun_update
+// on stderr (host clock; each phase ends at a stream sync of its own)
+struct PhaseClock {
+    bool on = false;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    PhaseClock() {
+        const char* e = getenv("KT_FG_TIMING");
+        on = e && e[0] == '1';
+    }
+    double lap() {  // ms since the previous lap
+        const auto now = std::chrono::steady_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(now - t).count();
+        t = now;
+        return ms;
     }
 };
 
@@ -360,8 +381,59 @@ static void sym_eigvals_pair(kt_context_s* ctx, int n, const std::vector<double>
              [&] { w2 = sym_eigvals(ctx, n, M2); });
 }
 
+// Bounds lo <= ||D||_2 <= hi for symmetric n x n D (fro2 = ||D||_F^2, c2 = the
+// largest squared column norm) from k normalised squarings on the device:
+// N_0 = D / ||D||_F, N_i = N_{i-1}^2 / ||N_{i-1}^2||_F, D^(2^i) = s_i N_i with
+// log s_i = 2 log s_{i-1} + log ||N_{i-1}^2||_F.  false: no bounds (KT_NORM_POW=0).
+constexpr int kNormPowMin = 96;
+static bool sym_norm2_power_bounds(kt_context_s* ctx, int n, const std::vector<double>& D, double fro2,
+                                   double c2, double& lo, double& hi) {
+    const char* e = getenv("KT_NORM_POW");
+    if (e && e[0] == '0') return false;
+    constexpr int K = 6;
+    const size_t nn = (size_t)n * n;
+    DevBuf& b = ctx->ws.expm;
+    b.ensure(sizeof(double) * (2 * nn + 2 * K + 2));
+    double* M0 = b.as<double>();
+    double* M1 = M0 + nn;
+    double* out = M1 + nn;
+    const double s0 = std::sqrt(fro2);
+    std::vector<double> N0(nn);
+    for (size_t t = 0; t < nn; ++t) N0[t] = D[t] / s0;
+    hipStream_t st = ctx->stream;
+    KT_HIP(hipMemcpyAsync(M0, N0.data(), sizeof(double) * nn, hipMemcpyHostToDevice, st));
+    const double one = 1.0, zero = 0.0;
+    double* cur = M0;
+    double* nxt = M1;
+    for (int i = 0; i < K; ++i) {
+        if (rocblas_dgemm(blas(ctx), rocblas_operation_none, rocblas_operation_none, n, n, n, &one, cur, n, cur, n,
+                          &zero, nxt, n) != rocblas_status_success)
+            fail(KT_ERR_HIP, "rocblas_dgemm(norm powers) failed");
+        KT_HIP(launch_fro_colmax_scale(n, nxt, out + 2 * i, st));
+        std::swap(cur, nxt);
+    }
+    double h[2 * K];
+    KT_HIP(hipMemcpyAsync(h, out, sizeof(h), hipMemcpyDeviceToHost, st));
+    KT_HIP(hipStreamSynchronize(st));
+    lo = std::sqrt(c2);
+    hi = s0;
+    double logs = std::log(s0);
+    double m = 1.0;
+    for (int i = 0; i < K; ++i) {
+        const double f2 = h[2 * i], cm2 = h[2 * i + 1];
+        if (!(f2 > 0.0) || !std::isfinite(f2)) break;  // D^(2^i) vanished (nilpotent to rounding)
+        logs = 2.0 * logs + 0.5 * std::log(f2);
+        m *= 2.0;
+        // ||N_i||_F = 1 after the scaling; its largest column norm is sqrt(cm2 / f2)
+        hi = std::min(hi, std::exp(logs / m));
+        lo = std::max(lo, std::exp((logs + 0.5 * std::log(cm2 / f2)) / m));
+    }
+    return true;
+}
+
 // ||D||_2 < tol for symmetric n x n D, decided from bounds when they settle
-// it (max column 2-norm <= ||D||_2 <= ||D||_F), else from the spectrum
+// it (max column 2-norm <= ||D||_2 <= ||D||_F, then the power bounds above),
+// else from the spectrum
 static bool sym_norm2_below(kt_context_s* ctx, int n, const std::vector<double>& D, double tol) {
     double fro2 = 0.0, col2max = 0.0;
     for (int j = 0; j < n; ++j) {
@@ -372,6 +444,19 @@ static bool sym_norm2_below(kt_context_s* ctx, int n, const std::vector<double>&
     }
     if (std::sqrt(fro2) < tol) return true;
     if (std::sqrt(col2max) >= tol) return false;
+    // Tighter bounds from powers: for symmetric D and m = 2^k,
+    //   maxcol(D^m)^(1/m) <= ||D||_2 <= ||D^m||_F^(1/m) <= n^(1/(2m)) ||D||_2,
+    // so k normalised squarings on the device (one n^3 GEMM each, tens of us)
+    // close the gap to a factor n^(1/2^(k+1)) (1.04 at n = 225, k = 6) instead
+    // of a host eigensolve (1.3-1.6 ms at n = 225).  Only a bracket that
+    // still straddles tol goes on to the spectrum.
+    if (n >= kNormPowMin) {
+        double lo = 0.0, hi = HUGE_VAL;
+        if (sym_norm2_power_bounds(ctx, n, D, fro2, col2max, lo, hi)) {
+            if (hi * (1.0 + 1e-10) < tol) return true;
+            if (lo * (1.0 - 1e-10) >= tol) return false;
+        }
+    }
     const std::vector<double> ev = sym_eigvals(ctx, n, D);
     return std::max(std::fabs(ev.front()), std::fabs(ev.back())) < tol;
 }
@@ -444,7 +529,7 @@ struct BlockLanczos {
     void start(const double* U) {  // U: host n x bs column-major (original numbering)
         upload_rows(A, U, bs, slot(0), 2 * PB);
         std::vector<double> R;
-        householder_qr(ctx, n, slot(0), 2 * PB, bs, R);  // [V, ~] = qr(b, 0)    :48
+        block_qr(ctx, n, slot(0), 2 * PB, bs, R);  // [V, ~] = qr(b, 0)    :48
         cur = 0;
         prev = -1;
         Hr = bs;
@@ -488,7 +573,7 @@ struct BlockLanczos {
             combine(ctx, n, win.col(0), ld, 2 * PB, C, bs, 1.0, W.col(0), PB);
         }
         std::vector<double> R;
-        householder_qr(ctx, n, W.col(0), PB, bs, R);  // [w, R] = qr(w, 0)   :90
+        block_qr(ctx, n, W.col(0), PB, bs, R);  // [w, R] = qr(w, 0)   :90
         if (hg) {
             KT_HIP(hipStreamSynchronize(ctx->stream));  // (the QR's read of R has drained the copies)
             for (size_t t = 0; t < cnt; ++t) h[t] = (0.0 + hg[t]) + hg[cnt + t];  // h += g, twice
@@ -554,7 +639,7 @@ struct BlockArnoldi {
     void start(const double* U) {
         upload_rows(A, U, bs, blk(0), ld());
         std::vector<double> R;
-        householder_qr(ctx, n, blk(0), ld(), bs, R);  // [V, ~] = qr(b, 0)   :50
+        block_qr(ctx, n, blk(0), ld(), bs, R);  // [V, ~] = qr(b, 0)   :50
         nblk = 1;
         Hr = bs;
         Hc = 0;
@@ -592,7 +677,7 @@ struct BlockArnoldi {
         };
         for (int pass = 0; pass < 2; ++pass) project(pass * cnt);
         std::vector<double> r;
-        householder_qr(ctx, n, W.col(0), PB, bs, r);  // [w, r] = qr(w, 0)   :99
+        block_qr(ctx, n, W.col(0), PB, bs, r);  // [w, r] = qr(w, 0)   :99
         lucky = norm2_small(bs, bs, r.data()) < 1e-12;  // :100-102
         KT_HIP(hipStreamSynchronize(ctx->stream));    // (the QR's read of r has drained the copies)
         std::vector<double> h(cnt);
@@ -655,6 +740,97 @@ static std::vector<double> top_left(const std::vector<double>& M, int Mr, int nn
 }
 
 // ---------------------------------------------------------------------------
+// In-order worker thread for the projected-matrix work of a block-Krylov run
+// (trace_fun_update / fun_update): job k runs while the caller's thread
+// extends the basis by one more step.  wait(k) blocks until jobs 0..k have
+// finished and rethrows the first failure; once a job failed the rest are
+// skipped.  The destructor drops jobs not yet started and joins.
+// ---------------------------------------------------------------------------
+class StepWorker {
+   public:
+    explicit StepWorker(int device) : device_(device) { th_ = std::thread([this] { loop(); }); }
+    StepWorker(const StepWorker&) = delete;
+    StepWorker& operator=(const StepWorker&) = delete;
+    ~StepWorker() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+            q_.clear();
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    void submit(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            q_.push_back(std::move(f));
+        }
+        cv_.notify_all();
+    }
+    void wait(int k) {
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [&] { return done_ > k || err_; });
+        if (err_) std::rethrow_exception(err_);
+    }
+
+   private:
+    void loop() {
+        (void)hipSetDevice(device_);
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;  // stop_ with nothing queued
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            std::exception_ptr e;
+            if (!err_) {
+                try {
+                    f();
+                } catch (...) {
+                    e = std::current_exception();
+                }
+            }
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                if (e && !err_) err_ = e;
+                ++done_;
+            }
+            done_cv_.notify_all();
+        }
+    }
+    int device_;
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<std::function<void()>> q_;
+    int done_ = 0;
+    bool stop_ = false;
+    std::exception_ptr err_;
+    std::thread th_;
+};
+
+// The context a pipelined block-Krylov run hands its projected work to
+// (ctx->helper, created on first use), or nullptr for the serial loop:
+// env_name set to "0", or the helper cannot be created.
+static kt_context_s* pipeline_helper(kt_context_s* ctx, const char* env_name) {
+    const char* e = getenv(env_name);  // read per call (A/B within one process)
+    if (e && e[0] == '0') return nullptr;
+    if (!ctx->helper) {
+        kt_context_t h = nullptr;
+        if (kt_context_create(ctx->device, &h) != KT_OK) {
+            (void)hipGetLastError();
+            KT_HIP(hipSetDevice(ctx->device));
+            return nullptr;
+        }
+        ctx->helper = h;
+        KT_HIP(hipSetDevice(ctx->device));
+    }
+    return ctx->helper;
+}
+
+// ---------------------------------------------------------------------------
 // trace_fun_update.m
 // ---------------------------------------------------------------------------
 double trace_fun_update_impl(kt_matrix_s* A, int rk, const double* U, const double* B, double tol,
@@ -681,11 +857,42 @@ double trace_fun_update_impl(kt_matrix_s* A, int rk, const double* U, const doub
     if (!herm) fail(KT_ERR_UNSUPPORTED, "trace_fun_update: non-Hermitian B (needs a general eig)");
     BlockLanczos L(A, rk);
     const int d = 2;  // :58
+    // As in fun_update_impl: step j's eigenvalues and Xm (:83-89) only decide
+    // whether to go on, so they run on a worker thread (helper context for
+    // the projections too large for the host solver) while this thread runs
+    // Lanczos step j + 1; the stop test (:104-118) is applied in step order
+    // on the worker, and the loop ends at the first step that says stop.
+    // Identical results to the serial loop (KT_TFU_PIPE=0).
+    struct Step {
+        double Xm = 0.0;
+        bool stop = false, lucky = false;
+    };
+    std::vector<Step> steps((size_t)it + 2);
     double Xstop[2] = {0.0, 0.0};
+    const ScalarFn sfn = tl_scalar_fn;  // the elementwise handle travels to the worker thread
+    auto project = [&](kt_context_s* c, int jj, int nn, std::vector<double>& tGm, std::vector<double>& Gm) {
+        tl_scalar_fn = sfn;
+        std::vector<double> w1, w2;
+        sym_eigvals_pair(c, nn, tGm, Gm, w1, w2);
+        Step& S = steps[jj];
+        S.Xm = trace_diff(w1, w2, fun);  // :83-89
+        if (jj <= d) {                   // :104-118
+            Xstop[jj - 1] = S.Xm;
+        } else {
+            S.stop = std::fabs(S.Xm - Xstop[0]) < tol;
+            if (!S.stop) {
+                Xstop[0] = Xstop[1];
+                Xstop[1] = S.Xm;
+            }
+        }
+    };
+    kt_context_s* hctx = pipeline_helper(ctx, "KT_TFU_PIPE");
+    std::unique_ptr<StepWorker> W;  // destroyed (joined) before steps / Xstop
+    if (hctx) W.reset(new StepWorker(ctx->device));
     std::vector<double> Cm;
-    double Xm = 0.0;
-    int j = 0;
-    for (j = 1; j <= it; ++j) {
+    int jfin = 0;
+    PhaseClock pc;
+    for (int j = 1; j <= it; ++j) {
         if (j == 1) {
             L.start(U);                                                        // :64
             const double* V1 = L.win.col(L.prev * L.PB);                       // Um(:, 1:end-rk)
@@ -693,33 +900,52 @@ double trace_fun_update_impl(kt_matrix_s* A, int rk, const double* U, const doub
         } else {
             L.extend();                                                        // :68
         }
+        steps[j].lucky = L.lucky;
+        const double t_ext = pc.on ? pc.lap() : 0.0;
+        if (W && j >= 2) {
+            W->wait(j - 2);
+            if (pc.on)
+                fprintf(stderr, "[kt tfu] step %d stop %d (waited %.3f ms after extend %d: %.3f ms)\n", j - 1,
+                        (int)steps[j - 1].stop, pc.lap(), j, t_ext);
+            if (steps[j - 1].stop) {
+                jfin = j - 1;
+                break;
+            }
+        }
         const int nn = L.Hr - rk;                                              // :72-73
         std::vector<double> Gm = top_left(L.H, L.Hr, nn), tGm = Gm;
         for (int jj = 0; jj < rk; ++jj)
             for (int ii = 0; ii < rk; ++ii) tGm[ii + (size_t)jj * nn] += Cm[ii + (size_t)jj * rk];  // :74-77
         for (int b = 0; b < nn; ++b)                                           // :78-81
             for (int a = 0; a < b; ++a) {
-                double s = 0.5 * (Gm[a + (size_t)b * nn] + Gm[b + (size_t)a * nn]);
-                Gm[a + (size_t)b * nn] = Gm[b + (size_t)a * nn] = s;
-                s = 0.5 * (tGm[a + (size_t)b * nn] + tGm[b + (size_t)a * nn]);
-                tGm[a + (size_t)b * nn] = tGm[b + (size_t)a * nn] = s;
+                double sv = 0.5 * (Gm[a + (size_t)b * nn] + Gm[b + (size_t)a * nn]);
+                Gm[a + (size_t)b * nn] = Gm[b + (size_t)a * nn] = sv;
+                sv = 0.5 * (tGm[a + (size_t)b * nn] + tGm[b + (size_t)a * nn]);
+                tGm[a + (size_t)b * nn] = tGm[b + (size_t)a * nn] = sv;
             }
-        std::vector<double> w1, w2;
-        sym_eigvals_pair(ctx, nn, tGm, Gm, w1, w2);
-        Xm = trace_diff(w1, w2, fun);  // :83-89
-        if (j <= d) {                                                          // :104-118
-            Xstop[j - 1] = Xm;
+        const bool last = steps[j].lucky || j == it;                           // :119-124 / loop end
+        if (W) {
+            W->submit([&, j, nn, tGm = std::move(tGm), Gm = std::move(Gm)]() mutable {
+                project(hctx, j, nn, tGm, Gm);
+            });
+            if (last) {
+                W->wait(j - 1);
+                jfin = j;
+                break;
+            }
         } else {
-            if (std::fabs(Xm - Xstop[0]) < tol) break;
-            Xstop[0] = Xstop[1];
-            Xstop[1] = Xm;
+            project(ctx, j, nn, tGm, Gm);
+            if (pc.on) fprintf(stderr, "[kt tfu] step %d nn %d extend %.3f eig %.3f ms\n", j, nn, t_ext, pc.lap());
+            if (steps[j].stop || last) {
+                jfin = j;
+                break;
+            }
         }
-        if (L.lucky) break;                                                    // :119-124
     }
-    if (j > it) j = it;
-    if (iter_out) *iter_out = j;
-    if (lucky_out) *lucky_out = L.lucky ? 1 : 0;
-    return Xm;
+    W.reset();
+    if (iter_out) *iter_out = jfin;
+    if (lucky_out) *lucky_out = steps[jfin].lucky ? 1 : 0;
+    return steps[jfin].Xm;
 }
 
 // ---------------------------------------------------------------------------
@@ -741,26 +967,79 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
     const int64_t n = A->n;
     if (it <= 0) it = (int)std::min<int64_t>(100, n);  // :24-26
     const bool herm = b_hermitian(rk, B);              // :41
+    if (!herm) fail(KT_ERR_UNSUPPORTED, "fun_update: non-Hermitian B");
     FunUpdateResult res;
     // basis never needs more than ~n/2 columns before the dense fallback (:85)
     const int maxblk = (int)std::min<int64_t>(it + 1, n / (2 * (int64_t)rk) + 2);
     res.basis.reset(new BlockArnoldi(A, rk, std::max(maxblk, 2)));
     BlockArnoldi& Ar = *res.basis;
     const int d = 2;
+    // Step j's projected work -- Xm = f(tGm) - f(Gm) (:93-106) and the stop
+    // test (:108-126) -- decides only WHETHER to go on; the next Arnoldi step
+    // does not read it.  So it runs on a worker thread with the helper
+    // context (own stream and rocBLAS handle) while this thread extends the
+    // basis to step j + 1 on the device; the loop then reads step j's
+    // decision and stops there if it says so (the speculative block is
+    // ignored: Xm, nx, iter, lucky are step j's, and Um is the basis'
+    // first nx columns).  Same arithmetic, same order: results identical to
+    // the serial loop (KT_FU_PIPE=0).
+    struct Step {
+        std::vector<double> F1;
+        int nn = 0;
+        bool stop = false, lucky = false;
+    };
+    std::vector<Step> steps((size_t)it + 2);
     std::vector<std::vector<double>> Xstop;
+    auto project = [&](kt_context_s* c, int jj, std::vector<double>& tGm, std::vector<double>& Gm) {
+        Step& S = steps[jj];
+        S.F1 = sym_matfun_diff(c, S.nn, tGm, Gm, fun);                      // :106
+        if (jj <= d) {                                                       // :109-126
+            Xstop.push_back(S.F1);
+            return;
+        }
+        const int nn = S.nn;
+        const int n0 = (int)std::lround(std::sqrt((double)Xstop[0].size()));
+        std::vector<double> D = S.F1;
+        for (int b = 0; b < n0; ++b)
+            for (int a = 0; a < n0; ++a) D[a + (size_t)b * nn] -= Xstop[0][a + (size_t)b * n0];
+        // 2-norm of the symmetric difference (= max |eig|) below tol?
+        S.stop = sym_norm2_below(c, nn, D, tol);
+        if (!S.stop) {
+            Xstop.erase(Xstop.begin());
+            Xstop.push_back(S.F1);
+        }
+    };
+    kt_context_s* hctx = pipeline_helper(ctx, "KT_FU_PIPE");
+    std::unique_ptr<StepWorker> W;  // destroyed (joined) before steps / Xstop
+    if (hctx) W.reset(new StepWorker(ctx->device));
     std::vector<double> Cm;
-    int j = 0;
-    for (j = 1; j <= it; ++j) {
+    int jfin = 0;
+    PhaseClock pc;
+    for (int j = 1; j <= it; ++j) {
         if (j == 1) {
             Ar.start(U);                                                     // :79
             Cm = make_Cm(ctx, A, Ar.blk(0), Ar.ld(), rk, U, rk, B);         // :80-81
         } else {
             Ar.extend();                                                     // :83
         }
+        steps[j].lucky = Ar.lucky;
+        const double t_ext = pc.on ? pc.lap() : 0.0;
+        // the previous step's decision (its work ran during this extension)
+        if (W && j >= 2) {
+            W->wait(j - 2);
+            if (pc.on)
+                fprintf(stderr, "[kt fu] step %d nn %d stop %d (waited %.3f ms after extend %d: %.3f ms)\n", j - 1,
+                        steps[j - 1].nn, (int)steps[j - 1].stop, pc.lap(), j, t_ext);
+            if (steps[j - 1].stop) {
+                jfin = j - 1;
+                break;
+            }
+        }
         if (2 * (int64_t)Ar.nblk * rk >= n) {  // size(Um,2) >= size(Um,1)/2   :85-90
             std::vector<double> fA = dense_A(A), fAt = fA;
             add_UBUt(fAt, n, rk, U, B);
             std::vector<double> F1 = sym_matfun_diff(ctx, (int)n, fAt, fA, fun);
+            W.reset();
             res.Xm.swap(F1);
             res.nx = (int)n;
             res.iter = j;
@@ -774,35 +1053,37 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
         std::vector<double> Gm = top_left(Ar.H, Ar.Hr, nn);
         for (int b = 0; b < nn; ++b)                                         // :94
             for (int a = 0; a < b; ++a) {
-                const double s = 0.5 * (Gm[a + (size_t)b * nn] + Gm[b + (size_t)a * nn]);
-                Gm[a + (size_t)b * nn] = Gm[b + (size_t)a * nn] = s;
+                const double sv = 0.5 * (Gm[a + (size_t)b * nn] + Gm[b + (size_t)a * nn]);
+                Gm[a + (size_t)b * nn] = Gm[b + (size_t)a * nn] = sv;
             }
         std::vector<double> tGm = Gm;
         for (int jj = 0; jj < rk; ++jj)                                      // :97-104
             for (int ii = 0; ii < rk; ++ii)
-                tGm[ii + (size_t)jj * nn] += herm ? 0.5 * (Cm[ii + (size_t)jj * rk] + Cm[jj + (size_t)ii * rk])
-                                                  : Cm[ii + (size_t)jj * rk];
-        if (!herm) fail(KT_ERR_UNSUPPORTED, "fun_update: non-Hermitian B");
-        std::vector<double> F1 = sym_matfun_diff(ctx, nn, tGm, Gm, fun);     // :106
-        res.Xm = F1;
-        res.nx = nn;
-        if (j <= d) {                                                        // :109-126
-            Xstop.push_back(F1);
+                tGm[ii + (size_t)jj * nn] += 0.5 * (Cm[ii + (size_t)jj * rk] + Cm[jj + (size_t)ii * rk]);
+        steps[j].nn = nn;
+        const bool last = steps[j].lucky || j == it;                         // :127-130 / loop end
+        if (W) {
+            W->submit([&, j, tGm = std::move(tGm), Gm = std::move(Gm)]() mutable { project(hctx, j, tGm, Gm); });
+            if (last) {
+                W->wait(j - 1);
+                jfin = j;
+                break;
+            }
         } else {
-            const int n0 = (int)std::lround(std::sqrt((double)Xstop[0].size()));
-            std::vector<double> D = F1;
-            for (int b = 0; b < n0; ++b)
-                for (int a = 0; a < n0; ++a) D[a + (size_t)b * nn] -= Xstop[0][a + (size_t)b * n0];
-            // 2-norm of the symmetric difference (= max |eig|) below tol?
-            if (sym_norm2_below(ctx, nn, D, tol)) break;
-            Xstop.erase(Xstop.begin());
-            Xstop.push_back(F1);
+            project(ctx, j, tGm, Gm);
+            if (pc.on) fprintf(stderr, "[kt fu] step %d nn %d extend %.3f project %.3f ms\n", j, nn, t_ext, pc.lap());
+            if (steps[j].stop || last) {
+                jfin = j;
+                break;
+            }
         }
-        if (Ar.lucky) break;                                                 // :127-130
     }
-    if (j > it) j = it;
-    res.iter = j;
-    res.lucky = Ar.lucky;
+    W.reset();
+    Step& S = steps[jfin];
+    res.Xm.swap(S.F1);
+    res.nx = S.nn;
+    res.iter = jfin;
+    res.lucky = S.lucky;
     ctx->fu_last_cols = res.nx;
     return res;
 }

@@ -98,6 +98,15 @@ hipError_t launch_ycoef(int P, const double* partial, int nblk, int start, int l
                         hipStream_t st);
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st);
 // out[i] = D[off[i]], i < count
+// tall-skinny Gram / combine (kt_gemm_ts.hip)
+int gram_ts_chunks(int64_t n);
+hipError_t launch_gram_ts(int64_t n, const double* X, int ldx, int px, const double* Y, int ldy, int py,
+                          double* part, double* G, hipStream_t st);
+hipError_t launch_combine_ts(int64_t n, const double* X, int ldx, int px, const double* C, int q, double alpha,
+                             double beta, double* Y, int ldy, hipStream_t st);
+hipError_t launch_fro_colmax_scale(int n, double* M, double* out, hipStream_t st);
+hipError_t launch_scatter_elems(int64_t count, const int64_t* off, const double* val, double* D,
+                                hipStream_t st);
 hipError_t launch_gather_elems(int64_t count, const double* D, const int64_t* off, double* out,
                                hipStream_t st);
 // out (nr x cols, column-major) = rows[r] of the row-major block D (leading dimension ldd)

@@ -306,6 +306,10 @@ int kt_context_create(int device, kt_context_t* out) {
 int kt_context_destroy(kt_context_t ctx) {
     KT_GUARD_BEGIN
     if (!ctx) return KT_OK;
+    if (ctx->helper) {
+        (void)kt_context_destroy(ctx->helper);
+        ctx->helper = nullptr;
+    }
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& s : ctx->prof)

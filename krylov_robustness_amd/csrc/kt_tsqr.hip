@@ -61,32 +61,43 @@ __global__ __launch_bounds__(kTsBlock) void k_ts_step(int n, int bs, int BP, int
     const int r1 = min(n, r0 + rows_per_blk);
     const int rstart = max(r0, k < 0 ? 0 : k);
     double acc = 0.0;
-    // uniform trip count across the workgroup (barrier inside)
-    for (int base = rstart; base < r1; base += rpi) {
-        const int r = base + sub;
-        const bool live = r < r1 && c < bs;
-        double wk = 0.0, wn = 0.0, wc = 0.0;
-        if (live) {
-            if (k >= 0) wk = W[(int64_t)r * ld + k];
-            if (kn < bs) wn = W[(int64_t)r * ld + kn];
-            wc = W[(int64_t)r * ld + c];
+    // Rows go in chunks of kTsU row slots: every load of a chunk is issued
+    // (3 kTsU per thread, one memory round trip) before the barrier that
+    // orders the chunk's reads before its writes (a thread's row is read by
+    // all BP threads of that row, W(r, kn) is rewritten by one of them); the
+    // rows and the accumulation order are the single-slot loop's.  Trip
+    // counts are uniform across the workgroup (barrier inside).
+    constexpr int kTsU = 8;
+    for (int base0 = rstart; base0 < r1; base0 += kTsU * rpi) {
+        double wk[kTsU], wn[kTsU], wc[kTsU];
+#pragma unroll
+        for (int u = 0; u < kTsU; ++u) {
+            const int r = base0 + u * rpi + sub;
+            const bool live = r < r1 && c < bs;
+            wk[u] = (live && k >= 0) ? W[(int64_t)r * ld + k] : 0.0;
+            wn[u] = (live && kn < bs) ? W[(int64_t)r * ld + kn] : 0.0;
+            wc[u] = live ? W[(int64_t)r * ld + c] : 0.0;
         }
-        __syncthreads();  // every read of this row block before any write
-        if (live) {
+        __syncthreads();  // every read of this chunk before any write
+#pragma unroll
+        for (int u = 0; u < kTsU; ++u) {
+            const int r = base0 + u * rpi + sub;
+            if (!(r < r1 && c < bs)) continue;
             double v = 0.0;
+            double wcu = wc[u];
             if (k >= 0) {
-                v = (r == k) ? 1.0 : wk * scal;
+                v = (r == k) ? 1.0 : wk[u] * scal;
                 if (c == k) {
                     V[(int64_t)r * BP + k] = v;
                     if (r == k) W[(int64_t)r * ld + k] = beta;
                 } else if (c > k) {
-                    wc -= tau * v * tc;
-                    W[(int64_t)r * ld + c] = wc;
+                    wcu -= tau * v * tc;
+                    W[(int64_t)r * ld + c] = wcu;
                 }
             }
             if (kn < bs && c >= kn && r > kn) {
-                const double wn_new = k >= 0 ? wn - tau * v * tn : wn;
-                acc = fma(wn_new, wc, acc);
+                const double wn_new = k >= 0 ? wn[u] - tau * v * tn : wn[u];
+                acc = fma(wn_new, wcu, acc);
             }
         }
     }
