@@ -522,6 +522,15 @@ static void project(kt_context_s* ctx, int64_t n, const double* Q, int ld, int n
 }
 
 // mc_trace.m:1-63
+//
+// Round it + 1's S term -- Afun_{it+1}(S_{it+1}) = P_it..P_1 F(P_1..P_it S_{it+1})
+// (:43-45) -- needs only the Q blocks up to round it, not the round's trace
+// sums, so it runs speculatively on a third device copy of A (the twin's
+// twin: own stream, workspace and matrix) on a third host thread while the
+// round's Q and G terms run (:46, :49).  mc_trace never stops in round 1
+// (tr_old = 0), so round 2's S term is never wasted; a later one is discarded
+// when the round's relative change stops the loop.  Same kernels on the same
+// data: the estimate is bit-identical to the serial order (KT_MC_SPEC=0).
 void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isAreal, uint64_t seed,
                    double* tr_out, double* res_out, int* it_out, const Shard& sh = Shard()) {
     kt_context_s* ctx = A->ctx;
@@ -531,37 +540,70 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
     double tr = 0.0, tr_old = 0.0, tr_new = 0.0, res = 1.0;
     std::vector<DevMat> Qs;
     DevMat S, G, Z, Y, Zg2;
+    // G columns dealt over the ranks whenever the caller supplied the
+    // all-reduce (at world 1 too: rank 0 takes every column, the sums still
+    // travel through the collective); expmv stays replicated
+    const bool sharded = sh.allreduce != nullptr && F.kind != AFUN_EXPMV;
+    const char* se = getenv("KT_MC_SPEC");
+    kt_matrix_s* A3 = nullptr;  // the speculative S terms' matrix
+    if (!sharded && K > 1 && !(se && se[0] == '0')) {
+        kt_matrix_s* A2 = twin_of(A);
+        if (A2) A3 = twin_of(A2);
+    }
+    // the S-term output blocks (round parity) and the speculative run's
+    // scratch, allocated once on A3's context: never re-allocated while the
+    // speculative thread may use that context's pool
+    DevMat Yb[2], S3, Z3;
+    if (A3) {
+        for (auto& b : Yb) b.alloc(A3->ctx, n, ld);
+        S3.alloc(A3->ctx, n, ld);
+        Z3.alloc(A3->ctx, n, ld);
+        KT_HIP(hipStreamSynchronize(A3->ctx->stream));
+        KT_HIP(hipSetDevice(ctx->device));
+    }
+    // Y = Afun_itx(S_itx) into Yx on AX's stream (the matrix F works on)
+    auto s_term = [&](kt_matrix_s* AX, int itx, DevMat& Sx, DevMat& Zx, double* Yx) {
+        kt_context_s* cx = AX->ctx;
+        const int64_t base = (int64_t)(itx - 1) * 2 * mb;
+        KT_HIP(launch_rademacher(ld, (int)n, seed, base, nullptr, Sx.col(0), cx->stream));  // :43
+        zero_cols(cx, n, Sx.col(mb), ld, ld - mb);
+        copy_cols(cx, n, Sx.col(0), ld, Zx.col(0), ld, mb);
+        for (int q = itx - 2; q >= 0; --q) project(cx, n, Qs[q].col(0), ld, mb, Zx.col(0), mb);
+        AfunDev FX{AX, F.kind, F.fun, F.m};
+        FX.apply(Zx.col(0), ld, mb, Yx);
+        for (int q = 0; q <= itx - 2; ++q) project(cx, n, Qs[q].col(0), ld, mb, Yx, mb);
+    };
+    bool spec_ready = false;  // this round's S term was computed by the speculative thread
     int it = 0;
     for (it = 1; it <= K; ++it) {
         const int64_t base = (int64_t)(it - 1) * 2 * mb;
-        S.alloc(ctx, n, ld);
         G.alloc(ctx, n, ld);
-        KT_HIP(launch_rademacher(ld, (int)n, seed, base, nullptr, S.col(0), ctx->stream));       // :43
         KT_HIP(launch_rademacher(ld, (int)n, seed, base + mb, nullptr, G.col(0), ctx->stream));  // :44
-        zero_cols(ctx, n, S.col(mb), ld, ld - mb);
         zero_cols(ctx, n, G.col(mb), ld, ld - mb);
-        // Y = Afun_it(S) = P_{it-1}..P_1 F(P_1..P_{it-1} S)                       :45
         Z.alloc(ctx, n, ld);
-        Y.alloc(ctx, n, ld);
-        copy_cols(ctx, n, S.col(0), ld, Z.col(0), ld, mb);
-        for (int q = (int)Qs.size() - 1; q >= 0; --q) project(ctx, n, Qs[q].col(0), ld, mb, Z.col(0), mb);
-        F.apply(Z.col(0), ld, mb, Y.col(0));
-        for (size_t q = 0; q < Qs.size(); ++q) project(ctx, n, Qs[q].col(0), ld, mb, Y.col(0), mb);
+        double* Yc;
+        if (A3) {
+            Yc = Yb[it & 1].col(0);
+        } else {
+            Y.alloc(ctx, n, ld);
+            Yc = Y.col(0);
+        }
+        if (!spec_ready) {  // Y = Afun_it(S) = P_{it-1}..P_1 F(P_1..P_{it-1} S)          :45
+            S.alloc(ctx, n, ld);
+            s_term(A, it, S, Z, Yc);
+        }
+        spec_ready = false;
         std::vector<double> R;
-        householder_qr(ctx, n, Y.col(0), ld, mb, R);                               // [Q, ~] = qr(.,0)
+        householder_qr(ctx, n, Yc, ld, mb, R);                                     // [Q, ~] = qr(.,0)
         // tr += trace(Q' Afun_it(Q)) = sum quadforms of P_1..P_{it-1} Q          :46
-        copy_cols(ctx, n, Y.col(0), ld, Z.col(0), ld, mb);
+        copy_cols(ctx, n, Yc, ld, Z.col(0), ld, mb);
         for (int q = (int)Qs.size() - 1; q >= 0; --q) project(ctx, n, Qs[q].col(0), ld, mb, Z.col(0), mb);
-        // G columns dealt over the ranks whenever the caller supplied the
-        // all-reduce (at world 1 too: rank 0 takes every column, the sums
-        // still travel through the collective); expmv stays replicated
-        const bool sharded = sh.allreduce != nullptr && F.kind != AFUN_EXPMV;
         const bool split = !sharded;  // the G term is local
         kt_matrix_s* A2 = split ? twin_of(A) : nullptr;
         if (!A2) tr += F.trace_quad(Z.col(0), ld, mb);
         Qs.emplace_back();                                                         // :47-48
         Qs.back().alloc(ctx, n, ld);
-        copy_cols(ctx, n, Y.col(0), ld, Qs.back().col(0), ld, mb);
+        copy_cols(ctx, n, Yc, ld, Qs.back().col(0), ld, mb);
         // tr_new = tr + trace(G' Afun_{it+1}(G)) / m                              :49
         DevMat& Zg = A2 ? Zg2 : Z;
         if (A2) Zg.alloc(ctx, n, ld);
@@ -573,9 +615,10 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
             // the G term runs on the matrix's twin (own stream, workspace and
             // device copy; kt_krylov.cpp twin_of) on a second host thread
             // while the Q term runs here -- same kernels on the same data,
-            // so the sums are bit-identical to the serial order.
-            KT_HIP(hipStreamSynchronize(ctx->stream));  // Z and Zg are ready for both streams
-            Status gerr{KT_OK, ""};
+            // so the sums are bit-identical to the serial order.  The next
+            // round's S term (see above) starts on a third thread.
+            KT_HIP(hipStreamSynchronize(ctx->stream));  // Z, Zg and Q_it are ready for every stream
+            Status gerr{KT_OK, ""}, serr{KT_OK, ""};
             std::thread th([&] {
                 try {
                     KT_HIP(hipSetDevice(A2->ctx->device));
@@ -588,14 +631,38 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
                     gerr = Status{KT_ERR_HIP, "mc_trace: G term on the twin failed"};
                 }
             });
+            std::thread th3;
+            if (A3 && it < K)
+                th3 = std::thread([&] {
+                    try {
+                        KT_HIP(hipSetDevice(A3->ctx->device));
+                        s_term(A3, it + 1, S3, Z3, Yb[(it + 1) & 1].col(0));
+                        KT_HIP(hipStreamSynchronize(A3->ctx->stream));
+                    } catch (const Status& e) {
+                        serr = e;
+                    } catch (...) {
+                        serr = Status{KT_ERR_HIP, "mc_trace: speculative S term failed"};
+                    }
+                });
             double qsum = 0.0;
             try {
                 qsum = F.trace_quad(Z.col(0), ld, mb);
             } catch (...) {
                 th.join();
+                if (th3.joinable()) th3.join();
                 throw;
             }
             th.join();
+            if (th3.joinable()) {
+                th3.join();
+                if (serr.code == KT_OK) {
+                    spec_ready = true;
+                } else if (serr.code != KT_ERR_ALLOC) {
+                    throw serr;
+                }  // out of memory: the next round computes its S term here
+                (void)hipGetLastError();
+                KT_HIP(hipSetDevice(ctx->device));
+            }
             if (gerr.code == KT_ERR_ALLOC) {
                 // the twin's workspace did not fit: give its idle blocks back
                 // and run the G term in the serial order on A (as
@@ -611,11 +678,11 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
         } else if (sharded) {
             std::vector<double> qv(mb, 0.0), qm;
             int nm = 0;
-            for (int c = sh.rank; c < mb; c += sh.world) copy_cols(ctx, n, Z.col(c), ld, Y.col(nm++), ld, 1);
+            for (int c = sh.rank; c < mb; c += sh.world) copy_cols(ctx, n, Z.col(c), ld, Yc + nm++, ld, 1);
             if (nm > 0) {
-                zero_cols(ctx, n, Y.col(nm), ld, ld - nm);
+                zero_cols(ctx, n, Yc + nm, ld, ld - nm);
                 qm.assign(nm, 0.0);
-                F.quad_cols(Y.col(0), ld, nm, qm.data());
+                F.quad_cols(Yc, ld, nm, qm.data());
                 for (int c = sh.rank, t = 0; c < mb; c += sh.world, ++t) qv[c] = qm[t];
             }
             if (sh.allreduce(qv.data(), mb, sh.user) != 0) fail(KT_ERR_CALLBACK, "mc_trace: all-reduce callback failed");

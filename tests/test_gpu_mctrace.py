@@ -163,6 +163,28 @@ def test_mc_trace_twin_split_is_bit_identical(kra, gpu_ctx, monkeypatch, afun):
         ser = kra.mc_trace(afun, A=D2, ctx=gpu_ctx, **args)
     assert par == ser
     assert par[2] > 1  # several rounds (nested deflation) were run
+    # the speculative next-round S term (third device copy, third thread) off:
+    # still the same numbers
+    monkeypatch.setenv("KT_TWIN", "1")
+    monkeypatch.setenv("KT_MC_SPEC", "0")
+    D3 = kra.DeviceMatrix(A, gpu_ctx)
+    if afun == "matrix":
+        nos = kra.mc_trace(D3, ctx=gpu_ctx, **args)
+    else:
+        nos = kra.mc_trace(afun, A=D3, ctx=gpu_ctx, **args)
+    assert nos == par
+
+
+def test_trace_exp_speculative_rounds_bit_identical(kra, gpu_ctx, monkeypatch):
+    """trace_exp.m's composition (Afun = expmv, tol 1e-4, maxit 1000) with the
+    next round's S term computed speculatively during the current round's Q
+    and G terms (default) vs KT_MC_SPEC=0: the same estimate, bit for bit."""
+    A = load_graph("oregon_A0")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    spec = kra.trace_exp(D, method="expmv", seed=2, ctx=gpu_ctx)
+    monkeypatch.setenv("KT_MC_SPEC", "0")
+    D2 = kra.DeviceMatrix(A, gpu_ctx)
+    assert kra.trace_exp(D2, method="expmv", seed=2, ctx=gpu_ctx) == spec
 
 
 @pytest.mark.parametrize("kind", ["loops", "signed"])
