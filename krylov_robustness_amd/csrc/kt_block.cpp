@@ -4,6 +4,7 @@
 #include <cstring>
 
 #include "kt_block.h"
+#include <chrono>
 
 #include <rocsolver/rocsolver.h>
 
@@ -83,7 +84,7 @@ void ScratchPool::clear() {
     free.clear();
 }
 
-void DevMat::alloc(kt_context_s* c, int64_t n_, int ld_) {
+void DevMat::alloc(kt_context_s* c, int64_t n_, int ld_, bool zero) {
     n = n_;
     ld = ld_;
     const size_t want = sizeof(double) * (size_t)std::max<int64_t>(n, 1) * (size_t)std::max(ld, 1);
@@ -92,7 +93,12 @@ void DevMat::alloc(kt_context_s* c, int64_t n_, int ld_) {
         ctx = c;
         ptr = ctx->pool.take(want, &bytes);
     }
-    KT_HIP(hipMemsetAsync(ptr, 0, want, ctx->stream));
+    if (zero) {
+        if (getenv("KT_DEVMAT_FILL") && getenv("KT_DEVMAT_FILL")[0] == '1' && want / 8 < (size_t)1 << 31)
+            KT_HIP(launch_fill(static_cast<double*>(ptr), (int)(want / 8), 0.0, ctx->stream));
+        else
+            KT_HIP(hipMemsetAsync(ptr, 0, want, ctx->stream));
+    }
 }
 
 void DevMat::release() {
@@ -317,7 +323,17 @@ void upload_rows(kt_matrix_s* A, const double* H, int cols, double* D, int ldd) 
         }
         if (sparse) {
             hipStream_t st = A->ctx->stream;
+            static const bool tdbg = getenv("KT_FG_TIMING") && getenv("KT_FG_TIMING")[0] == '1';
+            auto now = [] { return std::chrono::steady_clock::now(); };
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            auto t0 = now();
+            if (tdbg) KT_HIP(hipStreamSynchronize(st));
+            auto t1 = now();
             KT_HIP(hipMemset2DAsync(D, sizeof(double) * ldd, 0, sizeof(double) * cols, (size_t)n, st));
+            if (tdbg) KT_HIP(hipStreamSynchronize(st));
+            auto t2 = now();
+            if (tdbg) fprintf(stderr, "[kt upload_rows] pre-sync %.3f memset2d %.3f ms (n %lld cols %d ldd %d)\n",
+                              ms(t0, t1), ms(t1, t2), (long long)n, cols, ldd);
             const size_t m = off.size();
             if (m) {
                 DevBuf& d = A->ctx->ws.qrtmp;

@@ -38,7 +38,7 @@ struct DevMat {
         return *this;
     }
     ~DevMat() { release(); }
-    void alloc(kt_context_s* ctx, int64_t n_, int ld_);
+    void alloc(kt_context_s* ctx, int64_t n_, int ld_, bool zero = true);
     void release();
     double* col(int c) { return static_cast<double*>(ptr) + c; }
     const double* col(int c) const { return static_cast<const double*>(ptr) + c; }

@@ -188,6 +188,11 @@ struct kt_context_s {
     // workspace) for the projected-matrix work that a block-Krylov run hands
     // to a worker thread while its next step runs here (kt_krylov.cpp)
     kt_context_s* helper = nullptr;
+    // that worker thread (kt_krylov.cpp StepWorker), kept for the context's
+    // lifetime: a HIP thread started and joined per call stalled the next
+    // call's first stream sync by 20-30 ms (profiles/r03_fg_exp_worker.txt)
+    void* step_worker = nullptr;
+    void (*step_worker_free)(void*) = nullptr;
     kt::ProfSlot prof[kt::PROF_NSLOTS];
     kt::Workspace ws;
     kt::ScratchPool pool;  // DevMat scratch (kt_block.h)

@@ -94,6 +94,12 @@ template <int P> using GeoB = GeoW<P, (P >= 16) ? KT_BLK_VW : (P >= 2) ? 2 : 1>;
 // no acquire fence (cdna_hip_programming.md Guideline 16, R1 consume form).
 enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4, KF_NTY = 8, KF_SC1 = 16, KF_LDSC1 = 32 };
 
+// KT_KY_DIAG (diagnostic builds of the y-form pass only, tools/ky_diag.sh; their
+// results are wrong): 1 = gathers + own row, 2 = gathers only, 3 = row streams only
+#ifndef KT_KY_DIAG
+#define KT_KY_DIAG 0
+#endif
+
 typedef unsigned int kt_u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int kt_u32x2 __attribute__((ext_vector_type(2)));
 // VEC doubles of one lane at byte offset `boff` of the buffer, sc1 (write-through)
@@ -635,7 +641,21 @@ __device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s,
                                                double* d2, __amdgpu_buffer_rsrc_t orsrc) {
     using V = VecT<G::VEC>;
     const int64_t off = (int64_t)row * P + p0;
+#if KT_KY_DIAG == 2
+    // diagnostic build (tools/ky_diag.sh): gathers only -- no own-row read, no
+    // y_{j-1} read, no y_{j+1} store; the dots keep the gathered sums live
+#pragma unroll
+    for (int e = 0; e < G::VEC; ++e) d0[e] = fma(s[e], s[e], d0[e]);
+    return;
+#endif
     const typename V::T xi = V::load(X + off);
+#if KT_KY_DIAG == 1
+    // diagnostic build: gathers + the own-row read (alpha's y_j . t), no
+    // y_{j-1} read and no y_{j+1} store
+#pragma unroll
+    for (int e = 0; e < G::VEC; ++e) d0[e] = fma(V::get(xi, e), s[e], d0[e]);
+    return;
+#endif
     if (!Out) {  // last pass: only alpha (X.t) is still needed
 #pragma unroll
         for (int e = 0; e < G::VEC; ++e) d0[e] = fma(V::get(xi, e), s[e], d0[e]);
@@ -863,7 +883,9 @@ __global__ KT_KY_BOUNDS(BLOCK) void k_spmm_lanczos(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+#if KT_KY_DIAG != 3
             gather_row<P, FLAGS, G>(beg + grp, end, G::GPW, p0, col, val, X, s);
+#endif
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
@@ -882,7 +904,9 @@ __global__ KT_KY_BOUNDS(BLOCK) void k_spmm_lanczos(
             double s[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+#if KT_KY_DIAG != 3  // diagnostic build 3: the row streams alone (no column / gather loads)
             gather_row<P, FLAGS, G>(beg, end, 1, p0, col, val, X, s);
+#endif
             row_epilogue_y<P, FLAGS, G, decltype(cg)>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2,
                                            orsrc);
         }

@@ -27,6 +27,7 @@
 
 #include "kt_krylov.h"
 #include "kt_launch.h"
+#include "kt_pool.h"
 
 namespace kt {
 
@@ -621,7 +622,10 @@ struct BlockArnoldi {
                                                            maxblk(maxblk_) {
         PB = pow2_at_least(bs);
         if (PB > 128) fail(KT_ERR_UNSUPPORTED, "block size > 128");
-        V.alloc(ctx, n, maxblk * PB);
+        // V is written block by block (start: block 0 zeroed + the selector;
+        // extend: W's PB columns, zero padding included), so only what a step
+        // reads is ever initialised -- no memset of all maxblk blocks
+        V.alloc(ctx, n, maxblk * PB, false);
         W.alloc(ctx, n, PB);
     }
     int ld() const { return maxblk * PB; }
@@ -637,14 +641,22 @@ struct BlockArnoldi {
     }
 
     void start(const double* U) {
+        PhaseClock pc;
+        KT_HIP(hipMemset2DAsync(blk(0), sizeof(double) * ld(), 0, sizeof(double) * PB, (size_t)n, ctx->stream));
         upload_rows(A, U, bs, blk(0), ld());
+        const double t_up = pc.on ? pc.lap() : 0.0;
         std::vector<double> R;
         block_qr(ctx, n, blk(0), ld(), bs, R);  // [V, ~] = qr(b, 0)   :50
+        if (pc.on) KT_HIP(hipStreamSynchronize(ctx->stream));
+        const double t_qr = pc.on ? pc.lap() : 0.0;
         nblk = 1;
         Hr = bs;
         Hc = 0;
         H.clear();
         add_inf_pole(0);
+        if (pc.on)
+            fprintf(stderr, "[kt arnoldi start] n %lld bs %d ld %d: upload %.3f qr %.3f first pole %.3f ms\n",
+                    (long long)n, bs, ld(), t_up, t_qr, pc.lap());
     }
     void extend() { add_inf_pole(nblk - 1); }
 
@@ -742,9 +754,11 @@ static std::vector<double> top_left(const std::vector<double>& M, int Mr, int nn
 // ---------------------------------------------------------------------------
 // In-order worker thread for the projected-matrix work of a block-Krylov run
 // (trace_fun_update / fun_update): job k runs while the caller's thread
-// extends the basis by one more step.  wait(k) blocks until jobs 0..k have
-// finished and rethrows the first failure; once a job failed the rest are
-// skipped.  The destructor drops jobs not yet started and joins.
+// extends the basis by one more step.  wait(k) blocks until jobs 0..k of the
+// current run have finished and rethrows the first failure; once a job failed
+// the rest are skipped.  finish() ends a run: it drops the jobs not yet
+// started, waits for the running one and resets the job count, so the thread
+// serves the next run (one thread per context, ctx->step_worker).
 // ---------------------------------------------------------------------------
 class StepWorker {
    public:
@@ -759,6 +773,13 @@ class StepWorker {
         }
         cv_.notify_all();
         th_.join();
+    }
+    void finish() {
+        std::unique_lock<std::mutex> lk(m_);
+        q_.clear();
+        done_cv_.wait(lk, [&] { return !busy_; });
+        done_ = 0;
+        err_ = nullptr;
     }
     void submit(std::function<void()> f) {
         {
@@ -784,6 +805,7 @@ class StepWorker {
                 if (q_.empty()) return;  // stop_ with nothing queued
                 f = std::move(q_.front());
                 q_.pop_front();
+                busy_ = true;
             }
             std::exception_ptr e;
             if (!err_) {
@@ -797,6 +819,7 @@ class StepWorker {
                 std::lock_guard<std::mutex> lk(m_);
                 if (e && !err_) err_ = e;
                 ++done_;
+                busy_ = false;
             }
             done_cv_.notify_all();
         }
@@ -806,9 +829,34 @@ class StepWorker {
     std::condition_variable cv_, done_cv_;
     std::deque<std::function<void()>> q_;
     int done_ = 0;
-    bool stop_ = false;
+    bool stop_ = false, busy_ = false;
     std::exception_ptr err_;
     std::thread th_;
+};
+
+// The context's persistent worker thread (created on first use); a run ends
+// with RunWorker's finish(), so the next run starts with an idle worker.
+static StepWorker* step_worker(kt_context_s* ctx) {
+    if (!ctx->step_worker) {
+        ctx->step_worker = new StepWorker(ctx->device);
+        ctx->step_worker_free = [](void* p) { delete static_cast<StepWorker*>(p); };
+    }
+    return static_cast<StepWorker*>(ctx->step_worker);
+}
+// Scoped use of it by one run: finish() on every exit path, before the run's
+// steps / Xstop (captured by reference in the queued jobs) go out of scope.
+struct RunWorker {
+    StepWorker* w = nullptr;
+    RunWorker() = default;
+    RunWorker(const RunWorker&) = delete;
+    RunWorker& operator=(const RunWorker&) = delete;
+    ~RunWorker() { reset(); }
+    void reset(StepWorker* nw = nullptr) {
+        if (w) w->finish();
+        w = nw;
+    }
+    StepWorker* operator->() const { return w; }
+    explicit operator bool() const { return w != nullptr; }
 };
 
 // The context a pipelined block-Krylov run hands its projected work to
@@ -887,8 +935,8 @@ double trace_fun_update_impl(kt_matrix_s* A, int rk, const double* U, const doub
         }
     };
     kt_context_s* hctx = pipeline_helper(ctx, "KT_TFU_PIPE");
-    std::unique_ptr<StepWorker> W;  // destroyed (joined) before steps / Xstop
-    if (hctx) W.reset(new StepWorker(ctx->device));
+    RunWorker W;  // finished before steps / Xstop go out of scope
+    if (hctx) W.reset(step_worker(ctx));
     std::vector<double> Cm;
     int jfin = 0;
     PhaseClock pc;
@@ -971,7 +1019,23 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
     FunUpdateResult res;
     // basis never needs more than ~n/2 columns before the dense fallback (:85)
     const int maxblk = (int)std::min<int64_t>(it + 1, n / (2 * (int64_t)rk) + 2);
+    PhaseClock pc0;
+    if (pc0.on) {
+        KT_HIP(hipStreamSynchronize(ctx->stream));
+        const double ts = pc0.lap();
+        KT_HIP(hipDeviceSynchronize());
+        fprintf(stderr, "[kt fu] entry: stream drained %.3f ms, device drained %.3f ms\n", ts, pc0.lap());
+    }
     res.basis.reset(new BlockArnoldi(A, rk, std::max(maxblk, 2)));
+    if (pc0.on) {
+        const double ta = pc0.lap();
+        long spins = 0;
+        while (hipStreamQuery(ctx->stream) == hipErrorNotReady) ++spins;
+        fprintf(stderr, "[kt fu] query-spin %.3f ms (%ld polls)\n", pc0.lap(), spins);
+        KT_HIP(hipStreamSynchronize(ctx->stream));
+        fprintf(stderr, "[kt fu] basis alloc %.3f ms, its memset drained %.3f ms (maxblk %d, %zu bytes, pool held %zu, free %zu)\n",
+                ta, pc0.lap(), maxblk, res.basis->V.bytes, ctx->pool.held, ctx->pool.free.size());
+    }
     BlockArnoldi& Ar = *res.basis;
     const int d = 2;
     // Step j's projected work -- Xm = f(tGm) - f(Gm) (:93-106) and the stop
@@ -1010,20 +1074,22 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
         }
     };
     kt_context_s* hctx = pipeline_helper(ctx, "KT_FU_PIPE");
-    std::unique_ptr<StepWorker> W;  // destroyed (joined) before steps / Xstop
-    if (hctx) W.reset(new StepWorker(ctx->device));
+    RunWorker W;  // finished before steps / Xstop go out of scope
+    if (hctx) W.reset(step_worker(ctx));
     std::vector<double> Cm;
     int jfin = 0;
     PhaseClock pc;
     for (int j = 1; j <= it; ++j) {
         if (j == 1) {
             Ar.start(U);                                                     // :79
+            if (pc.on) fprintf(stderr, "[kt fu] Ar.start %.3f ms\n", pc.lap());
             Cm = make_Cm(ctx, A, Ar.blk(0), Ar.ld(), rk, U, rk, B);         // :80-81
         } else {
             Ar.extend();                                                     // :83
         }
         steps[j].lucky = Ar.lucky;
         const double t_ext = pc.on ? pc.lap() : 0.0;
+        if (pc.on && j == 1) fprintf(stderr, "[kt fu] start %.3f ms\n", t_ext);
         // the previous step's decision (its work ran during this extension)
         if (W && j >= 2) {
             W->wait(j - 2);
@@ -1078,7 +1144,19 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
             }
         }
     }
+    if (pc.on) pc.lap();
     W.reset();
+    if (pc.on) {
+        fprintf(stderr, "[kt fu] join %.3f ms\n", pc.lap());
+        if (hctx) {
+            long spins = 0;
+            while (hipStreamQuery(hctx->stream) == hipErrorNotReady) ++spins;
+            fprintf(stderr, "[kt fu] helper stream query-spin %.3f ms (%ld polls)\n", pc.lap(), spins);
+        }
+        long spins = 0;
+        while (hipStreamQuery(ctx->stream) == hipErrorNotReady) ++spins;
+        fprintf(stderr, "[kt fu] main stream query-spin %.3f ms (%ld polls)\n", pc.lap(), spins);
+    }
     Step& S = steps[jfin];
     res.Xm.swap(S.F1);
     res.nx = S.nn;
@@ -1181,19 +1259,26 @@ static void gradient(kt_matrix_s* A, FunUpdateResult& fu, int64_t nom, const dou
     std::vector<double> R;  // (2 nom) x (nblk PB), padded columns
     download_rows(A, Ar.V.col(0), Ar.ld(), Ar.nblk * Ar.PB, rows, R);
     const int nr = (int)rows.size();
-    auto um = [&](int r, int col) {  // Um(row r, unpadded column col)
-        const int b = col / Ar.bs, c = col % Ar.bs;
-        return R[r + (size_t)(b * Ar.PB + c) * nr];
-    };
-    for (int64_t t = 0; t < nom; ++t) {
+    // Um's rows O1_k, O2_k as contiguous nx-vectors (unpadded columns)
+    std::vector<double> Ur((size_t)nr * nx);
+    for (int col = 0; col < nx; ++col) {
+        const int pc = (col / Ar.bs) * Ar.PB + col % Ar.bs;
+        for (int r = 0; r < nr; ++r) Ur[(size_t)r * nx + col] = R[r + (size_t)pc * nr];
+    }
+    // one entry per task on the host pool (nom x nx^2 FMAs: 2.5 M for |Omega|
+    // = 30 at nx = 290, ~3 ms on one thread); same summation order as before
+    HostPool::get().run((int)nom, [&](int t) {
+        const double* u1 = Ur.data() + (size_t)t * nx;
+        const double* u2 = Ur.data() + (size_t)(t + nom) * nx;
         double s = 0.0;
         for (int b = 0; b < nx; ++b) {
+            const double* xc = fu.Xm.data() + (size_t)b * nx;
             double xb = 0.0;
-            for (int a = 0; a < nx; ++a) xb += um((int)t, a) * fu.Xm[a + (size_t)b * nx];
-            s += xb * um((int)(t + nom), b);
+            for (int a = 0; a < nx; ++a) xb += u1[a] * xc[a];
+            s += xb * u2[b];
         }
         gr[t] = -2.0 * (base[t] + s);
-    }
+    });
 }
 
 // Second device copy of A on its own context (stream + workspace), rebuilt
@@ -1371,11 +1456,14 @@ int kt_fun_and_grad_krylov_exp(kt_matrix_t A, int64_t nom, const double* X, cons
     std::vector<double> U, B;
     lowrank_from_edges(A->n, nom, X, Omega, aux, U, B);
     const int k = (int)aux.size();
+    PhaseClock pc;
     FunUpdateResult fu = fun_update_impl(A, k, U.data(), B.data(), KT_FUN_EXP, tol * std::exp(nrmA), it);  // :83
+    const double t_fu = pc.on ? pc.lap() : 0.0;
     double tr = 0.0;
     for (int i = 0; i < fu.nx; ++i) tr += fu.Xm[i + (size_t)i * fu.nx];
     *f = -tr;                                                                 // :84
     gradient(A, fu, nom, Omega, eA, gr);                                      // :85-88
+    if (pc.on) fprintf(stderr, "[kt fg_exp] fun_update %.3f ms, gradient %.3f ms\n", t_fu, pc.lap());
     KT_CATCH
 }
 

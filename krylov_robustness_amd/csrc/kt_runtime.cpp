@@ -306,6 +306,10 @@ int kt_context_create(int device, kt_context_t* out) {
 int kt_context_destroy(kt_context_t ctx) {
     KT_GUARD_BEGIN
     if (!ctx) return KT_OK;
+    if (ctx->step_worker) {  // joined before the helper context it drives goes away
+        ctx->step_worker_free(ctx->step_worker);
+        ctx->step_worker = nullptr;
+    }
     if (ctx->helper) {
         (void)kt_context_destroy(ctx->helper);
         ctx->helper = nullptr;

@@ -368,6 +368,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         }
         KT_HIP(hipStreamSynchronize(ctx->stream));
         for (int l = 1; l < lanes; ++l) KT_HIP(hipStreamSynchronize(ctx->aux_stream[l - 1]));
+#ifndef KT_KY_DIAG  // (diagnostic builds time the pass alone: no redo)
         if (ctx->yform) {  // sweeps with a guarded probe are redone by the explicit CGS2 sweep
             int64_t redone = 0;
             for (int64_t s = 0; s < nsweeps; ++s) {
@@ -383,6 +384,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
             }
             ctx->yform_redone += redone;
         }
+#endif
         prof_collect(ctx);
 
         std::vector<double> qv((size_t)nprobes);
