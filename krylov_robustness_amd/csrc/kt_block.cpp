@@ -4,7 +4,6 @@
 #include <cstring>
 
 #include "kt_block.h"
-#include <chrono>
 
 #include <rocsolver/rocsolver.h>
 
@@ -93,12 +92,7 @@ void DevMat::alloc(kt_context_s* c, int64_t n_, int ld_, bool zero) {
         ctx = c;
         ptr = ctx->pool.take(want, &bytes);
     }
-    if (zero) {
-        if (getenv("KT_DEVMAT_FILL") && getenv("KT_DEVMAT_FILL")[0] == '1' && want / 8 < (size_t)1 << 31)
-            KT_HIP(launch_fill(static_cast<double*>(ptr), (int)(want / 8), 0.0, ctx->stream));
-        else
-            KT_HIP(hipMemsetAsync(ptr, 0, want, ctx->stream));
-    }
+    if (zero) KT_HIP(hipMemsetAsync(ptr, 0, want, ctx->stream));
 }
 
 void DevMat::release() {
@@ -132,11 +126,17 @@ void gram(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const 
     std::memcpy(G.data(), pb.ptr, sizeof(double) * G.size());
 }
 
-// KT_GEMM_ROCBLAS=1: gram / combine through rocBLAS dgemm (the A/B switch of
-// kt_gemm_ts.hip); read per call
-static bool rocblas_gemm_path() {
+// gram / combine go through kt_gemm_ts.hip for tall blocks and through
+// rocBLAS dgemm below KT_GEMM_TS_MIN_N rows (default 8192): on India (n =
+// 3,228) the pipelined fun_update with the ts kernels stalled 20-30 ms at the
+// first stream operation of every call (profiles/r03_fg_exp_stall.txt), with
+// rocBLAS not.  KT_GEMM_ROCBLAS=1 forces rocBLAS for every n (A/B); read per call
+static bool rocblas_gemm_path(int64_t n) {
     const char* e = getenv("KT_GEMM_ROCBLAS");
-    return e && e[0] == '1';
+    if (e && e[0] == '1') return true;
+    const char* m = getenv("KT_GEMM_TS_MIN_N");
+    const int64_t min_n = m ? std::atoll(m) : 8192;
+    return n < min_n;
 }
 
 const double* gram_device(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* Y,
@@ -149,7 +149,7 @@ const double* gram_device(kt_context_s* ctx, int64_t n, const double* X, int ldx
     }
     const double one = 1.0, zero = 0.0;
     const int64_t count = (int64_t)px * py;
-    if (!rocblas_gemm_path()) {  // kt_gemm_ts.hip: MFMA row-chunk partials + fixed-order slab sum
+    if (!rocblas_gemm_path(n)) {  // kt_gemm_ts.hip: MFMA row-chunk partials + fixed-order slab sum
         const int S = gram_ts_chunks(n);
         d.ensure(sizeof(double) * (size_t)count * (S + 1));
         KT_HIP(launch_gram_ts(n, X, ldx, px, Y, ldy, py, d.as<double>() + count, d.as<double>(), ctx->stream));
@@ -188,7 +188,7 @@ const double* gram_device(kt_context_s* ctx, int64_t n, const double* X, int ldx
 void combine_device(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* dC, int q,
                     double alpha, double beta, double* Y, int ldy) {
     if (q == 0 || px == 0) return;
-    if (!rocblas_gemm_path()) {
+    if (!rocblas_gemm_path(n)) {
         KT_HIP(launch_combine_ts(n, X, ldx, px, dC, q, alpha, beta, Y, ldy, ctx->stream));
         return;
     }
@@ -231,7 +231,7 @@ void combine(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px,
     KT_HIP(hipEventRecord(ws.comb_ev, ctx->stream));
     ws.comb_pending = true;
     // Yc (q x n) = beta Yc + C' (q x px) * Xc (px x n)
-    if (!rocblas_gemm_path()) {
+    if (!rocblas_gemm_path(n)) {
         KT_HIP(launch_combine_ts(n, X, ldx, px, d.as<double>(), q, 1.0, beta, Y, ldy, ctx->stream));
         return;
     }
@@ -323,17 +323,7 @@ void upload_rows(kt_matrix_s* A, const double* H, int cols, double* D, int ldd) 
         }
         if (sparse) {
             hipStream_t st = A->ctx->stream;
-            static const bool tdbg = getenv("KT_FG_TIMING") && getenv("KT_FG_TIMING")[0] == '1';
-            auto now = [] { return std::chrono::steady_clock::now(); };
-            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-            auto t0 = now();
-            if (tdbg) KT_HIP(hipStreamSynchronize(st));
-            auto t1 = now();
             KT_HIP(hipMemset2DAsync(D, sizeof(double) * ldd, 0, sizeof(double) * cols, (size_t)n, st));
-            if (tdbg) KT_HIP(hipStreamSynchronize(st));
-            auto t2 = now();
-            if (tdbg) fprintf(stderr, "[kt upload_rows] pre-sync %.3f memset2d %.3f ms (n %lld cols %d ldd %d)\n",
-                              ms(t0, t1), ms(t1, t2), (long long)n, cols, ldd);
             const size_t m = off.size();
             if (m) {
                 DevBuf& d = A->ctx->ws.qrtmp;
@@ -497,7 +487,7 @@ namespace kt {
 static void apply_rinv(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, const std::vector<double>& R) {
     std::vector<double> Ri((size_t)bs * bs);
     tri_upper_inv(R.data(), bs, Ri.data());
-    if (bs <= 32 && !rocblas_gemm_path()) {
+    if (bs <= 32 && !rocblas_gemm_path(n)) {
         // in place: k_combine_ts has ONE workgroup per 64 rows when q <= 32,
         // and it reads all of its rows' X before it writes any Y
         combine(ctx, n, W, ld, bs, Ri, bs, 0.0, W, ld);

@@ -1019,23 +1019,7 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
     FunUpdateResult res;
     // basis never needs more than ~n/2 columns before the dense fallback (:85)
     const int maxblk = (int)std::min<int64_t>(it + 1, n / (2 * (int64_t)rk) + 2);
-    PhaseClock pc0;
-    if (pc0.on) {
-        KT_HIP(hipStreamSynchronize(ctx->stream));
-        const double ts = pc0.lap();
-        KT_HIP(hipDeviceSynchronize());
-        fprintf(stderr, "[kt fu] entry: stream drained %.3f ms, device drained %.3f ms\n", ts, pc0.lap());
-    }
     res.basis.reset(new BlockArnoldi(A, rk, std::max(maxblk, 2)));
-    if (pc0.on) {
-        const double ta = pc0.lap();
-        long spins = 0;
-        while (hipStreamQuery(ctx->stream) == hipErrorNotReady) ++spins;
-        fprintf(stderr, "[kt fu] query-spin %.3f ms (%ld polls)\n", pc0.lap(), spins);
-        KT_HIP(hipStreamSynchronize(ctx->stream));
-        fprintf(stderr, "[kt fu] basis alloc %.3f ms, its memset drained %.3f ms (maxblk %d, %zu bytes, pool held %zu, free %zu)\n",
-                ta, pc0.lap(), maxblk, res.basis->V.bytes, ctx->pool.held, ctx->pool.free.size());
-    }
     BlockArnoldi& Ar = *res.basis;
     const int d = 2;
     // Step j's projected work -- Xm = f(tGm) - f(Gm) (:93-106) and the stop
@@ -1146,17 +1130,7 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
     }
     if (pc.on) pc.lap();
     W.reset();
-    if (pc.on) {
-        fprintf(stderr, "[kt fu] join %.3f ms\n", pc.lap());
-        if (hctx) {
-            long spins = 0;
-            while (hipStreamQuery(hctx->stream) == hipErrorNotReady) ++spins;
-            fprintf(stderr, "[kt fu] helper stream query-spin %.3f ms (%ld polls)\n", pc.lap(), spins);
-        }
-        long spins = 0;
-        while (hipStreamQuery(ctx->stream) == hipErrorNotReady) ++spins;
-        fprintf(stderr, "[kt fu] main stream query-spin %.3f ms (%ld polls)\n", pc.lap(), spins);
-    }
+    if (pc.on) fprintf(stderr, "[kt fu] join %.3f ms\n", pc.lap());
     Step& S = steps[jfin];
     res.Xm.swap(S.F1);
     res.nx = S.nn;

@@ -253,9 +253,10 @@ def _ishermitian(B):
     return B.shape[0] == B.shape[1] and np.array_equal(B, B.T)
 
 
-def trace_fun_update(A, U, B, tol=1e-12, it=None, debug=0, fun="exp"):
+def trace_fun_update(A, U, B, tol=1e-12, it=None, debug=0, fun="exp", hist=None):
     """[Xm, iter, lucky] = trace_fun_update(A, U, B, tol, it, debug, fun)
-    (trace_fun_update.m:1-135)."""
+    (trace_fun_update.m:1-135).  hist (test aid, not in the reference): a list
+    that receives (j, err, Xm) for every lag-2 stop test evaluated."""
     U = np.asarray(U, dtype=np.float64)
     if U.ndim == 1:
         U = U[:, None]
@@ -303,6 +304,8 @@ def trace_fun_update(A, U, B, tol=1e-12, it=None, debug=0, fun="exp"):
             Xstop[j - 1] = Xm
         else:
             err = abs(Xm - Xstop[0])
+            if hist is not None:
+                hist.append((j, err, Xm))
             if err < tol:
                 break
             Xstop = np.array([*Xstop[1:d], Xm])

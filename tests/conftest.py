@@ -57,3 +57,22 @@ def values():
 def gpu_ctx():
     import krylov_robustness_amd as kra
     return kra.Context(0)
+
+
+def iter_matches(it_dev, it_oracle, hist, tol, rel=1e-11):
+    """Iteration counts of a lag-2 stop test (trace_fun_update.m:104-118) agree
+    exactly, or differ by one step where the oracle's decision at that step was
+    marginal: |err - tol| <= rel max(|Xm|, tol), the band that the device's
+    rounding-level difference in Xm (measured <= 1e-12 relative on these
+    graphs) can move err across.
+    hist: the oracle's [(j, err, Xm), ...] (krylov_oracle.trace_fun_update)."""
+    it_dev, it_oracle = int(it_dev), int(it_oracle)
+    if it_dev == it_oracle:
+        return True
+    if abs(it_dev - it_oracle) != 1:
+        return False
+    j = min(it_dev, it_oracle)  # one side stopped here, the other did not
+    for jj, err, xm in hist:
+        if jj == j:
+            return abs(err - tol) <= rel * max(abs(xm), tol)
+    return False

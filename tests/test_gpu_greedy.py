@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import scipy.sparse as sp
 
-from conftest import load_graph
+from conftest import iter_matches, load_graph
 from oracle import krylov_oracle as ko
 
 pytestmark = pytest.mark.gpu
@@ -50,9 +50,10 @@ def test_pairs_match_single_calls_and_oracle(kra, gpu_ctx):
         x1, i1, l1 = kra.trace_fun_update(D, _U(A.shape[0], *E[h]), BREAK, tol, 100, ctx=gpu_ctx)
         assert xm[h] == pytest.approx(x1, rel=1e-9, abs=1e-12)
         assert (it[h], lk[h]) == (i1, l1)
-        xo, io, lo = ko.trace_fun_update(A, _U(A.shape[0], *E[h]), BREAK, tol, 100)
+        hist = []
+        xo, io, lo = ko.trace_fun_update(A, _U(A.shape[0], *E[h]), BREAK, tol, 100, hist=hist)
         assert xm[h] == pytest.approx(xo, rel=1e-7, abs=tol)
-        assert abs(int(it[h]) - io) <= 1
+        assert iter_matches(it[h], io, hist, tol), (E[h], int(it[h]), io, hist[-3:])
 
 
 def test_pairs_leaf_candidates_rank_deficient(kra, gpu_ctx):
