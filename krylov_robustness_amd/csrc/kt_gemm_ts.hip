@@ -216,35 +216,43 @@ hipError_t launch_combine_ts(int64_t n, const double* X, int ldx, int px, const 
 // One workgroup: the Frobenius norm^2 and the largest column norm^2 of the
 // n x n column-major M into out[0], out[1], then M /= ||M||_F in place (the
 // normalised repeated squaring of the fun_update stop test, kt_krylov.cpp).
-// Fixed-order reductions: deterministic.
+// One wave per column (lanes down the column: coalesced; a thread per column
+// walked 225-long strided columns, 75 us at n = 225), fixed-order reductions:
+// deterministic.
 __global__ __launch_bounds__(1024) void k_fro_colmax_scale(int n, double* __restrict__ M,
                                                           double* __restrict__ out) {
-    __shared__ double s_sum[1024], s_max[1024];
-    double sum = 0.0, mx = 0.0;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    constexpr int kWaves = 1024 / 64;
+    __shared__ double s_sum[kWaves], s_max[kWaves];
+    __shared__ double s_inv;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    double sum = 0.0, mx = 0.0;  // this wave's columns, in column order (lane 0's copy is used)
+    for (int j = wave; j < n; j += kWaves) {
         const double* col = M + (int64_t)j * n;
         double c = 0.0;
-        for (int i = 0; i < n; ++i) c = fma(col[i], col[i], c);
+        for (int i = lane; i < n; i += 64) c = fma(col[i], col[i], c);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
         sum += c;
         mx = fmax(mx, c);
     }
-    s_sum[threadIdx.x] = sum;
-    s_max[threadIdx.x] = mx;
+    if (lane == 0) {
+        s_sum[wave] = sum;
+        s_max[wave] = mx;
+    }
     __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) {
-            s_sum[threadIdx.x] += s_sum[threadIdx.x + o];
-            s_max[threadIdx.x] = fmax(s_max[threadIdx.x], s_max[threadIdx.x + o]);
-        }
-        __syncthreads();
-    }
-    const double fro2 = s_sum[0];
     if (threadIdx.x == 0) {
-        out[0] = fro2;
-        out[1] = s_max[0];
+        double f = 0.0, m = 0.0;
+        for (int w = 0; w < kWaves; ++w) {
+            f += s_sum[w];
+            m = fmax(m, s_max[w]);
+        }
+        out[0] = f;
+        out[1] = m;
+        s_inv = f > 0.0 ? 1.0 / sqrt(f) : 0.0;
     }
-    if (!(fro2 > 0.0)) return;
-    const double inv = 1.0 / sqrt(fro2);
+    __syncthreads();
+    const double inv = s_inv;
+    if (!(inv > 0.0)) return;
     const int64_t nn = (int64_t)n * n;
     for (int64_t t = threadIdx.x; t < nn; t += blockDim.x) M[t] *= inv;
 }

@@ -110,6 +110,125 @@ __global__ __launch_bounds__(kTsBlock) void k_ts_step(int n, int bs, int BP, int
     }
 }
 
+// ---------------------------------------------------------------------------
+// The reflector sweep with ONE launch per column (k_ts_step1, default where
+// the grid fits): every workgroup first sums the previous launch's
+// per-workgroup partials itself -- the same fixed order in every workgroup,
+// so every workgroup derives identical coefficients -- and reads the pivot
+// row the previous launch snapshotted; then it applies H_k to its rows
+// (kTs1Rows per workgroup, 1024 threads) and leaves the next column's
+// partials and pivot row in the other half of two ping-pong buffers.  The
+// per-column reduce launch of the two-launch form goes away (bs + 1 launches
+// instead of 2 bs + 1); the sums group rows by workgroup instead of by
+// 64-row block, i.e. rounding-level differences from that form.
+// part: 2 x [BP][G] doubles, piv: 2 x BP doubles (slot = (k + 1) & 1 written).
+// ---------------------------------------------------------------------------
+constexpr int kTs1Block = 1024;
+constexpr int kTs1Rows = 384;
+constexpr int kTs1MaxG = 128;
+
+__global__ __launch_bounds__(kTs1Block) void k_ts_step1(int n, int bs, int BP, int k, int G, int rows_per_wg,
+                                                        double* __restrict__ W, int ld, double* __restrict__ V,
+                                                        double* __restrict__ part, double* __restrict__ piv,
+                                                        double* __restrict__ taus) {
+    __shared__ double s_sums[128], s_piv[128];
+    __shared__ double red[kTs1Block];
+    const int tid = threadIdx.x;
+    const int c = tid % BP;
+    const int sub = tid / BP;
+    const int rpi = kTs1Block / BP;
+    const int kn = k + 1;
+    const double* part_in = part + (size_t)(k & 1) * BP * G;   // written by launch k - 1
+    double* part_out = part + (size_t)(kn & 1) * BP * G;
+    const double* piv_in = piv + (size_t)(k & 1) * BP;
+    double* piv_out = piv + (size_t)(kn & 1) * BP;
+    double beta = 0.0, tau = 0.0, scal = 1.0, tc = 0.0, tn = 0.0;
+    if (k >= 0) {
+        // sums[j], j in [k, bs): one wave per column, lanes strided over the
+        // G partials, then a fixed xor tree -- identical in every workgroup
+        const int lane = tid & 63, wave = tid >> 6;
+        for (int j = k + wave; j < bs; j += kTs1Block / 64) {
+            double sm = 0.0;
+            for (int i = lane; i < G; i += 64) sm += part_in[(size_t)j * G + i];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+            if (lane == 0) s_sums[j] = sm;
+        }
+        if (tid < bs) s_piv[tid] = piv_in[tid];
+        __syncthreads();
+        ts_larfg(s_piv[k], s_sums[k], beta, tau, scal);
+        if (c > k && c < bs) tc = s_piv[c] + scal * s_sums[c];
+        if (kn < bs) tn = s_piv[kn] + scal * s_sums[kn];
+        if (blockIdx.x == 0 && tid == 0) taus[k] = tau;
+    }
+    const int r0 = blockIdx.x * rows_per_wg;
+    const int r1 = min(n, r0 + rows_per_wg);
+    const int rstart = max(r0, k < 0 ? 0 : k);
+    double acc = 0.0;
+    constexpr int kTsU = 8;  // as k_ts_step: all loads of a chunk before its barrier
+    for (int base0 = rstart; base0 < r1; base0 += kTsU * rpi) {
+        double wk[kTsU], wn[kTsU], wc[kTsU];
+#pragma unroll
+        for (int u = 0; u < kTsU; ++u) {
+            const int r = base0 + u * rpi + sub;
+            const bool live = r < r1 && c < bs;
+            wk[u] = (live && k >= 0) ? W[(int64_t)r * ld + k] : 0.0;
+            wn[u] = (live && kn < bs) ? W[(int64_t)r * ld + kn] : 0.0;
+            wc[u] = live ? W[(int64_t)r * ld + c] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kTsU; ++u) {
+            const int r = base0 + u * rpi + sub;
+            if (!(r < r1 && c < bs)) continue;
+            double v = 0.0;
+            double wcu = wc[u];
+            if (k >= 0) {
+                v = (r == k) ? 1.0 : wk[u] * scal;
+                if (c == k) {
+                    V[(int64_t)r * BP + k] = v;
+                    if (r == k) W[(int64_t)r * ld + k] = beta;
+                } else if (c > k) {
+                    wcu -= tau * v * tc;
+                    W[(int64_t)r * ld + c] = wcu;
+                }
+            }
+            if (kn < bs && r == kn) piv_out[c] = wcu;  // the next pivot row, W(kn, :) after H_k
+            if (kn < bs && c >= kn && r > kn) {
+                const double wn_new = k >= 0 ? wn[u] - tau * v * tn : wn[u];
+                acc = fma(wn_new, wcu, acc);
+            }
+        }
+    }
+    if (kn >= bs) return;
+    red[tid] = acc;
+    __syncthreads();
+    if (tid < BP) {
+        double sm = 0.0;
+        for (int q = 0; q < rpi; ++q) sm += red[q * BP + tid];
+        part_out[(size_t)tid * G + blockIdx.x] = sm;
+    }
+}
+
+// rows per workgroup and grid of the one-launch-per-column sweep; 0 when n
+// needs more than kTs1MaxG workgroups (the two-launch form then)
+int ts_step1_grid(int n, int* rows_per_wg) {
+    const int G = (n + kTs1Rows - 1) / kTs1Rows;
+    if (G > kTs1MaxG || G < 1) return 0;
+    *rows_per_wg = (n + G - 1) / G;
+    return G;
+}
+
+hipError_t launch_ts_reflectors1(int n, int bs, int BP, double* W, int ld, double* V, double* part, double* piv,
+                                 double* taus, hipStream_t st) {
+    int rpw = 0;
+    const int G = ts_step1_grid(n, &rpw);
+    if (!G || BP > 128) return hipErrorInvalidValue;
+    for (int k = -1; k < bs; ++k)
+        k_ts_step1<<<G, kTs1Block, 0, st>>>(n, bs, BP, k, G, rpw, W, ld, V, part, piv, taus);
+    return hipGetLastError();
+}
+
 // sums[j] = sum_b part[j][b] for j in [kn, bs); pivot[j] = W(kn, j) for all j
 __global__ __launch_bounds__(256) void k_ts_reduce(int bs, int kn, int nrb,
                                                    const double* __restrict__ part,
