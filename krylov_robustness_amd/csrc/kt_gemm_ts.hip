@@ -22,6 +22,7 @@
 // staged in LDS 64 x 64 at a time (C read as broadcasts).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "kt_launch.h"
@@ -213,52 +214,67 @@ hipError_t launch_combine_ts(int64_t n, const double* X, int ldx, int px, const 
     return hipGetLastError();
 }
 
-// One workgroup: the Frobenius norm^2 and the largest column norm^2 of the
-// n x n column-major M into out[0], out[1], then M /= ||M||_F in place (the
+// The Frobenius norm^2 and the largest column norm^2 of the n x n
+// column-major M into out[0], out[1], then M /= ||M||_F in place (the
 // normalised repeated squaring of the fun_update stop test, kt_krylov.cpp).
-// One wave per column (lanes down the column: coalesced; a thread per column
-// walked 225-long strided columns, 75 us at n = 225), fixed-order reductions:
-// deterministic.
-__global__ __launch_bounds__(1024) void k_fro_colmax_scale(int n, double* __restrict__ M,
-                                                          double* __restrict__ out) {
-    constexpr int kWaves = 1024 / 64;
-    __shared__ double s_sum[kWaves], s_max[kWaves];
-    __shared__ double s_inv;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    double sum = 0.0, mx = 0.0;  // this wave's columns, in column order (lane 0's copy is used)
-    for (int j = wave; j < n; j += kWaves) {
-        const double* col = M + (int64_t)j * n;
-        double c = 0.0;
-        for (int i = lane; i < n; i += 64) c = fma(col[i], col[i], c);
+// Two launches: one wave per column writes its squared norm (lanes down the
+// column, coalesced); then every workgroup of the scaling launch reduces the
+// n column norms itself in one fixed order (the same f and max everywhere:
+// deterministic) and scales its slice.  (One workgroup doing both walked the
+// matrix with a memory latency per element: 75 us at n = 225.)
+__global__ __launch_bounds__(256) void k_colsq(int n, const double* __restrict__ M, double* __restrict__ colsq) {
+    const int lane = threadIdx.x & 63;
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= n) return;
+    const double* col = M + (int64_t)j * n;
+    double c = 0.0;
+    for (int i = lane; i < n; i += 64) c = fma(col[i], col[i], c);
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-        sum += c;
-        mx = fmax(mx, c);
-    }
-    if (lane == 0) {
-        s_sum[wave] = sum;
-        s_max[wave] = mx;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double f = 0.0, m = 0.0;
-        for (int w = 0; w < kWaves; ++w) {
-            f += s_sum[w];
-            m = fmax(m, s_max[w]);
-        }
-        out[0] = f;
-        out[1] = m;
-        s_inv = f > 0.0 ? 1.0 / sqrt(f) : 0.0;
-    }
-    __syncthreads();
-    const double inv = s_inv;
-    if (!(inv > 0.0)) return;
-    const int64_t nn = (int64_t)n * n;
-    for (int64_t t = threadIdx.x; t < nn; t += blockDim.x) M[t] *= inv;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0) colsq[j] = c;
 }
 
-hipError_t launch_fro_colmax_scale(int n, double* M, double* out, hipStream_t st) {
-    k_fro_colmax_scale<<<1, 1024, 0, st>>>(n, M, out);
+__global__ __launch_bounds__(256) void k_fro_scale(int n, double* __restrict__ M, const double* __restrict__ colsq,
+                                                   double* __restrict__ out) {
+    __shared__ double s_f;
+    if (threadIdx.x < 64) {  // wave 0: lanes strided over the columns, then a fixed xor tree
+        const int lane = threadIdx.x;
+        double f = 0.0, m = 0.0;
+        for (int j = lane; j < n; j += 64) {
+            const double c = colsq[j];
+            f += c;
+            m = fmax(m, c);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            f += __shfl_xor(f, o, 64);
+            m = fmax(m, __shfl_xor(m, o, 64));
+        }
+        if (lane == 0) {
+            s_f = f;
+            if (blockIdx.x == 0) {
+                out[0] = f;
+                out[1] = m;
+            }
+        }
+    }
+    __syncthreads();
+    const double f = s_f;
+    if (!(f > 0.0)) return;
+    const double inv = 1.0 / sqrt(f);
+    const int64_t nn = (int64_t)n * n;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nn; t += (int64_t)gridDim.x * blockDim.x)
+        M[t] *= inv;
+}
+
+hipError_t launch_fro_colmax_scale(int n, double* M, double* out, double* colsq, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    k_colsq<<<(n + 3) / 4, 256, 0, st>>>(n, M, colsq);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t nn = (int64_t)n * n;
+    const int grid = (int)std::min<int64_t>(256, (nn + 256 * 4 - 1) / (256 * 4));
+    k_fro_scale<<<grid, 256, 0, st>>>(n, M, colsq, out);
     return hipGetLastError();
 }
 

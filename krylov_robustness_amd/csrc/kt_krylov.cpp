@@ -394,10 +394,11 @@ static bool sym_norm2_power_bounds(kt_context_s* ctx, int n, const std::vector<d
     constexpr int K = 6;
     const size_t nn = (size_t)n * n;
     DevBuf& b = ctx->ws.expm;
-    b.ensure(sizeof(double) * (2 * nn + 2 * K + 2));
+    b.ensure(sizeof(double) * (2 * nn + 2 * K + 2 + (size_t)n));
     double* M0 = b.as<double>();
     double* M1 = M0 + nn;
     double* out = M1 + nn;
+    double* colsq = out + 2 * K + 2;
     const double s0 = std::sqrt(fro2);
     std::vector<double> N0(nn);
     for (size_t t = 0; t < nn; ++t) N0[t] = D[t] / s0;
@@ -410,7 +411,7 @@ static bool sym_norm2_power_bounds(kt_context_s* ctx, int n, const std::vector<d
         if (rocblas_dgemm(blas(ctx), rocblas_operation_none, rocblas_operation_none, n, n, n, &one, cur, n, cur, n,
                           &zero, nxt, n) != rocblas_status_success)
             fail(KT_ERR_HIP, "rocblas_dgemm(norm powers) failed");
-        KT_HIP(launch_fro_colmax_scale(n, nxt, out + 2 * i, st));
+        KT_HIP(launch_fro_colmax_scale(n, nxt, out + 2 * i, colsq, st));
         std::swap(cur, nxt);
     }
     double h[2 * K];

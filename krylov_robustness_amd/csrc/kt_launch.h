@@ -104,7 +104,7 @@ hipError_t launch_gram_ts(int64_t n, const double* X, int ldx, int px, const dou
                           double* part, double* G, hipStream_t st);
 hipError_t launch_combine_ts(int64_t n, const double* X, int ldx, int px, const double* C, int q, double alpha,
                              double beta, double* Y, int ldy, hipStream_t st);
-hipError_t launch_fro_colmax_scale(int n, double* M, double* out, hipStream_t st);
+hipError_t launch_fro_colmax_scale(int n, double* M, double* out, double* colsq, hipStream_t st);
 hipError_t launch_scatter_elems(int64_t count, const int64_t* off, const double* val, double* D,
                                 hipStream_t st);
 hipError_t launch_gather_elems(int64_t count, const double* D, const int64_t* off, double* out,
