@@ -100,6 +100,7 @@ struct PinnedBuf {
 struct ProfSlot {
     std::vector<hipEvent_t> ev;  // start/stop pairs
     size_t used = 0;             // events used (2 per launch)
+    size_t done = 0;             // events already folded into the totals (prof_collect)
     int64_t launches = 0;
     double total_ms = 0.0;
     double busy_ms = 0.0;  // union of the launches' intervals
@@ -280,7 +281,13 @@ const DevCSR& hub_csr(kt_matrix_s* A);
 // profiling helpers (no-ops unless ctx->profile)
 void prof_begin(kt_context_s* ctx, int slot, hipStream_t st = nullptr);
 void prof_end(kt_context_s* ctx, int slot, hipStream_t st = nullptr);
-void prof_collect(kt_context_s* ctx);  // after stream sync: fold events into totals
+// fold recorded events into the totals: all of them (every one complete:
+// after a stream sync, or waited for here when `wait`), or, with `upto`,
+// only the events recorded before upto[slot] (a previous call's, complete)
+void prof_collect(kt_context_s* ctx, const size_t* upto = nullptr, bool wait = false);
+// at a call's start: recycle the events already folded in, keep the rest
+void prof_recycle(kt_context_s* ctx);
+void prof_reserve(kt_context_s* ctx, size_t per_slot);
 
 // dense host helpers (kt_dense.cpp)
 double fscalar(int fun, double x);

@@ -359,6 +359,11 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         const int lanes_env = le ? std::max(1, std::min(4, atoi(le))) : (ctx->yform ? 2 : 3);
         const int lanes = (int)std::min<int64_t>(nsweeps, lanes_env);
         const DevCSR& H = hub_csr(A);
+        // profiling: the previous calls' events (complete) are folded in while
+        // this call's sweeps run on the device
+        prof_recycle(ctx);
+        size_t prev_events[PROF_NSLOTS];
+        for (int k = 0; k < PROF_NSLOTS; ++k) prev_events[k] = ctx->prof[k].used;
         for (int64_t s = 0; s < nsweeps; ++s) {
             if (ctx->yform)
                 lanczos_sweep_y(A, H, P, m, seed, probe_offset + s * P, htrec + rec * s, (int)(s % lanes));
@@ -366,6 +371,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
                 lanczos_sweep(A, H, P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr,
                               htrec + rec * s, nullptr, nullptr, (int)(s % lanes));
         }
+        prof_collect(ctx, prev_events);
         KT_HIP(hipStreamSynchronize(ctx->stream));
         for (int l = 1; l < lanes; ++l) KT_HIP(hipStreamSynchronize(ctx->aux_stream[l - 1]));
 #ifndef KT_KY_DIAG  // (diagnostic builds time the pass alone: no redo)
@@ -385,7 +391,6 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
             ctx->yform_redone += redone;
         }
 #endif
-        prof_collect(ctx);
 
         std::vector<double> qv((size_t)nprobes);
         parallel_for(nprobes, 64, [&](int64_t pb, int64_t pe) {
