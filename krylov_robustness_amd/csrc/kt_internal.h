@@ -1,5 +1,6 @@
 // kt_internal.h -- shared internals of libkrylov_hip.so (not part of the ABI).
 #pragma once
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -41,6 +42,8 @@ struct DevBuf {
     ~DevBuf() { release(); }
     void ensure(size_t want) {
         if (want <= bytes) return;
+        // geometric growth below 64 MB (hipFree synchronises the device)
+        if (want < ((size_t)64 << 20)) want = std::max(want, std::max<size_t>(2 * bytes, 64 << 10));
         if (ptr) (void)hipFree(ptr);
         ptr = nullptr;
         bytes = 0;
@@ -82,6 +85,10 @@ struct PinnedBuf {
     ~PinnedBuf() { release(); }
     void ensure(size_t want) {
         if (want <= bytes) return;
+        // grow geometrically below 64 MB: a buffer that follows a growing
+        // basis (one more block per Krylov step) was freed and re-pinned every
+        // step, and hipHostFree costs ~0.25 ms with the device synchronised
+        if (want < ((size_t)64 << 20)) want = std::max(want, std::max<size_t>(2 * bytes, 64 << 10));
         if (ptr) (void)hipHostFree(ptr);
         ptr = nullptr;
         bytes = 0;
@@ -189,11 +196,11 @@ struct kt_context_s {
     // workspace) for the projected-matrix work that a block-Krylov run hands
     // to a worker thread while its next step runs here (kt_krylov.cpp)
     kt_context_s* helper = nullptr;
-    // that worker thread (kt_krylov.cpp StepWorker), kept for the context's
-    // lifetime: a HIP thread started and joined per call stalled the next
-    // call's first stream sync by 20-30 ms (profiles/r03_fg_exp_worker.txt)
-    void* step_worker = nullptr;
-    void (*step_worker_free)(void*) = nullptr;
+    // persistent host worker threads (kt_worker.h StepWorker), kept for the
+    // context's lifetime: HIP threads started and joined per call stalled the
+    // device's other streams when they exited
+    void* workers[3] = {nullptr, nullptr, nullptr};
+    void (*workers_free)(void*) = nullptr;
     kt::ProfSlot prof[kt::PROF_NSLOTS];
     kt::Workspace ws;
     kt::ScratchPool pool;  // DevMat scratch (kt_block.h)

@@ -28,6 +28,7 @@
 #include "kt_krylov.h"
 #include "kt_launch.h"
 #include "kt_pool.h"
+#include "kt_worker.h"
 
 namespace kt {
 
@@ -752,114 +753,6 @@ static std::vector<double> top_left(const std::vector<double>& M, int Mr, int nn
     return T;
 }
 
-// ---------------------------------------------------------------------------
-// In-order worker thread for the projected-matrix work of a block-Krylov run
-// (trace_fun_update / fun_update): job k runs while the caller's thread
-// extends the basis by one more step.  wait(k) blocks until jobs 0..k of the
-// current run have finished and rethrows the first failure; once a job failed
-// the rest are skipped.  finish() ends a run: it drops the jobs not yet
-// started, waits for the running one and resets the job count, so the thread
-// serves the next run (one thread per context, ctx->step_worker).
-// ---------------------------------------------------------------------------
-class StepWorker {
-   public:
-    explicit StepWorker(int device) : device_(device) { th_ = std::thread([this] { loop(); }); }
-    StepWorker(const StepWorker&) = delete;
-    StepWorker& operator=(const StepWorker&) = delete;
-    ~StepWorker() {
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            stop_ = true;
-            q_.clear();
-        }
-        cv_.notify_all();
-        th_.join();
-    }
-    void finish() {
-        std::unique_lock<std::mutex> lk(m_);
-        q_.clear();
-        done_cv_.wait(lk, [&] { return !busy_; });
-        done_ = 0;
-        err_ = nullptr;
-    }
-    void submit(std::function<void()> f) {
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            q_.push_back(std::move(f));
-        }
-        cv_.notify_all();
-    }
-    void wait(int k) {
-        std::unique_lock<std::mutex> lk(m_);
-        done_cv_.wait(lk, [&] { return done_ > k || err_; });
-        if (err_) std::rethrow_exception(err_);
-    }
-
-   private:
-    void loop() {
-        (void)hipSetDevice(device_);
-        for (;;) {
-            std::function<void()> f;
-            {
-                std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-                if (q_.empty()) return;  // stop_ with nothing queued
-                f = std::move(q_.front());
-                q_.pop_front();
-                busy_ = true;
-            }
-            std::exception_ptr e;
-            if (!err_) {
-                try {
-                    f();
-                } catch (...) {
-                    e = std::current_exception();
-                }
-            }
-            {
-                std::lock_guard<std::mutex> lk(m_);
-                if (e && !err_) err_ = e;
-                ++done_;
-                busy_ = false;
-            }
-            done_cv_.notify_all();
-        }
-    }
-    int device_;
-    std::mutex m_;
-    std::condition_variable cv_, done_cv_;
-    std::deque<std::function<void()>> q_;
-    int done_ = 0;
-    bool stop_ = false, busy_ = false;
-    std::exception_ptr err_;
-    std::thread th_;
-};
-
-// The context's persistent worker thread (created on first use); a run ends
-// with RunWorker's finish(), so the next run starts with an idle worker.
-static StepWorker* step_worker(kt_context_s* ctx) {
-    if (!ctx->step_worker) {
-        ctx->step_worker = new StepWorker(ctx->device);
-        ctx->step_worker_free = [](void* p) { delete static_cast<StepWorker*>(p); };
-    }
-    return static_cast<StepWorker*>(ctx->step_worker);
-}
-// Scoped use of it by one run: finish() on every exit path, before the run's
-// steps / Xstop (captured by reference in the queued jobs) go out of scope.
-struct RunWorker {
-    StepWorker* w = nullptr;
-    RunWorker() = default;
-    RunWorker(const RunWorker&) = delete;
-    RunWorker& operator=(const RunWorker&) = delete;
-    ~RunWorker() { reset(); }
-    void reset(StepWorker* nw = nullptr) {
-        if (w) w->finish();
-        w = nw;
-    }
-    StepWorker* operator->() const { return w; }
-    explicit operator bool() const { return w != nullptr; }
-};
-
 // The context a pipelined block-Krylov run hands its projected work to
 // (ctx->helper, created on first use), or nullptr for the serial loop:
 // env_name set to "0", or the helper cannot be created.
@@ -937,7 +830,7 @@ double trace_fun_update_impl(kt_matrix_s* A, int rk, const double* U, const doub
     };
     kt_context_s* hctx = pipeline_helper(ctx, "KT_TFU_PIPE");
     RunWorker W;  // finished before steps / Xstop go out of scope
-    if (hctx) W.reset(step_worker(ctx));
+    if (hctx) W.reset(ctx_worker(ctx, kWorkerPipeline));
     std::vector<double> Cm;
     int jfin = 0;
     PhaseClock pc;
@@ -1060,7 +953,7 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
     };
     kt_context_s* hctx = pipeline_helper(ctx, "KT_FU_PIPE");
     RunWorker W;  // finished before steps / Xstop go out of scope
-    if (hctx) W.reset(step_worker(ctx));
+    if (hctx) W.reset(ctx_worker(ctx, kWorkerPipeline));
     std::vector<double> Cm;
     int jfin = 0;
     PhaseClock pc;
@@ -1470,9 +1363,10 @@ int kt_fun_and_grad_krylov_fun(kt_matrix_t A, int64_t nom, const double* X, cons
     kt_matrix_s* A2 = twin_of(A);
     double fval = 0.0;
     Status terr{KT_OK, ""};
-    std::thread th;
-    if (A2)
-        th = std::thread([&] {
+    RunWorker T;  // the twin's call on a persistent thread of A's context (finished on every exit)
+    if (A2) {
+        T.reset(ctx_worker(A->ctx, kWorkerTwin));
+        T->submit([&] {
             try {
                 KT_HIP(hipSetDevice(A2->ctx->device));
                 fval = trace_fun_update_impl(A2, k, U.data(), B.data(), tol_f, it, fun, nullptr, nullptr);
@@ -1482,16 +1376,11 @@ int kt_fun_and_grad_krylov_fun(kt_matrix_t A, int64_t nom, const double* X, cons
                 terr = Status{KT_ERR_HIP, "trace_fun_update (twin) failed"};
             }
         });
-    struct Join {
-        std::thread& t;
-        ~Join() {
-            if (t.joinable()) t.join();
-        }
-    } join{th};
+    }
     FunUpdateResult fu = fun_update_impl(A, k, U.data(), B.data(), dfun, tol_df, it);          // :64
     bool serial = !A2;
     if (A2) {
-        th.join();
+        T->wait(0);
         if (terr.code == KT_ERR_ALLOC) {  // the twin's workspace did not fit: serial order
             (void)hipGetLastError();
             A2->ctx->pool.clear();  // its idle scratch blocks back to the device

@@ -15,6 +15,7 @@
 #include <thread>
 
 #include "kt_krylov.h"
+#include "kt_worker.h"
 #include "kt_launch.h"
 #include "kt_slq.h"
 
@@ -619,7 +620,11 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
             // round's S term (see above) starts on a third thread.
             KT_HIP(hipStreamSynchronize(ctx->stream));  // Z, Zg and Q_it are ready for every stream
             Status gerr{KT_OK, ""}, serr{KT_OK, ""};
-            std::thread th([&] {
+            // persistent threads of this context (kt_worker.h): finished on
+            // every exit path before the captured locals go out of scope
+            RunWorker tg, ts;
+            tg.reset(ctx_worker(ctx, kWorkerTwin));
+            tg->submit([&] {
                 try {
                     KT_HIP(hipSetDevice(A2->ctx->device));
                     AfunDev F2{A2, F.kind, F.fun, F.m};
@@ -631,9 +636,9 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
                     gerr = Status{KT_ERR_HIP, "mc_trace: G term on the twin failed"};
                 }
             });
-            std::thread th3;
-            if (A3 && it < K)
-                th3 = std::thread([&] {
+            if (A3 && it < K) {
+                ts.reset(ctx_worker(ctx, kWorkerSpec));
+                ts->submit([&] {
                     try {
                         KT_HIP(hipSetDevice(A3->ctx->device));
                         s_term(A3, it + 1, S3, Z3, Yb[(it + 1) & 1].col(0));
@@ -644,17 +649,11 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
                         serr = Status{KT_ERR_HIP, "mc_trace: speculative S term failed"};
                     }
                 });
-            double qsum = 0.0;
-            try {
-                qsum = F.trace_quad(Z.col(0), ld, mb);
-            } catch (...) {
-                th.join();
-                if (th3.joinable()) th3.join();
-                throw;
             }
-            th.join();
-            if (th3.joinable()) {
-                th3.join();
+            const double qsum = F.trace_quad(Z.col(0), ld, mb);  // (on a throw, tg / ts finish first)
+            tg->wait(0);
+            if (ts) {
+                ts->wait(0);
                 if (serr.code == KT_OK) {
                     spec_ready = true;
                 } else if (serr.code != KT_ERR_ALLOC) {

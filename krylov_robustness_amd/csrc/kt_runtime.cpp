@@ -338,10 +338,11 @@ int kt_context_create(int device, kt_context_t* out) {
 int kt_context_destroy(kt_context_t ctx) {
     KT_GUARD_BEGIN
     if (!ctx) return KT_OK;
-    if (ctx->step_worker) {  // joined before the helper context it drives goes away
-        ctx->step_worker_free(ctx->step_worker);
-        ctx->step_worker = nullptr;
-    }
+    for (auto& w : ctx->workers)  // joined before the helper / twin contexts they drive go away
+        if (w) {
+            ctx->workers_free(w);
+            w = nullptr;
+        }
     if (ctx->helper) {
         (void)kt_context_destroy(ctx->helper);
         ctx->helper = nullptr;

@@ -25,7 +25,7 @@ X = np.random.default_rng(11).uniform(-0.5, 1.0, size=30)
 if X.sum() > 10:
     X *= 10 / X.sum()
 U_cols = len(np.unique(Om))
-for r in range(4):
+for r in range(int(os.environ.get("KT_FG_REPS", "4"))):
     t0 = time.perf_counter()
     f, gr = kra.fun_and_grad_krylov_fun(X, D, Om, "sinh", "cosh", dfA, 1e-6 * np.sinh(nrm), 100, ctx=ctx)
     print(f"fg {time.perf_counter() - t0:.4f} s  f={f:.6f} distinct nodes {U_cols}", flush=True)
