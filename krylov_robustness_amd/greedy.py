@@ -154,12 +154,13 @@ def find_top_edges(A, centrality, num, order="mult"):
         score = c[I] * c[J]
         ind = np.argsort(-score, kind="stable")
     elif order == "min":  # :26-37
-        sc = np.sort(c)[::-1]
-        first = {}
-        for pos, v in enumerate(sc):
-            first.setdefault(v, pos + 1)
-        c1 = np.array([first[v] for v in c[I]], dtype=np.float64)
-        c2 = np.array([first[v] for v in c[J]], dtype=np.float64)
+        # find(sc == v, 1) with sc = sort(c, 'descend'): the first descending
+        # position of v is n - (last ascending position of v), i.e.
+        # n - searchsorted(ascending, v, 'right') + 1 (1-based), vectorised
+        asc = np.sort(c)
+        nc = len(c)
+        c1 = (nc - np.searchsorted(asc, c[I], side="right") + 1).astype(np.float64)
+        c2 = (nc - np.searchsorted(asc, c[J], side="right") + 1).astype(np.float64)
         mn, mx = np.minimum(c1, c2), np.maximum(c1, c2)
         ind = np.argsort(mx * (mx - 1) / 2 + mn, kind="stable")
     else:
