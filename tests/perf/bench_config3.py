@@ -64,6 +64,20 @@ def main():
         ex = json.load(open(vp))["exact_tr_sinh"]
         out["tr_sinh_exact"] = ex
         out["tr_sinh_rel_err"] = abs(tr - ex) / abs(ex)
+        # statistical bound of the plain Hutchinson estimate: the sample
+        # standard error of the per-probe quadratic forms
+        s1, s2, _ = kra.slq_quadforms(D, a.probes, a.m, seed=3, fun="sinh", ctx=ctx)
+        N = a.probes
+        se = float(np.sqrt(max(s2 - s1 * s1 / N, 0.0) / (N - 1) / N))
+        out["tr_sinh_slq_stderr"] = se
+        out["tr_sinh_slq_err_in_stderrs"] = abs(tr - ex) / se
+        # the same trace in the reference's Hutch++ structure (mc_trace.m:42-58,
+        # Lanczos-sinh Afun, tol 1e-4, maxit 1000 as trace_exp.m sets them)
+        (hpp, t_h) = best(lambda: kra.mc_trace("lanczos", None, 1e-4, 1000, 1, 0, seed=3, fun="sinh", m=a.m,
+                                              A=D, ctx=ctx), 1)
+        out.update({"tr_sinh_hutchpp": hpp[0], "tr_sinh_hutchpp_res": hpp[1], "tr_sinh_hutchpp_rounds": hpp[2],
+                    "tr_sinh_hutchpp_s": t_h, "tr_sinh_hutchpp_rel_err": abs(hpp[0] - ex) / abs(ex),
+                    "tr_sinh_hutchpp_probe_columns": 30 * hpp[2]})
     # 2. Omega from centrality + function_multiple_entries(cosh)
     c = kra.compute_centrality(A)
     E = kra.find_top_edges(A, c, 100, "min")
