@@ -558,6 +558,8 @@ void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std
     // barriers per column cost more than the two launches, profiles/r02_tsqr_persistent.txt)
     const char* pe = std::getenv("KT_TSQR_PERSIST");
     const int pgrid = (pe && pe[0] == '1') ? ts_qr_grid((int)n, BP, ctx->num_cu) : 0;
+    int rpw_q1 = 0;
+    const int qgrid1 = (pe && pe[0] == '2') ? ts_qr1_grid((int)n, BP, ctx->num_cu, &rpw_q1) : 0;
     // KT_TSQR_STEP1=1: one launch per column (k_ts_step1) where its grid fits
     // (n <= 49,152) -- measured equal to the two-launch form (config 3: 13.05
     // us per column launch vs 8.43 + 5.01 us, fun_and_grad 9.6-10.0 vs
@@ -566,8 +568,13 @@ void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std
     // inside one launch, so it stays opt-in
     const char* s1e = std::getenv("KT_TSQR_STEP1");
     int rpw1 = 0;
-    const int g1 = (pgrid == 0 && s1e && s1e[0] == '1') ? ts_step1_grid((int)n, &rpw1) : 0;
-    if (g1 > 0) {
+    const int g1 = (pgrid == 0 && qgrid1 == 0 && s1e && s1e[0] == '1') ? ts_step1_grid((int)n, &rpw1) : 0;
+    if (qgrid1 > 0) {
+        ws.ts_pub.ensure(sizeof(double) * ts_qr1_pub_doubles((int)n, BP, ctx->num_cu));
+        ws.ts_bar.ensure(ts_qr_bar_bytes());
+        KT_HIP(launch_ts_qr1((int)n, bs, BP, ctx->num_cu, W, ld, V, ws.ts_pub.as<double>(), taus, ws.ts_bar.ptr,
+                             ctx->stream));
+    } else if (g1 > 0) {
         ws.ts_part.ensure(sizeof(double) * ((size_t)2 * BP * g1 + 2 * (size_t)BP));
         double* part1 = ws.ts_part.as<double>();
         KT_HIP(launch_ts_reflectors1((int)n, bs, BP, W, ld, V, part1, part1 + (size_t)2 * BP * g1, taus,
@@ -589,7 +596,7 @@ void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std
     double* ptau = pV1 + (size_t)bs * BP;
     unsigned* ptmo = reinterpret_cast<unsigned*>(ptau + bs);
     *ptmo = 0;
-    if (pgrid > 0)
+    if (pgrid > 0 || qgrid1 > 0)
         KT_HIP(hipMemcpyAsync(ptmo, static_cast<char*>(ws.ts_bar.ptr) + ts_qr_tmo_offset(), sizeof(unsigned),
                               hipMemcpyDeviceToHost, ctx->stream));
     KT_HIP(hipMemcpy2DAsync(ptop, sizeof(double) * bs, W, sizeof(double) * ld, sizeof(double) * bs, (size_t)bs,

@@ -159,6 +159,12 @@ hipError_t launch_ts_qr(int n, int bs, int BP, int num_cu, double* W, int ld, do
 int ts_step1_grid(int n, int* rows_per_wg);
 hipError_t launch_ts_reflectors1(int n, int bs, int BP, double* W, int ld, double* V, double* part, double* piv,
                                  double* taus, hipStream_t st);
+// one grid barrier per column (k_ts_qr1, KT_TSQR_PERSIST=2): ts_qr1_grid > 0
+// when it applies; pub: ts_qr1_pub_doubles doubles; bar as launch_ts_qr
+int ts_qr1_grid(int n, int BP, int num_cu, int* rows_per_wg);
+size_t ts_qr1_pub_doubles(int n, int BP, int num_cu);
+hipError_t launch_ts_qr1(int n, int bs, int BP, int num_cu, double* W, int ld, double* V, double* pub, double* taus,
+                         void* bar, hipStream_t st);
 hipError_t launch_ts_formq(int n, int bs, int BP, const double* V, const double* M, double* W,
                            int ld, hipStream_t st);
 hipError_t launch_sum_slabs(int count, int S, const double* part, double* G, hipStream_t st);

@@ -14,6 +14,7 @@
 // factor T (dlarft, host) in one more pass.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstddef>
 
 #include "kt_launch.h"
@@ -457,6 +458,142 @@ __global__ __launch_bounds__(kTsBlock) void k_ts_qr(int n, int bs, int BP, int r
 
 size_t ts_qr_bar_bytes() { return sizeof(TsBar); }
 size_t ts_qr_tmo_offset() { return offsetof(TsBar, tmo); }
+
+// ---------------------------------------------------------------------------
+// The persistent sweep with ONE grid barrier per column (k_ts_qr1,
+// KT_TSQR_PERSIST=2): every workgroup keeps its row slice in LDS (1024
+// threads), publishes one partial per column (its rows summed) and the next
+// pivot row write-through (sc1), and after the barrier sums the G partials
+// itself in one fixed order -- identical coefficients in every workgroup, no
+// second barrier for a reduce.  Rounding-level differences from the
+// two-launch form (reductions grouped by workgroup).
+// pub: 2 slots x [BP x G partials | BP pivot].
+// ---------------------------------------------------------------------------
+constexpr int kTsQ1Block = 1024;
+constexpr size_t kTsQ1Lds = 136 * 1024;  // the row slice; + 8 KB reduce + 2 KB coefficients
+
+__global__ __launch_bounds__(kTsQ1Block) void k_ts_qr1(int n, int bs, int BP, int rpw, double* __restrict__ W, int ld,
+                                                       double* __restrict__ V, double* __restrict__ pub,
+                                                       double* __restrict__ taus, TsBar* bar) {
+    extern __shared__ double lw[];  // [rows of this workgroup][BP]
+    __shared__ double red[kTsQ1Block];
+    __shared__ double s_sums[128], s_piv[128];
+    const int G = (int)gridDim.x, g = (int)blockIdx.x, tid = (int)threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int c = tid % BP, sub = tid / BP, rpi = kTsQ1Block / BP;
+    const int r0 = min(n, g * rpw), r1 = min(n, r0 + rpw);
+    const int nr = r1 - r0;
+    const size_t slot_sz = (size_t)BP * G + BP;
+    for (int t = tid; t < nr * BP; t += kTsQ1Block) {
+        const int rr = t / BP, cc = t % BP;
+        lw[t] = cc < bs ? W[(int64_t)(r0 + rr) * ld + cc] : 0.0;
+    }
+    __syncthreads();
+    unsigned epoch = 0;
+    bool ok = true;
+    for (int k = -1; k < bs && ok; ++k) {
+        const int kn = k + 1;
+        double beta = 0.0, tau = 0.0, scal = 1.0, tc = 0.0, tn = 0.0;
+        if (k >= 0) {
+            ts_larfg(s_piv[k], s_sums[k], beta, tau, scal);
+            if (c > k && c < bs) tc = s_piv[c] + scal * s_sums[c];
+            if (kn < bs) tn = s_piv[kn] + scal * s_sums[kn];
+            if (g == 0 && tid == 0) taus[k] = tau;
+        }
+        double* slot = pub + (size_t)((epoch + 1) & 1) * slot_sz;
+        const int rstart = max(r0, k < 0 ? 0 : k);
+        double acc = 0.0;
+        for (int base = rstart; base < r1; base += rpi) {  // uniform trip count (barrier inside)
+            const int r = base + sub;
+            const bool live = r < r1 && c < bs;
+            double* row = lw + (size_t)(r - r0) * BP;
+            double wk = 0.0, wn = 0.0, wc = 0.0;
+            if (live) {
+                if (k >= 0) wk = row[k];
+                if (kn < bs) wn = row[kn];
+                wc = row[c];
+            }
+            __syncthreads();  // every read of this row slot before any write
+            if (live) {
+                double v = 0.0;
+                if (k >= 0) {
+                    v = (r == k) ? 1.0 : wk * scal;
+                    if (c == k) {
+                        V[(int64_t)r * BP + k] = v;
+                        if (r == k) row[k] = beta;
+                    } else if (c > k) {
+                        wc -= tau * v * tc;
+                        row[c] = wc;
+                    }
+                }
+                if (kn < bs && c >= kn && r > kn) {
+                    const double wn_new = k >= 0 ? wn - tau * v * tn : wn;
+                    acc = fma(wn_new, wc, acc);
+                }
+            }
+        }
+        if (kn >= bs) break;
+        red[tid] = acc;
+        __syncthreads();
+        if (tid < BP) {
+            double sm = 0.0;
+            for (int q = 0; q < rpi; ++q) sm += red[q * BP + tid];
+            ts_st(slot + (size_t)tid * G + g, sm);
+        }
+        if (kn >= r0 && kn < r1 && tid < BP)  // the next pivot row, W(kn, :) after H_k
+            ts_st(slot + (size_t)BP * G + tid, tid < bs ? lw[(size_t)(kn - r0) * BP + tid] : 0.0);
+        ok = ts_grid_sync(bar, ++epoch, G, g);
+        if (!ok) break;
+        // every workgroup: sums[j], j in [kn, bs), one wave per column, lanes
+        // over the G partials, a fixed xor tree
+        for (int j = kn + wave; j < bs; j += kTsQ1Block / 64) {
+            double sm = 0.0;
+            for (int i = lane; i < G; i += 64) sm += ts_ld(slot + (size_t)j * G + i);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+            if (lane == 0) s_sums[j] = sm;
+        }
+        if (tid < BP) s_piv[tid] = ts_ld(slot + (size_t)BP * G + tid);
+        __syncthreads();
+    }
+    // R: rows 0..bs-1 of W back to memory (Q is formed from V afterwards)
+    for (int t = tid; t < nr * BP; t += kTsQ1Block) {
+        const int rr = t / BP, cc = t % BP;
+        if (r0 + rr < bs && cc < bs) W[(int64_t)(r0 + rr) * ld + cc] = lw[t];
+    }
+}
+
+// grid of k_ts_qr1 (0 when it does not apply): rows per workgroup from the LDS
+// budget, at most a quarter of the CUs (one workgroup per CU, co-resident
+// next to another context's work)
+int ts_qr1_grid(int n, int BP, int num_cu, int* rows_per_wg) {
+    const int rpw_max = (int)(kTsQ1Lds / (sizeof(double) * (size_t)BP));
+    int G = (n + rpw_max - 1) / rpw_max;
+    const int floor_g = std::min(16, num_cu / 4);  // spread small problems over a few CUs
+    G = std::max(G, std::min(floor_g, (n + 63) / 64));
+    if (G < 1 || G > num_cu / 4 || BP > 128) return 0;
+    *rows_per_wg = (n + G - 1) / G;
+    if ((size_t)*rows_per_wg * BP * sizeof(double) > kTsQ1Lds) return 0;
+    return G;
+}
+
+size_t ts_qr1_pub_doubles(int n, int BP, int num_cu) {
+    int rpw = 0;
+    const int G = ts_qr1_grid(n, BP, num_cu, &rpw);
+    return 2 * ((size_t)BP * std::max(G, 1) + BP);
+}
+
+hipError_t launch_ts_qr1(int n, int bs, int BP, int num_cu, double* W, int ld, double* V, double* pub, double* taus,
+                         void* bar, hipStream_t st) {
+    int rpw = 0;
+    const int G = ts_qr1_grid(n, BP, num_cu, &rpw);
+    if (!G) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(bar, 0, sizeof(TsBar), st);
+    if (e != hipSuccess) return e;
+    k_ts_qr1<<<G, kTsQ1Block, sizeof(double) * (size_t)rpw * BP, st>>>(n, bs, BP, rpw, W, ld, V, pub, taus,
+                                                                     static_cast<TsBar*>(bar));
+    return hipGetLastError();
+}
 
 static int ts_rows_per_blk(int n, int num_cu);
 

@@ -73,10 +73,13 @@ def test_qr_persistent_and_two_launch_forms_agree(kra, gpu_ctx, monkeypatch, n, 
         np.testing.assert_allclose(Q, Qr, rtol=0, atol=1e-11)
 
 
+@pytest.mark.parametrize("form", [("KT_TSQR_STEP1", "1"), ("KT_TSQR_PERSIST", "2")])
 @pytest.mark.parametrize("n,bs", [(3000, 45), (21774, 25), (10860, 10), (3228, 29)])
-def test_qr_one_launch_per_column_form(kra, gpu_ctx, monkeypatch, n, bs):
+def test_qr_one_launch_per_column_form(kra, gpu_ctx, monkeypatch, n, bs, form):
     """The one-launch-per-column sweep (KT_TSQR_STEP1=1, k_ts_step1: every
-    workgroup sums the previous launch's partials itself) groups the reductions by
+    workgroup sums the previous launch's partials itself) and the persistent
+    sweep with one grid barrier per column (KT_TSQR_PERSIST=2, k_ts_qr1) group
+    the reductions by
     workgroup instead of by 64-row block: on a full-rank block Q and R equal
     the two-launch form's and LAPACK's to rounding; on a rank-deficient one
     (repeated columns, a zero column) R agrees to rounding and Q is
@@ -84,21 +87,21 @@ def test_qr_one_launch_per_column_form(kra, gpu_ctx, monkeypatch, n, bs):
     columns are rounding-dependent in every implementation, LAPACK's included."""
     rng = np.random.default_rng(n + 3 * bs)
     Wr = rng.normal(size=(n, bs))
-    monkeypatch.setenv("KT_TSQR_STEP1", "1")
+    monkeypatch.setenv(*form)
     Q1, R1 = kra.householder_qr(Wr, ctx=gpu_ctx)
-    monkeypatch.setenv("KT_TSQR_STEP1", "0")
+    monkeypatch.delenv(form[0])
     Q2, R2 = kra.householder_qr(Wr, ctx=gpu_ctx)
     Qr, Rr = np.linalg.qr(Wr)
     np.testing.assert_allclose(R1, R2, rtol=0, atol=1e-13 * np.abs(R2).max())
     np.testing.assert_allclose(Q1, Q2, rtol=0, atol=1e-13)
     np.testing.assert_allclose(R1, Rr, rtol=0, atol=1e-12 * np.abs(Rr).max())
     np.testing.assert_allclose(Q1, Qr, rtol=0, atol=1e-12)
-    monkeypatch.setenv("KT_TSQR_STEP1", "1")
+    monkeypatch.setenv(*form)
     W = Wr.copy()
     W[:, bs // 2:] = W[:, :bs - bs // 2]
     W[:, -1] = 0.0
     Q1, R1 = kra.householder_qr(W, ctx=gpu_ctx)
-    monkeypatch.setenv("KT_TSQR_STEP1", "0")
+    monkeypatch.delenv(form[0])
     Q2, R2 = kra.householder_qr(W, ctx=gpu_ctx)
     np.testing.assert_allclose(np.abs(R1), np.abs(R2), rtol=0, atol=1e-12 * np.abs(R2).max())
     np.testing.assert_allclose(Q1.T @ Q1, np.eye(bs), atol=1e-12)
