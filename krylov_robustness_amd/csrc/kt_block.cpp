@@ -499,7 +499,46 @@ static void apply_rinv(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, 
     copy_cols(ctx, n, t.as<double>(), bs, W, ld, bs);
 }
 
-void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R) {
+// Shifted CholeskyQR3 on W (Fukaya, Kannan, Nakatsukasa, Yamamoto, Yanagisawa
+// 2020): one pass with the Gram shifted by 11 (n bs + bs (bs + 1)) eps ||W||_F^2,
+// then two plain CholeskyQR passes.  W is kept aside first; false (W restored)
+// when a Cholesky fails or the last pass's factor is not the identity to 1e-8
+// (Q not orthonormal): the caller then takes the Householder sweep.
+static bool shifted_cholqr3(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R) {
+    DevBuf& keep = ctx->ws.qrkeep;
+    keep.ensure(sizeof(double) * (size_t)std::max<int64_t>(n, 1) * bs);
+    copy_cols(ctx, n, W, ld, keep.as<double>(), bs, bs);
+    auto restore = [&] {
+        copy_cols(ctx, n, keep.as<double>(), bs, W, ld, bs);
+        return false;
+    };
+    std::vector<double> G;
+    gram(ctx, n, W, ld, bs, W, ld, bs, G);
+    double tr = 0.0;
+    for (int i = 0; i < bs; ++i) tr += G[i + (size_t)i * bs];
+    const double shift = 11.0 * ((double)n * bs + (double)bs * (bs + 1)) * DBL_EPSILON * tr;
+    for (int i = 0; i < bs; ++i) G[i + (size_t)i * bs] += shift;
+    if (!chol_upper(G.data(), bs)) return restore();
+    std::vector<double> R1 = G, R2, R3, T((size_t)bs * bs);
+    apply_rinv(ctx, n, W, ld, bs, R1);
+    for (std::vector<double>* Rp : {&R2, &R3}) {
+        gram(ctx, n, W, ld, bs, W, ld, bs, *Rp);
+        if (!chol_upper(Rp->data(), bs)) return restore();
+        apply_rinv(ctx, n, W, ld, bs, *Rp);
+    }
+    double dev = 0.0;
+    for (int j = 0; j < bs; ++j)
+        for (int i = 0; i <= j; ++i) dev = std::max(dev, std::fabs(R3[i + (size_t)j * bs] - (i == j ? 1.0 : 0.0)));
+    if (!(dev < 1e-8)) return restore();
+    matmul(bs, bs, bs, R2.data(), R1.data(), T.data());
+    R.assign((size_t)bs * bs, 0.0);
+    matmul(bs, bs, bs, R3.data(), T.data(), R.data());
+    for (int j = 0; j < bs; ++j)
+        for (int i = j + 1; i < bs; ++i) R[i + (size_t)j * bs] = 0.0;
+    return true;
+}
+
+void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R, bool allow_shifted) {
     const char* e = std::getenv("KT_QR_CHOL");
     if ((e && e[0] == '0') || n < 4 * (int64_t)bs || bs < 1) {
         householder_qr(ctx, n, W, ld, bs, R);
@@ -514,6 +553,21 @@ void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vect
         dmin = std::min(dmin, R1[k + (size_t)k * bs]);
     }
     if (!ok || !(dmin >= 1e-4 * dmax) || !(dmax > 1e-6)) {
+        // block Arnoldi (allow_shifted; KT_QR_SHIFTED=0 disables): an
+        // ill-conditioned block that is not at a breakdown takes shifted
+        // CholeskyQR3 (Fukaya et al.: Q orthonormal to O(eps) up to kappa ~
+        // 1/eps) -- 3 Gram / combine passes instead of 2 bs + 3 Householder
+        // launches; its completion of numerically dependent columns is as
+        // rounding-dependent as the Householder one, not the
+        // same, and fun_update's full-basis reorthogonalisation leaves the
+        // gradient on it unchanged to 1e-10 (test_gpu_configs, omega sweep).
+        // Exactly dependent columns fail its second Cholesky and keep
+        // Householder's tau = 0 completion.  Block Lanczos (trace_fun_update's
+        // 2-block window, where the completion direction enters the objective)
+        // never takes it.
+        const char* se = std::getenv("KT_QR_SHIFTED");
+        if (allow_shifted && !(se && se[0] == '0') && dmax > 1e-6 && shifted_cholqr3(ctx, n, W, ld, bs, R))
+            return;
         householder_qr(ctx, n, W, ld, bs, R);
         return;
     }

@@ -95,7 +95,10 @@ bool cholqr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector
 // Householder thin QR of W in place (rocSOLVER LQ of W'); R upper, signs as LAPACK.
 void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R);
 // block-Krylov thin QR: CholeskyQR2 where well conditioned, else householder_qr
-void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R);
+// allow_shifted: an ill-conditioned block may take shifted CholeskyQR3 instead
+// of the Householder sweep (block Arnoldi; KT_QR_SHIFTED=0 disables, kt_block.cpp)
+void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R,
+              bool allow_shifted = false);
 
 // small host helpers (column-major)
 void matmul(int m, int k, int n, const double* A, const double* B, double* C);  // C = A B

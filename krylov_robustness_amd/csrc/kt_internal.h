@@ -152,7 +152,7 @@ struct HostFlag {
 struct Workspace {
     SweepBufs sweep[4];
     HostFlag expmv_stop;  // the stage a k_expmv_step launch found stopped (expmv_device)
-    DevBuf small, small2, qrtmp, eigA, eigW, eigInfo;  // block-Krylov scratch
+    DevBuf small, small2, qrtmp, qrkeep, eigA, eigW, eigInfo;  // block-Krylov scratch
     DevBuf expm;                                       // batched device expm (6 x batch x n^2)
     DevBuf ck_part;                                    // block SpMM hub-row chunk partials
     DevBuf hist, norm_part;                             // sweep scale history, inf-norm partials

@@ -691,7 +691,7 @@ struct BlockArnoldi {
         };
         for (int pass = 0; pass < 2; ++pass) project(pass * cnt);
         std::vector<double> r;
-        block_qr(ctx, n, W.col(0), PB, bs, r);  // [w, r] = qr(w, 0)   :99
+        block_qr(ctx, n, W.col(0), PB, bs, r, true);  // [w, r] = qr(w, 0)   :99
         lucky = norm2_small(bs, bs, r.data()) < 1e-12;  // :100-102
         KT_HIP(hipStreamSynchronize(ctx->stream));    // (the QR's read of r has drained the copies)
         std::vector<double> h(cnt);
