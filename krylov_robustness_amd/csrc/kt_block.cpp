@@ -501,38 +501,58 @@ static void apply_rinv(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, 
 
 // Shifted CholeskyQR3 on W (Fukaya, Kannan, Nakatsukasa, Yamamoto, Yanagisawa
 // 2020): one pass with the Gram shifted by 11 (n bs + bs (bs + 1)) eps ||W||_F^2,
-// then two plain CholeskyQR passes.  W is kept aside first; false (W restored)
-// when a Cholesky fails or the last pass's factor is not the identity to 1e-8
-// (Q not orthonormal): the caller then takes the Householder sweep.
+// then two plain CholeskyQR passes, all on the device (Gram -> one-workgroup
+// Cholesky + inverse -> W R^-1, no host round trip between the passes); the
+// three factors and their status come back together.  W is kept aside first;
+// false (W restored) when a Cholesky failed or the last pass's factor is not
+// the identity to 1e-8 (Q not orthonormal): the caller then takes the
+// Householder sweep.
 static bool shifted_cholqr3(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R) {
+    if (bs > 64) return false;
+    const size_t bb = (size_t)bs * bs;
     DevBuf& keep = ctx->ws.qrkeep;
     keep.ensure(sizeof(double) * (size_t)std::max<int64_t>(n, 1) * bs);
     copy_cols(ctx, n, W, ld, keep.as<double>(), bs, bs);
-    auto restore = [&] {
-        copy_cols(ctx, n, keep.as<double>(), bs, W, ld, bs);
-        return false;
-    };
-    std::vector<double> G;
-    gram(ctx, n, W, ld, bs, W, ld, bs, G);
-    double tr = 0.0;
-    for (int i = 0; i < bs; ++i) tr += G[i + (size_t)i * bs];
-    const double shift = 11.0 * ((double)n * bs + (double)bs * (bs + 1)) * DBL_EPSILON * tr;
-    for (int i = 0; i < bs; ++i) G[i + (size_t)i * bs] += shift;
-    if (!chol_upper(G.data(), bs)) return restore();
-    std::vector<double> R1 = G, R2, R3, T((size_t)bs * bs);
-    apply_rinv(ctx, n, W, ld, bs, R1);
-    for (std::vector<double>* Rp : {&R2, &R3}) {
-        gram(ctx, n, W, ld, bs, W, ld, bs, *Rp);
-        if (!chol_upper(Rp->data(), bs)) return restore();
-        apply_rinv(ctx, n, W, ld, bs, *Rp);
+    DevBuf& f = ctx->ws.qrfac;  // R1 R2 R3 | Rinv | ok[3]
+    f.ensure(sizeof(double) * 4 * bb + 4 * sizeof(int));
+    double* dR = f.as<double>();
+    double* dRi = dR + 3 * bb;
+    int* dok = reinterpret_cast<int*>(dRi + bb);
+    const bool inplace = bs <= 32 && !rocblas_gemm_path(n);  // k_combine_ts reads its rows before writing
+    DevBuf& t = ctx->ws.qrtmp;
+    if (!inplace) t.ensure(sizeof(double) * (size_t)std::max<int64_t>(n, 1) * bs);
+    const double c0 = 11.0 * ((double)n * bs + (double)bs * (bs + 1)) * DBL_EPSILON;
+    for (int p = 0; p < 3; ++p) {
+        const double* dG = gram_device(ctx, n, W, ld, bs, W, ld, bs);
+        KT_HIP(launch_chol_rinv(bs, dG, p == 0 ? c0 : 0.0, dR + p * bb, dRi, dok + p, ctx->stream));
+        if (inplace) {
+            combine_device(ctx, n, W, ld, bs, dRi, bs, 1.0, 0.0, W, ld);
+        } else {
+            combine_device(ctx, n, W, ld, bs, dRi, bs, 1.0, 0.0, t.as<double>(), bs);
+            copy_cols(ctx, n, t.as<double>(), bs, W, ld, bs);
+        }
     }
+    PinnedBuf& hp = ctx->ws.pin_qrfac;
+    hp.ensure(sizeof(double) * 3 * bb + 4 * sizeof(int));
+    double* hR = hp.as<double>();
+    int* hok = reinterpret_cast<int*>(hR + 3 * bb);
+    KT_HIP(hipMemcpyAsync(hR, dR, sizeof(double) * 3 * bb, hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipMemcpyAsync(hok, dok, 3 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    KT_HIP(hipStreamSynchronize(ctx->stream));
+    const double* R1 = hR;
+    const double* R2 = hR + bb;
+    const double* R3 = hR + 2 * bb;
     double dev = 0.0;
     for (int j = 0; j < bs; ++j)
         for (int i = 0; i <= j; ++i) dev = std::max(dev, std::fabs(R3[i + (size_t)j * bs] - (i == j ? 1.0 : 0.0)));
-    if (!(dev < 1e-8)) return restore();
-    matmul(bs, bs, bs, R2.data(), R1.data(), T.data());
-    R.assign((size_t)bs * bs, 0.0);
-    matmul(bs, bs, bs, R3.data(), T.data(), R.data());
+    if (!(hok[0] && hok[1] && hok[2]) || !(dev < 1e-8)) {
+        copy_cols(ctx, n, keep.as<double>(), bs, W, ld, bs);
+        return false;
+    }
+    std::vector<double> T(bb);
+    matmul(bs, bs, bs, R2, R1, T.data());
+    R.assign(bb, 0.0);
+    matmul(bs, bs, bs, R3, T.data(), R.data());
     for (int j = 0; j < bs; ++j)
         for (int i = j + 1; i < bs; ++i) R[i + (size_t)j * bs] = 0.0;
     return true;

@@ -278,4 +278,74 @@ hipError_t launch_fro_colmax_scale(int n, double* M, double* out, double* colsq,
     return hipGetLastError();
 }
 
+// CholeskyQR on the device (kt_block.cpp shifted_cholqr3): one workgroup
+// factors the bs x bs Gram G (column-major) as R' R, R upper, with
+// shift_coef * trace(G) added to the diagonal, and inverts R; ok[0] = 0 when a
+// pivot is not positive.  R and Rinv are column-major bs x bs (zero below the
+// diagonal).  Right-looking: the same operations as the host chol_upper up to
+// the order of the trailing updates.  bs <= 64 (LDS).
+__global__ __launch_bounds__(256) void k_chol_rinv(int bs, const double* __restrict__ G, double shift_coef,
+                                                   double* __restrict__ R, double* __restrict__ Rinv,
+                                                   int* __restrict__ ok) {
+    __shared__ double A[64 * 64];
+    __shared__ double X[64 * 64];
+    __shared__ double s_shift;
+    __shared__ int s_ok;
+    const int tid = threadIdx.x;
+    for (int t = tid; t < bs * bs; t += blockDim.x) A[t] = G[t];
+    __syncthreads();
+    if (tid == 0) {
+        double tr = 0.0;
+        for (int i = 0; i < bs; ++i) tr += A[i + i * bs];
+        s_shift = shift_coef * tr;
+        s_ok = 1;
+    }
+    __syncthreads();
+    for (int i = tid; i < bs; i += blockDim.x) A[i + i * bs] += s_shift;
+    __syncthreads();
+    for (int j = 0; j < bs; ++j) {
+        if (tid == 0) {
+            const double d = A[j + j * bs];
+            if (!(d > 0.0)) s_ok = 0;
+            A[j + j * bs] = sqrt(d > 0.0 ? d : 1.0);
+        }
+        __syncthreads();
+        const double r = A[j + j * bs];
+        for (int q = j + 1 + tid; q < bs; q += blockDim.x) A[j + q * bs] /= r;  // R(j, q)
+        __syncthreads();
+        const int m = bs - j - 1;  // trailing (p, q), j < p <= q
+        for (int t = tid; t < m * m; t += blockDim.x) {
+            const int p = j + 1 + t % m, q = j + 1 + t / m;
+            if (p <= q) A[p + q * bs] -= A[j + p * bs] * A[j + q * bs];
+        }
+        __syncthreads();
+    }
+    // R out (zero below), then Rinv column by column (one thread per column)
+    for (int t = tid; t < bs * bs; t += blockDim.x) {
+        const int i = t % bs, q = t / bs;
+        R[t] = i <= q ? A[t] : 0.0;
+    }
+    for (int t = tid; t < bs * bs; t += blockDim.x) X[t] = 0.0;
+    __syncthreads();
+    for (int c = tid; c < bs; c += blockDim.x) {  // back substitution R x = e_c, in LDS
+        double* x = X + c * bs;
+        x[c] = 1.0 / A[c + c * bs];
+        for (int i = c - 1; i >= 0; --i) {
+            double sm = 0.0;
+            for (int k = i + 1; k <= c; ++k) sm = fma(A[i + k * bs], x[k], sm);
+            x[i] = -sm / A[i + i * bs];
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < bs * bs; t += blockDim.x) Rinv[t] = X[t];
+    if (tid == 0) ok[0] = s_ok;
+}
+
+hipError_t launch_chol_rinv(int bs, const double* G, double shift_coef, double* R, double* Rinv, int* ok,
+                            hipStream_t st) {
+    if (bs < 1 || bs > 64) return hipErrorInvalidValue;
+    k_chol_rinv<<<1, 256, 0, st>>>(bs, G, shift_coef, R, Rinv, ok);
+    return hipGetLastError();
+}
+
 }  // namespace kt

@@ -152,7 +152,7 @@ struct HostFlag {
 struct Workspace {
     SweepBufs sweep[4];
     HostFlag expmv_stop;  // the stage a k_expmv_step launch found stopped (expmv_device)
-    DevBuf small, small2, qrtmp, qrkeep, eigA, eigW, eigInfo;  // block-Krylov scratch
+    DevBuf small, small2, qrtmp, qrkeep, qrfac, eigA, eigW, eigInfo;  // block-Krylov scratch
     DevBuf expm;                                       // batched device expm (6 x batch x n^2)
     DevBuf ck_part;                                    // block SpMM hub-row chunk partials
     DevBuf hist, norm_part;                             // sweep scale history, inf-norm partials
@@ -161,7 +161,7 @@ struct Workspace {
     PinnedBuf pin_small;  // block-Krylov Gram blocks read back without a sync per pass
     // pinned staging for gram() read-backs, combine() uploads and the thin-QR
     // read-backs (pageable transfers are staged synchronously by the runtime)
-    PinnedBuf pin_gram, pin_comb, pin_qr;
+    PinnedBuf pin_gram, pin_comb, pin_qr, pin_qrfac;
     hipEvent_t comb_ev = nullptr;  // last combine() upload out of pin_comb
     bool comb_pending = false;
     // batched greedy candidates (kt_greedy.cpp): 3 pair blocks, indices,

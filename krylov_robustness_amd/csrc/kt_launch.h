@@ -105,6 +105,9 @@ hipError_t launch_gram_ts(int64_t n, const double* X, int ldx, int px, const dou
 hipError_t launch_combine_ts(int64_t n, const double* X, int ldx, int px, const double* C, int q, double alpha,
                              double beta, double* Y, int ldy, hipStream_t st);
 hipError_t launch_fro_colmax_scale(int n, double* M, double* out, double* colsq, hipStream_t st);
+// device CholeskyQR factor: G + shift_coef tr(G) I = R' R, Rinv = R^-1 (bs <= 64); ok[0] = 0 on a failed pivot
+hipError_t launch_chol_rinv(int bs, const double* G, double shift_coef, double* R, double* Rinv, int* ok,
+                            hipStream_t st);
 hipError_t launch_scatter_elems(int64_t count, const int64_t* off, const double* val, double* D,
                                 hipStream_t st);
 hipError_t launch_gather_elems(int64_t count, const double* D, const int64_t* off, double* out,
