@@ -141,33 +141,45 @@ def krylov_miobi_sharded(A, k, E, tol=1e-12, it=None, poles=np.inf, debug=0, mio
     return edges, rob, D
 
 
+def _stable_head(key, num):
+    """argsort(key, kind="stable")[:num] without sorting the whole key: every
+    entry at or below the num-th smallest value, in index order, then a
+    stable sort of those (same ties, same order)."""
+    if num >= len(key):
+        return np.argsort(key, kind="stable")
+    th = np.partition(key, num - 1)[num - 1]
+    cand = np.flatnonzero(key <= th)
+    return cand[np.argsort(key[cand], kind="stable")][:num]
+
+
 def find_top_edges(A, centrality, num, order="mult"):
     """find_top_edges.m:1-40: the top `num` existing edges (1-based, i > j)."""
     import scipy.sparse as sp
-    L = sp.tril(sp.csc_matrix(A), -1).tocsc()
-    L.eliminate_zeros()
-    L.sort_indices()
-    J = np.repeat(np.arange(L.shape[1]), np.diff(L.indptr))  # find(): column-major
-    I = L.indices.astype(np.int64)
+    L = A if sp.isspmatrix_csc(A) else sp.csc_matrix(A)
+    if not L.has_sorted_indices:
+        L = L.sorted_indices()
+    # find(tril(A, -1)) in column-major order, read straight off the CSC arrays
+    J = np.repeat(np.arange(L.shape[1], dtype=np.int64), np.diff(L.indptr))
+    keep = (L.indices > J) & (L.data != 0)
+    I = L.indices[keep].astype(np.int64)
+    J = J[keep]
     c = np.asarray(centrality, dtype=np.float64).ravel()
     if order == "mult":  # :22-25
-        score = c[I] * c[J]
-        ind = np.argsort(-score, kind="stable")
+        key = -(c[I] * c[J])
     elif order == "min":  # :26-37
         # find(sc == v, 1) with sc = sort(c, 'descend'): the first descending
         # position of v is n - (last ascending position of v), i.e.
-        # n - searchsorted(ascending, v, 'right') + 1 (1-based), vectorised
-        asc = np.sort(c)
+        # n - searchsorted(ascending, v, 'right') + 1 (1-based), once per node
         nc = len(c)
-        c1 = (nc - np.searchsorted(asc, c[I], side="right") + 1).astype(np.float64)
-        c2 = (nc - np.searchsorted(asc, c[J], side="right") + 1).astype(np.float64)
+        rank = (nc - np.searchsorted(np.sort(c), c, side="right") + 1).astype(np.float64)
+        c1, c2 = rank[I], rank[J]
         mn, mx = np.minimum(c1, c2), np.maximum(c1, c2)
-        ind = np.argsort(mx * (mx - 1) / 2 + mn, kind="stable")
+        key = mx * (mx - 1) / 2 + mn
     else:
         return np.stack([I + 1, J + 1], axis=1)
     if len(I) < num:
         raise IndexError("FIND_TOP_EDGES:: there are not enough edges in the graph")
-    ind = ind[:num]
+    ind = _stable_head(key, num)
     return np.stack([I[ind] + 1, J[ind] + 1], axis=1)
 
 
@@ -255,6 +267,17 @@ def compute_centrality(A, kind="eig", ctx: Optional[Context] = None):
     return np.abs(u[:, 0])
 
 
+def _is_symmetric(S):
+    """issymmetric(A) for the sorted CSC the device exports: CSR of A equals
+    its CSC exactly when A == A' entry for entry (the fast path); anything
+    else falls back to the elementwise comparison."""
+    R = S.tocsr()
+    if (R.has_sorted_indices and np.array_equal(R.indptr, S.indptr)
+            and np.array_equal(R.indices, S.indices) and np.array_equal(R.data, S.data)):
+        return True
+    return not (S != S.T).nnz
+
+
 def greedy_krylov(A, k, Q=0, centrality=None, order="mult", tol=1e-12, it=None, poles=np.inf,
                   debug=0, miobi="break", rescale=1.0, ctx: Optional[Context] = None):
     """[edges, rob_variation, A_new] = greedy_krylov(A, k, Q, centrality, order, tol, it,
@@ -262,7 +285,7 @@ def greedy_krylov(A, k, Q=0, centrality=None, order="mult", tol=1e-12, it=None, 
     the DeviceMatrix the edits were applied to (``.to_scipy()`` for the host copy)."""
     D = _dev(A, ctx)
     S = D.to_scipy()
-    if (S != S.T).nnz:  # :27-29
+    if not _is_symmetric(S):  # :27-29
         raise _lib.KrylovError(_lib.KT_ERR_NOT_HERMITIAN, "GREEDY_KRYLOV:: Adjacency matrix should be symmetric")
     if not Q:
         # :42-44 Q = max(sum(A, 1)); top_edges(1:Q, :) indexes floor(Q) rows, so
