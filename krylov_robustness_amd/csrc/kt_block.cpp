@@ -585,9 +585,20 @@ void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vect
         // Householder's tau = 0 completion.  Block Lanczos (trace_fun_update's
         // 2-block window, where the completion direction enters the objective)
         // never takes it.
+        // A block whose first plain Cholesky fails is left to Householder: on
+        // Hawaii those blocks are exactly dependent, and both the shifted form
+        // and a two-shift variant fail there and fall back, at +0.7-1 ms per
+        // call (profiles/r03_qr_paths.txt).  KT_QR_LOG=1 logs every block that
+        // leaves CholeskyQR2.
         const char* se = std::getenv("KT_QR_SHIFTED");
-        if (allow_shifted && !(se && se[0] == '0') && dmax > 1e-6 && shifted_cholqr3(ctx, n, W, ld, bs, R))
+        static const bool qlog = std::getenv("KT_QR_LOG") != nullptr;
+        if (allow_shifted && !(se && se[0] == '0') && dmax > 1e-6 && shifted_cholqr3(ctx, n, W, ld, bs, R)) {
+            if (qlog) fprintf(stderr, "[kt qr] shifted cholqr3 bs %d\n", bs);
             return;
+        }
+        if (qlog)
+            fprintf(stderr, "[kt qr] householder bs %d (%s, chol %s, dmin/dmax %.2e)\n", bs,
+                    allow_shifted ? "block Arnoldi" : "block Lanczos", ok ? "ok" : "failed", ok ? dmin / dmax : 0.0);
         householder_qr(ctx, n, W, ld, bs, R);
         return;
     }

@@ -1377,10 +1377,14 @@ int kt_fun_and_grad_krylov_fun(kt_matrix_t A, int64_t nom, const double* X, cons
             }
         });
     }
+    PhaseClock pc;
     FunUpdateResult fu = fun_update_impl(A, k, U.data(), B.data(), dfun, tol_df, it);          // :64
+    const double t_fu = pc.on ? pc.lap() : 0.0;
     bool serial = !A2;
     if (A2) {
         T->wait(0);
+        if (pc.on) fprintf(stderr, "[kt fg_fun] fun_update %.3f ms, then waited %.3f ms for the twin's trace_fun_update\n",
+                           t_fu, pc.lap());
         if (terr.code == KT_ERR_ALLOC) {  // the twin's workspace did not fit: serial order
             (void)hipGetLastError();
             A2->ctx->pool.clear();  // its idle scratch blocks back to the device
