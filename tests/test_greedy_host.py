@@ -30,6 +30,69 @@ def test_find_top_edges_ties_keep_find_order():
     assert np.all(E[:, 0] > E[:, 1])               # tril(A, -1)
 
 
+@pytest.mark.parametrize("order", ["mult", "min"])
+@pytest.mark.parametrize("num", [1, 37, 200, 323])
+def test_find_top_edges_partial_sort_ties_zeros_layouts(order, num):
+    """The partial stable sort (greedy._stable_head) and the CSC read-off
+    against the oracle's full sort: heavily tied centralities (so the cut at
+    `num` falls inside a run of equal keys), explicit stored zeros (find()
+    skips them), unsorted CSC indices, and CSR / dense inputs."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(num)
+    n = 60
+    M = sp.random(n, n, density=0.2, random_state=rng, format="csr")
+    M = ((M + M.T) > 0).astype(np.float64).tolil()
+    M.setdiag(0)
+    A = sp.csc_matrix(M)
+    A.eliminate_zeros()
+    c = rng.integers(0, 4, size=n).astype(np.float64)  # 4 distinct values: long tie runs
+    ref = ko.find_top_edges(A, c, num, order)
+    # one edge stored as explicit zeros in both triangles: find() skips it
+    Z = A.copy()
+    Z.data = Z.data.copy()
+    rows = Z.indices
+    cols = np.repeat(np.arange(n), np.diff(Z.indptr))
+    k = int(np.flatnonzero(rows > cols)[0])
+    i0, j0 = int(rows[k]), int(cols[k])
+    Z.data[k] = 0.0
+    Z.data[int(np.flatnonzero((rows == j0) & (cols == i0))[0])] = 0.0
+    Ze = Z.copy()
+    Ze.eliminate_zeros()
+    num_z = min(num, sp.tril(Ze, -1).nnz)
+    ref_z = ko.find_top_edges(Ze, c, num_z, order)
+    U = A.copy()  # reversed (unsorted) row indices within each column
+    for k in range(n):
+        a, b = U.indptr[k], U.indptr[k + 1]
+        U.indices[a:b] = U.indices[a:b][::-1].copy()
+        U.data[a:b] = U.data[a:b][::-1].copy()
+    U.has_sorted_indices = False
+    for X in (A, U, A.tocsr(), A.toarray()):
+        np.testing.assert_array_equal(kra.find_top_edges(X, c, num, order), ref)
+    assert Z.nnz == A.nnz  # the zeros are stored
+    np.testing.assert_array_equal(kra.find_top_edges(Z, c, num_z, order), ref_z)
+
+
+def test_greedy_symmetry_check():
+    """greedy_krylov.m:27-29's issymmetric: the CSR == CSC fast path and the
+    elementwise fallback (explicit zeros, unsorted indices) agree with A == A'."""
+    import scipy.sparse as sp
+    from krylov_robustness_amd.greedy import _is_symmetric
+    A = sp.csc_matrix(load_graph("india"))
+    assert _is_symmetric(A)
+    B = A.tolil()
+    B[0, 1] = 2.0
+    B[1, 0] = 2.0
+    assert _is_symmetric(sp.csc_matrix(B))
+    B[0, 2] = 3.0  # one triangle only
+    assert not _is_symmetric(sp.csc_matrix(B))
+    W = A.copy()  # weights that differ across the diagonal
+    W.data = W.data.copy()
+    W.data[0] = 5.0
+    assert not _is_symmetric(W)
+    Z = sp.csc_matrix((np.r_[A.data, 0.0], (np.r_[A.tocoo().row, 0], np.r_[A.tocoo().col, 5])), shape=A.shape)
+    assert _is_symmetric(Z)  # an explicit zero in one triangle is still A == A'
+
+
 def test_find_top_edges_too_few():
     A = load_graph("denmark")
     with pytest.raises(IndexError):
