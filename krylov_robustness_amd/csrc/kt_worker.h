@@ -63,6 +63,7 @@ class StepWorker {
         (void)hipSetDevice(device_);
         for (;;) {
             std::function<void()> f;
+            bool skip;
             {
                 std::unique_lock<std::mutex> lk(m_);
                 cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
@@ -70,9 +71,10 @@ class StepWorker {
                 f = std::move(q_.front());
                 q_.pop_front();
                 busy_ = true;
+                skip = err_ != nullptr;  // read under the lock: finish() / the failing job write it
             }
             std::exception_ptr e;
-            if (!err_) {
+            if (!skip) {
                 try {
                     f();
                 } catch (...) {
@@ -128,6 +130,5 @@ struct RunWorker {
     StepWorker* operator->() const { return w; }
     explicit operator bool() const { return w != nullptr; }
 };
-
 
 }  // namespace kt
