@@ -18,8 +18,18 @@ class ColArnoldi {
     int cols() const { return C_; }
     int steps() const { return j_; }
     // one Arnoldi step for every column (arnoldi_krylov.m:78-111)
-    void step();
-    // Gm = H(1:j, 1:j) of column c (column-major j x j)
+    void step() {
+        step_launch();
+        step_finish();
+    }
+    // the same step split in two: step_launch() queues the step's kernels and
+    // the asynchronous read-back of its H column (pinned); step_finish()
+    // waits for it and fills H.  Host work on the finished steps' H may run
+    // in between (function_multiple_entries: step j's projections while the
+    // device runs step j + 1).
+    void step_launch();
+    void step_finish();
+    // Gm = H(1:j, 1:j) of column c (column-major j x j), j = finished steps
     void gm(int c, std::vector<double>& G) const;
     // (V1' e_t)(1) of column c  (function_multiple_entries.m:94-95)
     double uaux(int c) const { return uaux_[c]; }
@@ -37,7 +47,8 @@ class ColArnoldi {
     kt_matrix_s* A_;
     kt_context_s* ctx_;
     int64_t n_;
-    int C_, P_, it_, j_ = 0, nrb_;
+    int C_, P_, it_, j_ = 0, done_ = 0, nrb_;
+    bool pending_ = false;
     int64_t vs_;
     DevBuf basis_, W_, part_, red_, idx_;
     std::vector<std::vector<double>> H_;  // (it+1) x it column-major per column

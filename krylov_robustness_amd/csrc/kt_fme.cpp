@@ -11,6 +11,7 @@
 // (function_multiple_entries.m:112-156).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <unordered_map>
 
@@ -88,7 +89,8 @@ void ColArnoldi::combine(const std::vector<double>& y, int nk, double* out) {
         for (int64_t i = 0; i < n_; ++i) out[i + (size_t)c * n_] = rm[(size_t)i * P_ + c];
 }
 
-void ColArnoldi::step() {
+void ColArnoldi::step_launch() {
+    if (pending_) fail(KT_ERR_UNSUPPORTED, "ColArnoldi: a step is already in flight");
     if (j_ >= it_) fail(KT_ERR_UNSUPPORTED, "ColArnoldi: step budget exhausted");
     const int j = ++j_;
     const int n = (int)n_;
@@ -115,12 +117,29 @@ void ColArnoldi::step() {
     // reorthogonalise: hh = V' w; w = w - V hh   (:104-106)
     KT_HIP(launch_col_dots(n, P_, j, vs_, V, Vj, 0, ctx_->num_cu, part, hh, st));
     KT_HIP(launch_col_update(n, P_, j, vs_, V, hh, Vj, st));
-    std::vector<double> hb1((size_t)j * P_), hb2((size_t)j * P_), hbh((size_t)j * P_), rb(P_);
-    KT_HIP(hipMemcpyAsync(hb1.data(), h1, sizeof(double) * hb1.size(), hipMemcpyDeviceToHost, st));
-    KT_HIP(hipMemcpyAsync(hb2.data(), h2, sizeof(double) * hb2.size(), hipMemcpyDeviceToHost, st));
-    KT_HIP(hipMemcpyAsync(hbh.data(), hh, sizeof(double) * hbh.size(), hipMemcpyDeviceToHost, st));
-    KT_HIP(hipMemcpyAsync(rb.data(), rr, sizeof(double) * P_, hipMemcpyDeviceToHost, st));
-    KT_HIP(hipStreamSynchronize(st));
+    // h1 | h2 | hh (j x P each) | r (P) into pinned staging (one buffer: the
+    // previous step was finished before this one was launched)
+    const size_t jp = (size_t)j * P_;
+    PinnedBuf& sg = ctx_->ws.pin_colarn;
+    sg.ensure(sizeof(double) * (3 * jp + P_));
+    double* s = sg.as<double>();
+    KT_HIP(hipMemcpyAsync(s, h1, sizeof(double) * jp, hipMemcpyDeviceToHost, st));
+    KT_HIP(hipMemcpyAsync(s + jp, h2, sizeof(double) * jp, hipMemcpyDeviceToHost, st));
+    KT_HIP(hipMemcpyAsync(s + 2 * jp, hh, sizeof(double) * jp, hipMemcpyDeviceToHost, st));
+    KT_HIP(hipMemcpyAsync(s + 3 * jp, rr, sizeof(double) * P_, hipMemcpyDeviceToHost, st));
+    pending_ = true;
+}
+
+void ColArnoldi::step_finish() {
+    if (!pending_) return;
+    KT_HIP(hipStreamSynchronize(ctx_->stream));
+    pending_ = false;
+    const int j = j_;
+    const size_t jp = (size_t)j * P_;
+    const double* hb1 = ctx_->ws.pin_colarn.as<double>();
+    const double* hb2 = hb1 + jp;
+    const double* hbh = hb2 + jp;
+    const double* rb = hbh + jp;
     const int Hld = it_ + 1;
     for (int c = 0; c < C_; ++c) {
         std::vector<double>& Hc = H_[c];
@@ -130,10 +149,11 @@ void ColArnoldi::step() {
                 (hb1[(size_t)k * P_ + c] + hb2[(size_t)k * P_ + c]) + hbh[(size_t)k * P_ + c] * r;
         Hc[j + (size_t)(j - 1) * Hld] = r;  // H(end, end) = r   (:108)
     }
+    done_ = j;
 }
 
 void ColArnoldi::gm(int c, std::vector<double>& G) const {
-    const int j = j_, Hld = it_ + 1;
+    const int j = done_, Hld = it_ + 1;
     G.resize((size_t)j * j);
     for (int b = 0; b < j; ++b)
         for (int a = 0; a < j; ++a) G[a + (size_t)b * j] = H_[c][a + (size_t)b * Hld];
@@ -192,8 +212,16 @@ int run_group(kt_matrix_s* A, const std::vector<int64_t>& rows, std::vector<Entr
     std::vector<char> col_live(C, 1);
     const int d = 3;  // lag (function_multiple_entries.m:63)
     int j = 0;
+    // step j's projections, f(G_c) e1 and the stop test run on the host while
+    // the device runs step j + 1 (launched first; when step j says stop, that
+    // step's basis block is never read: X uses blocks 0..j).  Same arithmetic
+    // and order as step-then-host (KT_FME_PIPE=0), so the same results.
+    const char* pe = getenv("KT_FME_PIPE");
+    const bool pipe = !(pe && pe[0] == '0');
+    if (pipe) ca.step();
     for (j = 1; j <= it; ++j) {
-        ca.step();
+        if (!pipe) ca.step();
+        else if (j < it) ca.step_launch();
         std::vector<std::vector<double>> F(C);
         std::vector<int> lc;  // live columns: f(G_c) e1 each, on the host worker pool
         for (int c = 0; c < C; ++c)
@@ -229,6 +257,7 @@ int run_group(kt_matrix_s* A, const std::vector<int64_t>& rows, std::vector<Entr
         std::fill(col_live.begin(), col_live.end(), 0);
         for (const Entry& e : ents)
             if (!e.conv) col_live[e.col] = 1;
+        if (pipe) ca.step_finish();
     }
     const int iter = std::min(j, it);
     // X(h) = Um(j2, 1:nn) * Xm(:, 1) * Uaux   (:163-165)

@@ -161,7 +161,7 @@ struct Workspace {
     PinnedBuf pin_small;  // block-Krylov Gram blocks read back without a sync per pass
     // pinned staging for gram() read-backs, combine() uploads and the thin-QR
     // read-backs (pageable transfers are staged synchronously by the runtime)
-    PinnedBuf pin_gram, pin_comb, pin_qr, pin_qrfac;
+    PinnedBuf pin_gram, pin_comb, pin_qr, pin_qrfac, pin_colarn;
     hipEvent_t comb_ev = nullptr;  // last combine() upload out of pin_comb
     bool comb_pending = false;
     // batched greedy candidates (kt_greedy.cpp): 3 pair blocks, indices,
