@@ -15,6 +15,7 @@
 // test of :172-195.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <unordered_map>
@@ -126,8 +127,19 @@ int frechet_entries_impl(kt_matrix_s* A, int64_t k, const int64_t* oi, const int
     }
     const int d = 3;  // :80
     int j = 0;
+    // one group (<= 128 distinct indices): the host work of step j below runs
+    // while the device runs step j + 1 (as function_multiple_entries; the
+    // speculative step's block is never read when step j stops).  Same
+    // arithmetic, same results; KT_FRECHET_PIPE=0 steps first, then works.
+    const char* pe = getenv("KT_FRECHET_PIPE");
+    const bool pipe = groups.size() == 1 && !(pe && pe[0] == '0');
+    if (pipe) groups[0]->step();
     for (j = 1; j <= it; ++j) {
-        for (auto& g : groups) g->step();
+        if (!pipe) {
+            for (auto& g : groups) g->step();
+        } else if (j < it) {
+            groups[0]->step_launch();
+        }
         // eigendecompositions of the live projections
         std::vector<char> live(T.size(), 0);
         for (const FEntry& e : ents)
@@ -195,6 +207,7 @@ int frechet_entries_impl(kt_matrix_s* A, int64_t k, const int64_t* oi, const int
         bool stop = true;
         for (char o : open_) stop = stop && !o;
         if (stop) break;
+        if (pipe) groups[0]->step_finish();
     }
     const int iter = std::min(j, it);
     // basis rows at every target row, for every index slot
