@@ -48,6 +48,7 @@ class ColArnoldi {
     kt_context_s* ctx_;
     int64_t n_;
     int C_, P_, it_, j_ = 0, done_ = 0, nrb_;
+    int rpb_lo_ = 64;  // rows per k_col_dots workgroup, at least (kt_colbatch.hip)
     bool pending_ = false;
     int64_t vs_;
     DevBuf basis_, W_, part_, red_, idx_;

@@ -132,15 +132,20 @@ __global__ void k_col_select(int C, int P, const int* __restrict__ idx, double* 
     if (c < C) X[(int64_t)idx[c] * P + c] = 1.0;
 }
 
-static int col_rows_per_blk(int n, int num_cu) {
+// rows per workgroup of k_col_dots: about 4 workgroups per CU, at least rpb_lo
+// rows each.  The unit-start runs of function_multiple_entries / the Frechet
+// entries take rpb_lo = 32 (config 3's call 4.72 -> 4.17 ms against 64,
+// profiles/r03_fme_pipeline.txt: with 64 the launch had ~5 waves per CU);
+// the eigs restarts keep 64.  The split fixes the partial-sum order.
+static int col_rows_per_blk(int n, int num_cu, int rpb_lo) {
     int want = 4 * num_cu;
     int rpb = (n + want - 1) / want;
-    if (rpb < 64) rpb = 64;
+    if (rpb < rpb_lo) rpb = rpb_lo;
     return rpb;
 }
 
-int col_nrb(int n, int num_cu) {
-    const int rpb = col_rows_per_blk(n, num_cu);
+int col_nrb(int n, int num_cu, int rpb_lo) {
+    const int rpb = col_rows_per_blk(n, num_cu, rpb_lo);
     return (n + rpb - 1) / rpb;
 }
 
@@ -151,9 +156,9 @@ static int stream_blocks(int64_t total) {
 }
 
 hipError_t launch_col_dots(int n, int P, int nb, int64_t vstride, const double* V, const double* W,
-                           int r_lo, int num_cu, double* part, double* out, hipStream_t st) {
+                           int r_lo, int num_cu, double* part, double* out, hipStream_t st, int rpb_lo) {
     if (nb <= 0) return hipSuccess;
-    const int rpb = col_rows_per_blk(n, num_cu);
+    const int rpb = col_rows_per_blk(n, num_cu, rpb_lo);
     const int nrb = (n + rpb - 1) / rpb;
     k_col_dots<<<nrb, kColBlock, 0, st>>>(n, P, nb, vstride, V, W, rpb, r_lo, part);
     const int count = nb * P;

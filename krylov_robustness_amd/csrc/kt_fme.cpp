@@ -27,7 +27,7 @@ void ColArnoldi::init_buffers() {
     vs_ = n_ * (int64_t)P_;
     basis_.ensure(sizeof(double) * (size_t)vs_ * (it_ + 1));
     W_.ensure(sizeof(double) * (size_t)vs_);
-    nrb_ = col_nrb((int)n_, ctx_->num_cu);
+    nrb_ = col_nrb((int)n_, ctx_->num_cu, rpb_lo_);
     part_.ensure(sizeof(double) * (size_t)nrb_ * P_ * (it_ + 1));
     // red: h1 | h2 | hh (it x P each) | s (P) | r (P)
     red_.ensure(sizeof(double) * ((size_t)3 * it_ * P_ + 2 * P_));
@@ -40,12 +40,12 @@ void ColArnoldi::start_qr() {
     double* V = basis_.as<double>();
     double* sq = red_.as<double>() + (size_t)3 * it_ * P_;
     double* rr = sq + P_;
-    KT_HIP(launch_col_dots((int)n_, P_, 1, 0, V, V, 1, ctx_->num_cu, part_.as<double>(), sq, ctx_->stream));
+    KT_HIP(launch_col_dots((int)n_, P_, 1, 0, V, V, 1, ctx_->num_cu, part_.as<double>(), sq, ctx_->stream, rpb_lo_));
     KT_HIP(launch_col_householder((int)n_, P_, sq, V, V, rr, ctx_->stream));
 }
 
 ColArnoldi::ColArnoldi(kt_matrix_s* A, const std::vector<int64_t>& starts, int it)
-    : A_(A), ctx_(A->ctx), n_(A->n), C_((int)starts.size()), it_(it) {
+    : A_(A), ctx_(A->ctx), n_(A->n), C_((int)starts.size()), it_(it), rpb_lo_(32) {
     init_buffers();
     std::vector<int> ridx(starts.begin(), starts.end());
     idx_.ensure(sizeof(int) * ridx.size());
@@ -107,15 +107,15 @@ void ColArnoldi::step_launch() {
     hipStream_t st = ctx_->stream;
     spmm(A_, Vj1, P_, W, P_, C_);  // w = A * V(:, end)   (arnoldi_krylov.m:86)
     // CGS2 against the whole basis (arnoldi_krylov.m:119-125)
-    KT_HIP(launch_col_dots(n, P_, j, vs_, V, W, 0, ctx_->num_cu, part, h1, st));
+    KT_HIP(launch_col_dots(n, P_, j, vs_, V, W, 0, ctx_->num_cu, part, h1, st, rpb_lo_));
     KT_HIP(launch_col_update(n, P_, j, vs_, V, h1, W, st));
-    KT_HIP(launch_col_dots(n, P_, j, vs_, V, W, 0, ctx_->num_cu, part, h2, st));
+    KT_HIP(launch_col_dots(n, P_, j, vs_, V, W, 0, ctx_->num_cu, part, h2, st, rpb_lo_));
     KT_HIP(launch_col_update(n, P_, j, vs_, V, h2, W, st));
     // [w, r] = qr(w, 0)   (:99)
-    KT_HIP(launch_col_dots(n, P_, 1, 0, W, W, 1, ctx_->num_cu, part, sq, st));
+    KT_HIP(launch_col_dots(n, P_, 1, 0, W, W, 1, ctx_->num_cu, part, sq, st, rpb_lo_));
     KT_HIP(launch_col_householder(n, P_, sq, W, Vj, rr, st));
     // reorthogonalise: hh = V' w; w = w - V hh   (:104-106)
-    KT_HIP(launch_col_dots(n, P_, j, vs_, V, Vj, 0, ctx_->num_cu, part, hh, st));
+    KT_HIP(launch_col_dots(n, P_, j, vs_, V, Vj, 0, ctx_->num_cu, part, hh, st, rpb_lo_));
     KT_HIP(launch_col_update(n, P_, j, vs_, V, hh, Vj, st));
     // h1 | h2 | hh (j x P each) | r (P) into pinned staging (one buffer: the
     // previous step was finished before this one was launched)

@@ -176,9 +176,9 @@ hipError_t launch_poly4(int n, double beta, const double* in, double c0, double 
                         hipStream_t st,
                         int batch = 1);
 // column-batched single-vector Arnoldi (kt_colbatch.hip); V blocks at stride vstride
-int col_nrb(int n, int num_cu);
+int col_nrb(int n, int num_cu, int rpb_lo = 64);
 hipError_t launch_col_dots(int n, int P, int nb, int64_t vstride, const double* V, const double* W,
-                           int r_lo, int num_cu, double* part, double* out, hipStream_t st);
+                           int r_lo, int num_cu, double* part, double* out, hipStream_t st, int rpb_lo = 64);
 hipError_t launch_col_update(int n, int P, int nb, int64_t vstride, const double* V,
                              const double* h, double* W, hipStream_t st);
 hipError_t launch_col_householder(int n, int P, const double* s, double* W, double* Q, double* r,
