@@ -577,10 +577,8 @@ struct BlockLanczos {
         }
         std::vector<double> R;
         block_qr(ctx, n, W.col(0), PB, bs, R);  // [w, R] = qr(w, 0)   :90
-        if (hg) {
-            KT_HIP(hipStreamSynchronize(ctx->stream));  // (the QR's read of R has drained the copies)
+        if (hg)  // (block_qr synchronised the stream after the read-backs were queued)
             for (size_t t = 0; t < cnt; ++t) h[t] = (0.0 + hg[t]) + hg[cnt + t];  // h += g, twice
-        }
         // H(max(1,end-3bs+1):end-bs, end-bs+1:end) = h      :88
         const int c0 = Hc - bs;
         auto put = [&](int s, int row0) {
@@ -693,7 +691,9 @@ struct BlockArnoldi {
         std::vector<double> r;
         block_qr(ctx, n, W.col(0), PB, bs, r, true);  // [w, r] = qr(w, 0)   :99
         lucky = norm2_small(bs, bs, r.data()) < 1e-12;  // :100-102
-        KT_HIP(hipStreamSynchronize(ctx->stream));    // (the QR's read of r has drained the copies)
+        // (no sync here: every block_qr path synchronises the stream after the
+        // two Gram read-backs were queued -- its own Gram or factor read-back --
+        // so hg is complete; the QR's trailing W R^-1 may still run)
         std::vector<double> h(cnt);
         for (size_t t = 0; t < cnt; ++t) h[t] = (0.0 + hg[t]) + hg[cnt + t];  // h += g, twice
         grow(bs);  // :93-94
