@@ -159,6 +159,7 @@ struct Workspace {
     DevBuf expmv_state;                                 // expmv stage stop state (device)
     PinnedBuf host_trec;
     PinnedBuf pin_small;  // block-Krylov Gram blocks read back without a sync per pass
+    PinnedBuf pin_arn;    // block Arnoldi's Gram read-backs, two step slots (sized once per run)
     // pinned staging for gram() read-backs, combine() uploads and the thin-QR
     // read-backs (pageable transfers are staged synchronously by the runtime)
     PinnedBuf pin_gram, pin_comb, pin_qr, pin_qrfac, pin_colarn;

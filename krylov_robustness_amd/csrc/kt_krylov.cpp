@@ -642,6 +642,13 @@ struct BlockArnoldi {
 
     void start(const double* U) {
         PhaseClock pc;
+        pre_ = false;
+        hpar_ = 0;
+        // the Gram read-backs of two consecutive steps (the next step's first
+        // passes are queued before this step's last read-back is consumed):
+        // sized once for the whole run, so no reallocation under a copy
+        slot_ = (size_t)3 * (size_t)maxblk * PB * bs;
+        ctx->ws.pin_arn.ensure(sizeof(double) * 2 * slot_);
         KT_HIP(hipMemset2DAsync(blk(0), sizeof(double) * ld(), 0, sizeof(double) * PB, (size_t)n, ctx->stream));
         upload_rows(A, U, bs, blk(0), ld());
         const double t_up = pc.on ? pc.lap() : 0.0;
@@ -660,21 +667,37 @@ struct BlockArnoldi {
     }
     void extend() { add_inf_pole(nblk - 1); }
 
+    // w = A * V(:, last block), then the two CGS passes against the nb blocks
+    // V(:, 0:nb) (:86, :119-125) with the Gram blocks kept on the device and
+    // read back (pinned, asynchronously) into step slot `par`
+    void head(int last, int nb, int par) {
+        const int L = ld();
+        const int pv = nb * PB;
+        spmm(A, blk(last), L, W.col(0), PB, bs);  // w = A * w   :86
+        if (gram_host_path()) return;             // (the host-path A/B projects in add_inf_pole)
+        const size_t cnt = (size_t)pv * bs;
+        double* hg = ctx->ws.pin_arn.as<double>() + (size_t)par * slot_;
+        for (int pass = 0; pass < 2; ++pass) {
+            const double* dG = gram_device(ctx, n, V.col(0), L, pv, W.col(0), PB, bs);
+            KT_HIP(hipMemcpyAsync(hg + pass * cnt, dG, sizeof(double) * cnt, hipMemcpyDeviceToHost, ctx->stream));
+            combine_device(ctx, n, V.col(0), L, pv, dG, bs, -1.0, 1.0, W.col(0), PB);
+        }
+    }
+
     void add_inf_pole(int last) {
         if (nblk >= maxblk) fail(KT_ERR_UNSUPPORTED, "Arnoldi basis capacity exceeded");
         const int L = ld();
         const int pv = nblk * PB;
-        spmm(A, blk(last), L, W.col(0), PB, bs);  // w = A * w   :86
-        // CGS2 :119-125 with the Gram blocks kept on the device: each pass's
-        // h_p = V'w feeds w = w - V h_p directly; the two blocks are read back
-        // (pinned, asynchronously) for H and summed once the QR below has synced
         const size_t cnt = (size_t)pv * bs;
-        PinnedBuf& hp = ctx->ws.pin_small;
-        hp.ensure(sizeof(double) * 3 * cnt);
-        double* hg = hp.as<double>();
+        const bool host_path = gram_host_path();
+        // the spmm and the first two CGS2 passes of this step were queued at
+        // the end of the previous one (pre_), while its last read-back drained
+        if (!pre_) head(last, nblk, hpar_);
+        pre_ = false;
+        double* hg = ctx->ws.pin_arn.as<double>() + (size_t)hpar_ * slot_;
         // w = w - V (V'w), the Gram block read back into hg + off
         auto project = [&](size_t off) {
-            if (gram_host_path()) {  // A/B: through the host, one round trip per pass
+            if (host_path) {  // A/B: through the host, one round trip per pass
                 std::vector<double> g;
                 gram(ctx, n, V.col(0), L, pv, W.col(0), PB, bs, g);
                 std::vector<double> C(g.size());
@@ -687,7 +710,8 @@ struct BlockArnoldi {
             KT_HIP(hipMemcpyAsync(hg + off, dG, sizeof(double) * cnt, hipMemcpyDeviceToHost, ctx->stream));
             combine_device(ctx, n, V.col(0), L, pv, dG, bs, -1.0, 1.0, W.col(0), PB);
         };
-        for (int pass = 0; pass < 2; ++pass) project(pass * cnt);
+        if (host_path)
+            for (int pass = 0; pass < 2; ++pass) project(pass * cnt);
         std::vector<double> r;
         block_qr(ctx, n, W.col(0), PB, bs, r, true);  // [w, r] = qr(w, 0)   :99
         lucky = norm2_small(bs, bs, r.data()) < 1e-12;  // :100-102
@@ -704,8 +728,21 @@ struct BlockArnoldi {
                 if (i % PB < bs) H[hrow(i) + (size_t)(c0 + j) * Hr] = h[i + (size_t)j * pv];  // :96
         // reorthogonalise :104-106
         project(2 * cnt);
+        if (!host_path) {  // the read-back of hh is complete at this event
+            if (!hh_ev_) KT_HIP(hipEventCreateWithFlags(&hh_ev_, hipEventDisableTiming));
+            KT_HIP(hipEventRecord(hh_ev_, ctx->stream));
+        }
         copy_cols(ctx, n, W.col(0), PB, blk(nblk), L, PB);  // V = [V, w]   :110
-        KT_HIP(hipStreamSynchronize(ctx->stream));
+        // queue the next step's spmm and first two passes (they read the block
+        // just copied; stream order) before waiting for this read-back, so the
+        // device keeps working through the host's turn-around.  When the run
+        // stops here they are never used (W and the other slot only).
+        if (!host_path && nblk + 1 < maxblk && !lucky) {
+            head(nblk, nblk + 1, hpar_ ^ 1);
+            pre_ = true;
+        }
+        if (pre_) KT_HIP(hipEventSynchronize(hh_ev_));  // (not the queued head behind it)
+        else KT_HIP(hipStreamSynchronize(ctx->stream));
         std::vector<double> hh(hg + 2 * cnt, hg + 3 * cnt);
         std::vector<double> hr((size_t)pv * bs);
         matmul(pv, bs, bs, hh.data(), r.data(), hr.data());
@@ -715,7 +752,20 @@ struct BlockArnoldi {
         for (int j = 0; j < bs; ++j)  // :108
             for (int i = 0; i < bs; ++i) H[(Hr - bs + i) + (size_t)(c0 + j) * Hr] = r[i + (size_t)j * bs];
         nblk += 1;
+        if (pre_) hpar_ ^= 1;
     }
+
+    ~BlockArnoldi() {
+        if (hh_ev_) (void)hipEventDestroy(hh_ev_);
+    }
+    BlockArnoldi(const BlockArnoldi&) = delete;
+    BlockArnoldi& operator=(const BlockArnoldi&) = delete;
+
+   private:
+    hipEvent_t hh_ev_ = nullptr;
+    bool pre_ = false;  // the next step's head() is queued
+    int hpar_ = 0;      // pinned read-back slot of the current step
+    size_t slot_ = 0;   // doubles per slot
 };
 
 // Cm = (V1' U) B (V1' U)'   (trace_fun_update.m:65-66, fun_update.m:80-81)
