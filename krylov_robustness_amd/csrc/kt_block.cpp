@@ -522,9 +522,20 @@ static bool shifted_cholqr3(kt_context_s* ctx, int64_t n, double* W, int ld, int
     DevBuf& t = ctx->ws.qrtmp;
     if (!inplace) t.ensure(sizeof(double) * (size_t)std::max<int64_t>(n, 1) * bs);
     const double c0 = 11.0 * ((double)n * bs + (double)bs * (bs + 1)) * DBL_EPSILON;
+    PinnedBuf& hp = ctx->ws.pin_qrfac;
+    hp.ensure(sizeof(double) * 3 * bb + 4 * sizeof(int));
+    double* hR = hp.as<double>();
+    int* hok = reinterpret_cast<int*>(hR + 3 * bb);
+    Workspace& ws = ctx->ws;
+    if (!ws.qrfac_ev) KT_HIP(hipEventCreateWithFlags(&ws.qrfac_ev, hipEventDisableTiming));
     for (int p = 0; p < 3; ++p) {
         const double* dG = gram_device(ctx, n, W, ld, bs, W, ld, bs);
         KT_HIP(launch_chol_rinv(bs, dG, p == 0 ? c0 : 0.0, dR + p * bb, dRi, dok + p, ctx->stream));
+        if (p == 2) {  // the factors come back while the last W R^-1 runs (the host waits for them only)
+            KT_HIP(hipMemcpyAsync(hR, dR, sizeof(double) * 3 * bb, hipMemcpyDeviceToHost, ctx->stream));
+            KT_HIP(hipMemcpyAsync(hok, dok, 3 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+            KT_HIP(hipEventRecord(ws.qrfac_ev, ctx->stream));
+        }
         if (inplace) {
             combine_device(ctx, n, W, ld, bs, dRi, bs, 1.0, 0.0, W, ld);
         } else {
@@ -532,13 +543,7 @@ static bool shifted_cholqr3(kt_context_s* ctx, int64_t n, double* W, int ld, int
             copy_cols(ctx, n, t.as<double>(), bs, W, ld, bs);
         }
     }
-    PinnedBuf& hp = ctx->ws.pin_qrfac;
-    hp.ensure(sizeof(double) * 3 * bb + 4 * sizeof(int));
-    double* hR = hp.as<double>();
-    int* hok = reinterpret_cast<int*>(hR + 3 * bb);
-    KT_HIP(hipMemcpyAsync(hR, dR, sizeof(double) * 3 * bb, hipMemcpyDeviceToHost, ctx->stream));
-    KT_HIP(hipMemcpyAsync(hok, dok, 3 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    KT_HIP(hipStreamSynchronize(ctx->stream));
+    KT_HIP(hipEventSynchronize(ws.qrfac_ev));
     const double* R1 = hR;
     const double* R2 = hR + bb;
     const double* R3 = hR + 2 * bb;

@@ -164,6 +164,7 @@ struct Workspace {
     // read-backs (pageable transfers are staged synchronously by the runtime)
     PinnedBuf pin_gram, pin_comb, pin_qr, pin_qrfac, pin_colarn;
     hipEvent_t comb_ev = nullptr;  // last combine() upload out of pin_comb
+    hipEvent_t qrfac_ev = nullptr;  // shifted CholeskyQR3's factor read-back (kt_block.cpp)
     bool comb_pending = false;
     // batched greedy candidates (kt_greedy.cpp): 3 pair blocks, indices,
     // per-candidate coefficients / partials / host records

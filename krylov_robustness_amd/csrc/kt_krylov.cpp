@@ -715,9 +715,9 @@ struct BlockArnoldi {
         std::vector<double> r;
         block_qr(ctx, n, W.col(0), PB, bs, r, true);  // [w, r] = qr(w, 0)   :99
         lucky = norm2_small(bs, bs, r.data()) < 1e-12;  // :100-102
-        // (no sync here: every block_qr path synchronises the stream after the
-        // two Gram read-backs were queued -- its own Gram or factor read-back --
-        // so hg is complete; the QR's trailing W R^-1 may still run)
+        // (no sync here: every block_qr path waits for the stream up to a point
+        // queued after the two Gram read-backs -- its own Gram or factor
+        // read-back -- so hg is complete; the QR's trailing W R^-1 may still run)
         std::vector<double> h(cnt);
         for (size_t t = 0; t < cnt; ++t) h[t] = (0.0 + hg[t]) + hg[cnt + t];  // h += g, twice
         grow(bs);  // :93-94
