@@ -721,9 +721,18 @@ void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std
             for (int l = k; l < bs; ++l) s += T[k + (size_t)l * bs] * V1[(size_t)j * BP + l];
             M[(size_t)k * bs + j] = s;
         }
-    KT_HIP(hipMemcpyAsync(Md, M.data(), sizeof(double) * M.size(), hipMemcpyHostToDevice, ctx->stream));
+    // M goes up through pinned staging guarded by an event (rewritten only
+    // once the previous upload out of it completed), so the formation of Q
+    // runs on without a stream sync here
+    if (ws.qrm_pending) KT_HIP(hipEventSynchronize(ws.qrm_ev));
+    ws.qrm_pending = false;
+    if (!ws.qrm_ev) KT_HIP(hipEventCreateWithFlags(&ws.qrm_ev, hipEventDisableTiming));
+    ws.pin_qrm.ensure(sizeof(double) * M.size());
+    std::memcpy(ws.pin_qrm.ptr, M.data(), sizeof(double) * M.size());
+    KT_HIP(hipMemcpyAsync(Md, ws.pin_qrm.ptr, sizeof(double) * M.size(), hipMemcpyHostToDevice, ctx->stream));
+    KT_HIP(hipEventRecord(ws.qrm_ev, ctx->stream));
+    ws.qrm_pending = true;
     KT_HIP(launch_ts_formq((int)n, bs, BP, V, Md, W, ld, ctx->stream));
-    KT_HIP(hipStreamSynchronize(ctx->stream));  // M lives on this frame
 }
 
 }  // namespace kt

@@ -162,9 +162,11 @@ struct Workspace {
     PinnedBuf pin_arn;    // block Arnoldi's Gram read-backs, two step slots (sized once per run)
     // pinned staging for gram() read-backs, combine() uploads and the thin-QR
     // read-backs (pageable transfers are staged synchronously by the runtime)
-    PinnedBuf pin_gram, pin_comb, pin_qr, pin_qrfac, pin_colarn;
+    PinnedBuf pin_gram, pin_comb, pin_qr, pin_qrfac, pin_colarn, pin_qrm;
     hipEvent_t comb_ev = nullptr;  // last combine() upload out of pin_comb
     hipEvent_t qrfac_ev = nullptr;  // shifted CholeskyQR3's factor read-back (kt_block.cpp)
+    hipEvent_t qrm_ev = nullptr;    // last upload of the thin QR's T V1' out of pin_qrm
+    bool qrm_pending = false;
     bool comb_pending = false;
     // batched greedy candidates (kt_greedy.cpp): 3 pair blocks, indices,
     // per-candidate coefficients / partials / host records

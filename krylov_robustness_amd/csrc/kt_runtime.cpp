@@ -365,6 +365,7 @@ int kt_context_destroy(kt_context_t ctx) {
     if (ctx->blas) rocblas_destroy_handle(static_cast<rocblas_handle>(ctx->blas));
     if (w.comb_ev) (void)hipEventDestroy(w.comb_ev);
     if (w.qrfac_ev) (void)hipEventDestroy(w.qrfac_ev);
+    if (w.qrm_ev) (void)hipEventDestroy(w.qrm_ev);
     w.host_trec.release();
     for (auto a : ctx->aux_stream)
         if (a) (void)hipStreamDestroy(a);
