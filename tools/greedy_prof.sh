@@ -1,8 +1,12 @@
-# Config-5 greedy: parity tests, bench (3 repeats), rocprofv3 kernel stats.
+# rocprofv3 kernel stats of the config-5 greedy bench (device-queued loop)
 set -e
-mkdir -p gpurun_out/gp
-timeout -k 10 400 python -m pytest tests/test_gpu_greedy.py tests/test_gpu_datasets.py -q -x > gpurun_out/gp/tests.log 2>&1
-timeout -k 10 300 python tests/perf/bench_greedy.py --cpu-steps 0 --repeat 3 > gpurun_out/gp/bench.json 2> gpurun_out/gp/bench.err
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/gp/prof -o run -- python3 $GRAFT_REPO_ROOT/tests/perf/bench_greedy.py --cpu-steps 0 --repeat 1 > $GRAFT_REPO_ROOT/gpurun_out/gp/prof.log 2>&1
-echo done
+O=gpurun_out/grprof; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/p -o run --output-format csv -- python3 tests/perf/bench_greedy.py --cpu-steps 0 --repeat 3 > $O/log.txt 2>&1
+find $O/p -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+python3 - <<'PY'
+import csv
+rows = list(csv.DictReader(open("gpurun_out/grprof/kernel_stats.csv")))
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:10]:
+    print(f'{r["Name"][:60]:60s} {int(r["Calls"]):6d} calls {float(r["AverageNs"])/1e3:8.2f} us avg {float(r["TotalDurationNs"])/1e6:8.2f} ms')
+PY
