@@ -148,6 +148,8 @@ def _stable_head(key, num):
     if num >= len(key):
         return np.argsort(key, kind="stable")
     th = np.partition(key, num - 1)[num - 1]
+    if np.isnan(th):  # NaN keys sort last in argsort: take the full sort
+        return np.argsort(key, kind="stable")[:num]
     cand = np.flatnonzero(key <= th)
     return cand[np.argsort(key[cand], kind="stable")][:num]
 

@@ -72,6 +72,18 @@ def test_find_top_edges_partial_sort_ties_zeros_layouts(order, num):
     np.testing.assert_array_equal(kra.find_top_edges(Z, c, num_z, order), ref_z)
 
 
+def test_stable_head_matches_full_sort():
+    """greedy._stable_head == argsort(kind="stable")[:num], NaN keys included."""
+    from krylov_robustness_amd.greedy import _stable_head
+    rng = np.random.default_rng(3)
+    for trial in range(20):
+        key = rng.integers(0, 5, size=50).astype(np.float64)
+        if trial % 4 == 0:
+            key[rng.integers(0, 50, size=30)] = np.nan
+        for num in (1, 7, 25, 49, 50):
+            np.testing.assert_array_equal(_stable_head(key, num), np.argsort(key, kind="stable")[:num])
+
+
 def test_greedy_symmetry_check():
     """greedy_krylov.m:27-29's issymmetric: the CSR == CSC fast path and the
     elementwise fallback (explicit zeros, unsorted indices) agree with A == A'."""
