@@ -48,6 +48,18 @@ def parse():
                          "0 = the library default: 2 for the y-form pass, 3 for the explicit sweep)")
     ap.add_argument("--explicit", action="store_true",
                     help="explicit K1/K2 CGS2 sweep instead of the y-form pass (KT_SLQ_YFORM=0)")
+    ap.add_argument("--weighted", action="store_true",
+                    help="seeded fp64 weights on the graph (graphs.symmetric_weights, uniform [0.5, 1.5)): "
+                         "the weighted drivers' A, values read (12 B per nonzero)")
+    ap.add_argument("--estimator", default="hutchinson", choices=["hutchinson", "mc_trace"],
+                    help="headline estimator: plain Hutchinson over N probes (BASELINE configs[3]) or "
+                         "trace_exp.m's own mc_trace structure (Lanczos-exp Afun, tol 1e-4, maxit 1000)")
+    ap.add_argument("--mc-steps", type=int, default=5,
+                    help="timed trace_exp (mc_trace) evaluations reported beside the headline "
+                         "(0 = skip that leg unless --estimator mc_trace)")
+    ap.add_argument("--bitstable", action="store_true",
+                    help="all-gather the per-probe forms and sum them in global probe order on every "
+                         "rank (SURVEY §8e): the estimate is bit-identical for any number of ranks")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
@@ -56,13 +68,37 @@ def parse():
     return ap.parse_args()
 
 
-def make_graph(config):
+def make_graph(config, weighted=False):
     from krylov_robustness_amd import graphs
     if config == "sf1m":
-        return graphs.chung_lu(1_000_000, 10_000_000, gamma=2.5, seed=0), 1024, \
-            "chung_lu n=1M nnz=10M gamma=2.5 (BASELINE configs[3])"
-    return graphs.erdos_renyi(100_000, 500_000, seed=0), 128, \
-        "erdos_renyi n=100k nnz~1M (BASELINE configs[1])"
+        A, N, wl = (graphs.chung_lu(1_000_000, 10_000_000, gamma=2.5, seed=0), 1024,
+                    "chung_lu n=1M nnz=10M gamma=2.5 (BASELINE configs[3])")
+    else:
+        A, N, wl = (graphs.erdos_renyi(100_000, 500_000, seed=0), 128,
+                    "erdos_renyi n=100k nnz~1M (BASELINE configs[1])")
+    if weighted:
+        A = graphs.symmetric_weights(A, seed=1)
+        wl += ", weighted: symmetric_weights(seed=1) uniform [0.5, 1.5)"
+    return A, N, wl
+
+
+def reference_trace(config, weighted=False):
+    """tr(exp(A)) of the bench graph from its spectrum (tests/golden/
+    config4_values.json, written in the build container by
+    tests/golden/make_config4_fixture.py: scipy eigsh top 16, every other
+    term bounded by exp(lambda_16)), or None for graphs without one."""
+    if config != "sf1m":
+        return None
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "config4_values.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    spec = d["weighted"]["spectrum"] if weighted else d["spectrum"]
+    return {"value": spec["tr_exp_topk"], "rel_uncertainty": spec["tr_exp_rel_uncertainty"],
+            "lambda1": spec["lambda_desc"][0],
+            "source": "tests/golden/config4_values.json: sum exp(lambda_i) over the top 16 "
+                      "eigenvalues (scipy eigsh, tol 0), the rest bounded by (n-16) exp(lambda_16)"}
 
 
 def cpu_share():
@@ -135,19 +171,22 @@ def _kernel_template_args(name):
     return base.strip(), [a.strip() for a in rest.rstrip(">").split(",")] if rest else []
 
 
-def _pmc_traffic(kernel, P):
+def _pmc_traffic(kernel, P, config="sf1m", weighted=False):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    counter summary (profiles/traffic.json, produced by tools/gpu_prof.sh +
-    tools/pmc_traffic.py on this same bench command), or None.  Matches the
-    kernel's name and its first template argument (the probe block P)
-    exactly, so P = 1 never picks up the P = 16 entry."""
+    counter summary (profiles/traffic.json, section = the bench workload,
+    written by tools/pmc_traffic.py from counter passes of this same bench
+    command), or None.  Matches the kernel's name and its first template
+    argument (the probe block P) exactly, so P = 1 never picks up P = 16."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    for k, v in t.items():
+    sec = t.get(config + ("_weighted" if weighted else ""))
+    if not isinstance(sec, dict):
+        return None
+    for k, v in sec.items():
         base, targs = _kernel_template_args(k)
         if base == kernel and targs[:1] == [str(P)] and isinstance(v, dict):
             return v.get("hbm_bytes_per_launch")
@@ -163,6 +202,23 @@ def _metric_name(n, nnz):
         return str(x)
     # BASELINE.json's metric string, with n / nnz of the graph actually used
     return f"trace(exp(A)) evals/sec + achieved HBM GB/s, n={short(n)} nnz={short(nnz)}, 1/2/4/8 GPU"
+
+
+def _hutchinson(s1, m2, N):
+    """Plain Hutchinson over N probes: estimate = mean q, standard error from
+    the sample variance of the N quadratic forms (m2 = sum (q - mean)^2)."""
+    tr = s1 / N
+    return tr, (math.sqrt(m2 / (N - 1) / N) if N > 1 else None)
+
+
+def _pooled(sums, N):
+    """Hutchinson over the forms of several evaluations of N probes each: the
+    pooled mean and its standard error (Chan et al.'s combination of the
+    per-evaluation centred moments)."""
+    K = len(sums)
+    mu = sum(s for s, _ in sums) / (N * K)
+    m2 = sum(m for _, m in sums) + sum(N * (s / N - mu) ** 2 for s, _ in sums)
+    return mu, (math.sqrt(m2 / (N * K - 1) / (N * K)) if N * K > 1 else None)
 
 
 def main():
@@ -193,7 +249,7 @@ def main():
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # where the sums meet
 
     import krylov_robustness_amd as kra
-    A, N, wl = make_graph(args.config)
+    A, N, wl = make_graph(args.config, args.weighted)
     if args.nprobes:
         N = args.nprobes
     m = args.m
@@ -201,153 +257,266 @@ def main():
     ctx = kra.Context(local_rank)
     D = kra.DeviceMatrix(A, ctx)
     off, cnt = kdist.probe_shard(N, rank, world)
-    P = args.block or kra.slq_plan(D, cnt, ctx=ctx)
+    counts = [kdist.probe_shard(N, r, world)[1] for r in range(world)]
+    # --bitstable plans the sweep width on the GLOBAL probe count, so every
+    # world size runs each probe in a sweep of the same width
+    P = args.block or kra.slq_plan(D, N if args.bitstable else cnt, ctx=ctx)
+    ref = reference_trace(args.config, args.weighted) if m >= 20 else None
 
     def step(seed):
-        s1, s2, _ = kra.slq_quadforms(D, cnt, m, seed=seed, probe_offset=off, block=P, ctx=ctx)
-        s1, s2 = kdist.allreduce_sums([s1, s2], device=coll_dev, force=use_pg)
-        return s1, s2
+        s1, s2, q = kra.slq_quadforms(D, cnt, m, seed=seed, probe_offset=off, block=P, ctx=ctx)
+        if args.bitstable:  # every rank reduces all N forms in global probe order
+            return kdist.bitstable_sums(q, counts)
+        return kdist.centred_sums(q, N, device=coll_dev, force=use_pg)
 
     def barrier():
         if use_pg:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    for w in range(args.warmup):
-        step(1000 + w)
-    if not args.no_profile:
-        ctx.profile_reset()
-        ctx.profile(True)
-    barrier()
-    t0 = time.perf_counter()
-    sums = None
-    for s in range(args.steps):
-        sums = step(s)
-    barrier()
-    el = time.perf_counter() - t0
-    if not args.no_profile:
-        ctx.profile(False)
-    el_max = kdist.allreduce_max(el, device=coll_dev, force=use_pg)
-    # plain Hutchinson over N probes: estimate = mean q, standard error from
-    # the sample variance of the N quadratic forms (sum q, sum q^2)
-    tr = sums[0] / N
-    var = max(sums[1] - N * tr * tr, 0.0) / (N - 1) if N > 1 else float("nan")
-    tr_stderr = math.sqrt(var / N) if N > 1 else None
-    k1_overlapped = None
-    timed = None
-    if not args.no_profile:
-        l1, ms1 = ctx.profile_read(0)
-        k1_overlapped = round(ms1 / l1 * 1e3, 2) if l1 else None
-        # union of the launches' event intervals over the lanes' streams:
-        # time with >= 1 dominant launch in flight, overlap counted once
-        timed = (l1, ctx.profile_busy(0)) if l1 else None
-        # Roofline pass: with several lanes in flight the per-launch event
-        # times include the other lanes' kernels, so the dominant kernel's
-        # duration is measured on an isolated single-lane pass (4 sweeps of
-        # the same P-probe block, m steps each) right after the timed region.
-        os.environ["KT_SLQ_LANES"] = "1"
-        ctx.profile_reset()
-        ctx.profile(True)
-        kra.slq_quadforms(D, 4 * P, m, seed=777, probe_offset=0, block=P, ctx=ctx)
-        ctx.profile(False)
-        os.environ["KT_SLQ_LANES"] = str(args.lanes)
-
-    ms_per_step = el_max * 1e3 / args.steps
-    value = args.steps / el_max
-    # algorithmic bytes: one launch of the dominant kernel = one
-    # Lanczos step of one P-probe sweep: CSR (12 nnz + 4(n+1)) + gather source,
-    # previous vector, next vector (8nP each).  The y-form pass
-    # (k_spmm_lanczos) moves exactly these streams; the explicit sweep's K1 is
-    # charged the whole step although its K2 streams two of them.
-    kbase = "k_spmm_dot" if args.explicit else "k_spmm_lanczos"
-    kname = f"{kbase}<{P}"
-    # SURVEY's per-unit figure charges fp64 values + int32 columns (12 B per
-    # nonzero).  A unit-weight matrix (every stored value 1.0, detected when
-    # the device matrix is created) never reads the values: its kernels'
-    # compulsory CSR bytes are 4 B per nonzero, and that is the figure the
-    # roofline fraction uses (the SURVEY figure is kept beside it, labelled).
-    unit = bool(A.nnz) and bool(np.all(A.data == 1.0))
-    per_nnz = 4 if unit else 12
-    k1_bytes_survey = 12 * nnz + 4 * (n + 1) + 24 * n * P
-    k1_bytes = per_nnz * nnz + 4 * (n + 1) + 24 * n * P
-    sweeps = math.ceil(cnt / P)
-    b_eval_rank = m * (sweeps * (per_nnz * nnz + 4 * (n + 1)) + 24 * n * cnt)
-    b_eval_rank_survey = m * (sweeps * (12 * nnz + 4 * (n + 1)) + 24 * n * cnt)
-    roof = None
+    run_hutch = args.estimator == "hutchinson"
     extra = {}
-    if not args.no_profile:
-        l1, ms1 = ctx.profile_read(0)
-        l2, ms2 = ctx.profile_read(1)
-        if l1 and timed:
-            iso_ms = ms1 / l1
-            iso_gbs = k1_bytes / (iso_ms * 1e-3) / 1e9
-            tl, busy_ms = timed
-            k1_ms = busy_ms / tl  # effective duration per launch in the timed region
-            achieved = k1_bytes / (k1_ms * 1e-3) / 1e9
-            # PMC bytes were profiled on the sf1m graph (tools/gpu_prof.sh); other
-            # graphs report traffic null
-            traffic = _pmc_traffic(kbase, P) if args.config == "sf1m" else None
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": kname + ">", "avg_launch_us": round(k1_ms * 1e3, 2),
-                    "launches": tl, "algorithmic_bytes_per_launch": k1_bytes,
-                    "algorithmic_bytes_basis": ("unit-weight matrix: 4 nnz (int32 columns; values "
-                                                "never read) + 4 (n+1) + 24 n P" if unit else
-                                                "12 nnz + 4 (n+1) + 24 n P"),
-                    "survey_bytes_per_launch": k1_bytes_survey,
-                    "survey_frac": round(k1_bytes_survey / (k1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                    "measured": "HIP events around every launch of the kernel in the timed region, "
-                                "on each sweep lane's stream; avg_launch_us = union of their intervals "
-                                "(time with >= 1 launch in flight, lane overlap counted once) / launches",
-                    "timed_region_busy_ms": round(busy_ms, 3),
-                    "timed_region_avg_launch_us_overlapped": k1_overlapped,
-                    "isolated_pass": {"avg_launch_us": round(iso_ms * 1e3, 2), "launches": l1,
-                                      "achieved": round(iso_gbs, 1),
-                                      "frac": round(iso_gbs / HBM_PEAK_GBS, 4),
-                                      "measured": "HIP events on a single-lane pass (4 sweeps x m "
-                                                  "steps) after the timed region: the kernel alone"}}
-            if traffic:  # memory-side rate: PMC bytes per launch over the same durations
-                tgbs = traffic / (k1_ms * 1e-3) / 1e9
-                roof["traffic_GBs"] = round(tgbs, 1)
-                roof["traffic_frac"] = round(tgbs / HBM_PEAK_GBS, 4)
-                roof["isolated_pass"]["traffic_GBs"] = round(traffic / (iso_ms * 1e-3) / 1e9, 1)
-            if l2:
-                extra["k2_update_avg_us"] = round(ms2 / l2 * 1e3, 2)
-            l3, ms3 = ctx.profile_read(2)
-            if l3:
-                extra["start_pass_avg_us"] = round(ms3 / l3 * 1e3, 2)
-    extra["sweep"] = "explicit K1/K2 CGS2" if args.explicit else "y-form single pass"
-    extra["yform_redone_sweeps"] = ctx.yform_redone()
-    eval_gbs = b_eval_rank / (ms_per_step * 1e-3) / 1e9
-    extra["eval_roofline"] = {"B_eval_bytes_per_rank": b_eval_rank, "achieved_GBs_per_rank":
-                              round(eval_gbs, 1), "frac": round(eval_gbs / HBM_PEAK_GBS, 4),
-                              "B_eval_bytes_per_rank_survey": b_eval_rank_survey,
-                              "unit_weight_matrix": unit}
-    extra["collective"] = (f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all_reduce of "
-                           f"(sum q, sum q^2) per evaluation" if use_pg else None)
+    value = ms_per_step = None
+    roof = None
+    if run_hutch:
+        for w in range(args.warmup):
+            step(1000 + w)
+        if not args.no_profile:
+            ctx.profile_reset()
+            ctx.profile(True)
+        barrier()
+        t0 = time.perf_counter()
+        sums = []
+        for s in range(args.steps):
+            sums.append(step(s))
+        barrier()
+        el = time.perf_counter() - t0
+        if not args.no_profile:
+            ctx.profile(False)
+        el_max = kdist.allreduce_max(el, device=coll_dev, force=use_pg)
+        tr, tr_stderr = _hutchinson(*sums[-1], N)
+        k1_overlapped = None
+        timed = None
+        if not args.no_profile:
+            l1, ms1 = ctx.profile_read(0)
+            k1_overlapped = round(ms1 / l1 * 1e3, 2) if l1 else None
+            # union of the launches' event intervals over the lanes' streams:
+            # time with >= 1 dominant launch in flight, overlap counted once
+            timed = (l1, ctx.profile_busy(0)) if l1 else None
+            # Roofline pass: with several lanes in flight the per-launch event
+            # times include the other lanes' kernels, so the dominant kernel's
+            # duration is measured on an isolated single-lane pass (4 sweeps of
+            # the same P-probe block, m steps each) right after the timed region.
+            os.environ["KT_SLQ_LANES"] = "1"
+            ctx.profile_reset()
+            ctx.profile(True)
+            kra.slq_quadforms(D, 4 * P, m, seed=777, probe_offset=0, block=P, ctx=ctx)
+            ctx.profile(False)
+            os.environ["KT_SLQ_LANES"] = str(args.lanes)
+
+        ms_per_step = el_max * 1e3 / args.steps
+        value = args.steps / el_max
+        # algorithmic bytes: one launch of the dominant kernel = one
+        # Lanczos step of one P-probe sweep: CSR (12 nnz + 4(n+1)) + gather source,
+        # previous vector, next vector (8nP each).  The y-form pass
+        # (k_spmm_lanczos) moves exactly these streams; the explicit sweep's K1 is
+        # charged the whole step although its K2 streams two of them.
+        kbase = "k_spmm_dot" if args.explicit else "k_spmm_lanczos"
+        kname = f"{kbase}<{P}"
+        # SURVEY's per-unit figure charges fp64 values + int32 columns (12 B per
+        # nonzero).  A unit-weight matrix (every stored value 1.0, detected when
+        # the device matrix is created) never reads the values: its kernels'
+        # compulsory CSR bytes are 4 B per nonzero, and that is the figure the
+        # roofline fraction uses (the SURVEY figure is kept beside it, labelled).
+        unit = bool(A.nnz) and bool(np.all(A.data == 1.0))
+        per_nnz = 4 if unit else 12
+        k1_bytes_survey = 12 * nnz + 4 * (n + 1) + 24 * n * P
+        k1_bytes = per_nnz * nnz + 4 * (n + 1) + 24 * n * P
+        sweeps = math.ceil(cnt / P)
+        b_eval_rank = m * (sweeps * (per_nnz * nnz + 4 * (n + 1)) + 24 * n * cnt)
+        b_eval_rank_survey = m * (sweeps * (12 * nnz + 4 * (n + 1)) + 24 * n * cnt)
+        if not args.no_profile:
+            l1, ms1 = ctx.profile_read(0)
+            l2, ms2 = ctx.profile_read(1)
+            if l1 and timed:
+                iso_ms = ms1 / l1
+                iso_gbs = k1_bytes / (iso_ms * 1e-3) / 1e9
+                tl, busy_ms = timed
+                k1_ms = busy_ms / tl  # effective duration per launch in the timed region
+                achieved = k1_bytes / (k1_ms * 1e-3) / 1e9
+                # PMC bytes were profiled per graph (profiles/traffic.json keyed by
+                # kernel and, for other graphs than sf1m, by config)
+                traffic = _pmc_traffic(kbase, P, args.config, args.weighted)
+                roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "kernel": kname + ">", "avg_launch_us": round(k1_ms * 1e3, 2),
+                        "launches": tl, "algorithmic_bytes_per_launch": k1_bytes,
+                        "algorithmic_bytes_basis": ("unit-weight matrix: 4 nnz (int32 columns; values "
+                                                    "never read) + 4 (n+1) + 24 n P" if unit else
+                                                    "12 nnz + 4 (n+1) + 24 n P"),
+                        "survey_bytes_per_launch": k1_bytes_survey,
+                        "survey_frac": round(k1_bytes_survey / (k1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "measured": "HIP events around every launch of the kernel in the timed region, "
+                                    "on each sweep lane's stream; avg_launch_us = union of their intervals "
+                                    "(time with >= 1 launch in flight, lane overlap counted once) / launches",
+                        "timed_region_busy_ms": round(busy_ms, 3),
+                        "timed_region_avg_launch_us_overlapped": k1_overlapped,
+                        "isolated_pass": {"avg_launch_us": round(iso_ms * 1e3, 2), "launches": l1,
+                                          "achieved": round(iso_gbs, 1),
+                                          "frac": round(iso_gbs / HBM_PEAK_GBS, 4),
+                                          "measured": "HIP events on a single-lane pass (4 sweeps x m "
+                                                      "steps) after the timed region: the kernel alone"}}
+                if traffic:  # memory-side rate: PMC bytes per launch over the same durations
+                    tgbs = traffic / (k1_ms * 1e-3) / 1e9
+                    roof["traffic_GBs"] = round(tgbs, 1)
+                    roof["traffic_frac"] = round(tgbs / HBM_PEAK_GBS, 4)
+                    roof["isolated_pass"]["traffic_GBs"] = round(traffic / (iso_ms * 1e-3) / 1e9, 1)
+                if l2:
+                    extra["k2_update_avg_us"] = round(ms2 / l2 * 1e3, 2)
+                l3, ms3 = ctx.profile_read(2)
+                if l3:
+                    extra["start_pass_avg_us"] = round(ms3 / l3 * 1e3, 2)
+        extra["sweep"] = "explicit K1/K2 CGS2" if args.explicit else "y-form single pass"
+        extra["yform_redone_sweeps"] = ctx.yform_redone()
+        eval_gbs = b_eval_rank / (ms_per_step * 1e-3) / 1e9
+        extra["eval_roofline"] = {"B_eval_bytes_per_rank": b_eval_rank, "achieved_GBs_per_rank":
+                                  round(eval_gbs, 1), "frac": round(eval_gbs / HBM_PEAK_GBS, 4),
+                                  "B_eval_bytes_per_rank_survey": b_eval_rank_survey,
+                                  "unit_weight_matrix": unit}
+        extra["collective"] = (("all_gather of the per-probe forms, summed in global probe order"
+                                if args.bitstable else "all_reduce of sum q, then of sum (q - mean)^2, "
+                                                       "per evaluation")
+                               if use_pg else None)
+        if extra["collective"]:
+            extra["collective"] = f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} {extra['collective']}"
+        extra["trace_estimate"] = tr
+        extra["trace_stderr"] = tr_stderr
+        extra["trace_stderr_basis"] = (f"sample standard deviation of the {N} per-probe quadratic "
+                                       f"forms / sqrt({N}) (plain Hutchinson), last timed evaluation")
+        ests = [_hutchinson(a, b, N)[0] for a, b in sums]
+        pooled, pooled_se = _pooled(sums, N)
+        extra["evaluations"] = {"seeds": f"0..{args.steps - 1}", "estimates": ests,
+                                "pooled_estimate": pooled, "pooled_stderr": pooled_se,
+                                "pooled_basis": f"all {N * len(sums)} forms of the timed evaluations"}
+        if ref:
+            extra["reference_trace"] = ref
+            extra["rel_err"] = (tr - ref["value"]) / ref["value"]
+            extra["err_in_stderr"] = (tr - ref["value"]) / tr_stderr if tr_stderr else None
+            extra["evaluations"]["rel_err"] = [(e - ref["value"]) / ref["value"] for e in ests]
+            extra["evaluations"]["pooled_rel_err"] = (pooled - ref["value"]) / ref["value"]
+
+    # ---- trace_exp.m's own estimator: mc_trace with the Lanczos-exp Afun ----
+    mc = None
+    mc_steps = args.mc_steps if run_hutch else max(args.mc_steps, 1)
+    if args.estimator == "mc_trace" and args.steps:
+        mc_steps = args.steps
+    if mc_steps > 0:
+        mc = _mc_trace_leg(args, kra, kdist, D, ctx, m, mc_steps, use_pg, barrier, coll_dev, world, ref,
+                           n, nnz, A)
+        if not run_hutch:
+            value, ms_per_step = mc.pop("evals_per_s"), mc.pop("ms_per_eval")
+            roof = mc.pop("roofline")
+            extra.update({k: mc.pop(k) for k in list(mc) if k not in ("estimator",)})
+            extra["estimator"] = mc["estimator"]
+            mc = None
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_seconds > 0 and run_hutch:
         cpu = cpu_baseline(A, m, args.cpu_seconds, N, args.cpu_threads)
 
     if rank == 0:
+        cfg = {"workload": wl, "n": n, "nnz": nnz, "lanczos_m": m, "fun": "exp"}
+        if run_hutch:
+            cfg.update({"estimator": "plain Hutchinson (BASELINE configs[3])", "probes_per_eval": N,
+                        "probes_per_sweep": P, "sweep_lanes": args.lanes,
+                        "parallelism": f"probes sharded x{world}"})
+        else:
+            cfg.update({"estimator": "mc_trace (trace_exp.m:5-6: tol 1e-4, maxit 1000, Lanczos-exp Afun)",
+                        "parallelism": f"G-probe columns dealt over x{world}, S/Q replicated"})
         out = {
             "metric": _metric_name(n, nnz),
-            "value": round(value, 4), "unit": "evals/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 4), "unit": "evals/s", "n_gpus": world,
+            "steps": args.steps if run_hutch else mc_steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": wl, "n": n, "nnz": nnz, "probes_per_eval": N, "lanczos_m": m,
-                       "probes_per_sweep": P, "sweep_lanes": args.lanes, "fun": "exp",
-                       "parallelism": f"probes sharded x{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "trace_estimate": tr,
-            "trace_stderr": tr_stderr,
-            "trace_stderr_basis": f"sample standard deviation of the {N} per-probe quadratic "
-                                  f"forms / sqrt({N}) (plain Hutchinson)",
+            "config": cfg, "roofline": roof, "cpu_baseline": cpu,
             **extra,
         }
+        if mc is not None:
+            out["mc_trace"] = mc
         print(json.dumps(out), flush=True)
     if use_pg:
         dist.destroy_process_group()
+
+
+def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev, world, ref, n, nnz, A):
+    """tr = trace_exp(A) as trace_exp.m:5-6 computes it: mc_trace's block
+    Hutchinson with nested deflation (mc_trace.m:42-58; K = ceil(1000/30)
+    rounds at most, stop at relative change < 1e-4) with the Lanczos-exp Afun
+    (m steps per column).  At N > 1 kt_mc_trace_sharded: S, Q replicated, the
+    10 G columns of each round dealt over the ranks, one all-reduce per round.
+    Timed like the headline (barrier + sync on both sides, max over ranks);
+    the dominant kernel's duration from an isolated serial pass (KT_TWIN=0)."""
+    def one(seed):
+        if use_pg:
+            return kdist.mc_trace_sharded("lanczos", None, 1e-4, 1000, 1, 0, seed, "exp", m, A=D, ctx=ctx,
+                                          force=True)
+        return kra.mc_trace("lanczos", None, 1e-4, 1000, 1, 0, seed=seed, fun="exp", m=m, A=D, ctx=ctx)
+
+    one(1000)  # warm-up: twin matrices, workspaces
+    barrier()
+    t0 = time.perf_counter()
+    res = [one(s) for s in range(steps)]
+    barrier()
+    el = kdist.allreduce_max(time.perf_counter() - t0, device=coll_dev, force=use_pg)
+    tr, r_last, it = res[-1]
+    out = {"estimator": "mc_trace (trace_exp.m:5-6 via mc_trace.m:42-58, Lanczos-exp Afun, m=%d)" % m,
+           "evals_per_s": round(steps / el, 4), "ms_per_eval": round(el * 1e3 / steps, 3),
+           "timed_evals": steps, "trace_estimate": tr, "rounds": it, "res": r_last,
+           "rounds_per_eval": [r[2] for r in res],
+           "probe_columns_per_eval": 30 * it,
+           "probe_columns_basis": "per round: 10 S columns, the 10 columns of Q, 10 G columns "
+                                  "(mc_trace.m:43-49), each one m-step Lanczos run"}
+    if ref:
+        out["reference_trace"] = ref["value"]
+        out["rel_err"] = (tr - ref["value"]) / ref["value"]
+        out["rel_err_max_over_evals"] = max(abs(r[0] - ref["value"]) / ref["value"] for r in res)
+    out["roofline"] = None
+    if not args.no_profile:
+        # isolated serial pass: every Afun call on this context (no twin threads)
+        prev = os.environ.get("KT_TWIN")
+        os.environ["KT_TWIN"] = "0"
+        ctx.profile_reset()
+        ctx.profile(True)
+        t1 = time.perf_counter()
+        kra.mc_trace("lanczos", None, 1e-4, 1000, 1, 0, seed=777, fun="exp", m=m, A=D, ctx=ctx)
+        serial_ms = (time.perf_counter() - t1) * 1e3
+        ctx.profile(False)
+        if prev is None:
+            os.environ.pop("KT_TWIN")
+        else:
+            os.environ["KT_TWIN"] = prev
+        l1, ms1 = ctx.profile_read(0)
+        l2, ms2 = ctx.profile_read(1)
+        if l1:
+            P = 16  # lanczos_columns: 10 columns per Afun call in one 16-wide sweep
+            unit = bool(A.nnz) and bool(np.all(A.data == 1.0))
+            per_nnz = 4 if unit else 12
+            kb = per_nnz * nnz + 4 * (n + 1) + 16 * n * P
+            us = ms1 / l1 * 1e3
+            gbs = kb / (us * 1e-6) / 1e9
+            out["roofline"] = {"bound": "hbm", "kernel": f"k_spmm_dot<{P}>", "achieved": round(gbs, 1),
+                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                               "traffic": _pmc_traffic("k_spmm_dot", P, args.config, args.weighted),
+                               "avg_launch_us": round(us, 2), "launches": l1,
+                               "algorithmic_bytes_per_launch": kb,
+                               "algorithmic_bytes_basis": f"{per_nnz} nnz + 4 (n+1) + 16 n P: the CSR, "
+                                                          "u_j gathered once, y = A u_j written",
+                               "k2_update_avg_us": round(ms2 / l2 * 1e3, 2) if l2 else None,
+                               "serial_eval_ms": round(serial_ms, 2),
+                               "measured": "HIP events around every K1 launch of one serial trace_exp "
+                                           "(KT_TWIN=0: all Afun calls on one stream) after the timed region"}
+    return out
 
 
 if __name__ == "__main__":

@@ -147,9 +147,13 @@ hipError_t launch_gram_ts(int64_t n, const double* X, int ldx, int px, const dou
 constexpr int kCombRows = 64;
 constexpr int kCombI = 64;
 
-__global__ __launch_bounds__(256) void k_combine_ts(int64_t n, const double* __restrict__ X, int ldx, int px,
+// X and Y may alias (apply_rinv and shifted_cholqr3 combine in place, q <= 32):
+// with q <= 32 the grid has one y-block, so each workgroup reads all px
+// columns of its 64 rows (the tile loop) before its first store, and no other
+// workgroup touches those rows -- hence no __restrict__ on X / Y.
+__global__ __launch_bounds__(256) void k_combine_ts(int64_t n, const double* X, int ldx, int px,
                                                     const double* __restrict__ C, int q, double alpha,
-                                                    double beta, double* __restrict__ Y, int ldy) {
+                                                    double beta, double* Y, int ldy) {
     __shared__ double Xs[kCombRows][kCombI + 1];
     __shared__ double Cs[kCombI][32];
     const int lane = threadIdx.x & 63;
@@ -209,6 +213,8 @@ __global__ __launch_bounds__(256) void k_combine_ts(int64_t n, const double* __r
 hipError_t launch_combine_ts(int64_t n, const double* X, int ldx, int px, const double* C, int q, double alpha,
                              double beta, double* Y, int ldy, hipStream_t st) {
     if (n <= 0 || q <= 0) return hipSuccess;
+    // in place only within one y-block (see k_combine_ts)
+    if (X == Y && q > 32) return hipErrorInvalidValue;
     dim3 grid((unsigned)((n + kCombRows - 1) / kCombRows), (q + 31) / 32);
     k_combine_ts<<<grid, 256, 0, st>>>(n, X, ldx, px, C, q, alpha, beta, Y, ldy);
     return hipGetLastError();

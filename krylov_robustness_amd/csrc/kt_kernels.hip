@@ -809,7 +809,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos_start(
         }
     }
     __syncthreads();
-    if (fz.tick) {  // fused coefficient step (default)
+    if (fz.tick) {  // fused coefficient step (opt-in, KT_KY_FUSED=1; kt_slq.cpp)
         fused_ycoef_tail<P, BLOCK>(red, fz);
         return;
     }
@@ -930,7 +930,7 @@ __global__ KT_KY_BOUNDS(BLOCK) void k_spmm_lanczos(
         }
     }
     __syncthreads();
-    if (fz.tick) {  // fused coefficient step (default)
+    if (fz.tick) {  // fused coefficient step (opt-in, KT_KY_FUSED=1; kt_slq.cpp)
         fused_ycoef_tail<P, BLOCK>(red, fz);
         return;
     }

@@ -374,7 +374,7 @@ extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_
         prof_collect(ctx, prev_events);
         KT_HIP(hipStreamSynchronize(ctx->stream));
         for (int l = 1; l < lanes; ++l) KT_HIP(hipStreamSynchronize(ctx->aux_stream[l - 1]));
-#ifndef KT_KY_DIAG  // (diagnostic builds time the pass alone: no redo)
+#if !defined(KT_KY_DIAG) || KT_KY_DIAG == 0  // (diagnostic builds time the pass alone: no redo)
         if (ctx->yform) {  // sweeps with a guarded probe are redone by the explicit CGS2 sweep
             int64_t redone = 0;
             for (int64_t s = 0; s < nsweeps; ++s) {

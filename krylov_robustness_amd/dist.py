@@ -72,6 +72,51 @@ def allgather_concat(x, counts, group=None):
     return np.concatenate([p[:int(c)].cpu().numpy() for p, c in zip(parts, counts)])
 
 
+def ordered_sums(q):
+    """(sum q, sum (q - mean)^2) accumulated in index order: the Hutchinson
+    estimate's sum and the centred second moment of the forms (two passes:
+    sum q^2 - N mean^2 cancels when the spread is small against the mean)."""
+    q = [float(v) for v in q]
+    s1 = 0.0
+    for v in q:
+        s1 += v
+    mu = s1 / len(q) if q else 0.0
+    m2 = 0.0
+    for v in q:
+        m2 += (v - mu) * (v - mu)
+    return s1, m2
+
+
+def centred_sums(q, nprobes, device=None, force=False):
+    """Hutchinson reduction over the ranks' probe shards: sum q by one
+    all-reduce, then every rank centres its forms on the global mean and a
+    second all-reduce sums (q - mean)^2.  Returns (sum q, sum (q - mean)^2);
+    the result differs from the single-process value only by the order the
+    shards' partial sums are added (rounding, not cancellation)."""
+    s_loc = 0.0
+    for v in q:
+        s_loc += float(v)
+    s1 = allreduce_sums([s_loc], device=device, force=force)[0]
+    mu = s1 / nprobes if nprobes else 0.0
+    m2_loc = 0.0
+    for v in q:
+        m2_loc += (float(v) - mu) * (float(v) - mu)
+    return s1, allreduce_sums([m2_loc], device=device, force=force)[0]
+
+
+def bitstable_sums(q, counts, group=None):
+    """SURVEY.md §8e's bit-stable reduction: all-gather every rank's per-probe
+    forms (rank r holds the counts[r] forms of its contiguous shard, so rank
+    order is global probe order) and reduce them in that order on every rank
+    (ordered_sums).  The per-probe forms are keyed by the global probe index,
+    so the result is bit-identical for any number of ranks, including a single
+    process (no group: the local forms, same order)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        q = allgather_concat(q, counts, group)
+    return ordered_sums(q)
+
+
 def reduce_callback(group=None, fail_on_rank=None):
     """A kt_reduce_fn (include/krylov_trace.h) that sums the buffer over the
     torch.distributed group: device tensors on RCCL ("nccl"), CPU tensors

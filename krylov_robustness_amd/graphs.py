@@ -88,3 +88,20 @@ def chung_lu(n: int = 1_000_000, nnz: int = 10_000_000, gamma: float = 2.5,
         perm = rng.permutation(n)
         i, j = perm[i], perm[j]
     return _sym_csr_from_pairs(np.minimum(i, j), np.maximum(i, j), n)
+
+
+def symmetric_weights(A, seed: int = 1, low: float = 0.5, high: float = 1.5):
+    """Seeded fp64 weights on a symmetric pattern: w_ij = w_ji uniform in
+    [low, high), drawn per undirected edge in (row, col) order of the upper
+    triangle.  The weighted drivers' A (Tests/test_weighted_exp_lbfgs.m, a
+    weighted symmetric adjacency) at the size of a synthetic pattern: every
+    stored value differs from 1, so the 12 B/nnz CSR path (values read) runs."""
+    rng = np.random.default_rng(seed)
+    U = sp.triu(sp.csr_matrix(A), k=1).tocoo()
+    order = np.lexsort((U.col, U.row))
+    r, c = U.row[order], U.col[order]
+    w = rng.uniform(low, high, r.size)
+    W = sp.coo_matrix((np.concatenate([w, w]), (np.concatenate([r, c]), np.concatenate([c, r]))),
+                      shape=A.shape).tocsr()
+    W.sort_indices()
+    return W

@@ -14,6 +14,7 @@ E(:, 1) >= E(:, 2) for krylov_miobi's candidate lists.
 from __future__ import annotations
 
 import ctypes as C
+import warnings
 from typing import Optional
 
 import numpy as np
@@ -158,8 +159,9 @@ def find_top_edges(A, centrality, num, order="mult"):
     """find_top_edges.m:1-40: the top `num` existing edges (1-based, i > j)."""
     import scipy.sparse as sp
     L = A if sp.isspmatrix_csc(A) else sp.csc_matrix(A)
-    if not L.has_sorted_indices:
-        L = L.sorted_indices()
+    if not L.has_canonical_format:  # duplicates summed (tril(A) sees sums), sorted
+        L = L.copy()
+        L.sum_duplicates()
     # find(tril(A, -1)) in column-major order, read straight off the CSC arrays
     J = np.repeat(np.arange(L.shape[1], dtype=np.int64), np.diff(L.indptr))
     keep = (L.indices > J) & (L.data != 0)
@@ -179,6 +181,11 @@ def find_top_edges(A, centrality, num, order="mult"):
         key = mx * (mx - 1) / 2 + mn
     else:
         return np.stack([I + 1, J + 1], axis=1)
+    # :19-21 warns when fewer than num edges exist; E(ind(1:num), :) then
+    # indexes floor(num) of them and fails only if those are missing too
+    if len(I) < num:
+        warnings.warn("FIND_TOP_EDGES:: there are not enough edges in the graph")
+    num = int(np.floor(num))
     if len(I) < num:
         raise IndexError("FIND_TOP_EDGES:: there are not enough edges in the graph")
     ind = _stable_head(key, num)
@@ -203,7 +210,7 @@ def find_top_missing_edges(A, centrality, num, order="min"):
             for t in np.flatnonzero(col == 0):
                 E.append((indC[t] + 1, indC[j] + 1))
             j += 1
-        return np.array(E[:num], dtype=np.int64)
+        return np.array(E[:int(np.floor(num))], dtype=np.int64)  # E(1:num, :) with a fractional num
     if order == "mult":  # :22-51
         if (n * n - A.nnz - n) / 2 <= num:
             raise RuntimeError("FIND_TOP_MISSING_EDGES:: output E is not assigned on this branch "
@@ -293,13 +300,17 @@ def greedy_krylov(A, k, Q=0, centrality=None, order="mult", tol=1e-12, it=None, 
         # :42-44 Q = max(sum(A, 1)); top_edges(1:Q, :) indexes floor(Q) rows, so
         # a weighted graph whose largest weighted degree is below 1 gives Q = 0,
         # an empty E, and krylov_miobi then scores every edge (krylov_miobi.m:43-46)
-        Q = int(np.floor(np.asarray(S.sum(axis=0)).max()))
+        Q = float(np.asarray(S.sum(axis=0)).max())
+    # the ranking is asked for Q + k edges unfloored (find_top_edges.m:19 warns
+    # against that count); every index use is 1:Q, i.e. floor(Q) rows
+    Qn = Q + k
+    Q = int(np.floor(Q))
     if miobi == "break" and S.nnz < 2 * k:  # :54-56
         raise _lib.KrylovError(_lib.KT_ERR_ARG, "GREEDY_KRYLOV:: edges to be removed are more than edges in the network")
     if centrality is None:
         centrality = compute_centrality(D, "eig", ctx=ctx)
-    top = (find_top_missing_edges(S, centrality, Q + k, order) if miobi == "make"
-           else find_top_edges(S, centrality, Q + k, order))  # :82 (first step)
+    top = (find_top_missing_edges(S, centrality, Qn, order) if miobi == "make"
+           else find_top_edges(S, centrality, Qn, order))  # :82 (first step)
     if len(top) >= int(k) > 0 and int(Q) >= 1:
         # the step loop in the library (kt_greedy_krylov_steps): krylov_miobi(A, 1,
         # top(1:Q)) per step, the selected pair dropped from the ranking (:84-89)

@@ -875,8 +875,11 @@ def krylov_miobi(A, k, E, tol=1e-12, it=None, poles=np.inf, debug=0, miobi="brea
 
 
 def find_top_edges(A, centrality, num, order="mult"):
-    """find_top_edges.m:14-39, written as the reference's loops."""
-    A = sp.csc_matrix(A)
+    """find_top_edges.m:14-39, written as the reference's loops.  A MATLAB
+    sparse matrix holds no duplicate entries (they are summed when it is
+    built), so duplicates of a SciPy input are summed first."""
+    A = sp.csc_matrix(A, copy=True)
+    A.sum_duplicates()
     n = A.shape[0]
     I, J = [], []
     for j in range(n):                                    # find(tril(A,-1)): column-major
@@ -899,7 +902,10 @@ def find_top_edges(A, centrality, num, order="mult"):
             mn, mx = min(c1, c2), max(c1, c2)
             scores.append(mx * (mx - 1) / 2 + mn)
         order_idx = sorted(range(len(I)), key=lambda h: scores[h])    # stable, ascending
-    if len(I) < num:
+    if len(I) < num:                                      # :19-21 (a warning)
+        warnings.warn("FIND_TOP_EDGES:: there are not enough edges in the graph")
+    num = int(math.floor(num))                            # E(ind(1:num), :)
+    if len(I) < num:                                      # index exceeds: MATLAB errors
         raise IndexError("FIND_TOP_EDGES:: there are not enough edges in the graph")
     return np.array([[I[h] + 1, J[h] + 1] for h in order_idx[:num]], dtype=np.int64)
 
@@ -916,7 +922,7 @@ def find_top_missing_edges_min(A, centrality, num):
             if A[indC[t], indC[j]] == 0:
                 E.append([indC[t] + 1, indC[j] + 1])
         j += 1
-    return np.array(E[:num], dtype=np.int64)
+    return np.array(E[:int(math.floor(num))], dtype=np.int64)  # E(1:num, :)
 
 
 def greedy_krylov(A, k, Q, centrality, order="mult", tol=1e-12, it=None, poles=np.inf, debug=0,
@@ -932,8 +938,8 @@ def greedy_krylov(A, k, Q, centrality, order="mult", tol=1e-12, it=None, poles=n
     Qi = int(np.floor(Q))                                 # 1:Q indexes floor(Q) rows
     for j in range(k):
         if j == 0:
-            top = (find_top_edges(A, centrality, Qi + k, order) if miobi == "break"
-                   else find_top_missing_edges_min(A, centrality, Qi + k))
+            top = (find_top_edges(A, centrality, Q + k, order) if miobi == "break"
+                   else find_top_missing_edges_min(A, centrality, Q + k))  # :69 / :80, unfloored
         else:
             hit = [h for h in range(len(top)) if tuple(top[h]) == tuple(tmp_edges[0])]
             # :84-86 with no match, [1 : ind-1, ind+1 : n] is empty: top_edges empties

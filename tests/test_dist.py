@@ -197,3 +197,52 @@ def test_gloo_world2_reduce_callback_failure_reaches_every_rank():
         assert st == 1                      # failed on both ranks
         assert buf == [float(rank)] * 10    # the buffer is left untouched
         assert st2 == 0 and buf2 == [2.0] * 3
+
+
+def _bitstable_worker(rank, world, port, out):
+    """bench.py --bitstable's reduction: each rank holds the oracle's forms of
+    its contiguous probe shard; dist.bitstable_sums all-gathers them and sums
+    in global probe order."""
+    import torch.distributed as dist
+    from oracle import slq_ref
+    from krylov_robustness_amd.dist import bitstable_sums, centred_sums
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    A = load_graph("rome")
+    N = 37  # ragged: 37 = 10 + 9 + 9 + 9 at world 4
+    counts = [probe_shard(N, r, world)[1] for r in range(world)]
+    off, cnt = probe_shard(N, rank, world)
+    _, q = slq_ref.slq_trace(A, cnt, 15, seed=3, probe_offset=off, nthreads=1)
+    out.put((rank, (bitstable_sums(q[:cnt], counts), centred_sums(q[:cnt], N))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_bitstable_sums_identical_across_world_sizes(world):
+    """Bit-identical (==, not approx) estimate on every rank and equal to the
+    single-process ordered sum of the same forms (SURVEY.md §8e option); the
+    default two-all-reduce centred form agrees to rounding."""
+    import torch.multiprocessing as mp
+    from oracle import slq_ref
+    from krylov_robustness_amd.dist import bitstable_sums, ordered_sums
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bitstable_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # the forms of one probe do not depend on the shard it was evaluated in
+    _, q1 = slq_ref.slq_trace(load_graph("rome"), 37, 15, seed=3, nthreads=1)
+    single = bitstable_sums(q1, [37])  # no process group: the local forms, same order
+    assert single == ordered_sums(q1)
+    for r in range(world):
+        assert got[r][0] == single
+        # the all-reduce form (bench.py default): the same to rounding
+        assert got[r][1][0] == pytest.approx(single[0], rel=1e-14)
+        assert got[r][1][1] == pytest.approx(single[1], rel=1e-12)

@@ -65,18 +65,68 @@ def test_bench_single_process_line():
     assert d["collective"] is None  # single process, no torchrun: no process group
 
 
-def test_bench_two_ranks_one_gpu_gloo():
+def _single_line(*extra):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, "--cpu-seconds", "0",
+                        "--no-profile", *extra], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return _json_lines(r.stdout)[0]
+
+
+def _ranks_line(world, port, *extra):
+    """bench.py under torchrun with `world` gloo ranks sharing GPU 0 (the N > 1
+    launch the driver uses, rehearsed on one card)."""
     env = dict(os.environ, KT_BENCH_ONE_DEVICE="1", MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29531", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", *SMALL, "--dist-backend", "gloo", "--no-profile"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), *SMALL, "--dist-backend", "gloo", "--no-profile", *extra]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1  # rank 0 only
     d = lines[0]
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "probes sharded x2"
+    assert d["n_gpus"] == world and d["config"]["parallelism"] == f"probes sharded x{world}"
     assert d["cpu_baseline"] is None and d["value"] > 0
+    return d
+
+
+def test_bench_two_ranks_one_gpu_gloo():
+    """Two ranks: the sharded evaluation gives the single-process estimate and
+    standard error (the only difference is the order the two shards' sums are
+    added: rel 1e-12), and so does the sharded mc_trace leg (G columns dealt
+    over the ranks; S, Q replicated)."""
+    d1 = _single_line("--mc-steps", "1")
+    d = _ranks_line(2, 29531, "--mc-steps", "1")
+    assert d["collective"].startswith("gloo all_reduce")
+    assert d["trace_estimate"] == pytest.approx(d1["trace_estimate"], rel=1e-12)
+    assert d["trace_stderr"] == pytest.approx(d1["trace_stderr"], rel=1e-12)
+    for a, b in zip(d["evaluations"]["estimates"], d1["evaluations"]["estimates"]):
+        assert a == pytest.approx(b, rel=1e-12)
+    assert d["mc_trace"]["trace_estimate"] == pytest.approx(d1["mc_trace"]["trace_estimate"], rel=1e-12)
+    assert d["mc_trace"]["rounds"] == d1["mc_trace"]["rounds"]
+
+
+def test_bench_four_ranks_one_gpu_gloo():
+    d1 = _single_line("--mc-steps", "0")
+    d = _ranks_line(4, 29537, "--mc-steps", "0")
+    assert d["trace_estimate"] == pytest.approx(d1["trace_estimate"], rel=1e-12)
+    assert d["trace_stderr"] == pytest.approx(d1["trace_stderr"], rel=1e-12)
+
+
+def test_bench_bitstable_identical_over_1_2_4_ranks():
+    """--bitstable: every rank all-gathers the per-probe forms
+    and sums them in global probe order, so 1, 2 and 4 ranks print the SAME
+    estimate and standard error, bit for bit."""
+    d1 = _single_line("--mc-steps", "0", "--bitstable")
+    d2 = _ranks_line(2, 29539, "--mc-steps", "0", "--bitstable")
+    d4 = _ranks_line(4, 29541, "--mc-steps", "0", "--bitstable")
+    assert d2["collective"].startswith("gloo all_gather")
+    for d in (d2, d4):
+        assert d["trace_estimate"] == d1["trace_estimate"]
+        assert d["trace_stderr"] == d1["trace_stderr"]
+        assert d["evaluations"]["estimates"] == d1["evaluations"]["estimates"]
+    # and it agrees with the all-reduce line to rounding
+    d0 = _single_line("--mc-steps", "0")
+    assert d1["trace_estimate"] == pytest.approx(d0["trace_estimate"], rel=1e-12)
 
 
 def test_bench_world1_torchrun_rccl():
@@ -97,10 +147,7 @@ def test_bench_world1_torchrun_rccl():
     assert d["n_gpus"] == 1 and d["collective"].startswith("RCCL all_reduce")
     assert d["value"] > 0 and d["roofline"]["avg_launch_us"] > 0
     # same probes, same estimate as the single-process line (the collective is a sum of one)
-    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *SMALL, "--cpu-seconds", "0",
-                         "--no-profile"], capture_output=True, text=True, timeout=300, cwd=ROOT)
-    assert r1.returncode == 0, r1.stderr[-2000:]
-    d1 = _json_lines(r1.stdout)[0]
+    d1 = _single_line()
     assert d["trace_estimate"] == d1["trace_estimate"]
     assert d["trace_stderr"] == d1["trace_stderr"]
 

@@ -154,3 +154,55 @@ def test_edge2low_rank_matches_edit():
     # shared endpoint: node appears once in U
     U3, B3 = edge2low_rank([[1, 2], [2, 3]], 5)
     assert U3.shape == (5, 3) and B3[0, 1] == -1 and B3[1, 2] == -1 and B3[0, 2] == 0
+
+
+def test_find_top_edges_duplicate_entries_summed():
+    """A CSC input with duplicate entries: MATLAB sparse sums them, so does the
+    ranking (an edge stored as +1 and -1 is absent; one stored as 0.5 + 0.5 is
+    present once) -- the same as the canonical matrix."""
+    import scipy.sparse as sp
+    A = sp.csc_matrix(load_graph("india"))
+    n = A.shape[0]
+    C = A.tocoo()
+    lower = np.flatnonzero(C.row > C.col)
+    e0, e1 = lower[0], lower[5]
+    i0, j0, i1, j1 = C.row[e0], C.col[e0], C.row[e1], C.col[e1]
+    extra_r = np.array([i0, j0, i1, j1])
+    extra_c = np.array([j0, i0, j1, i1])
+    extra_v = np.array([-1.0, -1.0, 0.0, 0.0])
+    Dup = sp.coo_matrix((np.concatenate([C.data, extra_v]),
+                         (np.concatenate([C.row, extra_r]), np.concatenate([C.col, extra_c]))),
+                        shape=(n, n))
+    # a CSC whose column arrays carry the duplicates explicitly
+    order = np.lexsort((Dup.row, Dup.col))
+    rows, cols, vals = Dup.row[order], Dup.col[order], Dup.data[order]
+    indptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(cols, minlength=n), out=indptr[1:])
+    X = sp.csc_matrix((vals, rows, indptr), shape=(n, n))
+    assert X.nnz == A.nnz + 4 and not X.has_canonical_format
+    canon = X.copy()
+    canon.sum_duplicates()
+    canon.eliminate_zeros()
+    c = kra.compute_centrality(A)
+    for order in ("mult", "min"):
+        ref = ko.find_top_edges(canon, c, 60, order)
+        np.testing.assert_array_equal(kra.find_top_edges(X, c, 60, order), ref)
+        np.testing.assert_array_equal(ko.find_top_edges(X, c, 60, order), ref)
+        assert not np.any((ref[:, 0] == i0 + 1) & (ref[:, 1] == j0 + 1))  # summed to 0
+
+
+def test_find_top_edges_fractional_count():
+    """find_top_edges.m:19-21 with num = Q + k fractional (a weighted graph's
+    Q = max(sum(A, 1))): fewer than num edges only warns; E(ind(1:num), :)
+    takes floor(num) and fails only when even those are missing."""
+    A = load_graph("denmark")
+    c = kra.compute_centrality(A)
+    ne = A.nnz // 2
+    with pytest.warns(UserWarning, match="FIND_TOP_EDGES"):
+        E = kra.find_top_edges(A, c, ne + 0.5, "mult")
+    assert len(E) == ne
+    with pytest.warns(UserWarning):
+        np.testing.assert_array_equal(E, ko.find_top_edges(A, c, ne + 0.5, "mult"))
+    with pytest.raises(IndexError), pytest.warns(UserWarning):
+        kra.find_top_edges(A, c, ne + 1.5, "mult")
+    np.testing.assert_array_equal(kra.find_top_edges(A, c, 10.7, "min"), ko.find_top_edges(A, c, 10, "min"))

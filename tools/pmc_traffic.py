@@ -5,7 +5,9 @@ one TCC pass on gfx950).  Per /opt/skills/guides/MI355X_MICROARCH.md §HBM,
 FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced reads on
 gfx950, so it is doubled; WRITE_SIZE is exact for 16 B/lane stores.  The
 doubling is checked on k_update, whose read bytes are known exactly (24nP).
-Usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON
+Usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON [SECTION]
+(with SECTION the result is merged into OUT_JSON under that key, e.g. sf1m,
+er100k, sf1m_weighted -- the bench workload bench.py looks it up by).
 """
 import collections
 import csv
@@ -25,7 +27,7 @@ def per_kernel(path, counter):
     return {k: sorted(v)[len(v) // 2] for k, v in agg.items()}  # median per launch
 
 
-def main(fetch_csv, write_csv, out_json):
+def main(fetch_csv, write_csv, out_json, section=None):
     f = per_kernel(fetch_csv, "FETCH_SIZE")
     w = per_kernel(write_csv, "WRITE_SIZE")
     res = {}
@@ -33,12 +35,21 @@ def main(fetch_csv, write_csv, out_json):
         fb = 2.0 * f.get(k, 0.0)
         wb = w.get(k, 0.0)
         res[k] = {"fetch_bytes_x2": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb}
-    res["_doc"] = ("median per launch; FETCH_SIZE doubled per the gfx950 calibration "
-                   "(MI355X_MICROARCH.md §HBM); Infinity-Cache hits are counted by these "
-                   "memory-side counters")
-    json.dump(res, open(out_json, "w"), indent=1)
+    doc = ("median per launch; FETCH_SIZE doubled per the gfx950 calibration "
+           "(MI355X_MICROARCH.md §HBM); Infinity-Cache hits are counted by these "
+           "memory-side counters")
+    if section:
+        try:
+            allr = json.load(open(out_json))
+        except (OSError, ValueError):
+            allr = {"_doc": doc}
+        allr[section] = res
+        json.dump(allr, open(out_json, "w"), indent=1)
+    else:
+        res["_doc"] = doc
+        json.dump(res, open(out_json, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
