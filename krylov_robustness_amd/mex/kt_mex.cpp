@@ -68,10 +68,13 @@ kt_context_t context() {
 }
 
 // A: MATLAB sparse (or full) real double, square (lanczos_krylov.m:36-38).
-kt_matrix_t matrix_arg(const mxArray* a) {
+// `nonsquare` is the reference's message for a non-square A on this entry:
+// the fun_and_grad_* files test ishermitian(A) first, which a non-square A
+// fails (fun_and_grad_krylov_exp.m:21-23, fun_and_grad_krylov_fun.m:22-24).
+kt_matrix_t matrix_arg(const mxArray* a, const char* nonsquare = "The matrix A should be square") {
     if (!mxIsDouble(a) || mxIsComplex(a)) mexErrMsgIdAndTxt("krylov_hip:A", "A must be real double");
     const mwSize n = mxGetM(a);
-    if (mxGetN(a) != n) mexErrMsgIdAndTxt("krylov_hip:A", "The matrix A should be square");
+    if (mxGetN(a) != n) mexErrMsgIdAndTxt("krylov_hip:A", "%s", nonsquare);
     std::vector<int64_t> jc(n + 1), ir;
     std::vector<double> pr;
     if (mxIsSparse(a)) {
@@ -424,29 +427,36 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
 #elif defined(KT_ENTRY_FG_EXP)
     // [f, gr] = fun_and_grad_krylov_exp(X, A, Omega, eA, tol, it, debug)   fun_and_grad_krylov_exp.m:1
     if (nrhs < 6) mexErrMsgIdAndTxt("krylov_hip:nargin", "fun_and_grad_krylov_exp(X, A, Omega, eA, tol, it, ...)");
+    kt_matrix_t A = matrix_arg(prhs[1], "FUN_AND_GRAD_KRYLOV:: matrix A is not Hermitian");
     const mwSize nom = mxGetM(prhs[2]);
-    plhs[0] = scalar(0.0);
-    mxArray* gr = mxCreateDoubleMatrix(nom, 1, mxREAL);
+    std::vector<double> gr(nom);
     double f = 0.0;
-    check(kt_fun_and_grad_krylov_exp(matrix_arg(prhs[1]), (int64_t)nom, mxGetDoubles(prhs[0]),
-                                     mxGetDoubles(prhs[2]), mxGetDoubles(prhs[3]), mxGetScalar(prhs[4]),
-                                     (int)mxGetScalar(prhs[5]), &f, mxGetDoubles(gr)),
+    check(kt_fun_and_grad_krylov_exp(A, (int64_t)nom, mxGetDoubles(prhs[0]), mxGetDoubles(prhs[2]),
+                                     mxGetDoubles(prhs[3]), mxGetScalar(prhs[4]), (int)mxGetScalar(prhs[5]), &f,
+                                     gr.data()),
           "fun_and_grad_krylov_exp");
-    mxGetDoubles(plhs[0])[0] = f;
-    if (nlhs > 1) plhs[1] = gr; else mxDestroyArray(gr);
+    plhs[0] = scalar(f);
+    if (nlhs > 1) {
+        plhs[1] = mxCreateDoubleMatrix(nom, 1, mxREAL);
+        memcpy(mxGetDoubles(plhs[1]), gr.data(), sizeof(double) * nom);
+    }
 #elif defined(KT_ENTRY_FG_FUN)
     // [f, gr] = fun_and_grad_krylov_fun(X, A, Omega, fun, dfun, dfA, tol, it, debug, fun_M)
     if (nrhs < 8) mexErrMsgIdAndTxt("krylov_hip:nargin", "fun_and_grad_krylov_fun(X, A, Omega, fun, dfun, dfA, tol, it, ...)");
+    kt_matrix_t A = matrix_arg(prhs[1], "FUN_AND_GRAD_KRYLOV_FCONNECTIVITY:: matrix A is not Hermitian");
+    const int fc = fun_arg(prhs[3], KT_FUN_EXP), dfc = fun_arg(prhs[4], KT_FUN_EXP);
     const mwSize nom = mxGetM(prhs[2]);
-    mxArray* gr = mxCreateDoubleMatrix(nom, 1, mxREAL);
+    std::vector<double> gr(nom);
     double f = 0.0;
-    check(kt_fun_and_grad_krylov_fun(matrix_arg(prhs[1]), (int64_t)nom, mxGetDoubles(prhs[0]),
-                                     mxGetDoubles(prhs[2]), fun_arg(prhs[3], KT_FUN_EXP),
-                                     fun_arg(prhs[4], KT_FUN_EXP), mxGetDoubles(prhs[5]),
-                                     mxGetScalar(prhs[6]), (int)mxGetScalar(prhs[7]), &f, mxGetDoubles(gr)),
+    check(kt_fun_and_grad_krylov_fun(A, (int64_t)nom, mxGetDoubles(prhs[0]), mxGetDoubles(prhs[2]), fc, dfc,
+                                     mxGetDoubles(prhs[5]), mxGetScalar(prhs[6]), (int)mxGetScalar(prhs[7]), &f,
+                                     gr.data()),
           "fun_and_grad_krylov_fun");
     plhs[0] = scalar(f);
-    if (nlhs > 1) plhs[1] = gr; else mxDestroyArray(gr);
+    if (nlhs > 1) {
+        plhs[1] = mxCreateDoubleMatrix(nom, 1, mxREAL);
+        memcpy(mxGetDoubles(plhs[1]), gr.data(), sizeof(double) * nom);
+    }
 #elif defined(KT_ENTRY_KRYLOV_MIOBI)
     // [edges, rob, A_new] = krylov_miobi(A, k, E, tol, it, poles, debug, miobi, rescale)
     //                                                                krylov_miobi.m:1

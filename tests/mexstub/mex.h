@@ -1,6 +1,9 @@
-/* Compile-check stub of the MATLAB MEX C API subset used by
- * krylov_robustness_amd/mex/kt_mex.cpp (TEST INFRASTRUCTURE ONLY: lets the
- * CPU suite type-check the shim; MATLAB is not installed, nothing is run). */
+/* Stub of the MATLAB MEX C API subset used by krylov_robustness_amd/mex/
+ * kt_mex.cpp (TEST INFRASTRUCTURE ONLY).  MATLAB is not installed: the CPU
+ * suite type-checks the shim against this header, and mex_runtime.cpp
+ * implements it so that the GPU suite can run the shim's mexFunction
+ * (tests/test_mex_exec.py).  As in MATLAB's own mex.h, mexFunction has C
+ * linkage. */
 #pragma once
 #include <stddef.h>
 typedef size_t mwSize;
@@ -37,4 +40,5 @@ void mexErrMsgIdAndTxt(const char*, const char*, ...);
 void mexWarnMsgIdAndTxt(const char*, const char*, ...);
 int mexAtExit(void (*)(void));
 void mexLock(void);
+void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]);
 }

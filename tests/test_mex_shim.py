@@ -24,3 +24,21 @@ def test_mex_shim_compiles(entry, tmp_path):
                         "-I", os.path.join(ROOT, "tests", "mexstub"), src],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.parametrize("entry", ENTRIES)
+def test_mex_entry_library_exports_mexfunction(entry):
+    """The per-entry builds against the stand-in runtime (make -C tests/mexstub,
+    run by __graft_entry__.build()) load next to libkrylov_hip.so and export
+    mexFunction with C linkage, as MATLAB's loader looks it up.  No call is
+    made here (no GPU); tests/test_mex_exec.py runs them on the GPU box."""
+    import ctypes
+    from krylov_robustness_amd import _lib
+    build = os.path.join(ROOT, "tests", "mexstub", "_build")
+    if not os.path.exists(os.path.join(build, f"kt_mex_{entry}.so")):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "mexstub")], check=True,
+                       capture_output=True)
+    _lib.load()
+    ctypes.CDLL(os.path.join(build, "libmexstub.so"), mode=ctypes.RTLD_GLOBAL)
+    lib = ctypes.CDLL(os.path.join(build, f"kt_mex_{entry}.so"))
+    assert hasattr(lib, "mexFunction")

@@ -1,0 +1,57 @@
+#!/bin/bash
+# One parametrised GPU-box script for the round's measurements (replaces the
+# per-call lease scripts).  Run from the repo root on the GPU box:
+#   bash tools/gpu_run.sh TASK TAG [extra bench args]
+# TASK
+#   tests    the -m gpu suite (pytest, one process)           -> gpu_tests.log
+#   smoke    __graft_entry__.smoke()                           -> smoke.log
+#   bench    bench legs: default line, --weighted, --estimator mc_trace, er100k
+#   configs  secondary configs (tests/perf/bench_*.py) + er100k bench
+#   prof     rocprofv3 --kernel-trace --stats of the default bench command,
+#            reconciled with the line it printed (tools/reconcile_trace.py)
+#   pmc      FETCH_SIZE / WRITE_SIZE passes (separate runs) of `bench.py
+#            --steps 1 --lanes 1 [extra]` -> traffic.json section
+#            (SECTION env, default sf1m)
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+TASK=$1; TAG=${2:-dev}; shift 2 || true
+O=$PWD/gpurun_out/$TAG; mkdir -p $O
+export TMPDIR=/tmp
+case $TASK in
+tests)
+    timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" \
+        > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+    tail -3 $O/gpu_tests.log ;;
+smoke)
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+    tail -1 $O/smoke.log ;;
+bench)
+    timeout -k 10 400 python -u bench.py "$@" > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
+    timeout -k 10 400 python -u bench.py --weighted --cpu-seconds 0 > $O/bench_weighted.json 2> $O/bench_weighted.err || { tail -20 $O/bench_weighted.err; exit 1; }
+    timeout -k 10 400 python -u bench.py --estimator mc_trace --steps 20 --cpu-seconds 0 > $O/bench_mc_trace.json 2> $O/bench_mc_trace.err || { tail -20 $O/bench_mc_trace.err; exit 1; }
+    timeout -k 10 400 python -u bench.py --config er100k --steps 100 --warmup 5 --cpu-seconds 5 > $O/bench_er100k.json 2> $O/bench_er100k.err || { tail -20 $O/bench_er100k.err; exit 1; }
+    for f in bench_default bench_weighted bench_mc_trace bench_er100k; do echo "== $f"; cut -c1-300 $O/$f.json; done ;;
+configs)
+    for s in bench_config1 bench_config3 bench_greedy bench_hessian; do
+        timeout -k 10 300 python tests/perf/$s.py > $O/$s.json 2> $O/$s.err || { echo "$s FAILED"; tail -5 $O/$s.err; exit 1; }
+        echo "== $s"; cut -c1-400 $O/$s.json
+    done ;;
+prof)
+    ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o def \
+        -- python3 $GRAFT_REPO_ROOT/bench.py "$@" > $O/bench.json 2> $O/bench.err ) || { tail -20 $O/bench.err; exit 1; }
+    cp $(find $O/stats -name "*kernel_stats.csv") $O/kernel_stats.csv
+    python3 tools/reconcile_trace.py $(find $O/stats -name "*kernel_trace.csv") $O/bench.json $O/reconcile.json || exit 1
+    rm -f $(find $O/stats -name "*kernel_trace.csv")
+    cat $O/reconcile.json; head -6 $O/kernel_stats.csv | cut -c1-200 ;;
+pmc)
+    SEC=${SECTION:-sf1m}
+    B="$GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --cpu-seconds 0 --lanes 1 --mc-steps 1 --no-profile $*"
+    R="spmm_dot|spmm_lanczos|k_update"
+    ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$R" -d $O/pmc_fetch -o f --output-format csv -- python3 $B > $O/pmc_fetch.log 2>&1 ) || { tail -20 $O/pmc_fetch.log; exit 1; }
+    ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$R" -d $O/pmc_write -o w --output-format csv -- python3 $B > $O/pmc_write.log 2>&1 ) || { tail -20 $O/pmc_write.log; exit 1; }
+    ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$R" -d $O/pmc_hit -o h --output-format csv -- python3 $B > $O/pmc_hit.log 2>&1 ) || { tail -20 $O/pmc_hit.log; exit 1; }
+    python3 tools/pmc_traffic.py $(find $O/pmc_fetch -name "*counter_collection.csv") $(find $O/pmc_write -name "*counter_collection.csv") $O/traffic.json $SEC \
+        $(find $O/pmc_hit -name "*counter_collection.csv") || exit 1 ;;
+*)
+    echo "unknown task $TASK"; exit 2 ;;
+esac
