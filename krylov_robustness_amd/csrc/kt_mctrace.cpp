@@ -522,6 +522,99 @@ static void project(kt_context_s* ctx, int64_t n, const double* Q, int ld, int n
     combine(ctx, n, Q, ld, nq, G, nc, 1.0, X, ld);
 }
 
+// X <- X - Q (Q' X) with separate leading dimensions for Q and X
+static void project_ld(kt_context_s* ctx, int64_t n, const double* Q, int ldq, int nq, double* X, int ldx,
+                       int nc) {
+    std::vector<double> G;
+    gram(ctx, n, Q, ldq, nq, X, ldx, nc, G);
+    for (double& g : G) g = -g;
+    combine(ctx, n, Q, ldq, nq, G, nc, 1.0, X, ldx);
+}
+
+// mc_trace.m:42-58 with the Lanczos-f Afun, one probe sweep per round.  The
+// round's Q term (:46), its G term (:49) and the NEXT round's S term
+// (:43-45, which needs only Q_1..Q_it) are independent Afun calls, so their
+// 30 columns share one Lanczos sweep (P = 32: per nonzero one 256-B probe-row
+// gather and one CSR pass instead of three 128-B gathers and three CSR
+// passes); round 1's S term runs alone.  Same probes, same projections in
+// the same order, and each column's Lanczos recurrence does not depend on
+// its neighbours in the sweep -- only the sweep width (the reduction grid)
+// differs from the per-call form, so the estimate agrees to rounding.  The
+// S term computed in the stopping round is discarded (mc_trace never stops
+// in round 1, so round 2's is always used).  KT_MC_BATCH=0: per-call form.
+// Multi-GPU (sh.allreduce set): S and Q replicated, G column c on rank
+// c % world, the 10 G forms all-reduced once per round and summed in column
+// order.  A column's form does not depend on the other columns of its
+// 32-wide sweep, so every world size gives the world-1 estimate bit for bit.
+static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int maxit, uint64_t seed,
+                             double* tr_out, double* res_out, int* it_out, const Shard& sh) {
+    kt_context_s* ctx = A->ctx;
+    hipStream_t st = ctx->stream;
+    const int64_t n = A->n;
+    const int mb = 10, ld = 16, LB = 32;
+    const int K = (maxit + 3 * mb - 1) / (3 * mb);  // :41
+    double tr = 0.0, tr_old = 0.0, tr_new = 0.0, res = 1.0;
+    std::vector<DevMat> Qs;
+    DevMat Bk, Yb, T;
+    Bk.alloc(ctx, n, LB);  // [S_{it+1} | P..P Q_it | P..P G_it | 0 0]
+    Yb.alloc(ctx, n, ld);  // Afun_it(S_it), then Q_it in place
+    T.alloc(ctx, n, ld);   // Rademacher columns before they enter the block
+    zero_cols(ctx, n, Bk.col(3 * mb), LB, LB - 3 * mb);
+    auto rademacher_into = [&](int64_t base, double* dst) {
+        KT_HIP(launch_rademacher(ld, (int)n, seed, base, nullptr, T.col(0), st));
+        copy_cols(ctx, n, T.col(0), ld, dst, LB, mb);
+    };
+    // round 1's S term alone: Y_1 = F(S_1)                                   :43-45
+    rademacher_into(0, Bk.col(0));
+    lanczos_columns_mixed(A, Bk.col(0), LB, mb, F.m, F.fun, nullptr, Yb.col(0), ld, mb, 16);
+    std::vector<double> q(3 * mb);
+    int it = 0;
+    for (it = 1; it <= K; ++it) {
+        const int64_t base = (int64_t)(it - 1) * 2 * mb;
+        std::vector<double> R;
+        householder_qr(ctx, n, Yb.col(0), ld, mb, R);                      // [Q, ~] = qr(Afun(S), 0)
+        // Q term input: P_{it-1}..P_1 Q_it                                   :46
+        copy_cols(ctx, n, Yb.col(0), ld, Bk.col(mb), LB, mb);
+        for (int k = (int)Qs.size() - 1; k >= 0; --k) project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(mb), LB, mb);
+        Qs.emplace_back();                                                 // :47-48
+        Qs.back().alloc(ctx, n, ld);
+        copy_cols(ctx, n, Yb.col(0), ld, Qs.back().col(0), ld, mb);
+        // G term input: P_it..P_1 G_it, this rank's columns c % world == rank  :44, :49
+        KT_HIP(launch_rademacher(ld, (int)n, seed, base + mb, nullptr, T.col(0), st));
+        int ng = 0;
+        for (int c = sh.rank; c < mb; c += sh.world) copy_cols(ctx, n, T.col(c), ld, Bk.col(2 * mb + ng++), LB, 1);
+        for (int k = (int)Qs.size() - 1; k >= 0 && ng > 0; --k)
+            project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(2 * mb), LB, ng);
+        // next round's S term input: P_it..P_1 S_{it+1}
+        const bool next = it < K;
+        if (next) {
+            rademacher_into(base + 2 * mb, Bk.col(0));
+            for (int k = (int)Qs.size() - 1; k >= 0; --k) project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(0), LB, mb);
+            lanczos_columns_mixed(A, Bk.col(0), LB, 2 * mb + ng, F.m, F.fun, q.data(), Yb.col(0), ld, mb, LB);
+        } else {
+            lanczos_columns_mixed(A, Bk.col(mb), LB, mb + ng, F.m, F.fun, q.data() + mb, nullptr, 0, 0, LB);
+        }
+        std::vector<double> qv(mb, 0.0);
+        for (int c = sh.rank, t = 0; c < mb; c += sh.world, ++t) qv[c] = q[2 * mb + t];
+        if (sh.allreduce && sh.allreduce(qv.data(), mb, sh.user) != 0)
+            fail(KT_ERR_CALLBACK, "mc_trace: all-reduce callback failed");
+        double qsum = 0.0, gsum = 0.0;  // column order, as trace_quad sums
+        for (int c = 0; c < mb; ++c) qsum += q[mb + c];
+        for (double v : qv) gsum += v;
+        tr += qsum;
+        tr_new = tr + gsum / mb;                                           // :49
+        res = std::fabs(tr_new - tr_old) / std::max(std::fabs(tr_new), std::fabs(tr_old));  // :50
+        if (res < tol) break;                                              // :54-56
+        tr_old = tr_new;
+        if (next)  // Y_{it+1} = P_1..P_it F(P_it..P_1 S_{it+1})              :45, :48
+            for (size_t k = 0; k < Qs.size(); ++k) project_ld(ctx, n, Qs[k].col(0), ld, mb, Yb.col(0), ld, mb);
+    }
+    if (it > K) it = K;
+    *tr_out = tr_new;
+    if (res_out) *res_out = res;
+    if (it_out) *it_out = it;
+}
+
 // mc_trace.m:1-63
 //
 // Round it + 1's S term -- Afun_{it+1}(S_{it+1}) = P_it..P_1 F(P_1..P_it S_{it+1})
@@ -536,6 +629,11 @@ void mc_trace_impl(kt_matrix_s* A, AfunDev& F, double tol, int maxit, int isArea
                    double* tr_out, double* res_out, int* it_out, const Shard& sh = Shard()) {
     kt_context_s* ctx = A->ctx;
     const int64_t n = A->n;
+    const char* be = getenv("KT_MC_BATCH");
+    if (F.kind == AFUN_LANCZOS && !(be && be[0] == '0')) {
+        mc_trace_batched(A, F, tol, maxit, seed, tr_out, res_out, it_out, sh);
+        return;
+    }
     const int mb = 10, ld = 16;                    // :36
     const int K = (maxit + 3 * mb - 1) / (3 * mb);  // :41 ceil(maxit/30)
     double tr = 0.0, tr_old = 0.0, tr_new = 0.0, res = 1.0;

@@ -260,22 +260,29 @@ static void parallel_for(int64_t count, int64_t serial_below, F&& f) {
 
 void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m, int fun,
                      double* quad, double* Y, int ldy) {
+    lanczos_columns_mixed(A, X, ldx, ncols, m, fun, quad, Y, ldy, Y ? ncols : 0, 16);
+}
+
+void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, int m, int fun,
+                           double* quad, double* Y, int ldy, int ny, int pmax) {
     kt_context_s* ctx = A->ctx;
     const int64_t n = A->n;
+    if (!Y) ny = 0;
     std::vector<double> nrm2;
     gram(ctx, n, X, ldx, ncols, X, ldx, ncols, nrm2);
     std::vector<double> norms2(ncols);
     for (int c = 0; c < ncols; ++c) norms2[c] = nrm2[c + (size_t)c * ncols];
     int P = 1;
-    while (P < ncols && P < 16) P <<= 1;
+    while (P < ncols && P < pmax) P <<= 1;
     for (int c0 = 0; c0 < ncols; c0 += P) {
         const int nc = std::min(P, ncols - c0);
+        const int nyc = std::max(0, std::min(nc, ny - c0));  // columns of this sweep that need f(A) x
         std::vector<double> rec((size_t)3 * m * P);
         DevMat basis;
         std::vector<double> hist;
-        if (Y) basis.alloc(ctx, n, m * P);
+        if (nyc) basis.alloc(ctx, n, m * P);
         lanczos_sweep(A, natural_csr(A), P, m, 0, 0, X + c0, ldx, nc, norms2.data() + c0, rec.data(),
-                      Y ? &basis : nullptr, Y ? &hist : nullptr);
+                      nyc ? &basis : nullptr, nyc ? &hist : nullptr);
         KT_HIP(hipStreamSynchronize(ctx->stream));
         std::vector<double> W((size_t)m * P, 0.0);  // weights for Y = sum_j u_j w_j
         for (int c = 0; c < nc; ++c) {
@@ -286,7 +293,7 @@ void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m,
                 continue;
             }
             if (quad) quad[c0 + c] = norms2[c0 + c] * tridiag_quadrature(steps, al.data(), off.data(), fun);
-            if (Y) {
+            if (c < nyc) {
                 // f(T) e1 = Z f(theta) Z(0,:)'
                 std::vector<double> T((size_t)steps * steps, 0.0), th(steps), Z((size_t)steps * steps);
                 for (int j = 0; j < steps; ++j) T[j + (size_t)j * steps] = al[j];
@@ -302,12 +309,12 @@ void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m,
                 }
             }
         }
-        if (Y) {
+        if (nyc) {
             DevBuf& dw = ctx->ws.small2;
             dw.ensure(sizeof(double) * W.size());
             KT_HIP(hipMemcpyAsync(dw.ptr, W.data(), sizeof(double) * W.size(), hipMemcpyHostToDevice,
                                   ctx->stream));
-            KT_HIP(launch_weighted_sum((int)n, m, P, nc, basis.col(0), basis.ld, dw.as<double>(),
+            KT_HIP(launch_weighted_sum((int)n, m, P, nyc, basis.col(0), basis.ld, dw.as<double>(),
                                        Y + c0, ldy, ctx->stream));
             KT_HIP(hipStreamSynchronize(ctx->stream));
         }

@@ -22,4 +22,11 @@ int record_tridiag(const double* R, int m, int P, int c, double* al, double* off
 void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m, int fun,
                      double* quad, double* Y, int ldy);
 
+// lanczos_columns for a block whose first ny columns need f(A) x (into Y)
+// and every column its quadratic form: sweeps of up to pmax (power of two
+// <= 128) columns, the basis kept only for sweeps holding Y columns.  Lets
+// several Afun calls of mc_trace share one sweep (kt_mctrace.cpp).
+void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, int m, int fun,
+                           double* quad, double* Y, int ldy, int ny, int pmax);
+
 }  // namespace kt

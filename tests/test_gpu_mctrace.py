@@ -211,3 +211,25 @@ def test_trace_exp_with_self_loops(kra, gpu_ctx):
     assert tr == pytest.approx(ko.trace_exp(A, seed=1), rel=1e-9)
     exact = float(np.exp(np.linalg.eigvalsh(A.toarray())).sum())
     assert tr == pytest.approx(exact, rel=1e-4)
+
+
+@pytest.mark.parametrize("name", ["oregon_A0", "rome", "oregon_A6"])
+def test_mc_trace_batched_rounds_match_per_call(kra, gpu_ctx, monkeypatch, name):
+    """The Lanczos-Afun mc_trace runs one probe sweep per round -- the round's
+    Q and G terms and the next round's S term share a 30-column sweep
+    (kt_mctrace.cpp mc_trace_batched) -- against the per-call form
+    (KT_MC_BATCH=0, one sweep per Afun call): same probes and projections,
+    only the sweep width differs, so the same rounds and the estimate to
+    rounding (1e-11), over several rounds of nested deflation; and the
+    oracle's numpy restatement of the same composition (1e-10)."""
+    A = load_graph(name)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    args = dict(n=A.shape[0], tol=1e-8, maxit=150, isAreal=1, seed=5, m=20)
+    b = kra.mc_trace("lanczos", A=D, ctx=gpu_ctx, **args)
+    monkeypatch.setenv("KT_MC_BATCH", "0")
+    p = kra.mc_trace("lanczos", A=D, ctx=gpu_ctx, **args)
+    assert b[2] == p[2] and b[2] > 1
+    assert b[0] == pytest.approx(p[0], rel=1e-11)
+    if name != "oregon_A6":  # the numpy restatement at n = 10,860 x 5 rounds is slow
+        tro, _, ito = ko.trace_exp_lanczos(A, m=20, tol=1e-8, maxit=150, seed=5)
+        assert b[2] == ito and b[0] == pytest.approx(tro, rel=1e-10)

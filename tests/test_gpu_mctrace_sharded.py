@@ -4,12 +4,17 @@ their quadratic forms all-reduced once per round.
 
 world = 1 must equal kt_mc_trace bit for bit.  world = 2, 3 are run in one
 process by one host thread per rank, each with its own context on the same
-GPU, joined by an in-process all-reduce; a rank's G columns then run as a
-narrower Lanczos block (P = 8 or 4 instead of 16), whose long-row and dot
-reductions round differently, so the estimate agrees with world = 1 to
-1e-12 relative and the round count is equal.  The expmv Afun is replicated
-(its Taylor degree is chosen per block) and never calls the reduction.  A
-2-process gloo run checks the torch.distributed callback end to end."""
+GPU, joined by an in-process all-reduce.  With the Lanczos Afun each round
+is one 32-wide probe sweep (kt_mctrace.cpp mc_trace_batched: the round's Q
+and G terms and the next S term); a rank's G columns sit in that sweep
+beside the replicated columns, and a column's form does not depend on its
+neighbours, so every world size returns the world-1 estimate BIT FOR BIT.
+The per-call form (KT_MC_BATCH=0) runs a rank's G columns as a narrower
+block (P = 8 or 4 instead of 16), whose reductions round differently: there
+the estimate agrees to 1e-12 relative with the same round count.  The expmv
+Afun is replicated (its Taylor degree is chosen per block) and never calls
+the reduction.  A 2-process gloo run checks the torch.distributed callback
+end to end."""
 import ctypes as C
 import os
 import socket
@@ -91,8 +96,20 @@ def test_world1_equals_mc_trace(kra, gpu_ctx, afun):
     assert got == ref
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_threads_world_matches_single(kra, gpu_ctx, world):
+    A = load_graph("oregon_A0")
+    kw = dict(tol=1e-6, maxit=120, isAreal=1, seed=3, fun="exp", m=20)
+    ref = kra.mc_trace("lanczos", None, A=kra.DeviceMatrix(A, gpu_ctx), ctx=gpu_ctx, **kw)
+    out, calls = _run_world(kra, A, world, "lanczos", **kw)
+    for r in out:
+        assert r == ref  # every rank, bit for bit
+    assert calls == ref[2]  # one all-reduce per round
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_threads_world_per_call_form(kra, gpu_ctx, monkeypatch, world):
+    monkeypatch.setenv("KT_MC_BATCH", "0")
     A = load_graph("oregon_A0")
     kw = dict(tol=1e-6, maxit=120, isAreal=1, seed=3, fun="exp", m=20)
     ref = kra.mc_trace("lanczos", None, A=kra.DeviceMatrix(A, gpu_ctx), ctx=gpu_ctx, **kw)
@@ -101,7 +118,7 @@ def test_threads_world_matches_single(kra, gpu_ctx, world):
         assert tr == out[0][0] and it == out[0][2]  # every rank returns the same estimate
         assert it == ref[2]
         assert tr == pytest.approx(ref[0], rel=1e-12)
-    assert calls == ref[2]  # one all-reduce per round
+    assert calls == ref[2]
 
 
 def test_threads_expmv_is_replicated(kra, gpu_ctx):
@@ -150,5 +167,4 @@ def test_gloo_two_processes_trace_exp(kra, gpu_ctx):
     got = dict(q.get(timeout=240) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
-    assert got[0] == got[1]
-    assert got[0] == pytest.approx(ref, rel=1e-12)
+    assert got[0] == got[1] == ref

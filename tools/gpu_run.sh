@@ -9,6 +9,8 @@
 #   configs  secondary configs (tests/perf/bench_*.py) + er100k bench
 #   prof     rocprofv3 --kernel-trace --stats of the default bench command,
 #            reconciled with the line it printed (tools/reconcile_trace.py)
+#   timeline rocprofv3 kernel trace of the er100k bench, per-evaluation
+#            breakdown (tools/eval_timeline.py)
 #   pmc      FETCH_SIZE / WRITE_SIZE passes (separate runs) of `bench.py
 #            --steps 1 --lanes 1 [extra]` -> traffic.json section
 #            (SECTION env, default sf1m)
@@ -43,6 +45,13 @@ prof)
     python3 tools/reconcile_trace.py $(find $O/stats -name "*kernel_trace.csv") $O/bench.json $O/reconcile.json || exit 1
     rm -f $(find $O/stats -name "*kernel_trace.csv")
     cat $O/reconcile.json; head -6 $O/kernel_stats.csv | cut -c1-200 ;;
+timeline)
+    # kernel trace of the er100k bench (config 2), evaluation by evaluation
+    ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/tl -o tl \
+        -- python3 $GRAFT_REPO_ROOT/bench.py --config er100k --steps 100 --warmup 5 --cpu-seconds 0 --mc-steps 0 "$@" \
+        > $O/bench_er100k_traced.json 2> $O/tl.err ) || { tail -20 $O/tl.err; exit 1; }
+    python3 tools/eval_timeline.py $(find $O/tl -name "*kernel_trace.csv") ${SWEEPS:-2} 100 $O/er100k_eval_timeline.json || exit 1
+    rm -f $(find $O/tl -name "*kernel_trace.csv") ;;
 pmc)
     SEC=${SECTION:-sf1m}
     B="$GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --cpu-seconds 0 --lanes 1 --mc-steps 1 --no-profile $*"
