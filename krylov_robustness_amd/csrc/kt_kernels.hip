@@ -1281,6 +1281,25 @@ __global__ __launch_bounds__(256) void k_weighted_sum(int n, int m, int P, int n
     }
 }
 
+// Row permutation of a row-major block: gather (dst[r] = src[perm[r]]) or
+// scatter (dst[perm[r]] = src[r]), cols columns -- natural-order blocks into
+// the hubs-first row order of the probe sweep and back (kt_slq.cpp).
+__global__ __launch_bounds__(256) void k_perm_rows(int n, int cols, const int* __restrict__ perm, int gather,
+                                                   const double* __restrict__ src, int lds,
+                                                   double* __restrict__ dst, int ldd) {
+    const int64_t total = (int64_t)n * cols;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = t / cols;
+        const int c = (int)(t % cols);
+        const int64_t p = perm[r];
+        if (gather)
+            dst[r * ldd + c] = src[p * lds + c];
+        else
+            dst[p * ldd + c] = src[r * lds + c];
+    }
+}
+
 // Y[:, 0:nc] = a X + b Y
 __global__ __launch_bounds__(256) void k_axpby(int n, int nc, double a, const double* __restrict__ X,
                                                int ldx, double b, double* __restrict__ Y, int ldy) {
@@ -2298,6 +2317,13 @@ static int stream_grid(int64_t total) {
 hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int ldu,
                                const double* W, double* Y, int ldy, hipStream_t st) {
     k_weighted_sum<<<stream_grid((int64_t)n * nc), 256, 0, st>>>(n, m, P, nc, U, ldu, W, Y, ldy);
+    return hipGetLastError();
+}
+
+hipError_t launch_perm_rows(int n, int cols, const int* perm, int gather, const double* src, int lds,
+                            double* dst, int ldd, hipStream_t st) {
+    if (n <= 0 || cols <= 0) return hipSuccess;
+    k_perm_rows<<<stream_grid((int64_t)n * cols), 256, 0, st>>>(n, cols, perm, gather, src, lds, dst, ldd);
     return hipGetLastError();
 }
 

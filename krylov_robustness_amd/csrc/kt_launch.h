@@ -117,6 +117,9 @@ hipError_t launch_gather_rows(int nr, int cols, const double* D, int ldd, const 
                               hipStream_t st);
 hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int ldu,
                                const double* W, double* Y, int ldy, hipStream_t st);
+// dst[r] = src[perm[r]] (gather != 0) or dst[perm[r]] = src[r], rows of `cols` doubles
+hipError_t launch_perm_rows(int n, int cols, const int* perm, int gather, const double* src, int lds,
+                            double* dst, int ldd, hipStream_t st);
 hipError_t launch_axpby(int n, int nc, double a, const double* X, int ldx, double b, double* Y,
                         int ldy, hipStream_t st);
 int inf_norm_blocks();

@@ -274,14 +274,39 @@ void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     for (int c = 0; c < ncols; ++c) norms2[c] = nrm2[c + (size_t)c * ncols];
     int P = 1;
     while (P < ncols && P < pmax) P <<= 1;
+    // The sweeps run on the hubs-first CSR (equal-length neighbouring rows,
+    // adjacent hub segments: the explicit K1 at P = 16 on the bench graph 264
+    // -> ~210 us): the block is permuted into that row order on the way in
+    // and f(A) x back out; quadratic forms are permutation invariant.
+    // KT_LC_HUB=0: natural row order.
+    const char* he = getenv("KT_LC_HUB");
+    const bool hub = !(he && he[0] == '0');
+    const DevCSR& M = hub ? hub_csr(A) : natural_csr(A);
+    const int* perm = hub ? M.perm : nullptr;
+    DevMat Xh, Yh;
+    const double* Xs = X;
+    int ldxs = ldx;
+    double* Ys = Y;
+    int ldys = ldy;
+    if (perm) {
+        Xh.alloc(ctx, n, ncols, false);
+        KT_HIP(launch_perm_rows((int)n, ncols, perm, 1, X, ldx, Xh.col(0), ncols, ctx->stream));
+        Xs = Xh.col(0);
+        ldxs = ncols;
+        if (ny) {
+            Yh.alloc(ctx, n, ny, false);
+            Ys = Yh.col(0);
+            ldys = ny;
+        }
+    }
     for (int c0 = 0; c0 < ncols; c0 += P) {
         const int nc = std::min(P, ncols - c0);
         const int nyc = std::max(0, std::min(nc, ny - c0));  // columns of this sweep that need f(A) x
         std::vector<double> rec((size_t)3 * m * P);
         DevMat basis;
         std::vector<double> hist;
-        if (nyc) basis.alloc(ctx, n, m * P);
-        lanczos_sweep(A, natural_csr(A), P, m, 0, 0, X + c0, ldx, nc, norms2.data() + c0, rec.data(),
+        if (nyc) basis.alloc(ctx, n, m * P, false);  // every slot is written by the sweep
+        lanczos_sweep(A, M, P, m, 0, 0, Xs + c0, ldxs, nc, norms2.data() + c0, rec.data(),
                       nyc ? &basis : nullptr, nyc ? &hist : nullptr);
         KT_HIP(hipStreamSynchronize(ctx->stream));
         std::vector<double> W((size_t)m * P, 0.0);  // weights for Y = sum_j u_j w_j
@@ -315,10 +340,11 @@ void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, 
             KT_HIP(hipMemcpyAsync(dw.ptr, W.data(), sizeof(double) * W.size(), hipMemcpyHostToDevice,
                                   ctx->stream));
             KT_HIP(launch_weighted_sum((int)n, m, P, nyc, basis.col(0), basis.ld, dw.as<double>(),
-                                       Y + c0, ldy, ctx->stream));
+                                       Ys + c0, ldys, ctx->stream));
             KT_HIP(hipStreamSynchronize(ctx->stream));
         }
     }
+    if (perm && ny) KT_HIP(launch_perm_rows((int)n, ny, perm, 0, Ys, ldys, Y, ldy, ctx->stream));
 }
 
 static bool pow2_le128(int b) { return b >= 1 && b <= 128 && (b & (b - 1)) == 0; }

@@ -54,13 +54,22 @@ def main(path, sweeps, evals, out=None):
         for a, b, nm in win:
             per[nm][0] += b - a
             per[nm][1].append((a, b))
-        # idle gaps inside the evaluation (> 2 us with nothing running)
-        inner, ce = 0, None
-        for a, b, _ in sorted(win):
+        # idle gaps (> 2 us with nothing running), each labelled by the kernel after it
+        gaps, ce = [], None
+        for a, b, nm in sorted(win):
             if ce is not None and a > ce + 2000:
-                inner += a - ce
+                gaps.append((a - ce, nm))
             ce = b if ce is None else max(ce, b)
+        gaps.sort(reverse=True)
+        inner = sum(g for g, _ in gaps)
+        host = gaps[0][0] if gaps and gaps[0][1] == "k_rademacher_signs" else 0  # the call turnaround
+        small = defaultdict(lambda: [0, 0])
+        for g, nm in gaps:
+            if not (host and (g, nm) == gaps[0]):
+                small[nm][0] += g
+                small[nm][1] += 1
         res.append({"wall": t1 - t0, "busy": busy, "tail_gap": t1 - last_end, "inner_gaps": inner,
+                    "host_turnaround": host, "other_gaps": {k: v for k, v in small.items()},
                     "kernels": {nm: {"sum": v[0], "union": union(v[1]), "launches": len(v[1])}
                                 for nm, v in per.items()}})
     med = lambda xs: st.median(xs) / 1e3  # us
@@ -69,6 +78,12 @@ def main(path, sweeps, evals, out=None):
             "gpu_busy_us": med([r["busy"] for r in res]),
             "tail_gap_us": med([r["tail_gap"] for r in res]),
             "inner_gaps_us": med([r["inner_gaps"] for r in res]),
+            "host_turnaround_us": med([r["host_turnaround"] for r in res]),
+            "host_turnaround_basis": "the idle gap before the next call's first kernel (k_rademacher_signs): "
+                                     "sync, host quadrature, the reduction, the next call's set-up",
+            "other_gaps_by_next_kernel": {nm: {"sum_us": med([r["other_gaps"].get(nm, [0, 0])[0] for r in res]),
+                                               "count": st.median([r["other_gaps"].get(nm, [0, 0])[1] for r in res])}
+                                          for nm in sorted({k for r in res for k in r["other_gaps"]})},
             "kernels": {nm: {"sum_us": med([r["kernels"].get(nm, {"sum": 0})["sum"] for r in res]),
                              "union_us": med([r["kernels"].get(nm, {"union": 0})["union"] for r in res]),
                              "launches": st.median([r["kernels"].get(nm, {"launches": 0})["launches"] for r in res])}

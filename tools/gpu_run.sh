@@ -51,7 +51,7 @@ timeline)
         -- python3 $GRAFT_REPO_ROOT/bench.py --config er100k --steps 100 --warmup 5 --cpu-seconds 0 --mc-steps 0 "$@" \
         > $O/bench_er100k_traced.json 2> $O/tl.err ) || { tail -20 $O/tl.err; exit 1; }
     python3 tools/eval_timeline.py $(find $O/tl -name "*kernel_trace.csv") ${SWEEPS:-2} 100 $O/er100k_eval_timeline.json || exit 1
-    rm -f $(find $O/tl -name "*kernel_trace.csv") ;;
+    gzip -f $(find $O/tl -name "*kernel_trace.csv") ;;
 pmc)
     SEC=${SECTION:-sf1m}
     B="$GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --cpu-seconds 0 --lanes 1 --mc-steps 1 --no-profile $*"
