@@ -263,11 +263,17 @@ def main():
     P = args.block or kra.slq_plan(D, N if args.bitstable else cnt, ctx=ctx)
     ref = reference_trace(args.config, args.weighted) if m >= 20 else None
 
-    def step(seed):
-        s1, s2, q = kra.slq_quadforms(D, cnt, m, seed=seed, probe_offset=off, block=P, ctx=ctx)
+    def submit(seed):
+        return kra.slq_submit(D, cnt, m, seed=seed, probe_offset=off, block=P, ctx=ctx)
+
+    def finish(pending):
+        _, _, q = kra.slq_collect(pending)
         if args.bitstable:  # every rank reduces all N forms in global probe order
             return kdist.bitstable_sums(q, counts)
         return kdist.centred_sums(q, N, device=coll_dev, force=use_pg)
+
+    def step(seed):
+        return finish(submit(seed))
 
     def barrier():
         if use_pg:
@@ -286,9 +292,19 @@ def main():
             ctx.profile(True)
         barrier()
         t0 = time.perf_counter()
+        # evaluations pipelined one deep: evaluation s's sweeps are queued on
+        # the device before the host finishes evaluation s-1 (its quadrature
+        # and reduction), so the host half hides under device work; every
+        # evaluation is complete and reduced inside the timed region
         sums = []
+        pending = None
         for s in range(args.steps):
-            sums.append(step(s))
+            nxt = submit(s)
+            if pending is not None:
+                sums.append(finish(pending))
+            pending = nxt
+        if pending is not None:
+            sums.append(finish(pending))
         barrier()
         el = time.perf_counter() - t0
         if not args.no_profile:

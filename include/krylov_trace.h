@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define KT_ABI_VERSION 2
+#define KT_ABI_VERSION 3
 
 enum kt_status {
     KT_OK = 0,
@@ -86,6 +86,19 @@ int kt_matrix_info(kt_matrix_t A, int64_t* n, int64_t* nnz);
  * plain-Hutchinson estimator of BASELINE.json configs 2-4. */
 int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_t probe_offset,
                  int64_t nprobes, int block, double* sum_q, double* sum_q2, double* q);
+
+/* kt_slq_trace in two halves, for a pipeline of evaluations: submit queues
+ * the probe sweeps on the device and returns at once with a ticket; collect
+ * waits for THAT call's sweeps only (not for work submitted after it), runs
+ * the guard redo and the host quadrature and returns what kt_slq_trace
+ * returns.  So evaluation k + 1's sweeps run on the device while the host
+ * finishes evaluation k.  At most two submissions outstanding per context,
+ * collected once each in submission order (KT_ERR_ARG otherwise);
+ * kt_slq_trace == submit + collect and refuses to run while submissions are
+ * outstanding. */
+int kt_slq_submit(kt_matrix_t A, int fun, int m, uint64_t seed, int64_t probe_offset, int64_t nprobes,
+                  int block, int* ticket);
+int kt_slq_collect(kt_matrix_t A, int ticket, double* sum_q, double* sum_q2, double* q);
 
 /* The probes-per-sweep width kt_slq_trace picks when block == 0. */
 int kt_slq_plan(kt_matrix_t A, int64_t nprobes, int* block);

@@ -12,7 +12,7 @@ from .core import (Context, DeviceMatrix, default_context, device_count, expmv,
                    eigs_leading, frechet_entries, function_multiple_entries, hessianfcn, hessianfcn_exp,
                    hessianfcn_fun, householder_qr,
                    fun_and_grad_krylov_exp, fun_and_grad_krylov_fun, fun_update, lanczos_fmv,
-                   mc_trace, normest, slq_plan, slq_quadforms, slq_trace, trace_exp,
+                   mc_trace, normest, slq_collect, slq_plan, slq_quadforms, slq_submit, slq_trace, trace_exp,
                    trace_fun_update)
 from .greedy import (compute_centrality, default_greedy_tol, edge2low_rank, find_top_edges,
                      find_top_missing_edges, greedy_krylov, krylov_miobi, krylov_miobi_sharded,
@@ -23,7 +23,7 @@ from .datasets import load_problem, load_unweighted, prepare_unweighted, prepare
 
 __all__ = [
     "KrylovError", "KrylovLibraryError", "FUN_CODES", "LIB_PATH", "Context", "DeviceMatrix",
-    "default_context", "device_count", "slq_plan", "slq_quadforms", "slq_trace", "normest",
+    "default_context", "device_count", "slq_plan", "slq_quadforms", "slq_submit", "slq_collect", "slq_trace", "normest",
     "trace_fun_update", "fun_update", "fun_and_grad_krylov_exp", "fun_and_grad_krylov_fun",
     "mc_trace", "trace_exp", "expmv", "lanczos_fmv", "trace_fun_update_pairs", "krylov_miobi",
     "greedy_krylov", "find_top_edges", "find_top_missing_edges", "compute_centrality",

@@ -61,6 +61,8 @@ SIGNATURES = [
     ("kt_matrix_info", C.c_int, [_mat_p, _i64p, _i64p]),
     ("kt_slq_trace", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int,
                                _dp, _dp, _dp]),
+    ("kt_slq_submit", C.c_int, [_mat_p, C.c_int, C.c_int, C.c_uint64, C.c_int64, C.c_int64, C.c_int, _ip]),
+    ("kt_slq_collect", C.c_int, [_mat_p, C.c_int, _dp, _dp, _dp]),
     ("kt_slq_plan", C.c_int, [_mat_p, C.c_int64, _ip]),
     ("kt_normest", C.c_int, [_mat_p, C.c_double, _dp]),
     ("kt_trace_fun_update", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_double, C.c_int, C.c_int,

@@ -201,6 +201,31 @@ def slq_quadforms(A, nprobes: int, m: int, seed: int = 0, fun="exp", probe_offse
     return float(s1.value), float(s2.value), q[:nprobes]
 
 
+def slq_submit(A, nprobes: int, m: int, seed: int = 0, fun="exp", probe_offset: int = 0,
+               block: int = 0, ctx: Optional[Context] = None):
+    """First half of slq_quadforms (kt_slq_submit): queue the probe sweeps on
+    the device and return at once.  Returns a pending handle for
+    slq_collect; at most two outstanding per context, collected in order."""
+    D = _dev(A, ctx)
+    t = C.c_int()
+    _lib.check(_lib.load().kt_slq_submit(
+        D.handle, _fun_code(fun), int(m), int(seed) & 0xFFFFFFFFFFFFFFFF, int(probe_offset),
+        int(nprobes), int(block), C.byref(t)))
+    return (D, int(t.value), int(nprobes))
+
+
+def slq_collect(pending):
+    """Second half (kt_slq_collect): wait for that submission's sweeps, host
+    quadrature.  Returns what slq_quadforms returns: (sum, sum_sq, q)."""
+    D, t, nprobes = pending
+    q = np.zeros(max(nprobes, 1), dtype=np.float64)
+    s1 = C.c_double()
+    s2 = C.c_double()
+    _lib.check(_lib.load().kt_slq_collect(D.handle, t, C.byref(s1), C.byref(s2),
+                                          q.ctypes.data_as(C.POINTER(C.c_double))))
+    return float(s1.value), float(s2.value), q[:nprobes]
+
+
 def slq_plan(A, nprobes: int, ctx: Optional[Context] = None) -> int:
     """Probes per SpMM sweep that slq_quadforms uses with block=0."""
     D = _dev(A, ctx)

@@ -149,6 +149,18 @@ struct HostFlag {
     }
 };
 
+// One kt_slq_submit call awaiting its host half (kt_slq_collect): the
+// parameters, its host record slot and one event per sweep lane recorded
+// after the lane's last record copy.
+struct SlqPending {
+    bool live = false;
+    int fun = 0, m = 0, P = 1, lanes = 1;
+    uint64_t seed = 0;
+    int64_t offset = 0, nprobes = 0, nsweeps = 0;
+    size_t rec = 0;
+    hipEvent_t done[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
 struct Workspace {
     SweepBufs sweep[4];
     HostFlag expmv_stop;  // the stage a k_expmv_step launch found stopped (expmv_device)
@@ -157,7 +169,9 @@ struct Workspace {
     DevBuf ck_part;                                    // block SpMM hub-row chunk partials
     DevBuf hist, norm_part;                             // sweep scale history, inf-norm partials
     DevBuf expmv_state;                                 // expmv stage stop state (device)
-    PinnedBuf host_trec;
+    PinnedBuf host_trec[2];  // sweep records of the (at most two) submitted kt_slq calls
+    SlqPending slq_pend[2];
+    uint64_t slq_submitted = 0, slq_collected = 0;
     PinnedBuf pin_small;  // block-Krylov Gram blocks read back without a sync per pass
     PinnedBuf pin_arn;    // block Arnoldi's Gram read-backs, two step slots (sized once per run)
     // pinned staging for gram() read-backs, combine() uploads and the thin-QR

@@ -366,7 +366,10 @@ int kt_context_destroy(kt_context_t ctx) {
     if (w.comb_ev) (void)hipEventDestroy(w.comb_ev);
     if (w.qrfac_ev) (void)hipEventDestroy(w.qrfac_ev);
     if (w.qrm_ev) (void)hipEventDestroy(w.qrm_ev);
-    w.host_trec.release();
+    for (auto& b : w.host_trec) b.release();
+    for (auto& pd : w.slq_pend)
+        for (auto& e : pd.done)
+            if (e) (void)hipEventDestroy(e);
     for (auto a : ctx->aux_stream)
         if (a) (void)hipStreamDestroy(a);
     (void)hipStreamDestroy(ctx->stream);

@@ -13,11 +13,14 @@
 #include "kt_slq.h"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <thread>
 
 #include "kt_launch.h"
+#include "kt_pool.h"
 
 namespace kt {
 
@@ -245,19 +248,6 @@ int record_tridiag(const double* R, int m, int P, int c, double* al, double* off
     return steps;
 }
 
-template <class F>
-static void parallel_for(int64_t count, int64_t serial_below, F&& f) {
-    unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    if (count < serial_below) nth = 1;
-    if (nth == 1) {
-        f((int64_t)0, count);
-        return;
-    }
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nth; ++t) th.emplace_back(f, count * t / nth, count * (t + 1) / nth);
-    for (auto& t : th) t.join();
-}
-
 void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m, int fun,
                      double* quad, double* Y, int ldy) {
     lanczos_columns_mixed(A, X, ldx, ncols, m, fun, quad, Y, ldy, Y ? ncols : 0, 16);
@@ -362,92 +352,187 @@ extern "C" int kt_slq_plan(kt_matrix_t A, int64_t nprobes, int* block) {
     return KT_OK;
 }
 
-extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_t probe_offset,
-                            int64_t nprobes, int block, double* sum_q, double* sum_q2, double* q) {
-    try {
-        if (!A) fail(KT_ERR_ARG, "A is NULL");
-        if (fun < KT_FUN_EXP || fun > KT_FUN_SQRT) fail(KT_ERR_ARG, "unknown fun code");
-        if (m < 1 || m > 256) fail(KT_ERR_ARG, "m must be in [1, 256]");
-        if (nprobes < 0 || probe_offset < 0) fail(KT_ERR_ARG, "negative probe range");
-        if (block != 0 && !pow2_le128(block)) fail(KT_ERR_ARG, "block must be 0 or a power of two <= 128");
-        kt_context_s* ctx = A->ctx;
-        const int64_t n = A->n;
-        if (sum_q) *sum_q = 0.0;
-        if (sum_q2) *sum_q2 = 0.0;
-        if (nprobes == 0 || n == 0) return KT_OK;
-        const int P = block ? block : slq_auto_block(n, nprobes);
-        const int64_t nsweeps = (nprobes + P - 1) / P;
+namespace kt {
+
+// The device half of kt_slq_trace: queue the sweeps (their record copies
+// land in this call's host slot) and record one event per lane.  Returns the
+// ticket; at most two calls may be outstanding per context.
+static int slq_submit(kt_matrix_s* A, int fun, int m, uint64_t seed, int64_t probe_offset, int64_t nprobes,
+                      int block) {
+    if (fun < KT_FUN_EXP || fun > KT_FUN_SQRT) fail(KT_ERR_ARG, "unknown fun code");
+    if (m < 1 || m > 256) fail(KT_ERR_ARG, "m must be in [1, 256]");
+    if (nprobes < 0 || probe_offset < 0) fail(KT_ERR_ARG, "negative probe range");
+    if (block != 0 && !pow2_le128(block)) fail(KT_ERR_ARG, "block must be 0 or a power of two <= 128");
+    kt_context_s* ctx = A->ctx;
+    Workspace& w = ctx->ws;
+    if (w.slq_submitted - w.slq_collected >= 2)
+        fail(KT_ERR_ARG, "kt_slq_submit: two calls already outstanding (collect one first)");
+    const uint64_t ticket = w.slq_submitted;
+    SlqPending& pd = w.slq_pend[ticket & 1];
+    const int64_t n = A->n;
+    pd.live = false;
+    pd.fun = fun;
+    pd.m = m;
+    pd.seed = seed;
+    pd.offset = probe_offset;
+    pd.nprobes = (n == 0) ? 0 : nprobes;
+    pd.P = block ? block : slq_auto_block(n, std::max<int64_t>(nprobes, 1));
+    pd.nsweeps = pd.nprobes ? (pd.nprobes + pd.P - 1) / pd.P : 0;
+    // record per sweep: [alpha | up | low][m][P] (+ guard[P] in y-form)
+    pd.rec = (size_t)3 * m * pd.P + pd.P;
+    // KT_SLQ_LANES=L (<= 4): sweeps round-robin over L streams, so one
+    // sweep's small launches (and, in the explicit sweep, its streaming K2)
+    // overlap another sweep's gather-bound pass; measured best
+    // (profiles/r01_yform_lanes.txt): 2 for the y-form pass, 3 for the
+    // explicit K1/K2 sweep
+    const char* le = getenv("KT_SLQ_LANES");
+    const int lanes_env = le ? std::max(1, std::min(4, atoi(le))) : (ctx->yform ? 2 : 3);
+    pd.lanes = (int)std::max<int64_t>(1, std::min<int64_t>(pd.nsweeps, lanes_env));
+    if (pd.nsweeps) {
         KT_HIP(hipSetDevice(ctx->device));
-        // record per sweep: [alpha | up | low][m][P] (+ guard[P] in y-form)
-        const size_t rec = (size_t)3 * m * P + P;
-        Workspace& w = ctx->ws;
-        w.host_trec.ensure(sizeof(double) * rec * nsweeps);
-        double* htrec = w.host_trec.as<double>();
-        // KT_SLQ_LANES=L (<= 4): sweeps round-robin over L streams, so one
-        // sweep's small launches (and, in the explicit sweep, its streaming
-        // K2) overlap another sweep's gather-bound pass
-        const char* le = getenv("KT_SLQ_LANES");
-        // measured best (profiles/r01_yform_lanes.txt): 2 for the y-form pass, 3 for
-        // the explicit K1/K2 sweep
-        const int lanes_env = le ? std::max(1, std::min(4, atoi(le))) : (ctx->yform ? 2 : 3);
-        const int lanes = (int)std::min<int64_t>(nsweeps, lanes_env);
+        PinnedBuf& hb = w.host_trec[ticket & 1];
+        hb.ensure(sizeof(double) * pd.rec * pd.nsweeps);
+        double* htrec = hb.as<double>();
         const DevCSR& H = hub_csr(A);
-        // profiling: the previous calls' events (complete) are folded in while
-        // this call's sweeps run on the device
+        // profiling: the previous calls' events are folded in while this
+        // call's sweeps run on the device
         prof_recycle(ctx);
         size_t prev_events[PROF_NSLOTS];
         for (int k = 0; k < PROF_NSLOTS; ++k) prev_events[k] = ctx->prof[k].used;
-        for (int64_t s = 0; s < nsweeps; ++s) {
+        for (int64_t sw = 0; sw < pd.nsweeps; ++sw) {
             if (ctx->yform)
-                lanczos_sweep_y(A, H, P, m, seed, probe_offset + s * P, htrec + rec * s, (int)(s % lanes));
+                lanczos_sweep_y(A, H, pd.P, m, seed, probe_offset + sw * pd.P, htrec + pd.rec * sw,
+                                (int)(sw % pd.lanes));
             else
-                lanczos_sweep(A, H, P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr,
-                              htrec + rec * s, nullptr, nullptr, (int)(s % lanes));
+                lanczos_sweep(A, H, pd.P, m, seed, probe_offset + sw * pd.P, nullptr, 0, 0, nullptr,
+                              htrec + pd.rec * sw, nullptr, nullptr, (int)(sw % pd.lanes));
         }
-        prof_collect(ctx, prev_events);
-        KT_HIP(hipStreamSynchronize(ctx->stream));
-        for (int l = 1; l < lanes; ++l) KT_HIP(hipStreamSynchronize(ctx->aux_stream[l - 1]));
-#if !defined(KT_KY_DIAG) || KT_KY_DIAG == 0  // (diagnostic builds time the pass alone: no redo)
-        if (ctx->yform) {  // sweeps with a guarded probe are redone by the explicit CGS2 sweep
-            int64_t redone = 0;
-            for (int64_t s = 0; s < nsweeps; ++s) {
-                const double* g = htrec + rec * s + (size_t)3 * m * P;
-                const int64_t live = std::min<int64_t>(P, nprobes - s * P);
-                bool bad = false;
-                for (int64_t c = 0; c < live; ++c) bad |= !(g[c] >= kYformGuard);
-                if (!bad) continue;
-                lanczos_sweep(A, H, P, m, seed, probe_offset + s * P, nullptr, 0, 0, nullptr,
-                              htrec + rec * s, nullptr, nullptr, 0);
-                KT_HIP(hipStreamSynchronize(ctx->stream));
-                ++redone;
-            }
-            ctx->yform_redone += redone;
+        for (int l = 0; l < pd.lanes; ++l) {
+            if (!pd.done[l]) KT_HIP(hipEventCreateWithFlags(&pd.done[l], hipEventDisableTiming));
+            KT_HIP(hipEventRecord(pd.done[l], l ? ctx->aux_stream[l - 1] : ctx->stream));
         }
-#endif
-
-        std::vector<double> qv((size_t)nprobes);
-        parallel_for(nprobes, 64, [&](int64_t pb, int64_t pe) {
-            std::vector<double> al(m), off(m);
-            for (int64_t p = pb; p < pe; ++p) {
-                const int steps = record_tridiag(htrec + rec * (p / P), m, P, (int)(p % P),
-                                                 al.data(), off.data());
-                qv[p] = (double)n * tridiag_quadrature(steps, al.data(), off.data(), fun);
-            }
-        });
-        double s1 = 0.0, s2 = 0.0;
-        for (int64_t p = 0; p < nprobes; ++p) {
-            s1 += qv[p];
-            s2 += qv[p] * qv[p];
-            if (q) q[p] = qv[p];
-        }
-        if (sum_q) *sum_q = s1;
-        if (sum_q2) *sum_q2 = s2;
-    } catch (const kt::Status& s) {
-        kt::set_error(s.msg);
-        return s.code;
-    } catch (const std::exception& e) {
-        kt::set_error(e.what());
-        return KT_ERR_ARG;
+        // (those may still be in flight when the previous submission is not
+        // collected yet: wait for them -- this call's sweeps are queued already)
+        prof_collect(ctx, prev_events, true);
     }
+    pd.live = true;
+    ++w.slq_submitted;
+    return (int)(ticket & 0x7fffffff);
+}
+
+// The host half: wait for the call's sweeps (its lane events only, not work
+// submitted after it), redo guarded sweeps with the explicit CGS2 sweep,
+// host Gauss quadrature, sums.
+static void slq_collect(kt_matrix_s* A, int ticket, double* sum_q, double* sum_q2, double* q) {
+    kt_context_s* ctx = A->ctx;
+    Workspace& w = ctx->ws;
+    if (w.slq_collected == w.slq_submitted || (uint64_t)ticket != (w.slq_collected & 0x7fffffff))
+        fail(KT_ERR_ARG, "kt_slq_collect: tickets must be collected once each, in submission order");
+    SlqPending& pd = w.slq_pend[w.slq_collected & 1];
+    const uint64_t slot = w.slq_collected & 1;
+    ++w.slq_collected;
+    if (!pd.live) fail(KT_ERR_ARG, "kt_slq_collect: the submission failed");
+    pd.live = false;
+    if (sum_q) *sum_q = 0.0;
+    if (sum_q2) *sum_q2 = 0.0;
+    if (pd.nprobes == 0) return;
+    const int64_t n = A->n, nprobes = pd.nprobes;
+    const int m = pd.m, P = pd.P, fun = pd.fun;
+    const size_t rec = pd.rec;
+    double* htrec = w.host_trec[slot].as<double>();
+    // KT_SLQ_PHASES=1 (diagnostic): host-side phase times of the call on stderr
+    const char* phe = getenv("KT_SLQ_PHASES");
+    const bool phases = phe && phe[0] == '1';
+    auto clk = [] { return std::chrono::steady_clock::now(); };
+    const auto t_in = clk();
+    KT_HIP(hipSetDevice(ctx->device));
+    for (int l = 0; l < pd.lanes; ++l) KT_HIP(hipEventSynchronize(pd.done[l]));
+    const auto t_synced = clk();
+#if !defined(KT_KY_DIAG) || KT_KY_DIAG == 0  // (diagnostic builds time the pass alone: no redo)
+    if (ctx->yform) {  // sweeps with a guarded probe are redone by the explicit CGS2 sweep
+        const DevCSR& H = hub_csr(A);
+        int64_t redone = 0;
+        for (int64_t sw = 0; sw < pd.nsweeps; ++sw) {
+            const double* g = htrec + rec * sw + (size_t)3 * m * P;
+            const int64_t live = std::min<int64_t>(P, nprobes - sw * P);
+            bool bad = false;
+            for (int64_t c = 0; c < live; ++c) bad |= !(g[c] >= kYformGuard);
+            if (!bad) continue;
+            lanczos_sweep(A, H, P, m, pd.seed, pd.offset + sw * P, nullptr, 0, 0, nullptr, htrec + rec * sw,
+                          nullptr, nullptr, 0);
+            KT_HIP(hipStreamSynchronize(ctx->stream));
+            ++redone;
+        }
+        ctx->yform_redone += redone;
+    }
+#endif
+    // host Gauss quadrature, 16 probes per task on the persistent pool
+    // (threads spawned and joined per call cost ~0.1-0.3 ms per call)
+    std::vector<double> qv((size_t)nprobes);
+    const int64_t chunk = 16;
+    HostPool::get().run((int)((nprobes + chunk - 1) / chunk), [&](int t) {
+        std::vector<double> al(m), off(m);
+        const int64_t pb = t * chunk, pe = std::min<int64_t>(nprobes, pb + chunk);
+        for (int64_t p = pb; p < pe; ++p) {
+            const int steps = record_tridiag(htrec + rec * (p / P), m, P, (int)(p % P), al.data(), off.data());
+            qv[p] = (double)n * tridiag_quadrature(steps, al.data(), off.data(), fun);
+        }
+    }, 4);
+    if (phases) {
+        auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::micro>(b - a).count();
+        };
+        std::fprintf(stderr, "[kt slq] wait %.1f us, redo + quadrature %.1f us (%lld probes)\n", us(t_in, t_synced),
+                     us(t_synced, clk()), (long long)nprobes);
+    }
+    double s1 = 0.0, s2 = 0.0;
+    for (int64_t p = 0; p < nprobes; ++p) {
+        s1 += qv[p];
+        s2 += qv[p] * qv[p];
+        if (q) q[p] = qv[p];
+    }
+    if (sum_q) *sum_q = s1;
+    if (sum_q2) *sum_q2 = s2;
+}
+
+}  // namespace kt
+
+#define KT_SLQ_TRY try {
+#define KT_SLQ_CATCH                         \
+    }                                        \
+    catch (const kt::Status& s) {            \
+        kt::set_error(s.msg);                \
+        return s.code;                       \
+    }                                        \
+    catch (const std::exception& e) {        \
+        kt::set_error(e.what());             \
+        return KT_ERR_ARG;                   \
+    }                                        \
     return KT_OK;
+
+extern "C" int kt_slq_trace(kt_matrix_t A, int fun, int m, uint64_t seed, int64_t probe_offset,
+                            int64_t nprobes, int block, double* sum_q, double* sum_q2, double* q) {
+    KT_SLQ_TRY
+    if (!A) fail(KT_ERR_ARG, "A is NULL");
+    Workspace& w = A->ctx->ws;
+    if (w.slq_submitted != w.slq_collected)
+        fail(KT_ERR_ARG, "kt_slq_trace: kt_slq_submit calls are outstanding on this context");
+    const int t = slq_submit(A, fun, m, seed, probe_offset, nprobes, block);
+    slq_collect(A, t, sum_q, sum_q2, q);
+    KT_SLQ_CATCH
+}
+
+extern "C" int kt_slq_submit(kt_matrix_t A, int fun, int m, uint64_t seed, int64_t probe_offset,
+                             int64_t nprobes, int block, int* ticket) {
+    KT_SLQ_TRY
+    if (!A || !ticket) fail(KT_ERR_ARG, "NULL argument");
+    *ticket = slq_submit(A, fun, m, seed, probe_offset, nprobes, block);
+    KT_SLQ_CATCH
+}
+
+extern "C" int kt_slq_collect(kt_matrix_t A, int ticket, double* sum_q, double* sum_q2, double* q) {
+    KT_SLQ_TRY
+    if (!A) fail(KT_ERR_ARG, "A is NULL");
+    slq_collect(A, ticket, sum_q, sum_q2, q);
+    KT_SLQ_CATCH
 }

@@ -37,18 +37,20 @@ def allreduce_sums(vals, device=None, force: bool = False):
     """Sum a short list of doubles over the default process group."""
     import torch
     import torch.distributed as dist
+    if not _group_ready(force):  # nothing to reduce: no device tensor, no copies, no sync
+        return [float(x) for x in vals]
     t = torch.tensor(list(vals), dtype=torch.float64, device=device)
-    if _group_ready(force):
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [float(x) for x in t.cpu().tolist()]
 
 
 def allreduce_max(val: float, device=None, force: bool = False):
     import torch
     import torch.distributed as dist
+    if not _group_ready(force):
+        return float(val)
     t = torch.tensor([float(val)], dtype=torch.float64, device=device)
-    if _group_ready(force):
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 

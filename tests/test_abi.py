@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_null_arguments():
     from krylov_robustness_amd import _lib
     lib = _lib.load()
-    assert lib.kt_abi_version() == 2
+    assert lib.kt_abi_version() == 3
     h = C.c_void_p()
     # NULL context -> KT_ERR_ARG with a message, never a crash
     st = lib.kt_matrix_create_csc(None, 0, None, None, None, 0, C.byref(h))

@@ -230,3 +230,60 @@ def test_slq_fused_tickets_survive_resize(kra, gpu_ctx):
         _, _, q = kra.slq_quadforms(D, 18, 30, seed=3, block=16, ctx=gpu_ctx)
         _, q_ref = slq_ref.slq_trace(A, 3, 30, seed=3)
         np.testing.assert_allclose(q[:3], q_ref, rtol=RTOL)
+
+
+def test_slq_submit_collect_pipeline_bit_identical(kra, gpu_ctx):
+    """kt_slq_submit / kt_slq_collect (the bench's one-deep pipeline): two
+    evaluations in flight -- the second queued before the first's host half
+    runs -- return exactly what kt_slq_trace returns for each, ragged probe
+    counts and offsets included; the collect of the first waits only for its
+    own sweeps."""
+    from krylov_robustness_amd import graphs
+    A = graphs.chung_lu(200_000, 2_000_000, seed=3)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    ref = [kra.slq_quadforms(D, 77, 20, seed=s, probe_offset=o, ctx=gpu_ctx) for s, o in ((1, 0), (2, 5), (3, 9))]
+    p1 = kra.slq_submit(D, 77, 20, seed=1, probe_offset=0, ctx=gpu_ctx)
+    p2 = kra.slq_submit(D, 77, 20, seed=2, probe_offset=5, ctx=gpu_ctx)
+    got = [kra.slq_collect(p1)]
+    p3 = kra.slq_submit(D, 77, 20, seed=3, probe_offset=9, ctx=gpu_ctx)
+    got += [kra.slq_collect(p2), kra.slq_collect(p3)]
+    for (a1, a2, aq), (b1, b2, bq) in zip(got, ref):
+        assert a1 == b1 and a2 == b2 and np.array_equal(aq, bq)
+
+
+def test_slq_submit_collect_rules(kra, gpu_ctx):
+    from krylov_robustness_amd import _lib
+    A = load_graph("rome")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    p1 = kra.slq_submit(D, 10, 10, seed=1, ctx=gpu_ctx)
+    p2 = kra.slq_submit(D, 10, 10, seed=2, ctx=gpu_ctx)
+    with pytest.raises(_lib.KrylovError):  # a third outstanding submission
+        kra.slq_submit(D, 10, 10, seed=3, ctx=gpu_ctx)
+    with pytest.raises(_lib.KrylovError):  # kt_slq_trace while submissions are outstanding
+        kra.slq_quadforms(D, 10, 10, seed=4, ctx=gpu_ctx)
+    with pytest.raises(_lib.KrylovError):  # out of order
+        kra.slq_collect(p2)
+    a = kra.slq_collect(p1)
+    b = kra.slq_collect(p2)
+    with pytest.raises(_lib.KrylovError):  # collected twice
+        kra.slq_collect(p2)
+    assert np.array_equal(a[2], kra.slq_quadforms(D, 10, 10, seed=1, ctx=gpu_ctx)[2])
+    assert np.array_equal(b[2], kra.slq_quadforms(D, 10, 10, seed=2, ctx=gpu_ctx)[2])
+    e = kra.slq_submit(D, 0, 10, seed=1, ctx=gpu_ctx)  # empty submission
+    assert kra.slq_collect(e)[0] == 0.0
+
+
+def test_slq_pipelined_guard_redo(kra, monkeypatch):
+    """The y-form guard's explicit-sweep redo runs in the host half; with the
+    next evaluation already queued on the same lanes the redo still sees its
+    own records (stream order) and gives the oracle's forms."""
+    A = sp.csr_matrix(np.ones((50, 50)) - np.eye(50))
+    ctx = _ctx_with(monkeypatch, kra, KT_SLQ_YFORM="1")
+    D = kra.DeviceMatrix(A, ctx)
+    p1 = kra.slq_submit(D, 20, 30, seed=6, block=16, ctx=ctx)
+    p2 = kra.slq_submit(D, 20, 30, seed=7, block=16, ctx=ctx)
+    _, _, q1 = kra.slq_collect(p1)
+    _, _, q2 = kra.slq_collect(p2)
+    assert ctx.yform_redone() == 4
+    np.testing.assert_allclose(q1, slq_ref.slq_trace(A, 20, 30, seed=6)[1], rtol=1e-10)
+    np.testing.assert_allclose(q2, slq_ref.slq_trace(A, 20, 30, seed=7)[1], rtol=1e-10)

@@ -9,6 +9,8 @@
 #   configs  secondary configs (tests/perf/bench_*.py) + er100k bench
 #   prof     rocprofv3 --kernel-trace --stats of the default bench command,
 #            reconciled with the line it printed (tools/reconcile_trace.py)
+#   secondary latency floors (tools/latency_floor) + kernel stats of the
+#            config-1/3/5 drivers under rocprofv3
 #   timeline rocprofv3 kernel trace of the er100k bench, per-evaluation
 #            breakdown (tools/eval_timeline.py)
 #   pmc      FETCH_SIZE / WRITE_SIZE passes (separate runs) of `bench.py
@@ -52,6 +54,17 @@ timeline)
         > $O/bench_er100k_traced.json 2> $O/tl.err ) || { tail -20 $O/tl.err; exit 1; }
     python3 tools/eval_timeline.py $(find $O/tl -name "*kernel_trace.csv") ${SWEEPS:-2} 100 $O/er100k_eval_timeline.json || exit 1
     gzip -f $(find $O/tl -name "*kernel_trace.csv") ;;
+secondary)
+    # latency floors + rocprofv3 kernel stats of the secondary configs' drivers
+    timeout -k 10 120 tools/latency_floor/latency_floor > $O/latency_floor.txt 2>&1 || { cat $O/latency_floor.txt; exit 1; }
+    cat $O/latency_floor.txt
+    for s in bench_config1 bench_config3 bench_greedy; do
+        ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/st_$s -o $s \
+            -- python3 $GRAFT_REPO_ROOT/tests/perf/$s.py > $O/$s.json 2> $O/$s.err ) || { tail -5 $O/$s.err; exit 1; }
+        cp $(find $O/st_$s -name "*kernel_stats.csv") $O/${s}_kernel_stats.csv
+        gzip -f $(find $O/st_$s -name "*kernel_trace.csv")
+        echo "== $s"; cut -c1-300 $O/$s.json
+    done ;;
 pmc)
     SEC=${SECTION:-sf1m}
     B="$GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --cpu-seconds 0 --lanes 1 --mc-steps 1 --no-profile $*"
