@@ -1856,6 +1856,17 @@ double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev
     return xm;
 }
 
+// One gathered row (2 doubles) of the LDS block X; the KT_REG_DIAG=1
+// diagnostic build replaces it by a register value (no gather; its results
+// are wrong by construction, only its clocks mean anything)
+__device__ __forceinline__ double2 reg_gather(const double* X, int c) {
+#if defined(KT_REG_DIAG) && KT_REG_DIAG >= 1
+    return make_double2((double)c, 1.0);
+#else
+    return *reinterpret_cast<const double2*>(X + 2 * c);
+#endif
+}
+
 // CSR: 0 = CSR in global memory, 1 = row pointers + u16 columns in LDS, 2 = and
 // the weights.  A template argument, so every CSR access has a known address
 // space (a pointer chosen at run time between LDS and global memory compiles
@@ -1952,24 +1963,46 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
             double s0 = 0.0, s1 = 0.0;
             if (r < n && (nl == 0 || slot[r] < 0)) {
                 const int rb = rp[r], re = rp[r + 1];
-                for (int k0 = rb; k0 < re; k0 += 4) {
-                    int cc[4];
-                    double a[4];
+                // four nonzeros per round; the indices are clamped into the row
+                // (a masked weight drops the repeats) so that every load is
+                // unconditional: the four column reads issue together, then the
+                // four gathers -- predicated loads compiled to one branch and
+                // one LDS round trip EACH (the SpMM took ~13 us per Lanczos step)
+                if (M.unit) {
+                    for (int k0 = rb; k0 < re; k0 += 4) {
+                        int cc[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const bool ok = k0 + u < re;
-                        cc[u] = ok ? col(k0 + u) : 0;
-                        a[u] = ok ? (M.unit ? 1.0 : va[k0 + u]) : 0.0;
-                    }
-                    double2 v[4];
+                        for (int u = 0; u < 4; ++u) cc[u] = col(min(k0 + u, re - 1));
+                        double2 v[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const double2*>(X + 2 * cc[u]);
+                        for (int u = 0; u < 4; ++u) v[u] = reg_gather(X, cc[u]);
 #pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (k0 + u < re) {
-                            s0 = fma(a[u], v[u].x, s0);
-                            s1 = fma(a[u], v[u].y, s1);
+                        for (int u = 0; u < 4; ++u) {
+                            const double a = (k0 + u < re) ? 1.0 : 0.0;
+                            s0 = fma(a, v[u].x, s0);
+                            s1 = fma(a, v[u].y, s1);
                         }
+                    }
+                } else {
+                    for (int k0 = rb; k0 < re; k0 += 4) {
+                        int cc[4];
+                        double a[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int k = min(k0 + u, re - 1);
+                            cc[u] = col(k);
+                            a[u] = va[k];
+                        }
+                        double2 v[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) v[u] = reg_gather(X, cc[u]);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const double w = (k0 + u < re) ? a[u] : 0.0;
+                            s0 = fma(w, v[u].x, s0);
+                            s1 = fma(w, v[u].y, s1);
+                        }
+                    }
                 }
             }
             W[q] = make_double2(s0, s1);
