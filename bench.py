@@ -515,23 +515,37 @@ def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev,
         l1, ms1 = ctx.profile_read(0)
         l2, ms2 = ctx.profile_read(1)
         if l1:
-            P = 16  # lanczos_columns: 10 columns per Afun call in one 16-wide sweep
+            # mc_trace_batched: round 1's S term is one 16-wide sweep (m K1
+            # launches), every round after it one 32-wide sweep (the round's Q
+            # and G terms and the next S term); the K1 launches of the pass are
+            # charged their own width's bytes
             unit = bool(A.nnz) and bool(np.all(A.data == 1.0))
             per_nnz = 4 if unit else 12
-            kb = per_nnz * nnz + 4 * (n + 1) + 16 * n * P
+
+            def kb(P):
+                return per_nnz * nnz + 4 * (n + 1) + 16 * n * P
+            l16 = min(m, l1)
+            l32 = l1 - l16
+            bytes_total = l16 * kb(16) + l32 * kb(32)
             us = ms1 / l1 * 1e3
-            gbs = kb / (us * 1e-6) / 1e9
-            out["roofline"] = {"bound": "hbm", "kernel": f"k_spmm_dot<{P}>", "achieved": round(gbs, 1),
+            gbs = bytes_total / (ms1 * 1e-3) / 1e9
+            t16 = _pmc_traffic("k_spmm_dot", 16, args.config, args.weighted)
+            t32 = _pmc_traffic("k_spmm_dot", 32, args.config, args.weighted)
+            traffic = (l16 * t16 + l32 * t32) / l1 if (t16 and t32) else None
+            out["roofline"] = {"bound": "hbm", "kernel": "k_spmm_dot<16|32>", "achieved": round(gbs, 1),
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                               "traffic": _pmc_traffic("k_spmm_dot", P, args.config, args.weighted),
-                               "avg_launch_us": round(us, 2), "launches": l1,
-                               "algorithmic_bytes_per_launch": kb,
-                               "algorithmic_bytes_basis": f"{per_nnz} nnz + 4 (n+1) + 16 n P: the CSR, "
-                                                          "u_j gathered once, y = A u_j written",
+                               "traffic": traffic, "avg_launch_us": round(us, 2), "launches": l1,
+                               "launches_by_width": {"16": l16, "32": l32},
+                               "algorithmic_bytes_per_launch": round(bytes_total / l1),
+                               "algorithmic_bytes_basis": f"{per_nnz} nnz + 4 (n+1) + 16 n P per launch (the "
+                                                          "CSR, u_j gathered once, y = A u_j written), P = 16 "
+                                                          "for round 1's S sweep, 32 for the rest; mean",
                                "k2_update_avg_us": round(ms2 / l2 * 1e3, 2) if l2 else None,
                                "serial_eval_ms": round(serial_ms, 2),
                                "measured": "HIP events around every K1 launch of one serial trace_exp "
                                            "(KT_TWIN=0: all Afun calls on one stream) after the timed region"}
+            if traffic:
+                out["roofline"]["traffic_GBs"] = round(traffic * l1 / (ms1 * 1e-3) / 1e9, 1)
     return out
 
 

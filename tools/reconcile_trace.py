@@ -51,6 +51,18 @@ def main(trace_csv, bench_json, out_json):
                 "(the steps x sweeps x (m-1) launches before the isolated pass) and the isolated "
                 "single-lane roofline pass (the last `launches` launches)",
     }
+    mc = (b.get("mc_trace") or {}).get("roofline")
+    if mc:
+        # the mc_trace leg's serial roofline pass: its K1 launches (16- and
+        # 32-wide) are the last `launches` k_spmm_dot launches of the run
+        allk = [r for r in csv.DictReader(open(trace_csv))
+                if "kt::k_spmm_dot<16," in r["Kernel_Name"] or "kt::k_spmm_dot<32," in r["Kernel_Name"]]
+        allk.sort(key=lambda r: int(r["Start_Timestamp"]))
+        last = allk[-mc["launches"]:]
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in last]
+        out["mc_trace_serial_pass"] = {"kernel": mc["kernel"], "launches": len(d),
+                                       "rocprof_avg_us": round(sum(d) / len(d), 2),
+                                       "bench_avg_launch_us": mc["avg_launch_us"]}
     json.dump(out, open(out_json, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
