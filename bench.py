@@ -32,7 +32,9 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed evaluations (default 5; 100 with --config er100k, whose evaluations "
+                         "take ~5 ms)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="sf1m", choices=["sf1m", "er100k"])
     ap.add_argument("--nprobes", type=int, default=None)
@@ -223,6 +225,8 @@ def _pooled(sums, N):
 
 def main():
     args = parse()
+    if args.steps is None:
+        args.steps = 100 if args.config == "er100k" else 5
     if args.lanes == 0:
         args.lanes = 3 if args.explicit else 2
     os.environ["KT_SLQ_LANES"] = str(args.lanes)
