@@ -39,24 +39,32 @@ __device__ __forceinline__ double4_t mfma_f64(double a, double b, double4_t c) {
 
 // grid: x = row chunk, y = group of 4 i-tiles (128 columns of X), z = j-tile
 // (32 columns of Y).  part: slabs of px*py doubles, slab = chunk.
+//
+// px <= 32 (one i-tile): the four waves split the chunk's rows instead (wave w
+// takes rows rb + 32 w + 128 t), and their four tiles are summed through LDS
+// in wave order before the slab is written -- otherwise three of the four
+// waves would idle and each CU would have one wave's loads in flight.
 __global__ __launch_bounds__(256) void k_gram_mfma(int64_t n, const double* __restrict__ X, int ldx, int px,
                                                    const double* __restrict__ Y, int ldy, int py,
                                                    int rows_per_chunk, double* __restrict__ part) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int i0 = (blockIdx.y * 4 + wave) * 32;
+    const bool rsplit = px <= 32;  // uniform over the grid
+    const int i0 = rsplit ? 0 : (blockIdx.y * 4 + wave) * 32;
     const int j0 = blockIdx.z * 32;
     if (i0 >= px) return;  // whole wave idle (uniform)
-    const int64_t rb = (int64_t)blockIdx.x * rows_per_chunk;
-    const int64_t re = min(n, rb + rows_per_chunk);
+    const int64_t cb = (int64_t)blockIdx.x * rows_per_chunk;
+    const int64_t re = min(n, cb + rows_per_chunk);
+    constexpr int KU = 8;
+    const int64_t rb = rsplit ? cb + wave * 4 * KU : cb;
+    const int64_t rstep = rsplit ? 4 * 4 * KU : 4 * KU;
     const int li = lane & 15, lk = lane >> 4;
     const int ia = i0 + li, ib = i0 + 16 + li, ja = j0 + li, jb = j0 + 16 + li;
     const bool va = ia < px, vb = ib < px, wa = ja < py, wb = jb < py;
     double4_t c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
     // 4 rows per MFMA k-step; 8 k-steps (32 rows, 32 loads per lane) in flight
     // per iteration: a chunk is 4 round trips, not one per row group
-    constexpr int KU = 8;
-    for (int64_t r0 = rb; r0 < re; r0 += 4 * KU) {
+    for (int64_t r0 = rb; r0 < re; r0 += rstep) {
         double xa[KU], xb[KU], ya[KU], yb[KU];
 #pragma unroll
         for (int u = 0; u < KU; ++u) {
@@ -76,6 +84,28 @@ __global__ __launch_bounds__(256) void k_gram_mfma(int64_t n, const double* __re
             c10 = mfma_f64(xb[u], ya[u], c10);
             c11 = mfma_f64(xb[u], yb[u], c11);
         }
+    }
+    if (rsplit) {  // the four waves' tiles summed in wave order (deterministic)
+        __shared__ double tl[3][16][64];
+        if (wave > 0)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                tl[wave - 1][g][lane] = c00[g];
+                tl[wave - 1][4 + g][lane] = c01[g];
+                tl[wave - 1][8 + g][lane] = c10[g];
+                tl[wave - 1][12 + g][lane] = c11[g];
+            }
+        __syncthreads();
+        if (wave > 0) return;
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                c00[g] += tl[w][g][lane];
+                c01[g] += tl[w][4 + g][lane];
+                c10[g] += tl[w][8 + g][lane];
+                c11[g] += tl[w][12 + g][lane];
+            }
     }
     // D layout (f64 16x16x4): column = lane & 15 (j), row = (lane >> 4) + 4 reg (i)
     double* slab = part + (int64_t)blockIdx.x * px * py;

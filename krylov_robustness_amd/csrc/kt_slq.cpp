@@ -45,7 +45,8 @@ int slq_auto_block(int64_t n, int64_t nprobes) {
 // columns, original-column norms^2 in norms2) is copied into the sweep block.
 void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base,
                    const double* x, int ldx, int ncols, const double* norms2, double* rec_host,
-                   DevMat* basis, std::vector<double>* scale_hist, int lane) {
+                   DevMat* basis, std::vector<double>* scale_hist, int lane, int bcols) {
+    if (bcols <= 0 || bcols > P) bcols = P;
     kt_context_s* ctx = A->ctx;
     const int n = (int)A->n;
     if (lane < 0 || lane > 3) fail(KT_ERR_ARG, "sweep lane out of range");
@@ -103,9 +104,9 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
     }
     for (int j = 0; j < m; ++j) {
         const int first = (j == 0);
-        if (basis) {  // record u_j and s_j (v_j = s_j u_j)
-            KT_HIP(hipMemcpy2DAsync(basis->col(j * P), sizeof(double) * basis->ld, ucur,
-                                    sizeof(double) * P, sizeof(double) * P, (size_t)n,
+        if (basis) {  // record u_j (its first bcols columns) and s_j (v_j = s_j u_j)
+            KT_HIP(hipMemcpy2DAsync(basis->col(j * bcols), sizeof(double) * basis->ld, ucur,
+                                    sizeof(double) * P, sizeof(double) * bcols, (size_t)n,
                                     hipMemcpyDeviceToDevice, st));
             KT_HIP(hipMemcpyAsync(hist_dev->as<double>() + (size_t)j * P, sc, sizeof(double) * P,
                                   hipMemcpyDeviceToDevice, st));
@@ -295,11 +296,14 @@ void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, 
         std::vector<double> rec((size_t)3 * m * P);
         DevMat basis;
         std::vector<double> hist;
-        if (nyc) basis.alloc(ctx, n, m * P, false);  // every slot is written by the sweep
+        // the basis keeps only the nyc columns whose f(A) x is wanted (slot j
+        // = columns j*nyc .. j*nyc + nyc - 1): a 30-column sweep with 10 such
+        // columns copies and re-reads a third of the bytes
+        if (nyc) basis.alloc(ctx, n, m * nyc, false);  // every slot is written by the sweep
         lanczos_sweep(A, M, P, m, 0, 0, Xs + c0, ldxs, nc, norms2.data() + c0, rec.data(),
-                      nyc ? &basis : nullptr, nyc ? &hist : nullptr);
+                      nyc ? &basis : nullptr, nyc ? &hist : nullptr, 0, nyc);
         KT_HIP(hipStreamSynchronize(ctx->stream));
-        std::vector<double> W((size_t)m * P, 0.0);  // weights for Y = sum_j u_j w_j
+        std::vector<double> W((size_t)m * std::max(nyc, 1), 0.0);  // weights for Y = sum_j u_j w_j, [j * nyc + c]
         for (int c = 0; c < nc; ++c) {
             std::vector<double> al(m), off(m);
             const int steps = record_tridiag(rec.data(), m, P, c, al.data(), off.data());
@@ -320,7 +324,7 @@ void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, 
                     double cj = 0.0;
                     for (int k = 0; k < steps; ++k)
                         cj += Z[j + (size_t)k * steps] * fscalar(fun, th[k]) * Z[(size_t)k * steps];
-                    W[(size_t)j * P + c] = nx * hist[(size_t)j * P + c] * cj;  // v_j = s_j u_j
+                    W[(size_t)j * nyc + c] = nx * hist[(size_t)j * P + c] * cj;  // v_j = s_j u_j
                 }
             }
         }
@@ -329,7 +333,7 @@ void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, 
             dw.ensure(sizeof(double) * W.size());
             KT_HIP(hipMemcpyAsync(dw.ptr, W.data(), sizeof(double) * W.size(), hipMemcpyHostToDevice,
                                   ctx->stream));
-            KT_HIP(launch_weighted_sum((int)n, m, P, nyc, basis.col(0), basis.ld, dw.as<double>(),
+            KT_HIP(launch_weighted_sum((int)n, m, nyc, nyc, basis.col(0), basis.ld, dw.as<double>(),
                                        Ys + c0, ldys, ctx->stream));
             KT_HIP(hipStreamSynchronize(ctx->stream));
         }

@@ -12,7 +12,7 @@ int slq_auto_block(int64_t n, int64_t nprobes);
 // ctx->aux_stream[l-1] with ws.sweep[l] (independent sweeps overlap).
 void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base,
                    const double* x, int ldx, int ncols, const double* norms2, double* rec_host,
-                   DevMat* basis, std::vector<double>* scale_hist, int lane = 0);
+                   DevMat* basis, std::vector<double>* scale_hist, int lane = 0, int bcols = 0);
 
 int record_tridiag(const double* R, int m, int P, int c, double* al, double* off);
 
