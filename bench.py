@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--mc-steps", type=int, default=5,
                     help="timed trace_exp (mc_trace) evaluations reported beside the headline "
                          "(0 = skip that leg unless --estimator mc_trace)")
+    ap.add_argument("--ref-cpu-seconds", type=float, default=15.0,
+                    help="trace_exp as the reference composes it (mc_trace + expmv Afun): one serial GPU "
+                         "run, and the oracle's CPU restatement timed on a bounded sample of it (rank 0, "
+                         "N=1, config sf1m, beside the mc_trace leg); 0 disables")
     ap.add_argument("--bitstable", action="store_true",
                     help="all-gather the per-probe forms and sum them in global probe order on every "
                          "rank (SURVEY §8e): the estimate is bit-identical for any number of ranks")
@@ -433,6 +437,8 @@ def main():
     if mc_steps > 0:
         mc = _mc_trace_leg(args, kra, kdist, D, ctx, m, mc_steps, use_pg, barrier, coll_dev, world, ref,
                            n, nnz, A)
+        if rank == 0 and world == 1 and args.ref_cpu_seconds > 0 and args.config == "sf1m":
+            mc["reference_composition"] = _reference_composition(kra, D, ctx, A, ref, args.ref_cpu_seconds)
         if not run_hutch:
             value, ms_per_step = mc.pop("evals_per_s"), mc.pop("ms_per_eval")
             roof = mc.pop("roofline")
@@ -467,6 +473,72 @@ def main():
         print(json.dumps(out), flush=True)
     if use_pg:
         dist.destroy_process_group()
+
+
+def _reference_composition(kra, D, ctx, A, ref, budget_s):
+    """trace_exp as the reference composes it (trace_exp.m:5-6: mc_trace with
+    the expmv Afun; expmv.m with select_taylor_degree.m / normAm.m) on the
+    bench graph, twice:
+      * on the GPU, once: kt_mc_trace with the device expmv Afun, serial
+        (KT_TWIN=0, KT_MC_SPEC=0: every expmv call on this context, counted
+        by kt_context_stat 3 / 4);
+      * SURVEY §8d plan (i)'s CPU baseline: the oracle's numpy/SciPy
+        restatement of the same algorithm (oracle/krylov_oracle.py: expmv,
+        select_taylor_degree; SciPy's sparse @ dense is single-threaded),
+        timed on a bounded sample -- one select_taylor_degree call and the
+        first Taylor terms (expmv.m:75-82) of one 10-column expmv call --
+        and extrapolated with the GPU run's call and term counts.  mc_trace's
+        own host work (QR, projections) is left out: a lower bound on the
+        CPU time."""
+    from oracle import krylov_oracle as O
+    saved = {k: os.environ.get(k) for k in ("KT_TWIN", "KT_MC_SPEC")}
+    os.environ["KT_TWIN"] = "0"
+    os.environ["KT_MC_SPEC"] = "0"
+    try:
+        c0, k0 = ctx.stat(3), ctx.stat(4)
+        t0 = time.perf_counter()
+        tr, res, it = kra.mc_trace("expmv", None, 1e-4, 1000, 1, 0, seed=0, A=D, ctx=ctx)
+        gpu_s = time.perf_counter() - t0
+        calls, terms = ctx.stat(3) - c0, ctx.stat(4) - k0
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    out = {"afun": "expmv (trace_exp.m:5-6 as the reference composes it), tol 1e-4, maxit 1000, seed 0",
+           "gpu_ms": round(gpu_s * 1e3, 2), "gpu_evals_per_s": round(1.0 / gpu_s, 4), "rounds": it,
+           "trace_estimate": tr, "expmv_calls": calls, "taylor_terms": terms,
+           "gpu_mode": "serial: every expmv call on one stream (KT_TWIN=0, KT_MC_SPEC=0)"}
+    if ref:
+        out["rel_err"] = (tr - ref["value"]) / ref["value"]
+    Acsr = A.tocsr()
+    n = Acsr.shape[0]
+    b = O.rademacher(n, range(10), 0)
+    t0 = time.perf_counter()
+    O.select_taylor_degree(Acsr, b)
+    t_sel = time.perf_counter() - t0
+    f = b.copy()
+    k = 0
+    t0 = time.perf_counter()
+    while k < 200 and (k == 0 or time.perf_counter() - t0 < budget_s):
+        k += 1
+        b = (1.0 / (20.0 * k)) * (Acsr @ b)  # b = (t/(s k)) A b, expmv.m:75 (mu = 0: no diagonal)
+        f = f + b
+        c2 = np.max(np.sum(np.abs(b), axis=1))  # the stop test's norms, expmv.m:79-80
+        nf = np.max(np.sum(np.abs(f), axis=1))
+        del c2, nf
+    t_term = (time.perf_counter() - t0) / k
+    est = calls * t_sel + terms * t_term
+    out["cpu_baseline"] = {
+        "value": 1.0 / est if est > 0 else None, "unit": "evals/s", "cores": 1, "kind": "port",
+        "algorithm": "the reference's: mc_trace + expmv (oracle/krylov_oracle.py restatement)",
+        "seconds_per_eval": round(est, 1), "select_taylor_degree_s": round(t_sel, 3),
+        "taylor_term_s": round(t_term, 4),
+        "sample": f"one select_taylor_degree call ({t_sel:.1f} s) and {k} Taylor terms on a 10-column "
+                  f"block ({t_term:.3f} s each), one thread (SciPy sparse @ dense), extrapolated to the "
+                  f"GPU run's {calls} expmv calls and {terms} Taylor terms"}
+    return out
 
 
 def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev, world, ref, n, nnz, A):

@@ -314,7 +314,10 @@ int kt_profile_busy(kt_context_t ctx, int kernel, double* busy_ms);
  * counted since context creation.  stat 1: fun_update runs (kt_fun_update,
  * kt_fun_and_grad_krylov_*) that took the dense fallback of fun_update.m:85-90,
  * since context creation.  stat 2: the projected size (basis columns) of the
- * last fun_update run on this context (n when it went dense). */
+ * last fun_update run on this context (n when it went dense).  stat 3: expmv
+ * calls (kt_expmv and mc_trace's expmv Afun), stat 4: the Taylor terms they
+ * executed (one A b product on the block each, expmv.m:75), since context
+ * creation. */
 int kt_context_stat(kt_context_t ctx, int stat, int64_t* value);
 
 #ifdef __cplusplus

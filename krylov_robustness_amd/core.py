@@ -70,7 +70,8 @@ class Context:
 
     def stat(self, which: int) -> int:
         """kt_context_stat: 0 y-form sweeps redone, 1 fun_update dense
-        fallbacks, 2 basis columns of the last fun_update."""
+        fallbacks, 2 basis columns of the last fun_update, 3 expmv calls,
+        4 Taylor terms those calls executed."""
         v = C.c_int64()
         _lib.check(_lib.load().kt_context_stat(self._h, int(which), C.byref(v)))
         return int(v.value)

@@ -207,6 +207,8 @@ struct kt_context_s {
     int64_t yform_redone = 0;  // y-form sweeps recomputed by the explicit sweep (guard)
     int64_t fu_dense = 0;      // fun_update calls that took the dense fallback (fun_update.m:85-90)
     int64_t fu_last_cols = 0;  // projected size of the last fun_update (n when dense)
+    int64_t expmv_calls = 0;   // expmv_device calls (kt_expmv and the expmv Afun of mc_trace)
+    int64_t expmv_terms = 0;   // Taylor terms those calls executed (one A b product each, expmv.m:75)
     int ky_flags = 8;   // KT_KY_FLAGS: y-form pass flags (8 = nontemporal store of y_{j+1}, +0.3 %)
     bool yform = true;  // KT_SLQ_YFORM=0: the hot path runs the explicit K1/K2 sweep
     void* blas = nullptr;  // rocblas_handle, created on first block-Krylov use

@@ -1432,11 +1432,20 @@ __global__ __launch_bounds__(256) void k_scatter_elems(int64_t count, const int6
 // active = 1 while the stage runs; every kernel of a term (the SpMM through
 // its skip flag, k_expmv_term, k_expmv_check) is a no-op once active = 0.
 // ---------------------------------------------------------------------------
+// term maxima of the fused expmv path: 64 slots per term, one 128-B line
+// each (workgroup b folds into slot b % 64), so same-address atomics stay few
+// (config 1: 340 workgroups, 31k at n = 1M)
+constexpr int kTermSlots = 64, kTermSlotStride = 16;
 struct ExpmvState {
     int active;
     int mv;
     double c1;
     double c1s[2];  // fused path: c1 of the check of term j in c1s[j & 1]
+    // fused path: term j's row-sum maxima of |b| and |f| in set j % 3, as
+    // the bit patterns of the (non-negative) doubles, so an unsigned atomic
+    // max is the exact fmax; term j zeroes set (j + 1) % 3 for the next
+    // term, k_expmv_begin set 1 for a stage's first term
+    unsigned long long term_max[3][kTermSlots][kTermSlotStride];
 };
 
 // stage start: c1 = norm(b, inf) from k_inf_norm partials; active = 1   (:73)
@@ -1452,6 +1461,10 @@ __global__ __launch_bounds__(256) void k_expmv_begin(const double* __restrict__ 
         st->c1 = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
         st->c1s[1] = st->c1;
         st->active = 1;
+    }
+    if (threadIdx.x < kTermSlots) {
+        st->term_max[1][threadIdx.x][0] = 0ull;
+        st->term_max[1][threadIdx.x][1] = 0ull;
     }
 }
 
@@ -1548,11 +1561,20 @@ __device__ __forceinline__ void expmv_row_update(int row, int p0, const double* 
 
 // One whole Taylor term in one launch (SpMM fused with the update and with
 // the previous term's stop test):
-//   the check of term k-1 (expmv.m:79-82) from that term's norm partials
-//   (pin, 2 x gridDim.x) and c1 = st->c1s[(k-1) & 1] -- stop: st->active = 0;
-//   otherwise c1s[k & 1] = c2 (every block stores the same value);
-//   bout = coef (A bin - mu bin), F = F + bout, and the partial maxima of the
-//   row sums of |bout| and |F| into pout; block 0 counts the term (mv).
+//   the check of term k-1 (expmv.m:79-82) from that term's maxima
+//   (the 64 slots of st->term_max[(k-1) % 3], read by wave 0) and
+//   c1 = st->c1s[(k-1) & 1] -- stop: st->active = 0; otherwise
+//   c1s[k & 1] = c2 (every block stores the same value);
+//   bout = coef (A bin - mu bin), F = F + bout, and the workgroup's maxima of
+//   the row sums of |bout| and |F| folded into slot blockIdx % 64 of
+//   st->term_max[k % 3] by one atomic max each (max is exact: any arrival
+//   order gives the same value); block 0 counts the term (mv) and zeroes set
+//   (k + 1) % 3.
+// Each workgroup reads 64 slots for the check, not the previous term's
+// 2 x gridDim.x partials: at n = 1M (31k workgroups) that all-to-all read was
+// 15 GB per term (8.3 ms per term on config 4's expmv Afun); one slot per
+// term instead serialised 62k same-address atomics (3.5 ms per term, and
+// config 1 13.2 -> 30.7 ms).
 // A small matrix makes this a chain of dependent memory latencies, so the
 // reads of the check and the gathers are issued before anything is decided
 // (only the writes wait for the decision), and no row is a long serial
@@ -1561,8 +1583,8 @@ __device__ __forceinline__ void expmv_row_update(int row, int p0, const double* 
 // ceil(n_med / 4) blocks one row of kMedThresh < degree <= long_thresh per
 // WAVE (16 row groups, 8 deep: one round trip), the rest one row of degree
 // <= kMedThresh per row group (8 deep).
-// bin / bout and pin / pout ping-pong between terms; columns nc..P-1 of the
-// blocks stay zero so the P-wide gathers read finite values.
+// bin / bout ping-pong between terms; columns nc..P-1 of the blocks stay zero
+// so the P-wide gathers read finite values.
 // waves per block of the per-term expmv kernel (a row longer than long_thresh
 // is one block's, its gather chain degree / (16 WAVES) deep).  8 waves were
 // measured slower than 4 on config 1 (trace_exp 18.1 vs 16.1 ms,
@@ -1571,15 +1593,24 @@ __device__ __forceinline__ void expmv_row_update(int row, int p0, const double* 
 #define KT_EXPMV_WAVES 4
 #endif
 constexpr int kExpmvWaves = KT_EXPMV_WAVES;
+// grids above this many workgroups take the SPLIT term kernel (config 1: 340
+// workgroups, fused; n = 1M: 31k, split)
+constexpr int kExpmvSplitBlocks = 1024;
 
-template <int P, int FLAGS>
+//
+// SPLIT (large grids, expmv_split_check): the check of term k-1 is not in
+// this kernel but in k_expmv_slot_check, launched after term k-1; every
+// workgroup reads st->active FIRST and a stopped term returns before its
+// gathers.  The fused form issues the gathers before the decision (latency
+// hiding on small matrices), which at n = 1M made each of the ~20 no-op terms
+// a stage queues ahead of its stop cost a full SpMM (300 us).
+template <int P, int FLAGS, bool SPLIT>
 __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
     const int* __restrict__ rp, const int* __restrict__ ci, const double* __restrict__ va, int n,
     const int* __restrict__ long_rows, int n_long, const int* __restrict__ med_rows, int n_med,
     int nc, int ld, double mu, double coef, double tol, int k, const double* __restrict__ bin,
-    double* __restrict__ bout, double* __restrict__ F, const double* __restrict__ pin,
-    double* __restrict__ pout, ExpmvState* st, int* hflag, int stage) {
-    constexpr int WAVES = kExpmvWaves, THREADS = 64 * WAVES;
+    double* __restrict__ bout, double* __restrict__ F, ExpmvState* st, int* hflag, int stage) {
+    constexpr int WAVES = kExpmvWaves;
     using G = GeoW<P, (P >= 2) ? 2 : 1>;                          // short rows
     using GL = GeoW<P, (P >= 4) ? 4 : (P >= 2) ? 2 : 1>;          // medium / long rows
     __shared__ double red[2][WAVES];
@@ -1587,19 +1618,20 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
     __shared__ int decide;  // 0 = skip (stopped), 1 = run
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int nb = (int)gridDim.x;
     const int med_blocks = (n_med + WAVES - 1) / WAVES;
     const int kind = ((int)blockIdx.x < n_long) ? 2 : ((int)blockIdx.x < n_long + med_blocks) ? 1 : 0;
-    // (1) reads of the check, consumed after the gathers
-    const int act = (threadIdx.x == 0) ? st->active : 0;
-    const double c1 = (k > 1) ? st->c1s[(k - 1) & 1] : 0.0;
-    double pb[4], pf[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int i = (int)threadIdx.x + u * THREADS;
-        const bool ok = k > 1 && i < nb;
-        pb[u] = ok ? pin[i] : 0.0;
-        pf[u] = ok ? pin[nb + i] : 0.0;
+    if constexpr (SPLIT) {
+        if (threadIdx.x == 0) decide = st->active;
+        __syncthreads();
+        if (!decide) return;
+    }
+    // (1) reads of the check (thread 0), consumed after the gathers
+    const int act = (!SPLIT && threadIdx.x == 0) ? st->active : 0;
+    const double c1 = (!SPLIT && k > 1) ? st->c1s[(k - 1) & 1] : 0.0;
+    unsigned long long pmb = 0ull, pmf = 0ull;
+    if (!SPLIT && wave == 0 && k > 1) {
+        pmb = st->term_max[(k - 1) % 3][lane][0];
+        pmf = st->term_max[(k - 1) % 3][lane][1];
     }
     // (2) the gathers of this term
     const int subL = lane % GL::LPR, grpL = lane / GL::LPR, p0L = subL * GL::VEC;
@@ -1645,34 +1677,18 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
 #pragma unroll
         for (int e = 0; e < GL::VEC; ++e) lred[wave][p0L + e] = sl[e];
     // (3) the check, block-uniform
-    double mb = 0.0, mf = 0.0;
+    if constexpr (!SPLIT) {
+    if (wave == 0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        mb = fmax(mb, pb[u]);
-        mf = fmax(mf, pf[u]);
-    }
-    for (int i = (int)threadIdx.x + 4 * THREADS; k > 1 && i < nb; i += THREADS) {  // grids above 4 THREADS blocks
-        mb = fmax(mb, pin[i]);
-        mf = fmax(mf, pin[nb + i]);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mb = fmax(mb, __shfl_xor(mb, o, 64));
-        mf = fmax(mf, __shfl_xor(mf, o, 64));
-    }
-    if (lane == 0) {
-        red[0][wave] = mb;
-        red[1][wave] = mf;
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long xb = __shfl_xor(pmb, o, 64), xf = __shfl_xor(pmf, o, 64);
+            pmb = xb > pmb ? xb : pmb;
+            pmf = xf > pmf ? xf : pmf;
+        }
     }
     if (threadIdx.x == 0) decide = act;
-    __syncthreads();
     if (threadIdx.x == 0 && act && k > 1) {
-        double c2 = red[0][0], nf = red[1][0];
-#pragma unroll
-        for (int w = 1; w < WAVES; ++w) {
-            c2 = fmax(c2, red[0][w]);
-            nf = fmax(nf, red[1][w]);
-        }
+        const double c2 = __longlong_as_double((long long)pmb), nf = __longlong_as_double((long long)pmf);
         if (c1 + c2 <= tol * nf) {
             st->active = 0;
             decide = 0;
@@ -1686,7 +1702,16 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
     }
     __syncthreads();
     if (!decide) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->mv += 1;
+    } else {
+        __syncthreads();  // lred (long rows) complete
+    }
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) st->mv += 1;
+        if (!SPLIT && threadIdx.x < kTermSlots) {  // the next term's set (last read by term k - 1)
+            st->term_max[(k + 1) % 3][threadIdx.x][0] = 0ull;
+            st->term_max[(k + 1) % 3][threadIdx.x][1] = 0ull;
+        }
+    }
     // (4) update, norm partials of this term
     double sb = 0.0, sf = 0.0;
     if (kind == 0) {
@@ -1715,14 +1740,12 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
             sf += __shfl_xor(sf, o, 64);
         }
     }
-    mb = sb;
-    mf = sf;
+    double mb = sb, mf = sf;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         mb = fmax(mb, __shfl_xor(mb, o, 64));
         mf = fmax(mf, __shfl_xor(mf, o, 64));
     }
-    __syncthreads();  // red reused
     if (lane == 0) {
         red[0][wave] = mb;
         red[1][wave] = mf;
@@ -1735,8 +1758,39 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
             x = fmax(x, red[0][w]);
             y = fmax(y, red[1][w]);
         }
-        pout[blockIdx.x] = x;
-        pout[gridDim.x + blockIdx.x] = y;
+        unsigned long long* slot = st->term_max[k % 3][blockIdx.x % kTermSlots];
+        __hip_atomic_fetch_max(slot, (unsigned long long)__double_as_longlong(x), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(slot + 1, (unsigned long long)__double_as_longlong(y), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// The check of term k (expmv.m:79-82) for the SPLIT term kernel, one wave:
+// c2 / nf = the maxima in the 64 slots of set k % 3, c1 = st->c1s[k & 1];
+// stop: active = 0 (and the host flag); else c1s[(k + 1) & 1] = c2.  Zeroes
+// set (k + 1) % 3 for term k + 1 (its last reader was the check of term k - 2).
+__global__ __launch_bounds__(64) void k_expmv_slot_check(ExpmvState* st, int k, double tol, int* hflag,
+                                                         int stage) {
+    const int lane = threadIdx.x;
+    st->term_max[(k + 1) % 3][lane][0] = 0ull;
+    st->term_max[(k + 1) % 3][lane][1] = 0ull;
+    if (!st->active) return;
+    unsigned long long mb = st->term_max[k % 3][lane][0], mf = st->term_max[k % 3][lane][1];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long xb = __shfl_xor(mb, o, 64), xf = __shfl_xor(mf, o, 64);
+        mb = xb > mb ? xb : mb;
+        mf = xf > mf ? xf : mf;
+    }
+    if (lane != 0) return;
+    const double c1 = st->c1s[k & 1];
+    const double c2 = __longlong_as_double((long long)mb), nf = __longlong_as_double((long long)mf);
+    if (c1 + c2 <= tol * nf) {
+        st->active = 0;
+        if (hflag) __hip_atomic_store(hflag, stage, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+        st->c1s[(k + 1) & 1] = c2;
     }
 }
 
@@ -2373,21 +2427,33 @@ int expmv_step_blocks(int n, int P, int n_long, int n_med, int waves) {
     return n_long + (n_med + waves - 1) / waves + (n + waves * gpw - 1) / (waves * gpw);
 }
 
+bool expmv_split_check(int n, int P, int n_long, int n_med) {
+    return expmv_step_blocks(n, P, n_long, n_med) > kExpmvSplitBlocks;
+}
+
+hipError_t launch_expmv_slot_check(void* state, int k, double tol, hipStream_t st, int* hflag, int stage) {
+    k_expmv_slot_check<<<1, 64, 0, st>>>(static_cast<ExpmvState*>(state), k, tol, hflag, stage);
+    return hipGetLastError();
+}
+
 hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_rows, int n_med, int nc,
                              int ld, double mu, double coef, double tol, int k, const double* bin,
-                             double* bout, double* F, const double* pin, double* pout, void* state,
-                             hipStream_t st, int* hflag, int stage) {
+                             double* bout, double* F, void* state, hipStream_t st, bool split, int* hflag,
+                             int stage) {
     const int grid = expmv_step_blocks(M.n, P, M.n_long, n_med);
     ExpmvState* s = static_cast<ExpmvState*>(state);
+#define KT_EXPMV_LAUNCH(PP, F_, SP)                                                                \
+    k_expmv_step<PP, F_, SP><<<grid, 64 * kExpmvWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, \
+                                                               M.n_long, med_rows, n_med, nc, ld, mu, \
+                                                               coef, tol, k, bin, bout, F, s, hflag, stage)
 #define KT_EXPMV_STEP(PP)                                                                          \
-    if (unit)                                                                                      \
-        k_expmv_step<PP, KF_UNIT><<<grid, 64 * kExpmvWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long,  \
-                                                        med_rows, n_med, nc, ld, mu, coef, tol, k,    \
-                                                        bin, bout, F, pin, pout, s, hflag, stage);   \
-    else                                                                                           \
-        k_expmv_step<PP, 0><<<grid, 64 * kExpmvWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long,        \
-                                                  med_rows, n_med, nc, ld, mu, coef, tol, k, bin,    \
-                                                  bout, F, pin, pout, s, hflag, stage);
+    if (unit) {                                                                                    \
+        if (split) KT_EXPMV_LAUNCH(PP, KF_UNIT, true);                                             \
+        else KT_EXPMV_LAUNCH(PP, KF_UNIT, false);                                                  \
+    } else {                                                                                       \
+        if (split) KT_EXPMV_LAUNCH(PP, 0, true);                                                   \
+        else KT_EXPMV_LAUNCH(PP, 0, false);                                                        \
+    }
     switch (P) {
     case 1: KT_EXPMV_STEP(1) break;
     case 2: KT_EXPMV_STEP(2) break;
@@ -2398,6 +2464,7 @@ hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_
     default: return hipErrorInvalidValue;
     }
 #undef KT_EXPMV_STEP
+#undef KT_EXPMV_LAUNCH
     return hipGetLastError();
 }
 

@@ -198,15 +198,19 @@ hipError_t launch_expmv_term(int n, int nc, double mu, double coef, const double
                              double* F, int ld, double* partial, const void* state, hipStream_t st);
 hipError_t launch_expmv_check(int n, const double* partial, double tol, void* state, hipStream_t st);
 // one fused launch per Taylor term k (P = pow2 >= nc, P <= 32, ld >= P): the
-// check of term k-1 (from pin), SpMM of the natural-order CSR (M), update,
-// norm partials of term k into pout (each 2 * expmv_step_blocks doubles)
+// check of term k-1, SpMM of the natural-order CSR (M), update, the maxima
+// of term k's row sums folded into the state (term_max slot k % 3)
 // waves: per block (0: the per-term kernel's; the persistent form uses 4)
 int expmv_step_blocks(int n, int P, int n_long, int n_med, int waves = 0);
+// the default form of launch_expmv_step for this shape (true: SPLIT, grids
+// above 1,024 workgroups); with split the host launches
+// launch_expmv_slot_check after every term but a stage's last
+bool expmv_split_check(int n, int P, int n_long, int n_med);
+hipError_t launch_expmv_slot_check(void* state, int k, double tol, hipStream_t st, int* hflag, int stage);
 hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_rows, int n_med, int nc,
                              int ld, double mu, double coef,
                              double tol, int k, const double* bin, double* bout, double* F,
-                             const double* pin, double* pout, void* state, hipStream_t st,
-                             int* hflag = nullptr, int stage = 0);
+                             void* state, hipStream_t st, bool split, int* hflag = nullptr, int stage = 0);
 // the whole expmv call (s stages x up to m terms, stop tests, f = eta f) in
 // ONE persistent launch of `grid` workgroups (capped so all are resident);
 // b0 / F hold the input block, b1 is scratch (n x ld each, zero padded);

@@ -205,6 +205,7 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
     const int64_t n = A->n;
     hipStream_t st = ctx->stream;
     Expmv r;
+    ctx->expmv_calls += 1;
     // shift + degree selection, cached per (A version, t, block width): the
     // reference recomputes them every call from the same inputs; the
     // selection's matrix products still count in mv, as expmv.m's mv does
@@ -404,17 +405,19 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
             }
         }
         r.mv += terms;
+        ctx->expmv_terms += terms;
         return r;
     }
     if (P <= 32 && ld >= P && !std::getenv("KT_EXPMV_UNFUSED")) {
         // One launch per term (k_expmv_step: the previous term's stop test,
-        // SpMM, update, norm partials); b and the partials ping-pong.
+        // SpMM, update, the term's norm maxima); b ping-pongs, the maxima
+        // rotate through three slots of the state.
         const DevCSR& M = natural_csr(A);
         const CsrView V{M.rowptr, M.col, M.val, (int)n, M.long_rows, M.n_long, A->long_thresh,
                         kSplitThresh, M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split};
-        const int nbs = expmv_step_blocks((int)n, P, M.n_long, M.n_med);
-        ctx->ws.norm_part.ensure(sizeof(double) * std::max(2 * nb, 4 * nbs));
-        part = ctx->ws.norm_part.as<double>();
+        // KT_EXPMV_SPLIT=0 / 1 forces the fused / split term form (read per call)
+        const char* spe = std::getenv("KT_EXPMV_SPLIT");
+        const bool split = spe ? spe[0] == '1' : expmv_split_check((int)n, P, M.n_long, M.n_med);
         // The launch that finds a stage's stop test satisfied also stores the
         // stage index into a coherent host flag; the host, which queues terms
         // only slightly ahead of the device here, stops queueing that stage's
@@ -435,9 +438,9 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
             double* nxt = Ab.col(0);
             for (int k = 1; k <= r.m; ++k) {
                 if (use_flag && k > 2 && __atomic_load_n(ctx->ws.expmv_stop.host, __ATOMIC_ACQUIRE) >= i) break;
-                KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu, t / ((double)r.s * k), tol, k, cur,
-                                         nxt, F, part + (size_t)((k - 1) & 1) * 2 * nbs,
-                                         part + (size_t)(k & 1) * 2 * nbs, state, st, hflag, i));
+                KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu,
+                                         t / ((double)r.s * k), tol, k, cur, nxt, F, state, st, split, hflag, i));
+                if (split && k < r.m) KT_HIP(launch_expmv_slot_check(state, k, tol, st, hflag, i));
                 std::swap(cur, nxt);
             }
             KT_HIP(launch_axpby((int)n, nc, eta, F, ld, 0.0, F, ld, st));  // f = eta f
@@ -447,6 +450,7 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
         KT_HIP(hipMemcpyAsync(hstate, state, sizeof(hstate), hipMemcpyDeviceToHost, st));
         KT_HIP(hipStreamSynchronize(st));
         r.mv += hstate[1];
+        ctx->expmv_terms += hstate[1];
         return r;
     }
     for (int i = 0; i < r.s; ++i) {
@@ -465,6 +469,7 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
     KT_HIP(hipMemcpyAsync(hstate, state, sizeof(hstate), hipMemcpyDeviceToHost, st));
     KT_HIP(hipStreamSynchronize(st));
     r.mv += hstate[1];
+    ctx->expmv_terms += hstate[1];
     return r;
 }
 

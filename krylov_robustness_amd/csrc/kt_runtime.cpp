@@ -499,8 +499,10 @@ int kt_profile_read(kt_context_t ctx, int kernel, int64_t* launches, double* tot
 
 int kt_context_stat(kt_context_t ctx, int stat, int64_t* value) {
     KT_GUARD_BEGIN
-    if (!ctx || !value || stat < 0 || stat > 2) fail(KT_ERR_ARG, "bad stat query");
-    *value = stat == 0 ? ctx->yform_redone : stat == 1 ? ctx->fu_dense : ctx->fu_last_cols;
+    if (!ctx || !value || stat < 0 || stat > 4) fail(KT_ERR_ARG, "bad stat query");
+    const int64_t v[5] = {ctx->yform_redone, ctx->fu_dense, ctx->fu_last_cols, ctx->expmv_calls,
+                          ctx->expmv_terms};
+    *value = v[stat];
     KT_GUARD_END
 }
 

@@ -50,6 +50,32 @@ def test_expmv_wide_block_and_unfused_form(kra, gpu_ctx, monkeypatch):
     np.testing.assert_allclose(Fu, Ff, rtol=1e-13, atol=1e-15 * np.abs(Ff).max())
 
 
+@pytest.mark.parametrize("graph", ["oregon_A6", "er100k"])
+def test_expmv_split_check_form(kra, gpu_ctx, monkeypatch, graph):
+    """Grids above 1,024 workgroups run the SPLIT term kernel (the stop test
+    in its own one-wave launch after each term, a stopped term returning
+    before its gathers) instead of the fused one.  On ER n = 100k (3,125
+    workgroups at 10 columns, split by default) and on oregon_A6 (340, fused
+    by default) both forms (KT_EXPMV_SPLIT=0 / 1) give the same F, s, m, mv
+    bit for bit, and agree with the oracle; the first column alone (P = 1:
+    391 / 43 workgroups) too."""
+    from krylov_robustness_amd import graphs
+    A = graphs.erdos_renyi(100_000, 500_000, seed=0) if graph == "er100k" else load_graph(graph)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    b = np.random.default_rng(7).normal(size=(A.shape[0], 10))
+    for B in (b, b[:, :1]):
+        outs = []
+        for v in ("0", "1"):
+            monkeypatch.setenv("KT_EXPMV_SPLIT", v)
+            outs.append(kra.expmv(1.0, D, B, ctx=gpu_ctx))
+        monkeypatch.delenv("KT_EXPMV_SPLIT")
+        assert tuple(outs[0][1:]) == tuple(outs[1][1:])
+        assert np.array_equal(outs[0][0], outs[1][0])
+        Fo, *ro = ko.expmv(1.0, A, B)
+        assert tuple(outs[0][1:]) == tuple(ro)
+        np.testing.assert_allclose(outs[0][0], Fo, rtol=1e-11, atol=1e-13 * np.abs(Fo).max())
+
+
 @pytest.mark.parametrize("name,loops", [("oregon_A6", False), ("oregon_A0", True), ("anaheim", False)])
 def test_expmv_persistent_launch_is_bit_identical(kra, gpu_ctx, monkeypatch, name, loops):
     """KT_EXPMV_PERSIST=1: the whole expmv call as ONE persistent launch
