@@ -412,12 +412,32 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
         // One launch per term (k_expmv_step: the previous term's stop test,
         // SpMM, update, the term's norm maxima); b ping-pongs, the maxima
         // rotate through three slots of the state.
-        const DevCSR& M = natural_csr(A);
+        // KT_EXPMV_HUB=1: run on the hubs-first CSR (as the Lanczos sweeps
+        // do): b and f are permuted into its row order on the way in and f
+        // back out; max row sums (the stop test) do not depend on the row
+        // order.  Read per call.
+        const char* hbe = std::getenv("KT_EXPMV_HUB");
+        const bool hub = hbe && hbe[0] == '1';
+        const DevCSR& M = hub ? hub_csr(A) : natural_csr(A);
         const CsrView V{M.rowptr, M.col, M.val, (int)n, M.long_rows, M.n_long, A->long_thresh,
                         kSplitThresh, M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split};
         // KT_EXPMV_SPLIT=0 / 1 forces the fused / split term form (read per call)
         const char* spe = std::getenv("KT_EXPMV_SPLIT");
         const bool split = spe ? spe[0] == '1' : expmv_split_check((int)n, P, M.n_long, M.n_med);
+        // KT_EXPMV_GS=1 (split form only): the term as a grid-stride launch of
+        // KT_EXPMV_GS_GRID (default 4 per CU) workgroups
+        const char* gse = std::getenv("KT_EXPMV_GS");
+        const bool gs = split && gse && gse[0] == '1';
+        const char* gge = std::getenv("KT_EXPMV_GS_GRID");
+        const int gs_grid = gge ? std::max(1, std::atoi(gge)) : 4 * ctx->num_cu;
+        double* Fout = F;
+        DevMat Fh;
+        if (hub) {
+            Fh.alloc(ctx, n, ld);
+            KT_HIP(launch_perm_rows((int)n, nc, M.perm, 1, Bsrc, ld, b.col(0), ld, st));
+            KT_HIP(launch_perm_rows((int)n, nc, M.perm, 1, Bsrc, ld, Fh.col(0), ld, st));
+            F = Fh.col(0);
+        }
         // The launch that finds a stage's stop test satisfied also stores the
         // stage index into a coherent host flag; the host, which queues terms
         // only slightly ahead of the device here, stops queueing that stage's
@@ -438,14 +458,20 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
             double* nxt = Ab.col(0);
             for (int k = 1; k <= r.m; ++k) {
                 if (use_flag && k > 2 && __atomic_load_n(ctx->ws.expmv_stop.host, __ATOMIC_ACQUIRE) >= i) break;
-                KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu,
-                                         t / ((double)r.s * k), tol, k, cur, nxt, F, state, st, split, hflag, i));
+                if (gs)
+                    KT_HIP(launch_expmv_step_gs(P, A->unit_values, gs_grid, V, M.med_rows, M.n_med, nc, ld, mu,
+                                                t / ((double)r.s * k), k, cur, nxt, F, state, st));
+                else
+                    KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu,
+                                             t / ((double)r.s * k), tol, k, cur, nxt, F, state, st, split, hflag,
+                                             i));
                 if (split && k < r.m) KT_HIP(launch_expmv_slot_check(state, k, tol, st, hflag, i));
                 std::swap(cur, nxt);
             }
             KT_HIP(launch_axpby((int)n, nc, eta, F, ld, 0.0, F, ld, st));  // f = eta f
             copy_cols(ctx, n, F, ld, b.col(0), ld, nc);                    // b = f
         }
+        if (hub) KT_HIP(launch_perm_rows((int)n, nc, M.perm, 0, F, ld, Fout, ld, st));
         int hstate[2] = {0, 0};  // {active, mv}
         KT_HIP(hipMemcpyAsync(hstate, state, sizeof(hstate), hipMemcpyDeviceToHost, st));
         KT_HIP(hipStreamSynchronize(st));
