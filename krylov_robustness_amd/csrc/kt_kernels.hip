@@ -2068,47 +2068,6 @@ __device__ __forceinline__ void expmv_vblock(const ExpmvRunArgs& a, int vb, int 
     mf = fmax(mf, sf);
 }
 
-// The SPLIT term as a grid-stride launch (KT_EXPMV_GS=1): gridDim.x
-// workgroups cycle over k_expmv_step's virtual blocks (expmv_vblock: the
-// same rows, gathers and arithmetic, so F equals the one-block-per-virtual-
-// block form bit for bit) and fold one pair of maxima each.
-template <int P, int FLAGS>
-__global__ __launch_bounds__(256) void k_expmv_step_gs(ExpmvRunArgs a, double coef, int k,
-                                                      const double* __restrict__ bin,
-                                                      double* __restrict__ bout, ExpmvState* st) {
-    __shared__ double lred[4][P];
-    __shared__ double red[2][4];
-    __shared__ int decide;
-    if (threadIdx.x == 0) decide = st->active;
-    __syncthreads();
-    if (!decide) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->mv += 1;
-    const int med_blocks = (a.n_med + 3) / 4;
-    double mb = 0.0, mf = 0.0;
-    for (int vb = blockIdx.x; vb < a.nvb; vb += gridDim.x)
-        expmv_vblock<P, FLAGS>(a, vb, med_blocks, coef, bin, bout, lred, mb, mf);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        mb = fmax(mb, __shfl_xor(mb, o, 64));
-        mf = fmax(mf, __shfl_xor(mf, o, 64));
-    }
-    if (lane == 0) {
-        red[0][wave] = mb;
-        red[1][wave] = mf;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const double x = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
-        const double y = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
-        unsigned long long* slot = st->term_max[k % 3][blockIdx.x % kTermSlots];
-        __hip_atomic_fetch_max(slot, (unsigned long long)__double_as_longlong(x), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_max(slot + 1, (unsigned long long)__double_as_longlong(y), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 template <int P, int FLAGS>
 __global__ __launch_bounds__(256) void k_expmv_run(ExpmvRunArgs a) {
     constexpr bool SC1 = (FLAGS & KF_LDSC1) != 0;
@@ -2506,31 +2465,6 @@ hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_
     }
 #undef KT_EXPMV_STEP
 #undef KT_EXPMV_LAUNCH
-    return hipGetLastError();
-}
-
-hipError_t launch_expmv_step_gs(int P, bool unit, int grid, const CsrView& M, const int* med_rows, int n_med,
-                                int nc, int ld, double mu, double coef, int k, const double* bin, double* bout,
-                                double* F, void* state, hipStream_t st) {
-    if (kExpmvWaves != 4) return hipErrorInvalidValue;  // expmv_vblock is the 4-wave virtual block
-    ExpmvRunArgs a{M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long, med_rows, n_med, nc, ld, mu, 0.0, 0.0, 0.0,
-                   0, 0, expmv_step_blocks(M.n, P, M.n_long, n_med, 4), nullptr, nullptr, F, nullptr,
-                   nullptr, nullptr};
-    ExpmvState* s = static_cast<ExpmvState*>(state);
-    const int g = std::max(1, std::min(grid, a.nvb));
-#define KT_EXPMV_GS(PP)                                                                            \
-    if (unit) k_expmv_step_gs<PP, KF_UNIT><<<g, 256, 0, st>>>(a, coef, k, bin, bout, s);           \
-    else k_expmv_step_gs<PP, 0><<<g, 256, 0, st>>>(a, coef, k, bin, bout, s);
-    switch (P) {
-    case 1: KT_EXPMV_GS(1) break;
-    case 2: KT_EXPMV_GS(2) break;
-    case 4: KT_EXPMV_GS(4) break;
-    case 8: KT_EXPMV_GS(8) break;
-    case 16: KT_EXPMV_GS(16) break;
-    case 32: KT_EXPMV_GS(32) break;
-    default: return hipErrorInvalidValue;
-    }
-#undef KT_EXPMV_GS
     return hipGetLastError();
 }
 

@@ -202,11 +202,6 @@ hipError_t launch_expmv_check(int n, const double* partial, double tol, void* st
 // of term k's row sums folded into the state (term_max slot k % 3)
 // waves: per block (0: the per-term kernel's; the persistent form uses 4)
 int expmv_step_blocks(int n, int P, int n_long, int n_med, int waves = 0);
-// the SPLIT term as a grid-stride launch of `grid` workgroups over the same
-// virtual blocks (bit-identical F; KT_EXPMV_GS)
-hipError_t launch_expmv_step_gs(int P, bool unit, int grid, const CsrView& M, const int* med_rows, int n_med,
-                                int nc, int ld, double mu, double coef, int k, const double* bin, double* bout,
-                                double* F, void* state, hipStream_t st);
 // the default form of launch_expmv_step for this shape (true: SPLIT, grids
 // above 1,024 workgroups); with split the host launches
 // launch_expmv_slot_check after every term but a stage's last

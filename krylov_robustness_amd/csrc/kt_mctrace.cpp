@@ -415,7 +415,10 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
         // KT_EXPMV_HUB=1: run on the hubs-first CSR (as the Lanczos sweeps
         // do): b and f are permuted into its row order on the way in and f
         // back out; max row sums (the stop test) do not depend on the row
-        // order.  Read per call.
+        // order.  Read per call.  Opt-in: 7 % faster at config 4, but a row's
+        // gathers then sum in another order than the reference's A*b, which
+        // moved one stage's stop by a term there (seed 1: 3,573 vs 3,575
+        // terms, profiles/r04/expmv_c4/variants.json).
         const char* hbe = std::getenv("KT_EXPMV_HUB");
         const bool hub = hbe && hbe[0] == '1';
         const DevCSR& M = hub ? hub_csr(A) : natural_csr(A);
@@ -424,12 +427,6 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
         // KT_EXPMV_SPLIT=0 / 1 forces the fused / split term form (read per call)
         const char* spe = std::getenv("KT_EXPMV_SPLIT");
         const bool split = spe ? spe[0] == '1' : expmv_split_check((int)n, P, M.n_long, M.n_med);
-        // KT_EXPMV_GS=1 (split form only): the term as a grid-stride launch of
-        // KT_EXPMV_GS_GRID (default 4 per CU) workgroups
-        const char* gse = std::getenv("KT_EXPMV_GS");
-        const bool gs = split && gse && gse[0] == '1';
-        const char* gge = std::getenv("KT_EXPMV_GS_GRID");
-        const int gs_grid = gge ? std::max(1, std::atoi(gge)) : 4 * ctx->num_cu;
         double* Fout = F;
         DevMat Fh;
         if (hub) {
@@ -458,13 +455,8 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
             double* nxt = Ab.col(0);
             for (int k = 1; k <= r.m; ++k) {
                 if (use_flag && k > 2 && __atomic_load_n(ctx->ws.expmv_stop.host, __ATOMIC_ACQUIRE) >= i) break;
-                if (gs)
-                    KT_HIP(launch_expmv_step_gs(P, A->unit_values, gs_grid, V, M.med_rows, M.n_med, nc, ld, mu,
-                                                t / ((double)r.s * k), k, cur, nxt, F, state, st));
-                else
-                    KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu,
-                                             t / ((double)r.s * k), tol, k, cur, nxt, F, state, st, split, hflag,
-                                             i));
+                KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu,
+                                         t / ((double)r.s * k), tol, k, cur, nxt, F, state, st, split, hflag, i));
                 if (split && k < r.m) KT_HIP(launch_expmv_slot_check(state, k, tol, st, hflag, i));
                 std::swap(cur, nxt);
             }

@@ -59,9 +59,8 @@ def test_expmv_split_check_form(kra, gpu_ctx, monkeypatch, graph):
     by default) both forms (KT_EXPMV_SPLIT=0 / 1) give the same F, s, m, mv
     bit for bit, and agree with the oracle; the first column alone (P = 1:
     391 / 43 workgroups) too.  Both row orders (KT_EXPMV_HUB: natural CSR or
-    the hubs-first CSR that large grids use) agree with the oracle (equal s,
-    m, mv).  The split term as a grid-stride launch (KT_EXPMV_GS=1, grids of
-    1,024 and 7 workgroups) is bit-identical as well."""
+    the opt-in hubs-first CSR) agree with the oracle (equal s,
+    m, mv)."""
     from krylov_robustness_amd import graphs
     A = graphs.erdos_renyi(100_000, 500_000, seed=0) if graph == "er100k" else load_graph(graph)
     D = kra.DeviceMatrix(A, gpu_ctx)
@@ -71,12 +70,6 @@ def test_expmv_split_check_form(kra, gpu_ctx, monkeypatch, graph):
         for v in ("0", "1"):
             monkeypatch.setenv("KT_EXPMV_SPLIT", v)
             outs.append(kra.expmv(1.0, D, B, ctx=gpu_ctx))
-        monkeypatch.setenv("KT_EXPMV_GS", "1")  # the split term as a grid-stride launch
-        for grid in ("1024", "7"):
-            monkeypatch.setenv("KT_EXPMV_GS_GRID", grid)
-            outs.append(kra.expmv(1.0, D, B, ctx=gpu_ctx))
-        monkeypatch.delenv("KT_EXPMV_GS")
-        monkeypatch.delenv("KT_EXPMV_GS_GRID")
         monkeypatch.delenv("KT_EXPMV_SPLIT")
         for o in outs[1:]:
             assert tuple(outs[0][1:]) == tuple(o[1:])
@@ -84,7 +77,7 @@ def test_expmv_split_check_form(kra, gpu_ctx, monkeypatch, graph):
         Fo, *ro = ko.expmv(1.0, A, B)
         assert tuple(outs[0][1:]) == tuple(ro)
         np.testing.assert_allclose(outs[0][0], Fo, rtol=1e-11, atol=1e-13 * np.abs(Fo).max())
-        # the other row order (hubs-first CSR by default on large grids)
+        # the other row order (KT_EXPMV_HUB=1: the hubs-first CSR)
         for v in ("0", "1"):
             monkeypatch.setenv("KT_EXPMV_HUB", v)
             Fh, *rh = kra.expmv(1.0, D, B, ctx=gpu_ctx)
