@@ -1132,7 +1132,9 @@ __global__ __launch_bounds__(256) void k_coef_cgs2(const double* __restrict__ pa
 
 // ---------------------------------------------------------------------------
 // K2: u_next = y - c0 s_prev u_prev - c1 s_cur u_cur (in place over u_prev);
-// partial slabs [3][P][grid]: ||u_next||^2, y.u_next, u_cur.u_next.
+// partial slabs [3][P][grid]: ||u_next||^2, y.u_next, u_cur.u_next.  rec
+// (optional): u_next's first bcols columns also stored to rec[row * bcols + c]
+// (the sweep's basis slot of the next step, kt_slq.cpp).
 // Pure streaming: rows are contiguous, so lanes cover 16 B each.
 // ---------------------------------------------------------------------------
 
@@ -1141,7 +1143,7 @@ __global__ __launch_bounds__(BLOCK) void k_update(
     int n, const double* __restrict__ y, double* __restrict__ uprev,
     const double* __restrict__ ucur, const double* __restrict__ scale_cur,
     const double* __restrict__ scale_prev, const double* __restrict__ coef, int first,
-    double* __restrict__ partial) {
+    double* __restrict__ partial, double* __restrict__ rec, int bcols) {
     using G = Geo<P>;
     using V = VecT<G::VEC>;
     constexpr int WAVES = BLOCK / 64;
@@ -1178,6 +1180,11 @@ __global__ __launch_bounds__(BLOCK) void k_update(
             cu[e] = fma(V::get(cv, e), u, cu[e]);
         }
         V::store(uprev + off, o);
+        if (rec && p0 < bcols) {
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e)
+                if (p0 + e < bcols) rec[(int64_t)row * bcols + p0 + e] = op[e];
+        }
     }
 #pragma unroll
     for (int o = G::LPR; o < 64; o <<= 1)
@@ -1265,10 +1272,11 @@ __global__ __launch_bounds__(192) void k_ycoef(const double* __restrict__ partia
 // ---------------------------------------------------------------------------
 // Small streaming kernels for the Afun paths (mc_trace.m / expmv.m).
 // ---------------------------------------------------------------------------
-// Y[r, c] = sum_j U[r, j*P + c] * W[j*P + c]   (f(A)x = ||x|| V f(T) e1)
+// Y[r, c] = sum_j U[r * ldu + j * sstride + c] * W[j*P + c]
+// (f(A)x = ||x|| V f(T) e1; slot j of the basis at U + j * sstride)
 __global__ __launch_bounds__(256) void k_weighted_sum(int n, int m, int P, int nc,
                                                       const double* __restrict__ U, int ldu,
-                                                      const double* __restrict__ W,
+                                                      int64_t sstride, const double* __restrict__ W,
                                                       double* __restrict__ Y, int ldy) {
     const int64_t total = (int64_t)n * nc;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
@@ -1276,7 +1284,7 @@ __global__ __launch_bounds__(256) void k_weighted_sum(int n, int m, int P, int n
         const int64_t r = t / nc;
         const int c = (int)(t % nc);
         double s = 0.0;
-        for (int j = 0; j < m; ++j) s = fma(U[r * ldu + (int64_t)j * P + c], W[j * P + c], s);
+        for (int j = 0; j < m; ++j) s = fma(U[r * ldu + (int64_t)j * sstride + c], W[j * P + c], s);
         Y[r * ldy + c] = s;
     }
 }
@@ -2264,14 +2272,15 @@ hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, c
 
 hipError_t launch_update(int P, int grid, int n, const double* y, double* uprev,
                          const double* ucur, const double* sc, const double* sp,
-                         const double* coef, int first, double* partial, hipStream_t st, bool nt) {
+                         const double* coef, int first, double* partial, hipStream_t st, bool nt,
+                         double* rec, int bcols) {
     return dispatch_p(P, [&](auto c) {
         if (nt)
-            k_update<decltype(c)::value, kBlock, true><<<grid, kBlock, 0, st>>>(n, y, uprev, ucur, sc,
-                                                                                sp, coef, first, partial);
+            k_update<decltype(c)::value, kBlock, true><<<grid, kBlock, 0, st>>>(
+                n, y, uprev, ucur, sc, sp, coef, first, partial, rec, bcols);
         else
-            k_update<decltype(c)::value, kBlock, false><<<grid, kBlock, 0, st>>>(n, y, uprev, ucur, sc,
-                                                                                 sp, coef, first, partial);
+            k_update<decltype(c)::value, kBlock, false><<<grid, kBlock, 0, st>>>(
+                n, y, uprev, ucur, sc, sp, coef, first, partial, rec, bcols);
     });
 }
 
@@ -2368,9 +2377,9 @@ static int stream_grid(int64_t total) {
     return g < 1 ? 1 : (int)g;
 }
 
-hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int ldu,
+hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int ldu, int64_t sstride,
                                const double* W, double* Y, int ldy, hipStream_t st) {
-    k_weighted_sum<<<stream_grid((int64_t)n * nc), 256, 0, st>>>(n, m, P, nc, U, ldu, W, Y, ldy);
+    k_weighted_sum<<<stream_grid((int64_t)n * nc), 256, 0, st>>>(n, m, P, nc, U, ldu, sstride, W, Y, ldy);
     return hipGetLastError();
 }
 

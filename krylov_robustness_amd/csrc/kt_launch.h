@@ -60,10 +60,11 @@ hipError_t launch_spmm_block(int P, int flags, int grid, const CsrView& M, const
 hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, const double* k2s,
                             const double* sc, const double* sp, double* coef, double* t_alpha,
                             double* t_up, hipStream_t st);
+// rec (optional): u_next's first bcols columns also to rec[row * bcols + c]
 hipError_t launch_update(int P, int grid, int n, const double* y, double* uprev,
                          const double* ucur, const double* sc, const double* sp,
                          const double* coef, int first, double* partial, hipStream_t st,
-                         bool nt = false);
+                         bool nt = false, double* rec = nullptr, int bcols = 0);
 hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, double* scale_next,
                        double* t_low, hipStream_t st);
 // y-form probe Lanczos (one pass per step) and its per-probe coefficients.
@@ -115,7 +116,8 @@ hipError_t launch_gather_elems(int64_t count, const double* D, const int64_t* of
 // out (nr x cols, column-major) = rows[r] of the row-major block D (leading dimension ldd)
 hipError_t launch_gather_rows(int nr, int cols, const double* D, int ldd, const int64_t* rows, double* out,
                               hipStream_t st);
-hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int ldu,
+// Y[r, c] = sum_j U[r * ldu + j * sstride + c] W[j * P + c]
+hipError_t launch_weighted_sum(int n, int m, int P, int nc, const double* U, int ldu, int64_t sstride,
                                const double* W, double* Y, int ldy, hipStream_t st);
 // dst[r] = src[perm[r]] (gather != 0) or dst[perm[r]] = src[r], rows of `cols` doubles
 hipError_t launch_perm_rows(int n, int cols, const int* perm, int gather, const double* src, int lds,

@@ -102,12 +102,16 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
         hist_dev = &ctx->ws.hist;
         hist_dev->ensure(sizeof(double) * (size_t)m * P);
     }
+    // basis slot j (u_j's first bcols columns, n x bcols row-major) at
+    // bbase + j n bcols: slot 0 copied from the start block, slot j + 1
+    // stored by step j's K2 as it forms u_{j+1} (no copy pass per step)
+    double* bbase = basis ? basis->col(0) : nullptr;
     for (int j = 0; j < m; ++j) {
         const int first = (j == 0);
-        if (basis) {  // record u_j (its first bcols columns) and s_j (v_j = s_j u_j)
-            KT_HIP(hipMemcpy2DAsync(basis->col(j * bcols), sizeof(double) * basis->ld, ucur,
-                                    sizeof(double) * P, sizeof(double) * bcols, (size_t)n,
-                                    hipMemcpyDeviceToDevice, st));
+        if (basis) {  // record s_j (v_j = s_j u_j); u_0 into slot 0
+            if (first)
+                KT_HIP(hipMemcpy2DAsync(bbase, sizeof(double) * bcols, ucur, sizeof(double) * P,
+                                        sizeof(double) * bcols, (size_t)n, hipMemcpyDeviceToDevice, st));
             KT_HIP(hipMemcpyAsync(hist_dev->as<double>() + (size_t)j * P, sc, sizeof(double) * P,
                                   hipMemcpyDeviceToDevice, st));
         }
@@ -119,8 +123,9 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
         KT_HIP(launch_coef_cgs2(P, part1, grid1, first, k2s, sc, sp, coef,
                                 trec + (size_t)(0 * m + j) * P, trec + (size_t)(1 * m + j) * P, st));
         prof_begin(ctx, PROF_UPDATE, st);
+        double* rec = (basis && j + 1 < m) ? bbase + (size_t)(j + 1) * n * bcols : nullptr;
         KT_HIP(launch_update(P, grid, n, w.Y.as<double>(), uprev, ucur, sc, sp, coef, first, part2,
-                             st, ctx->k2_nt));
+                             st, ctx->k2_nt, rec, bcols));
         prof_end(ctx, PROF_UPDATE, st);
         KT_HIP(launch_norm(P, part2, grid, k2s, sn, trec + (size_t)(2 * m + j) * P, st));
         std::swap(ucur, uprev);  // uprev now holds u_{j+1}
@@ -297,8 +302,8 @@ void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, 
         DevMat basis;
         std::vector<double> hist;
         // the basis keeps only the nyc columns whose f(A) x is wanted (slot j
-        // = columns j*nyc .. j*nyc + nyc - 1): a 30-column sweep with 10 such
-        // columns copies and re-reads a third of the bytes
+        // = an n x nyc block at basis.col(0) + j n nyc): a 30-column sweep
+        // with 10 such columns stores and re-reads a third of the bytes
         if (nyc) basis.alloc(ctx, n, m * nyc, false);  // every slot is written by the sweep
         lanczos_sweep(A, M, P, m, 0, 0, Xs + c0, ldxs, nc, norms2.data() + c0, rec.data(),
                       nyc ? &basis : nullptr, nyc ? &hist : nullptr, 0, nyc);
@@ -333,8 +338,8 @@ void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, 
             dw.ensure(sizeof(double) * W.size());
             KT_HIP(hipMemcpyAsync(dw.ptr, W.data(), sizeof(double) * W.size(), hipMemcpyHostToDevice,
                                   ctx->stream));
-            KT_HIP(launch_weighted_sum((int)n, m, nyc, nyc, basis.col(0), basis.ld, dw.as<double>(),
-                                       Ys + c0, ldys, ctx->stream));
+            KT_HIP(launch_weighted_sum((int)n, m, nyc, nyc, basis.col(0), nyc, (int64_t)n * nyc,
+                                       dw.as<double>(), Ys + c0, ldys, ctx->stream));
             KT_HIP(hipStreamSynchronize(ctx->stream));
         }
     }

@@ -10,6 +10,8 @@ int slq_auto_block(int64_t n, int64_t nprobes);
 // One sweep of P independent single-vector Lanczos runs (see kt_slq.cpp).
 // lane 0 runs on ctx->stream with ws.sweep[0]; lane l > 0 on
 // ctx->aux_stream[l-1] with ws.sweep[l] (independent sweeps overlap).
+// basis (optional, >= n m bcols doubles): slot j = u_j's first bcols columns
+// as an n x bcols row-major block at basis->col(0) + j n bcols.
 void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base,
                    const double* x, int ldx, int ncols, const double* norms2, double* rec_host,
                    DevMat* basis, std::vector<double>* scale_hist, int lane = 0, int bcols = 0);
