@@ -15,8 +15,9 @@ Tolerance rule (stated once, applied to every case):
     the reference algorithm's own error or its stopping tolerance:
     |f - f_exact| <= max(tol_f, |f_o - f_exact|), with tol_f = tol f(normest)
     the tolerance fun_and_grad_krylov_fun.m:65 hands to trace_fun_update and
-    f_exact from dense eigvalsh.  At least 36 of the 40 cases must take the
-    first branch (measured: 38; offset 60 takes the second for both funs).
+    f_exact from dense eigvalsh.  At least 38 of the 40 cases must take the
+    first branch: the measured count, offset 60 taking the second for both
+    funs (the slack of two cases that round 3 allowed is gone).
 The sweep also shows the reference algorithm's own inaccuracy: the oracle is
 further than tol_f from the exact objective in 4 of the 40 cases."""
 import json
@@ -57,4 +58,4 @@ def test_fun_and_grad_fun_omega_sweep(gpu_ctx, sweep):
             else:
                 report.append((fun, r["offset"], abs(f - f_o), abs(f - f_x), abs(f_o - f_x)))
                 assert abs(f - f_x) <= max(tol_f, abs(f_o - f_x)), (fun, r["offset"], f, f_o, f_x)
-    assert rounding >= 36, report
+    assert rounding >= 38, report
