@@ -1,6 +1,8 @@
 """Exact spectrum identities for config 3's graph (Hawaii LCC, n = 21,774):
-tr(sinh(A)), tr(cosh(A)), tr(exp(A)) from a dense eigvalsh (a few minutes, a
-~4 GB matrix) -> hawaii_values.json.  Build container only."""
+tr(sinh(A)), tr(cosh(A)), tr(exp(A)) and the squared Frobenius norms
+sum f(lambda)^2 (the bound 2 ||f(A)||_F^2 / N on a Rademacher Hutchinson
+estimate's variance) from a dense eigvalsh (a few minutes, a ~4 GB matrix)
+-> hawaii_values.json.  Build container only."""
 import json
 import os
 import sys
@@ -17,7 +19,9 @@ A = load_graph("hawaii")
 d = np.linalg.eigvalsh(A.toarray())
 rec = {"n": int(A.shape[0]), "nnz": int(A.nnz), "lambda_max": float(d.max()),
        "exact_tr_exp": float(np.sum(np.exp(d))), "exact_tr_sinh": float(np.sum(np.sinh(d))),
-       "exact_tr_cosh": float(np.sum(np.cosh(d))), "seconds": time.time() - t}
+       "exact_tr_cosh": float(np.sum(np.cosh(d))),
+       "frob2_sinh": float(np.sum(np.sinh(d) ** 2)), "frob2_cosh": float(np.sum(np.cosh(d) ** 2)),
+       "frob2_exp": float(np.sum(np.exp(d) ** 2)), "seconds": time.time() - t}
 with open(os.path.join(HERE, "hawaii_values.json"), "w") as f:
     json.dump(rec, f, indent=1)
 print(rec)

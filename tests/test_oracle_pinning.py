@@ -199,3 +199,26 @@ def test_expmv_matches_scipy_expm_multiply(name):
     ref = expm_multiply(A.tocsc(), b)
     assert np.max(np.abs(f - ref)) / np.max(np.abs(ref)) < 1e-12
     assert s >= 1 and 1 <= m <= 55 and mv >= s * 1
+
+
+def test_config3_fixture_estimates_within_spectral_bounds():
+    """The config-3 fixture's normalisers (tests/golden/config3_values.json,
+    the oracle's SLQ over 256 probes and its mc_trace) against the spectrum
+    of Hawaii (hawaii_values.json, dense eigvalsh): each Rademacher
+    Hutchinson estimate over N probes has sigma <= sqrt(2 ||f(A)||_F^2 / N),
+    and mc_trace's error is that of its last round's 10 G probes.  The
+    fixture's Frobenius norms are pinned by cosh^2 - sinh^2 = 1 summed over
+    the n eigenvalues."""
+    import json
+    import os
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "hawaii_values.json")) as f:
+        hv = json.load(f)
+    with open(os.path.join(GOLDEN, "config3_values.json")) as f:
+        c3 = json.load(f)
+    assert hv["frob2_cosh"] - hv["frob2_sinh"] == pytest.approx(hv["n"], rel=1e-9)
+    assert hv["exact_tr_sinh"] == pytest.approx(c3["exact_tr_sinh"], rel=1e-12)
+    exact, frob2 = c3["exact_tr_sinh"], hv["frob2_sinh"]
+    N = c3["slq_sinh"]["probes"]
+    assert abs(c3["slq_sinh"]["estimate"] - exact) <= 4 * math.sqrt(2 * frob2 / N)
+    assert abs(c3["mc_trace_lanczos_sinh"]["tr"] - exact) <= 4 * math.sqrt(2 * frob2 / 10)
