@@ -1612,8 +1612,11 @@ constexpr int kExpmvSplitBlocks = 1024;
 // gathers.  The fused form issues the gathers before the decision (latency
 // hiding on small matrices), which at n = 1M made each of the ~20 no-op terms
 // a stage queues ahead of its stop cost a full SpMM (300 us).
+// The split form is compiled for 6 waves per SIMD (80 VGPRs, 2 spilled: its
+// own-row loads wait until after the gathers); the fused form keeps the
+// compiler's choice (it would spill ~100 registers at that bound).
 template <int P, int FLAGS, bool SPLIT>
-__global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
+__global__ __launch_bounds__(64 * kExpmvWaves, SPLIT ? 6 : 1) void k_expmv_step(
     const int* __restrict__ rp, const int* __restrict__ ci, const double* __restrict__ va, int n,
     const int* __restrict__ long_rows, int n_long, const int* __restrict__ med_rows, int n_med,
     int nc, int ld, double mu, double coef, double tol, int k, const double* __restrict__ bin,
@@ -1653,14 +1656,14 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
     bool mine = false;  // this lane holds a finished row (of its row class)
     if (kind == 2) {
         row = long_rows[blockIdx.x];
-        if (wave == 0 && grpL == 0) expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
+        if (!SPLIT && wave == 0 && grpL == 0) expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
         row_gather8<P, FLAGS, GL>(rp[row] + wave * GL::GPW + grpL, rp[row + 1], WAVES * GL::GPW, p0L, ci,
                                   va, bin, sl, ld);
     } else if (kind == 1) {
         const int mi = ((int)blockIdx.x - n_long) * WAVES + wave;
         if (mi < n_med) {
             row = med_rows[mi];
-            if (grpL == 0) expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
+            if (!SPLIT && grpL == 0) expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
             row_gather8<P, FLAGS, GL>(rp[row] + grpL, rp[row + 1], GL::GPW, p0L, ci, va, bin, sl, ld);
             mine = grpL == 0;
         }
@@ -1669,7 +1672,7 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
         if (row < n) {
             const int beg = rp[row], end = rp[row + 1];
             if (end - beg <= kMedThresh) {
-                expmv_row_prefetch<G::VEC>(row, p0, nc, ld, mu, bin, F, fo, bo);
+                if (!SPLIT) expmv_row_prefetch<G::VEC>(row, p0, nc, ld, mu, bin, F, fo, bo);
                 row_gather8<P, FLAGS, G>(beg, end, 1, p0, ci, va, bin, s, ld);
                 mine = true;
             }
@@ -1723,7 +1726,11 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
     // (4) update, norm partials of this term
     double sb = 0.0, sf = 0.0;
     if (kind == 0) {
-        if (mine) expmv_row_update<G::VEC>(row, p0, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+        if (mine) {
+            // SPLIT (large grids): the row's own F, b after the gathers (fewer live registers)
+            if constexpr (SPLIT) expmv_row_prefetch<G::VEC>(row, p0, nc, ld, mu, bin, F, fo, bo);
+            expmv_row_update<G::VEC>(row, p0, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+        }
 #pragma unroll
         for (int o = 1; o < G::LPR; o <<= 1) {
             sb += __shfl_xor(sb, o, 64);
@@ -1741,7 +1748,10 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
             }
             mine = true;
         }
-        if (mine) expmv_row_update<GL::VEC>(row, p0L, sl, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+        if (mine) {
+            if constexpr (SPLIT) expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
+            expmv_row_update<GL::VEC>(row, p0L, sl, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+        }
 #pragma unroll
         for (int o = 1; o < GL::LPR; o <<= 1) {
             sb += __shfl_xor(sb, o, 64);
