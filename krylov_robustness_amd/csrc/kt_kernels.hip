@@ -1611,12 +1611,12 @@ constexpr int kExpmvSplitBlocks = 1024;
 // workgroup reads st->active FIRST and a stopped term returns before its
 // gathers.  The fused form issues the gathers before the decision (latency
 // hiding on small matrices), which at n = 1M made each of the ~20 no-op terms
-// a stage queues ahead of its stop cost a full SpMM (300 us).
-// The split form is compiled for 6 waves per SIMD (80 VGPRs, 2 spilled: its
-// own-row loads wait until after the gathers); the fused form keeps the
-// compiler's choice (it would spill ~100 registers at that bound).
+// a stage queues ahead of its stop cost a full SpMM (300 us).  The split form
+// also loads a row's own F and b after its gathers, not before (94 instead of
+// 124 VGPRs; config-4 expmv 6 % faster; compiled for 6 waves per SIMD at 80
+// VGPRs it measured no further gain).
 template <int P, int FLAGS, bool SPLIT>
-__global__ __launch_bounds__(64 * kExpmvWaves, SPLIT ? 6 : 1) void k_expmv_step(
+__global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
     const int* __restrict__ rp, const int* __restrict__ ci, const double* __restrict__ va, int n,
     const int* __restrict__ long_rows, int n_long, const int* __restrict__ med_rows, int n_med,
     int nc, int ld, double mu, double coef, double tol, int k, const double* __restrict__ bin,
