@@ -448,16 +448,36 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
             __atomic_store_n(ctx->ws.expmv_stop.host, -1, __ATOMIC_RELEASE);
             hflag = ctx->ws.expmv_stop.dev;
         }
+        // Split form (large grids, terms of ~0.4 ms): the host keeps at most
+        // KT_EXPMV_AHEAD (default 3; 0 = no limit) terms queued past the last
+        // finished one, so it sees a stage's stop flag before it has queued
+        // the stage's remaining terms (each a launch that returns at once,
+        // ~19 us with its check; ~2,000 of them per config-4 trace_exp).
+        const char* ae = std::getenv("KT_EXPMV_AHEAD");
+        const int ahead = (split && use_flag) ? (ae ? std::max(0, std::atoi(ae)) : 3) : 0;
+        std::vector<hipEvent_t> ring(ahead, nullptr);
+        for (auto& e : ring) KT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        struct RingGuard {
+            std::vector<hipEvent_t>& r;
+            ~RingGuard() {
+                for (hipEvent_t e : r)
+                    if (e) (void)hipEventDestroy(e);
+            }
+        } ring_guard{ring};
+        int64_t queued = 0;
         for (int i = 0; i < r.s; ++i) {
             KT_HIP(launch_inf_norm((int)n, nc, b.col(0), ld, part, st));   // c1 = norm(b, inf)
             KT_HIP(launch_expmv_begin(part, nb, state, st));
             double* cur = b.col(0);
             double* nxt = Ab.col(0);
             for (int k = 1; k <= r.m; ++k) {
+                if (ahead && queued >= ahead) KT_HIP(hipEventSynchronize(ring[queued % ahead]));
                 if (use_flag && k > 2 && __atomic_load_n(ctx->ws.expmv_stop.host, __ATOMIC_ACQUIRE) >= i) break;
                 KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu,
                                          t / ((double)r.s * k), tol, k, cur, nxt, F, state, st, split, hflag, i));
                 if (split && k < r.m) KT_HIP(launch_expmv_slot_check(state, k, tol, st, hflag, i));
+                if (ahead) KT_HIP(hipEventRecord(ring[queued % ahead], st));
+                ++queued;
                 std::swap(cur, nxt);
             }
             KT_HIP(launch_axpby((int)n, nc, eta, F, ld, 0.0, F, ld, st));  // f = eta f
