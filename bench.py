@@ -520,6 +520,7 @@ def _reference_composition(kra, D, ctx, A, ref, budget_s):
     t_sel = time.perf_counter() - t0
     f = b.copy()
     k = 0
+    ratio = 0.0  # the stop test's c2 / norm(f, inf), kept so the norms are used
     t0 = time.perf_counter()
     while k < 200 and (k == 0 or time.perf_counter() - t0 < budget_s):
         k += 1
@@ -527,14 +528,14 @@ def _reference_composition(kra, D, ctx, A, ref, budget_s):
         f = f + b
         c2 = np.max(np.sum(np.abs(b), axis=1))  # the stop test's norms, expmv.m:79-80
         nf = np.max(np.sum(np.abs(f), axis=1))
-        del c2, nf
+        ratio = c2 / nf if nf > 0 else ratio
     t_term = (time.perf_counter() - t0) / k
     est = calls * t_sel + terms * t_term
     out["cpu_baseline"] = {
         "value": 1.0 / est if est > 0 else None, "unit": "evals/s", "cores": 1, "kind": "port",
         "algorithm": "the reference's: mc_trace + expmv (oracle/krylov_oracle.py restatement)",
         "seconds_per_eval": round(est, 1), "select_taylor_degree_s": round(t_sel, 3),
-        "taylor_term_s": round(t_term, 4),
+        "taylor_term_s": round(t_term, 4), "sample_last_c2_over_normf": ratio,
         "sample": f"one select_taylor_degree call ({t_sel:.1f} s) and {k} Taylor terms on a 10-column "
                   f"block ({t_term:.3f} s each), one thread (SciPy sparse @ dense), extrapolated to the "
                   f"GPU run's {calls} expmv calls and {terms} Taylor terms"}
