@@ -53,7 +53,11 @@ void prof_collect(kt_context_s* ctx, const size_t* upto, bool wait) {
         ProfSlot& s = ctx->prof[k];
         const size_t end = upto ? std::min(upto[k], s.used) : s.used;
         if (end < s.done + 2) continue;
-        if (wait) KT_HIP(hipEventSynchronize(s.ev[end - 1]));
+        // the batch's events come from several sweep lanes (streams): the one
+        // recorded last by the host need not complete last, so wait on each
+        // (a completed event returns at once)
+        if (wait)
+            for (size_t i = s.done; i < end; ++i) KT_HIP(hipEventSynchronize(s.ev[i]));
         std::vector<std::pair<double, double>> iv;  // relative to the batch's first event
         for (size_t i = s.done; i + 1 < end; i += 2) {
             float ms = 0.f, a = 0.f, b = 0.f;
