@@ -227,8 +227,46 @@ def _pooled(sums, N):
     return mu, (math.sqrt(m2 / (N * K - 1) / (N * K)) if N * K > 1 else None)
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def self_launch_cmd(nproc, argv, port):
+    """The torchrun command bench.py runs as a child when asked for --gpus N
+    > 1 without a torchrun environment: N ranks, one per GPU, same flags."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def launch_guard(args, env=os.environ):
+    """Before anything touches a GPU.  Returns None to run in this process,
+    or the argv of a torchrun child that runs the N ranks:
+      * no torchrun environment and --gpus N > 1: launch N ranks as a CHILD
+        process (never exec: this process then only relays its exit status);
+      * under torchrun: WORLD_SIZE must equal --gpus (a line that says N GPUs
+        must have run on N ranks)."""
+    if "WORLD_SIZE" not in env:
+        if args.gpus > 1:
+            return self_launch_cmd(args.gpus, sys.argv[1:], _free_port())
+        return None
+    world = int(env["WORLD_SIZE"])
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but torchrun started WORLD_SIZE={world} ranks")
+    return None
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    child = launch_guard(args)
+    if child is not None:
+        import subprocess
+        rc = subprocess.run(child).returncode  # stdout/stderr inherited: rank 0's JSON line passes through
+        sys.exit(rc)
     if args.steps is None:
         args.steps = 100 if args.config == "er100k" else 5
     if args.lanes == 0:
@@ -317,6 +355,7 @@ def main():
         el = time.perf_counter() - t0
         if not args.no_profile:
             ctx.profile(False)
+        el_local = el
         el_max = kdist.allreduce_max(el, device=coll_dev, force=use_pg)
         tr, tr_stderr = _hutchinson(*sums[-1], N)
         k1_overlapped = None
@@ -366,6 +405,11 @@ def main():
                 iso_ms = ms1 / l1
                 iso_gbs = k1_bytes / (iso_ms * 1e-3) / 1e9
                 tl, busy_ms = timed
+                # the union of this rank's launches lies inside its own timed
+                # region (launches after t0, complete before the closing sync)
+                if busy_ms > el_local * 1e3:
+                    raise SystemExit(f"bench.py: profiled busy time {busy_ms:.3f} ms exceeds the timed "
+                                     f"region {el_local * 1e3:.3f} ms")
                 k1_ms = busy_ms / tl  # effective duration per launch in the timed region
                 achieved = k1_bytes / (k1_ms * 1e-3) / 1e9
                 # PMC bytes were profiled per graph (profiles/traffic.json keyed by
@@ -384,6 +428,7 @@ def main():
                                     "on each sweep lane's stream; avg_launch_us = union of their intervals "
                                     "(time with >= 1 launch in flight, lane overlap counted once) / launches",
                         "timed_region_busy_ms": round(busy_ms, 3),
+                        "timed_region_ms": round(el_local * 1e3, 3),
                         "timed_region_avg_launch_us_overlapped": k1_overlapped,
                         "isolated_pass": {"avg_launch_us": round(iso_ms * 1e3, 2), "launches": l1,
                                           "achieved": round(iso_gbs, 1),
@@ -450,6 +495,7 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0 and run_hutch:
         cpu = cpu_baseline(A, m, args.cpu_seconds, N, args.cpu_threads)
 
+    pg_world = dist.get_world_size() if use_pg else None
     if rank == 0:
         cfg = {"workload": wl, "n": n, "nnz": nnz, "lanczos_m": m, "fun": "exp"}
         if run_hutch:
@@ -461,13 +507,16 @@ def main():
                         "parallelism": f"G-probe columns dealt over x{world}, S/Q replicated"})
         out = {
             "metric": _metric_name(n, nnz),
-            "value": round(value, 4), "unit": "evals/s", "n_gpus": world,
+            "value": round(value, 4), "unit": "evals/s", "n_gpus": pg_world if use_pg else world,
             "steps": args.steps if run_hutch else mc_steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": cfg, "roofline": roof, "cpu_baseline": cpu,
             **extra,
         }
+        out["launch"] = {"process_group_world_size": pg_world, "backend": args.dist_backend if use_pg else None,
+                         "launcher": ("torchrun" if "TORCHELASTIC_RUN_ID" in os.environ else "single process"),
+                         "one_device_rehearsal": os.environ.get("KT_BENCH_ONE_DEVICE") == "1"}
         if mc is not None:
             out["mc_trace"] = mc
         print(json.dumps(out), flush=True)

@@ -139,6 +139,17 @@ int kt_fun_update(kt_matrix_t A, int64_t rk, const double* U, const double* B, i
                   int it, int64_t max_cols, double* Xm, int64_t* ncols, int* iter, int* lucky,
                   double* Um);
 
+/* [Xm, iter, lucky] = fun_update(A, U, B, fun, tol, it, debug) with at most
+ * three outputs (fun_update.m:69-76: the block-Lanczos branch over
+ * lanczos_krylov's 2-block window; Xm = f(tGm) - f(Gm) on the projected
+ * block tridiagonal, 2-norm lag-2 stop, no dense fallback).  Xm: ncols x
+ * ncols column-major (buffer of max_cols^2).  The reference then evaluates
+ * Um(:, 1:size(Xm, 1)) on the n x 2rk window (fun_update.m:137), which errors
+ * once ncols > 2 rk; that error is the caller's (the MEX shim raises it). */
+int kt_fun_update_lanczos(kt_matrix_t A, int64_t rk, const double* U, const double* B, int fun,
+                          double tol, int it, int64_t max_cols, double* Xm, int64_t* ncols, int* iter,
+                          int* lucky);
+
 /* [f, gr] = fun_and_grad_krylov_exp(X, A, Omega, eA, tol, it, debug)
  * (fun_and_grad_krylov_exp.m:1).  Omega: nomega x 2 column-major, 1-based
  * (MATLAB doubles); X, eA, gr: nomega.  KT_ERR_NOT_HERMITIAN if A is not
@@ -307,6 +318,12 @@ int kt_profile_reset(kt_context_t ctx);
  * each ran): with several lanes overlapping, summed per-launch durations
  * count shared time twice; this does not. */
 int kt_profile_busy(kt_context_t ctx, int kernel, double* busy_ms);
+
+/* Test hook: queue a kernel that keeps sweep lane `lane` (0 = the context's
+ * stream, 1..3 = the extra sweep-lane streams kt_slq_submit uses) busy for
+ * `microseconds` (<= 1e6) and return at once.  Lets a test make one lane's
+ * sweeps finish after another's (the profiler's out-of-order completion). */
+int kt_debug_delay(kt_context_t ctx, int lane, double microseconds);
 
 /* Hot-path statistics.  stat 0: kt_slq_trace sweeps whose y-form probe
  * Lanczos tripped the cancellation guard (a lucky breakdown, or a beta^2

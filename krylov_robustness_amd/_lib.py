@@ -71,6 +71,8 @@ SIGNATURES = [
                                          C.c_void_p, C.c_void_p, _dp, _ip, _ip]),
     ("kt_fun_update", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_int, C.c_double, C.c_int,
                                 C.c_int64, _dp, _i64p, _ip, _ip, _dp]),
+    ("kt_fun_update_lanczos", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_int, C.c_double, C.c_int,
+                                        C.c_int64, _dp, _i64p, _ip, _ip]),
     ("kt_fun_and_grad_krylov_exp", C.c_int, [_mat_p, C.c_int64, _dp, _dp, _dp, C.c_double, C.c_int,
                                              _dp, _dp]),
     ("kt_fun_and_grad_krylov_fun", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_int, C.c_int, _dp,
@@ -103,6 +105,7 @@ SIGNATURES = [
     ("kt_profile_read", C.c_int, [_ctx_p, C.c_int, _i64p, _dp]),
     ("kt_profile_reset", C.c_int, [_ctx_p]),
     ("kt_profile_busy", C.c_int, [_ctx_p, C.c_int, _dp]),
+    ("kt_debug_delay", C.c_int, [_ctx_p, C.c_int, C.c_double]),
     ("kt_context_stat", C.c_int, [_ctx_p, C.c_int, _i64p]),
 ]
 

@@ -63,6 +63,11 @@ class Context:
         _lib.check(_lib.load().kt_profile_busy(self._h, kernel, C.byref(ms)))
         return float(ms.value)
 
+    def debug_delay(self, lane: int, microseconds: float):
+        """Test hook (kt_debug_delay): keep sweep lane `lane`'s stream busy
+        for `microseconds`; returns at once."""
+        _lib.check(_lib.load().kt_debug_delay(self._h, int(lane), float(microseconds)))
+
     def yform_redone(self) -> int:
         """Sweeps of the y-form hot path recomputed by the explicit CGS2 sweep
         (cancellation guard / lucky breakdown), since context creation."""
@@ -318,15 +323,36 @@ def trace_fun_update(A, U, B, tol=1e-12, it=None, debug=0, fun="exp", ctx: Optio
 
 
 def fun_update(A, U, B, fun="exp", tol=1e-12, it=None, debug=0, want_um=True,
-               ctx: Optional[Context] = None):
+               ctx: Optional[Context] = None, nargout=4):
     """[Xm, iter, lucky, Um] = fun_update(A, U, B, fun, tol, it, debug)
-    (fun_update.m:1, the four-output Arnoldi branch)."""
+    (fun_update.m:1).  nargout = 4: the Arnoldi branch (:77-91) every caller
+    in the reference uses.  nargout <= 3: the block-Lanczos branch (:69-76,
+    kt_fun_update_lanczos), returning (Xm, iter, lucky); as in the reference
+    a run that took three or more steps then fails at :137
+    (Um(:, 1:size(Xm, 1)) on lanczos_krylov's 2-block window): IndexError."""
     D = _dev(A, ctx)
     U = _colmajor(U)
     B = _colmajor(np.atleast_2d(B))
     rk = U.shape[1]
     its = int(it or min(100, D.n))
     maxc = int(min(D.n, (its + 1) * rk))
+    if nargout <= 3:
+        Xm = np.zeros(maxc * maxc)
+        nc = C.c_int64()
+        itr = C.c_int()
+        lk = C.c_int()
+        _lib.check(_lib.load().kt_fun_update_lanczos(
+            D.handle, rk, _dptr(U), _dptr(B), _fun_code(fun), float(tol), int(it or 0), maxc,
+            _dptr(Xm), C.byref(nc), C.byref(itr), C.byref(lk)))
+        if lk.value:  # fun_update.m:127-130
+            warnings.warn("FUN_UPDATE:: Detected lucky breakdown")
+        if itr.value == its:  # :133-135
+            warnings.warn("FUN_UPDATE:: Reached maximum number of iterations")
+        k = int(nc.value)
+        if k > 2 * rk:  # :137 indexes the n x 2rk window with 1:size(Xm, 1)
+            raise IndexError(f"fun_update.m:137: index exceeds the {2 * rk} columns of the Lanczos window "
+                             f"(size(Xm, 1) = {k})")
+        return Xm[:k * k].reshape(k, k, order="F"), int(itr.value), int(lk.value)
     Xm = np.zeros(maxc * maxc)
     Um = np.zeros(D.n * maxc) if want_um else None
     nc = C.c_int64()

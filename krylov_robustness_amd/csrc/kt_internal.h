@@ -9,6 +9,8 @@
 
 #include "../../include/krylov_trace.h"
 
+struct kt_matrix_s;
+
 namespace kt {
 
 void set_error(const std::string& msg);
@@ -110,7 +112,13 @@ struct ProfSlot {
     size_t done = 0;             // events already folded into the totals (prof_collect)
     int64_t launches = 0;
     double total_ms = 0.0;
-    double busy_ms = 0.0;  // union of the launches' intervals
+    // every folded launch's [start, stop] in ms after `anchor` (recorded before
+    // the slot's first launch since the last reset): the union is formed over
+    // ALL of them when read, so launches of consecutive batches that overlap
+    // in time (pipelined calls, several lanes) are counted once
+    std::vector<std::pair<double, double>> iv;
+    hipEvent_t anchor = nullptr;
+    bool anchored = false;
 };
 
 enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_START = 2, PROF_NSLOTS = 3 };
@@ -154,6 +162,7 @@ struct HostFlag {
 // after the lane's last record copy.
 struct SlqPending {
     bool live = false;
+    const kt_matrix_s* A = nullptr;  // the submitting matrix (collect must name it)
     int fun = 0, m = 0, P = 1, lanes = 1;
     uint64_t seed = 0;
     int64_t offset = 0, nprobes = 0, nsweeps = 0;
@@ -315,6 +324,8 @@ void prof_collect(kt_context_s* ctx, const size_t* upto = nullptr, bool wait = f
 // at a call's start: recycle the events already folded in, keep the rest
 void prof_recycle(kt_context_s* ctx);
 void prof_reserve(kt_context_s* ctx, size_t per_slot);
+// union of the slot's folded launch intervals (ms)
+double prof_busy(const ProfSlot& s);
 
 // dense host helpers (kt_dense.cpp)
 double fscalar(int fun, double x);

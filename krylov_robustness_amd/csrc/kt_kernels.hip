@@ -2579,6 +2579,19 @@ hipError_t launch_absmax_idx(int n, const double* Z, double* pval, int* pidx, hi
     return hipGetLastError();
 }
 
+// test hook (kt_debug_delay): one wave that waits `ticks` of the 100 MHz
+// constant clock, so a stream is busy for a known time; every wave exits
+__global__ __launch_bounds__(64) void k_delay(long long ticks) {
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
+}
+
+hipError_t launch_delay(double microseconds, hipStream_t st) {
+    const long long ticks = (long long)(microseconds * 100.0);  // 100 MHz
+    k_delay<<<1, 64, 0, st>>>(ticks);
+    return hipGetLastError();
+}
+
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st) {
     int grid = (count + 255) / 256;
     if (grid < 1) grid = 1;

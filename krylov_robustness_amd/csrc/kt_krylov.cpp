@@ -1084,6 +1084,72 @@ FunUpdateResult fun_update_impl(kt_matrix_s* A, int rk, const double* U, const d
     return res;
 }
 
+// ---------------------------------------------------------------------------
+// fun_update.m's Lanczos branch (nargout <= 3, :69-76): the same loop as the
+// Arnoldi branch over lanczos_krylov's 2-block window (BlockLanczos, as
+// trace_fun_update runs it) -- Cm from the first block (:72-73), Gm the
+// projected block tridiagonal (:93-94), Xm = f(tGm) - f(Gm) (:106), the
+// 2-norm lag-2 stop (:108-126) -- with no dense fallback (:85-90 belongs to
+// the Arnoldi branch).  Serial.  The reference then indexes Um(:, 1:size(Xm,1))
+// on the n x 2rk window (:137), which fails once the run took three or more
+// steps; that error is the caller's to raise (the MEX shim does), the C ABI
+// returns Xm.
+// ---------------------------------------------------------------------------
+static FunUpdateResult fun_update_lanczos_impl(kt_matrix_s* A, int rk, const double* U, const double* B,
+                                               int fun, double tol, int it) {
+    kt_context_s* ctx = A->ctx;
+    const int64_t n = A->n;
+    if (it <= 0) it = (int)std::min<int64_t>(100, n);  // :24-26
+    if (!b_hermitian(rk, B)) fail(KT_ERR_UNSUPPORTED, "fun_update: non-Hermitian B");  // :41
+    FunUpdateResult res;
+    BlockLanczos L(A, rk);
+    const int d = 2;  // :63
+    std::vector<std::vector<double>> Xstop;
+    std::vector<double> Cm, F1;
+    int nn = 0, j = 1;
+    for (j = 1; j <= it; ++j) {
+        if (j == 1) {
+            L.start(U);                                                            // :71
+            Cm = make_Cm(ctx, A, L.win.col(L.prev * L.PB), 2 * L.PB, rk, U, rk, B);  // :72-73
+        } else {
+            L.extend();                                                            // :75
+        }
+        nn = L.Hr - rk;                                                            // :93
+        std::vector<double> Gm = top_left(L.H, L.Hr, nn);
+        for (int b = 0; b < nn; ++b)                                               // :94
+            for (int a = 0; a < b; ++a) {
+                const double sv = 0.5 * (Gm[a + (size_t)b * nn] + Gm[b + (size_t)a * nn]);
+                Gm[a + (size_t)b * nn] = Gm[b + (size_t)a * nn] = sv;
+            }
+        std::vector<double> tGm = Gm;
+        for (int jj = 0; jj < rk; ++jj)                                            // :97-104
+            for (int ii = 0; ii < rk; ++ii)
+                tGm[ii + (size_t)jj * nn] += 0.5 * (Cm[ii + (size_t)jj * rk] + Cm[jj + (size_t)ii * rk]);
+        F1 = sym_matfun_diff(ctx, nn, tGm, Gm, fun);                               // :106
+        bool stop = false;
+        if (j <= d) {                                                              // :109-110
+            Xstop.push_back(F1);
+        } else {                                                                   // :111-126
+            const int n0 = (int)std::lround(std::sqrt((double)Xstop[0].size()));
+            std::vector<double> D = F1;
+            for (int b = 0; b < n0; ++b)
+                for (int a = 0; a < n0; ++a) D[a + (size_t)b * nn] -= Xstop[0][a + (size_t)b * n0];
+            stop = sym_norm2_below(ctx, nn, D, tol);
+            if (!stop) {
+                Xstop.erase(Xstop.begin());
+                Xstop.push_back(F1);
+            }
+        }
+        if (stop || L.lucky) break;                                                // :122-130
+    }
+    res.Xm.swap(F1);
+    res.nx = nn;
+    res.iter = std::min(j, it);                                                    // :132
+    res.lucky = L.lucky;
+    ctx->fu_last_cols = nn;
+    return res;
+}
+
 // MATLAB normest (2-norm power estimate) on the device: x = sum(abs(A))',
 // repeat x = A'(A x)/||.|| until |e - e0| <= tol e.
 static double normest_compute(kt_matrix_s* A, double tol);
@@ -1353,6 +1419,22 @@ int kt_fun_update(kt_matrix_t A, int64_t rk, const double* U, const double* B, i
             }
         }
     }
+    KT_CATCH
+}
+
+int kt_fun_update_lanczos(kt_matrix_t A, int64_t rk, const double* U, const double* B, int fun, double tol,
+                          int it, int64_t max_cols, double* Xm, int64_t* ncols, int* iter, int* lucky) {
+    KT_TRY
+    if (!A || !U || !B || !Xm || !ncols) fail(KT_ERR_ARG, "NULL argument");
+    if (rk < 1 || rk > 128) fail(KT_ERR_ARG, "rk must be in [1, 128]");
+    if (fun < KT_FUN_EXP || fun > KT_FUN_SQRT) fail(KT_ERR_ARG, "unknown fun code");
+    KT_HIP(hipSetDevice(A->ctx->device));
+    FunUpdateResult r = fun_update_lanczos_impl(A, (int)rk, U, B, fun, tol, it);
+    if (r.nx > max_cols) fail(KT_ERR_ARG, "max_cols too small for the projected size");
+    std::copy(r.Xm.begin(), r.Xm.end(), Xm);
+    *ncols = r.nx;
+    if (iter) *iter = r.iter;
+    if (lucky) *lucky = r.lucky ? 1 : 0;
     KT_CATCH
 }
 

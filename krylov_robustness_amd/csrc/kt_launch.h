@@ -98,6 +98,7 @@ hipError_t launch_ycoef(int P, const double* partial, int nblk, int start, int l
                         double* ys, double* t_alpha, double* t_up, double* t_low, double* guard,
                         hipStream_t st);
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st);
+hipError_t launch_delay(double microseconds, hipStream_t st);
 // out[i] = D[off[i]], i < count
 // tall-skinny Gram / combine (kt_gemm_ts.hip)
 int gram_ts_chunks(int64_t n);

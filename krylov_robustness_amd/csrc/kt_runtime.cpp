@@ -33,6 +33,11 @@ void prof_begin(kt_context_s* ctx, int slot, hipStream_t st) {
             s.ev.push_back(e);
         }
     }
+    if (!s.anchored) {  // the time origin of every interval until the next reset
+        if (!s.anchor) KT_HIP(hipEventCreateWithFlags(&s.anchor, kProfEventFlags));
+        KT_HIP(hipEventRecord(s.anchor, st ? st : ctx->stream));
+        s.anchored = true;
+    }
     KT_HIP(hipEventRecord(s.ev[s.used], st ? st : ctx->stream));
 }
 
@@ -58,30 +63,36 @@ void prof_collect(kt_context_s* ctx, const size_t* upto, bool wait) {
         // (a completed event returns at once)
         if (wait)
             for (size_t i = s.done; i < end; ++i) KT_HIP(hipEventSynchronize(s.ev[i]));
-        std::vector<std::pair<double, double>> iv;  // relative to the batch's first event
         for (size_t i = s.done; i + 1 < end; i += 2) {
             float ms = 0.f, a = 0.f, b = 0.f;
             KT_HIP(hipEventElapsedTime(&ms, s.ev[i], s.ev[i + 1]));
-            KT_HIP(hipEventElapsedTime(&a, s.ev[s.done], s.ev[i]));
-            KT_HIP(hipEventElapsedTime(&b, s.ev[s.done], s.ev[i + 1]));
-            iv.push_back({a, b});
+            KT_HIP(hipEventElapsedTime(&a, s.anchor, s.ev[i]));
+            KT_HIP(hipEventElapsedTime(&b, s.anchor, s.ev[i + 1]));
+            s.iv.push_back({a, b});
             s.total_ms += ms;
             s.launches += 1;
         }
-        std::sort(iv.begin(), iv.end());
-        double cs = 0.0, ce = -1.0;
-        for (auto& x : iv) {  // union of the intervals
-            if (x.first > ce) {
-                if (ce > cs) s.busy_ms += ce - cs;
-                cs = x.first;
-                ce = x.second;
-            } else if (x.second > ce) {
-                ce = x.second;
-            }
-        }
-        if (ce > cs) s.busy_ms += ce - cs;
         s.done = end;
     }
+}
+
+double prof_busy(const ProfSlot& s) {
+    std::vector<std::pair<double, double>> iv(s.iv);
+    std::sort(iv.begin(), iv.end());
+    double busy = 0.0, cs = 0.0, ce = -1.0;
+    bool open = false;
+    for (auto& x : iv) {
+        if (!open || x.first > ce) {
+            if (open) busy += ce - cs;
+            cs = x.first;
+            ce = x.second;
+            open = true;
+        } else if (x.second > ce) {
+            ce = x.second;
+        }
+    }
+    if (open) busy += ce - cs;
+    return busy;
 }
 
 void prof_recycle(kt_context_s* ctx) {
@@ -353,8 +364,12 @@ int kt_context_destroy(kt_context_t ctx) {
     }
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    for (auto& s : ctx->prof)
+    for (auto a : ctx->aux_stream)
+        if (a) (void)hipStreamSynchronize(a);
+    for (auto& s : ctx->prof) {
         for (auto e : s.ev) (void)hipEventDestroy(e);
+        if (s.anchor) (void)hipEventDestroy(s.anchor);
+    }
     for (auto a : ctx->aux_stream)
         if (a) (void)hipStreamSynchronize(a);
     Workspace& w = ctx->ws;
@@ -464,7 +479,13 @@ int kt_matrix_destroy(kt_matrix_t A) {
     KT_GUARD_BEGIN
     if (!A) return KT_OK;
     (void)hipSetDevice(A->ctx->device);
+    // every lane: kt_slq_submit leaves sweeps queued on the aux streams that
+    // read this matrix's CSR until they are collected
     (void)hipStreamSynchronize(A->ctx->stream);
+    for (hipStream_t a : A->ctx->aux_stream)
+        if (a) (void)hipStreamSynchronize(a);
+    for (auto& pd : A->ctx->ws.slq_pend)  // an uncollected ticket of A: collect now fails
+        if (pd.A == A) pd.A = nullptr;
     if (A->twin) kt_matrix_destroy(A->twin);
     if (A->twin_ctx) kt_context_destroy(A->twin_ctx);
     (void)hipSetDevice(A->ctx->device);
@@ -513,7 +534,28 @@ int kt_context_stat(kt_context_t ctx, int stat, int64_t* value) {
 int kt_profile_reset(kt_context_t ctx) {
     KT_GUARD_BEGIN
     if (!ctx) fail(KT_ERR_ARG, "ctx is NULL");
-    for (auto& s : ctx->prof) { s.launches = 0; s.total_ms = 0.0; s.busy_ms = 0.0; s.used = 0; s.done = 0; }
+    KT_HIP(hipSetDevice(ctx->device));
+    // events of launches still in flight would be recorded into reused slots
+    prof_collect(ctx, nullptr, true);
+    for (auto& s : ctx->prof) {
+        s.launches = 0;
+        s.total_ms = 0.0;
+        s.iv.clear();
+        s.anchored = false;
+        s.used = 0;
+        s.done = 0;
+    }
+    KT_GUARD_END
+}
+
+int kt_debug_delay(kt_context_t ctx, int lane, double microseconds) {
+    KT_GUARD_BEGIN
+    if (!ctx || lane < 0 || lane > 3) fail(KT_ERR_ARG, "kt_debug_delay: bad context or lane");
+    if (!(microseconds >= 0.0 && microseconds <= 1e6)) fail(KT_ERR_ARG, "kt_debug_delay: 0 <= us <= 1e6");
+    KT_HIP(hipSetDevice(ctx->device));
+    if (lane && !ctx->aux_stream[lane - 1])
+        KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[lane - 1], hipStreamNonBlocking));
+    KT_HIP(launch_delay(microseconds, lane ? ctx->aux_stream[lane - 1] : ctx->stream));
     KT_GUARD_END
 }
 
@@ -522,7 +564,7 @@ int kt_profile_busy(kt_context_t ctx, int kernel, double* busy_ms) {
     if (!ctx || !busy_ms || kernel < 0 || kernel >= PROF_NSLOTS) fail(KT_ERR_ARG, "bad profile query");
     KT_HIP(hipSetDevice(ctx->device));
     prof_collect(ctx, nullptr, true);
-    *busy_ms = ctx->prof[kernel].busy_ms;
+    *busy_ms = prof_busy(ctx->prof[kernel]);
     KT_GUARD_END
 }
 

@@ -380,6 +380,7 @@ static int slq_submit(kt_matrix_s* A, int fun, int m, uint64_t seed, int64_t pro
     SlqPending& pd = w.slq_pend[ticket & 1];
     const int64_t n = A->n;
     pd.live = false;
+    pd.A = A;
     pd.fun = fun;
     pd.m = m;
     pd.seed = seed;
@@ -442,6 +443,10 @@ static void slq_collect(kt_matrix_s* A, int ticket, double* sum_q, double* sum_q
     ++w.slq_collected;
     if (!pd.live) fail(KT_ERR_ARG, "kt_slq_collect: the submission failed");
     pd.live = false;
+    // the record's n, CSR (guard redo) and lanes belong to the submitting matrix
+    if (pd.A != A)
+        fail(KT_ERR_ARG, pd.A ? "kt_slq_collect: the ticket was submitted with another matrix"
+                              : "kt_slq_collect: the submitting matrix was destroyed");
     if (sum_q) *sum_q = 0.0;
     if (sum_q2) *sum_q2 = 0.0;
     if (pd.nprobes == 0) return;

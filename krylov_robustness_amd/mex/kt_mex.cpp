@@ -317,11 +317,18 @@ mxArray* export_sparse(kt_matrix_t A) {
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
 #if defined(KT_ENTRY_TRACE_EXP)
     // tr = trace_exp(A)                                          trace_exp.m:1
-    if (nrhs != 1) mexErrMsgIdAndTxt("krylov_hip:nargin", "tr = trace_exp(A)");
-    // Afun: the Lanczos-quadrature Afun (north star, default) or the
-    // reference's own expmv handle (trace_exp.m:5) with KT_TRACE_EXP_AFUN=expmv
-    const char* af = getenv("KT_TRACE_EXP_AFUN");
-    const int afun = (af && strcmp(af, "expmv") == 0) ? KT_AFUN_EXPMV : KT_AFUN_LANCZOS;
+    // trace_exp(A) as the reference's callers write it; an optional second
+    // argument names the Afun: 'lanczos' (the north star's Lanczos-quadrature
+    // Afun, the default) or 'expmv' (the reference's own handle, trace_exp.m:5)
+    if (nrhs < 1 || nrhs > 2) mexErrMsgIdAndTxt("krylov_hip:nargin", "tr = trace_exp(A[, 'lanczos' | 'expmv'])");
+    int afun = KT_AFUN_LANCZOS;
+    if (nrhs == 2) {
+        char af[16] = {0};
+        if (!mxIsChar(prhs[1]) || mxGetString(prhs[1], af, sizeof(af)) != 0 ||
+            (strcmp(af, "expmv") != 0 && strcmp(af, "lanczos") != 0))
+            mexErrMsgIdAndTxt("krylov_hip:afun", "trace_exp: the Afun must be 'lanczos' or 'expmv'");
+        if (strcmp(af, "expmv") == 0) afun = KT_AFUN_EXPMV;
+    }
     double tr = 0.0;
     check(kt_trace_exp(matrix_arg(prhs[0]), afun, 30, 0, &tr), "trace_exp");
     plhs[0] = scalar(tr);
@@ -409,13 +416,28 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     std::vector<double> Um(nlhs > 3 ? (size_t)n * maxc : 0);
     int64_t nc = 0;
     int iter = 0, lucky = 0;
-    check(kt_fun_update(A, (int64_t)rk, mxGetDoubles(prhs[1]), mxGetDoubles(prhs[2]), fun_arg(prhs[3], KT_FUN_EXP),
-                        scalar_or(nrhs, prhs, 4, 1e-12), it, maxc, Xm.data(), &nc, &iter, &lucky,
-                        nlhs > 3 ? Um.data() : nullptr),
-          "fun_update");
+    // nargout <= 3 takes the block-Lanczos branch, 4 the Arnoldi branch (:69-91)
+    if (nlhs <= 3)
+        check(kt_fun_update_lanczos(A, (int64_t)rk, mxGetDoubles(prhs[1]), mxGetDoubles(prhs[2]),
+                                    fun_arg(prhs[3], KT_FUN_EXP), scalar_or(nrhs, prhs, 4, 1e-12), it, maxc,
+                                    Xm.data(), &nc, &iter, &lucky),
+              "fun_update");
+    else
+        check(kt_fun_update(A, (int64_t)rk, mxGetDoubles(prhs[1]), mxGetDoubles(prhs[2]),
+                            fun_arg(prhs[3], KT_FUN_EXP), scalar_or(nrhs, prhs, 4, 1e-12), it, maxc, Xm.data(),
+                            &nc, &iter, &lucky, Um.data()),
+              "fun_update");
     if (lucky) mexWarnMsgIdAndTxt("FUN_UPDATE:lucky", "FUN_UPDATE:: Detected lucky breakdown");  // fun_update.m:127-128
     if (iter == (it > 0 ? it : (int)(n < 100 ? n : 100)))
         mexWarnMsgIdAndTxt("FUN_UPDATE:maxit", "FUN_UPDATE:: Reached maximum number of iterations");  // :133-135
+    // :137 Um = Um(:, 1:size(Xm, 1)) runs on the Lanczos branch too, where Um
+    // is the n x 2rk window: past two steps the reference stops with MATLAB's
+    // index error, and so does the shim (never a silently different algorithm)
+    if (nlhs <= 3 && nc > (int64_t)(2 * rk))
+        mexErrMsgIdAndTxt("MATLAB:badsubscript",
+                          "Index in position 2 exceeds array bounds (must not exceed %d). (fun_update.m:137: "
+                          "Um(:, 1:size(Xm, 1)) on the 2-block Lanczos window, size(Xm, 1) = %d)",
+                          (int)(2 * rk), (int)nc);
     plhs[0] = mxCreateDoubleMatrix(nc, nc, mxREAL);
     memcpy(mxGetDoubles(plhs[0]), Xm.data(), sizeof(double) * nc * nc);
     if (nlhs > 1) plhs[1] = scalar(iter);

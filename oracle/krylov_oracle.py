@@ -388,6 +388,8 @@ def fun_update(A, U, B, fun="exp", tol=1e-12, it=None, debug=0, nargout=4):
     iter_ = j
     if iter_ == it:                                       # :133-135
         warnings.warn("FUN_UPDATE:: Reached maximum number of iterations")
+    if Xm.shape[0] > st.V.shape[1]:                       # :137 on the Lanczos branch's window
+        raise IndexError(f"fun_update.m:137: index exceeds the {st.V.shape[1]} columns of V")
     Um = st.V[:, :Xm.shape[0]]                            # :137
     return Xm, iter_, lucky, Um
 

@@ -180,6 +180,44 @@ double slq_ref_trace(int64_t n, const int64_t *rp, const int32_t *ci, const doub
     return nprobes > 0 ? total / nprobes : 0.0;
 }
 
+/* Diagonal entries e_i' exp(t_k A) e_i for rows i in [row0, row0 + nrows),
+ * k < nt: one m-step Lanczos run started from the unit vector e_i (the same
+ * recurrence as the probes: lanczos_krylov.m:30-115 with bs = 1) and the
+ * Gauss quadrature of its tridiagonal, sum_j tau_j^2 exp(t_k theta_j).
+ * Summed over every row this is tr(exp(t A)) with no sampling error: only
+ * the quadrature error of m nodes (for exp on a spectrum of width w it is
+ * below exp(t lambda_max) (t w)^{2m} / (2^{4m-1} (2m)!)) and rounding.
+ * out[(i - row0) * nt + k].  Used to pin config 2 (tests/golden/
+ * make_config2_fixture.py): t = 1 gives tr(exp A), t = 2 gives ||exp A||_F^2,
+ * from which the Rademacher Hutchinson variance follows exactly. */
+void slq_ref_unit_quad(int64_t n, const int64_t *rp, const int32_t *ci, const double *va,
+                       int64_t row0, int64_t nrows, int m, const double *t, int nt, int nthreads,
+                       double *out) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel
+    {
+        double *z = (double *)calloc((size_t)n, sizeof(double));
+        double alpha[256], off[256], d[256], zz[256];
+#pragma omp for schedule(dynamic, 4)
+        for (int64_t r = 0; r < nrows; ++r) {
+            const int64_t i = row0 + r;
+            z[i] = 1.0;
+            int steps = slq_ref_lanczos(n, rp, ci, va, z, m, alpha, off);
+            z[i] = 0.0;
+            for (int k = 0; k < nt; ++k) {
+                for (int j = 0; j < steps; ++j) d[j] = alpha[j];
+                tql_first_row(steps, d, off, zz);
+                double q = 0.0;
+                for (int j = 0; j < steps; ++j) q += zz[j] * zz[j] * exp(t[k] * d[j]);
+                out[r * nt + k] = q;
+            }
+        }
+        free(z);
+    }
+}
+
 int slq_ref_max_threads(void) {
 #ifdef _OPENMP
     return omp_get_max_threads();

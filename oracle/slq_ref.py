@@ -54,3 +54,23 @@ def slq_trace(A, nprobes, m, seed=0, fun="exp", probe_offset=0, nthreads=0):
 
 def max_threads():
     return int(load().slq_ref_max_threads())
+
+
+def unit_quad(A, row0, nrows, m, t=(1.0,), nthreads=0):
+    """e_i' exp(t_k A) e_i for rows [row0, row0 + nrows) by m-step Lanczos
+    from e_i + Gauss quadrature (slq_ref_unit_quad); returns (nrows, len(t))."""
+    import scipy.sparse as sp
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    rp = np.ascontiguousarray(A.indptr, dtype=np.int64)
+    ci = np.ascontiguousarray(A.indices, dtype=np.int32)
+    va = np.ascontiguousarray(A.data, dtype=np.float64)
+    tv = np.ascontiguousarray(t, dtype=np.float64)
+    out = np.zeros((int(nrows), tv.size))
+    lib = load()
+    lib.slq_ref_unit_quad.restype = None
+    lib.slq_ref_unit_quad(C.c_int64(A.shape[0]), C.c_void_p(rp.ctypes.data), C.c_void_p(ci.ctypes.data),
+                          C.c_void_p(va.ctypes.data), C.c_int64(int(row0)), C.c_int64(int(nrows)), C.c_int(int(m)),
+                          C.c_void_p(tv.ctypes.data), C.c_int(tv.size), C.c_int(int(nthreads)),
+                          C.c_void_p(out.ctypes.data))
+    return out

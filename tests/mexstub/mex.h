@@ -15,6 +15,7 @@ bool mxIsDouble(const mxArray*);
 bool mxIsComplex(const mxArray*);
 bool mxIsSparse(const mxArray*);
 bool mxIsEmpty(const mxArray*);
+bool mxIsChar(const mxArray*);
 mwSize mxGetM(const mxArray*);
 mwSize mxGetN(const mxArray*);
 mwIndex* mxGetJc(const mxArray*);

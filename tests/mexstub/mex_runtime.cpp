@@ -253,6 +253,7 @@ bool mxIsDouble(const mxArray* a) { return a->kind == mxArray_tag::DOUBLE || a->
 bool mxIsComplex(const mxArray*) { return false; }
 bool mxIsSparse(const mxArray* a) { return a->kind == mxArray_tag::SPARSE; }
 bool mxIsEmpty(const mxArray* a) { return a->m == 0 || a->n == 0; }
+bool mxIsChar(const mxArray* a) { return a->kind == mxArray_tag::CHAR; }
 mwSize mxGetM(const mxArray* a) { return a->m; }
 mwSize mxGetN(const mxArray* a) { return a->n; }
 mwIndex* mxGetJc(const mxArray* a) { return const_cast<mwIndex*>(a->jc.data()); }

@@ -180,13 +180,18 @@ def _nonsym(A):
 
 
 # ---- trace_exp / mc_trace ------------------------------------------------------
-def test_trace_exp_default_and_expmv(mex, kra, monkeypatch):
+def test_trace_exp_default_and_expmv(mex, kra):
+    """trace_exp(A) as the reference's callers write it takes the Lanczos Afun;
+    the optional second argument selects the reference's own expmv handle
+    (trace_exp.m:5) -- an argument, not a process-wide switch."""
     A = load_graph("oregon_A0")
     tr, = mex.call("TRACE_EXP", 1, A)
     assert tr == kra.trace_exp(A, "lanczos", m=30, seed=0)
-    monkeypatch.setenv("KT_TRACE_EXP_AFUN", "expmv")
-    tr2, = mex.call("TRACE_EXP", 1, A)
+    assert mex.call("TRACE_EXP", 1, A, "lanczos")[0] == tr
+    tr2, = mex.call("TRACE_EXP", 1, A, "expmv")
     assert tr2 == kra.trace_exp(A, "expmv", seed=0)
+    with pytest.raises(MexRaised, match="'lanczos' or 'expmv'"):
+        mex.call("TRACE_EXP", 1, A, "taylor")
     exact = ko.exact_trace_fun(A, "exp")
     assert abs(tr - exact) <= 1e-3 * exact and abs(tr2 - exact) <= 1e-3 * exact
     assert mex.rt.stub_lock_count() >= 1 and mex.rt.stub_atexit_count() >= 1  # mexLock + mexAtExit
@@ -289,6 +294,68 @@ def test_fun_update_four_outputs(mex, kra):
         rX, rit, rl, rU = kra.fun_update(A, U, B, "exp")
     assert np.array_equal(np.atleast_2d(Xm), rX) and (it, lucky) == (rit, rl)
     assert np.array_equal(Um, rU)
+
+
+def test_fun_update_three_outputs_is_the_lanczos_branch(mex, kra):
+    """nargout <= 3 (fun_update.m:69-76) runs the block-Lanczos branch, not
+    Arnoldi: with it = 2 (the run ends inside the 2-block window) Xm is the
+    Lanczos branch's, equal to the oracle's nargout=3 restatement; a run that
+    goes on to a third step stops where the reference does, at :137
+    (Um(:, 1:size(Xm, 1)) on the n x 2rk window), with MATLAB's index error."""
+    A = load_graph("austria")
+    n = A.shape[0]
+    U, B = _edge_UB(n, 3, 9)
+    Xm, it, lucky = mex.call("FUN_UPDATE", 3, A, U, B, "@exp", 1e-12, 2.0)
+    Xm = np.atleast_2d(Xm)
+    assert Xm.shape == (4, 4) and (it, lucky) == (2, 0)
+    assert ("FUN_UPDATE:maxit", "FUN_UPDATE:: Reached maximum number of iterations") in mex.warnings()
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        rX, rit, rl = kra.fun_update(A, U, B, "exp", 1e-12, 2, nargout=3)
+        oX, oit, ol, _ = ko.fun_update(A, U, B, "exp", 1e-12, 2, nargout=3)
+    assert np.array_equal(Xm, rX) and (rit, rl) == (2, 0)
+    # the second block's basis vectors carry qr(w, 0)'s reflector signs, which
+    # differ between the device Householder QR and the oracle's: Xm agrees up
+    # to D Xm D with D = diag(+-1) (entries in modulus, spectrum exactly)
+    tol = 1e-9 * np.abs(oX).max()
+    np.testing.assert_allclose(np.abs(Xm), np.abs(oX), rtol=1e-9, atol=tol)
+    np.testing.assert_allclose(np.linalg.eigvalsh(Xm), np.linalg.eigvalsh(oX), rtol=1e-9, atol=tol)
+    assert (oit, ol) == (2, False)
+    # the Arnoldi branch's Xm at the same step differs (it is another algorithm)
+    aX = kra.fun_update(A, U, B, "exp", 1e-12, 2)[0]
+    assert aX.shape == Xm.shape
+    mex.rt.stub_clear()
+    with pytest.raises(MexRaised) as e:
+        mex.call("FUN_UPDATE", 3, A, U, B, "@exp")
+    assert e.value.ident == "MATLAB:badsubscript" and "fun_update.m:137" in e.value.msg
+    with pytest.raises(IndexError, match="fun_update.m:137"):
+        kra.fun_update(A, U, B, "exp", nargout=3)
+    with pytest.raises(IndexError, match="fun_update.m:137"):
+        ko.fun_update(A, U, B, "exp", nargout=3)
+
+
+def test_fun_update_three_outputs_lucky_breakdown(mex, kra):
+    """A lucky breakdown in the first step (U spans an invariant subspace: a
+    separate two-node component) ends the Lanczos branch inside the window, so
+    the reference returns; the device result equals the oracle and the exact
+    f(A + UBU') - f(A) on that component."""
+    from scipy.linalg import expm
+    G = load_graph("austria")
+    n0 = G.shape[0]
+    A = sp.block_diag([G, sp.csr_matrix(np.array([[0.0, 1.0], [1.0, 0.0]]))]).tocsc()
+    U, B = _edge_UB(n0 + 2, n0, n0 + 1)
+    B = np.array([[0.0, 0.5], [0.5, 0.0]])
+    Xm, it, lucky = mex.call("FUN_UPDATE", 3, A, U, B, "@exp")
+    assert (it, lucky) == (1, 1)
+    assert ("FUN_UPDATE:lucky", "FUN_UPDATE:: Detected lucky breakdown") in mex.warnings()
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        oX, oit, ol, _ = ko.fun_update(A, U, B, "exp", nargout=3)
+    np.testing.assert_allclose(np.atleast_2d(Xm), oX, rtol=1e-10, atol=1e-12)
+    E = np.array([[0.0, 1.5], [1.5, 0.0]])
+    D = expm(E) - expm(np.array([[0.0, 1.0], [1.0, 0.0]]))
+    # Xm lives in the basis qr(U) = +-[e_i, e_j]: the same up to the reflector signs
+    np.testing.assert_allclose(np.abs(np.atleast_2d(Xm)), np.abs(D), rtol=1e-10, atol=1e-12)
 
 
 # ---- fun_and_grad_krylov_{exp,fun} ---------------------------------------------------
