@@ -59,10 +59,11 @@ def parse():
     ap.add_argument("--mc-steps", type=int, default=5,
                     help="timed trace_exp (mc_trace) evaluations reported beside the headline "
                          "(0 = skip that leg unless --estimator mc_trace)")
-    ap.add_argument("--ref-cpu-seconds", type=float, default=15.0,
+    ap.add_argument("--ref-cpu-seconds", type=float, default=8.0,
                     help="trace_exp as the reference composes it (mc_trace + expmv Afun): one serial GPU "
-                         "run, and the oracle's CPU restatement timed on a bounded sample of it (rank 0, "
-                         "N=1, config sf1m, beside the mc_trace leg); 0 disables")
+                         "run, and the CPU restatements timed on bounded samples of it -- the C/OpenMP one "
+                         "on one whole expmv call, the 1-thread SciPy one for this many seconds of Taylor "
+                         "terms (rank 0, N=1, config sf1m, beside the mc_trace leg); 0 disables")
     ap.add_argument("--bitstable", action="store_true",
                     help="all-gather the per-probe forms and sum them in global probe order on every "
                          "rank (SURVEY §8e): the estimate is bit-identical for any number of ranks")
@@ -89,10 +90,25 @@ def make_graph(config, weighted=False):
 
 
 def reference_trace(config, weighted=False):
-    """tr(exp(A)) of the bench graph from its spectrum (tests/golden/
-    config4_values.json, written in the build container by
-    tests/golden/make_config4_fixture.py: scipy eigsh top 16, every other
-    term bounded by exp(lambda_16)), or None for graphs without one."""
+    """tr(exp(A)) of the bench graph, or None for graphs without one:
+      * sf1m: from its spectrum (tests/golden/config4_values.json, written in
+        the build container by tests/golden/make_config4_fixture.py: scipy
+        eigsh top 16, every other term bounded by exp(lambda_16));
+      * er100k: the sum of all n diagonal entries e_i' exp(A) e_i, each by
+        m = 30 Lanczos from e_i + Gauss quadrature (tests/golden/
+        config2_values.json, make_config2_fixture.py), with the Rademacher
+        Hutchinson estimator's exact standard error."""
+    if config == "er100k" and not weighted:
+        try:
+            with open(os.path.join(ROOT, "tests", "golden", "config2_values.json")) as f:
+                ex = json.load(f)["exact"]
+        except (OSError, ValueError, KeyError):
+            return None
+        return {"value": ex["tr_exp"], "rel_uncertainty": ex["rel_uncertainty"],
+                "hutchinson_stderr_per_probe": math.sqrt(ex["hutchinson_var_per_probe"]),
+                "source": "tests/golden/config2_values.json: sum over all n rows of e_i' exp(A) e_i (m = 30 "
+                          "Lanczos from e_i + Gauss quadrature; m = 45 agrees to 7e-14), exact Hutchinson "
+                          "variance 2 (||exp A||_F^2 - sum exp(A)_ii^2) per probe"}
     if config != "sf1m":
         return None
     try:
@@ -471,6 +487,9 @@ def main():
             extra["reference_trace"] = ref
             extra["rel_err"] = (tr - ref["value"]) / ref["value"]
             extra["err_in_stderr"] = (tr - ref["value"]) / tr_stderr if tr_stderr else None
+            if "hutchinson_stderr_per_probe" in ref:  # the estimator's true standard error
+                extra["err_in_true_stderr"] = (tr - ref["value"]) / (ref["hutchinson_stderr_per_probe"] /
+                                                                     math.sqrt(N))
             extra["evaluations"]["rel_err"] = [(e - ref["value"]) / ref["value"] for e in ests]
             extra["evaluations"]["pooled_rel_err"] = (pooled - ref["value"]) / ref["value"]
 
@@ -531,14 +550,13 @@ def _reference_composition(kra, D, ctx, A, ref, budget_s):
       * on the GPU, once: kt_mc_trace with the device expmv Afun, serial
         (KT_TWIN=0, KT_MC_SPEC=0: every expmv call on this context, counted
         by kt_context_stat 3 / 4);
-      * SURVEY §8d plan (i)'s CPU baseline: the oracle's numpy/SciPy
-        restatement of the same algorithm (oracle/krylov_oracle.py: expmv,
-        select_taylor_degree; SciPy's sparse @ dense is single-threaded),
-        timed on a bounded sample -- one select_taylor_degree call and the
-        first Taylor terms (expmv.m:75-82) of one 10-column expmv call --
-        and extrapolated with the GPU run's call and term counts.  mc_trace's
-        own host work (QR, projections) is left out: a lower bound on the
-        CPU time."""
+      * SURVEY §8d plan (i)'s CPU baseline, the same algorithm restated in C
+        + OpenMP (oracle/mctrace_ref.c) on every CPU this process may use:
+        one whole expmv call (round 1's S block, every stage and term) and a
+        round's host work (qr, projection), extrapolated from that whole call
+        to the GPU run's call / term / round counts; beside it the numpy /
+        SciPy restatement (oracle/krylov_oracle.py) on one thread, a shorter
+        sample (one select_taylor_degree call, the first Taylor terms)."""
     from oracle import krylov_oracle as O
     saved = {k: os.environ.get(k) for k in ("KT_TWIN", "KT_MC_SPEC")}
     os.environ["KT_TWIN"] = "0"
@@ -563,7 +581,38 @@ def _reference_composition(kra, D, ctx, A, ref, budget_s):
         out["rel_err"] = (tr - ref["value"]) / ref["value"]
     Acsr = A.tocsr()
     n = Acsr.shape[0]
-    b = O.rademacher(n, range(10), 0)
+    # (1) the C + OpenMP restatement of the same algorithm (oracle/mctrace_ref.c)
+    # on every CPU this process may use: round 1's first Afun call -- one
+    # whole expmv call, every stage and term, on S_1 (mc_trace.m:43-45) --
+    # and the host work of a round (qr(., 0), one projection), extrapolated
+    # to the GPU run's calls, terms, rounds and projections
+    from oracle import mctrace_ref as MR
+    cores, detail = cpu_share()
+    S1 = O.rademacher(n, range(10), 0)
+    t0 = time.perf_counter()
+    _, s_c, m_c, mv_c, st = MR.expmv(1.0, Acsr, S1, nthreads=cores)
+    call_s = time.perf_counter() - t0
+    t_qr, t_proj = MR.round_host_times(n, seed=0, nthreads=cores)
+    t_term = st["t_terms"] / max(st["terms"], 1)
+    nproj = sum(6 * r - 4 for r in range(1, it + 1))  # block projections of `it` nested rounds
+    est = calls * st["t_select"] + terms * t_term + it * t_qr + nproj * t_proj
+    out["cpu_baseline"] = {
+        "value": 1.0 / est if est > 0 else None, "unit": "evals/s", "cores": cores, "kind": "port",
+        "algorithm": "the reference's: mc_trace + expmv + select_taylor_degree + normAm "
+                     "(oracle/mctrace_ref.c, C + OpenMP over rows; equals the numpy restatement)",
+        "seconds_per_eval": round(est, 2),
+        "sample": f"one whole expmv call (round 1's S block: s = {s_c}, m = {m_c}, {st['terms']} Taylor terms, "
+                  f"select_taylor_degree {st['t_select']:.2f} s, {call_s:.1f} s in all) and one qr(., 0) "
+                  f"({t_qr:.3f} s) + one projection ({t_proj:.3f} s) of an n x 10 block on {cores} OpenMP "
+                  f"threads, extrapolated from that whole call to the GPU run's {calls} expmv calls, {terms} "
+                  f"Taylor terms, {it} rounds and {nproj} projections",
+        "sample_call": {"s": s_c, "m": m_c, "terms": st["terms"], "mv": mv_c, "seconds": round(call_s, 3),
+                        "select_taylor_degree_s": round(st["t_select"], 3), "term_s": round(t_term, 5)},
+        "qr_s": round(t_qr, 4), "projection_s": round(t_proj, 4), **detail}
+    # (2) beside it, the numpy/SciPy restatement (oracle/krylov_oracle.py) on ONE
+    # thread (SciPy's sparse @ dense is single-threaded), a shorter sample: one
+    # select_taylor_degree call and the first Taylor terms of one 10-column call
+    b = S1.copy()
     t0 = time.perf_counter()
     O.select_taylor_degree(Acsr, b)
     t_sel = time.perf_counter() - t0
@@ -578,16 +627,16 @@ def _reference_composition(kra, D, ctx, A, ref, budget_s):
         c2 = np.max(np.sum(np.abs(b), axis=1))  # the stop test's norms, expmv.m:79-80
         nf = np.max(np.sum(np.abs(f), axis=1))
         ratio = c2 / nf if nf > 0 else ratio
-    t_term = (time.perf_counter() - t0) / k
-    est = calls * t_sel + terms * t_term
-    out["cpu_baseline"] = {
-        "value": 1.0 / est if est > 0 else None, "unit": "evals/s", "cores": 1, "kind": "port",
-        "algorithm": "the reference's: mc_trace + expmv (oracle/krylov_oracle.py restatement)",
-        "seconds_per_eval": round(est, 1), "select_taylor_degree_s": round(t_sel, 3),
-        "taylor_term_s": round(t_term, 4), "sample_last_c2_over_normf": ratio,
+    t_term1 = (time.perf_counter() - t0) / k
+    est1 = calls * t_sel + terms * t_term1
+    out["cpu_baseline_scipy_1thread"] = {
+        "value": 1.0 / est1 if est1 > 0 else None, "unit": "evals/s", "cores": 1, "kind": "port",
+        "algorithm": "the reference's: mc_trace + expmv (oracle/krylov_oracle.py restatement, SciPy)",
+        "seconds_per_eval": round(est1, 1), "select_taylor_degree_s": round(t_sel, 3),
+        "taylor_term_s": round(t_term1, 4), "sample_last_c2_over_normf": ratio,
         "sample": f"one select_taylor_degree call ({t_sel:.1f} s) and {k} Taylor terms on a 10-column "
-                  f"block ({t_term:.3f} s each), one thread (SciPy sparse @ dense), extrapolated to the "
-                  f"GPU run's {calls} expmv calls and {terms} Taylor terms"}
+                  f"block ({t_term1:.3f} s each), one thread, extrapolated to the GPU run's {calls} expmv "
+                  f"calls and {terms} Taylor terms (mc_trace's QR and projections left out: a lower bound)"}
     return out
 
 
@@ -606,6 +655,7 @@ def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev,
         return kra.mc_trace("lanczos", None, 1e-4, 1000, 1, 0, seed=seed, fun="exp", m=m, A=D, ctx=ctx)
 
     one(1000)  # warm-up: twin matrices, workspaces
+    redone0 = ctx.yform_redone()
     barrier()
     t0 = time.perf_counter()
     res = [one(s) for s in range(steps)]
@@ -617,6 +667,7 @@ def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev,
            "timed_evals": steps, "trace_estimate": tr, "rounds": it, "res": r_last,
            "rounds_per_eval": [r[2] for r in res],
            "probe_columns_per_eval": 30 * it,
+           "yform_redone_sweeps": ctx.yform_redone() - redone0,
            "probe_columns_basis": "per round: 10 S columns, the 10 columns of Q, 10 G columns "
                                   "(mc_trace.m:43-49), each one m-step Lanczos run"}
     if ref:

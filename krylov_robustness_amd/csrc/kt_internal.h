@@ -199,6 +199,10 @@ struct Workspace {
     PinnedBuf pair_active_host;
     DevBuf ts_V, ts_part, ts_small;  // tall-skinny Householder QR (kt_tsqr.hip)
     DevBuf ts_pub, ts_bar;           // its persistent form (k_ts_qr): hand-off slots, barrier words
+    // lanczos_columns_split (kt_slq.cpp): pinned sweep records, the y-form
+    // start scales per lane, the permuted block's ready event for the aux lanes
+    PinnedBuf pin_colrec, pin_ycoef[4];
+    hipEvent_t colsplit_ev = nullptr;
 };
 
 }  // namespace kt

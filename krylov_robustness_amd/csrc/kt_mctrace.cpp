@@ -574,21 +574,31 @@ static void project_ld(kt_context_s* ctx, int64_t n, const double* Q, int ldq, i
     combine(ctx, n, Q, ldq, nq, G, nc, 1.0, X, ldx);
 }
 
-// mc_trace.m:42-58 with the Lanczos-f Afun, one probe sweep per round.  The
-// round's Q term (:46), its G term (:49) and the NEXT round's S term
+// mc_trace.m:42-58 with the Lanczos-f Afun, one batch of sweeps per round.
+// The round's Q term (:46), its G term (:49) and the NEXT round's S term
 // (:43-45, which needs only Q_1..Q_it) are independent Afun calls, so their
-// 30 columns share one Lanczos sweep (P = 32: per nonzero one 256-B probe-row
+// 30 columns share one explicit 32-wide sweep (per nonzero one 256-B probe-row
 // gather and one CSR pass instead of three 128-B gathers and three CSR
-// passes); round 1's S term runs alone.  Same probes, same projections in
-// the same order, and each column's Lanczos recurrence does not depend on
-// its neighbours in the sweep -- only the sweep width (the reduction grid)
-// differs from the per-call form, so the estimate agrees to rounding.  The
-// S term computed in the stopping round is discarded (mc_trace never stops
-// in round 1, so round 2's is always used).  KT_MC_BATCH=0: per-call form.
+// passes), the basis kept for the 10 S columns whose f(A) x feeds the next
+// qr (:45).  Round 1's S term runs alone.
+//
+// The next round's S term is computed ahead in round `it` unless the round
+// is expected to stop the loop: |trace(G' Afun G)/m| of the previous round
+// below tol |tr_new| (the deflated remainder is already below the stopping
+// tolerance; on the config-4 graph, rank one to 1e-23, round 2 always
+// stops).  Such a round runs only its Q and G terms: Q by a 16-wide explicit
+// sweep, G -- quadratic forms of random probes, mc_trace.m:49 -- by y-form
+// sweeps (one pass per Lanczos step, no K2 stream) beside it on another
+// lane.  A wrong guess moves the S term to the start of the next round;
+// mc_trace never stops in round 1 (tr_old = 0), so round 2's S term is always
+// computed ahead.
+//
 // Multi-GPU (sh.allreduce set): S and Q replicated, G column c on rank
-// c % world, the 10 G forms all-reduced once per round and summed in column
-// order.  A column's form does not depend on the other columns of its
-// 32-wide sweep, so every world size gives the world-1 estimate bit for bit.
+// c % world in one of 10 fixed G slots (the others zero), the 10 G forms
+// all-reduced once per round and summed in column order.  The sweep widths
+// depend only on the slot layout and on the guess (made from all-reduced
+// sums, the same on every rank), never on the rank count, so every world size
+// gives the world-1 estimate bit for bit.
 static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int maxit, uint64_t seed,
                              double* tr_out, double* res_out, int* it_out, const Shard& sh) {
     kt_context_s* ctx = A->ctx;
@@ -599,18 +609,26 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
     double tr = 0.0, tr_old = 0.0, tr_new = 0.0, res = 1.0;
     std::vector<DevMat> Qs;
     DevMat Bk, Yb, T;
-    Bk.alloc(ctx, n, LB);  // [S_{it+1} | P..P Q_it | P..P G_it | 0 0]
+    Bk.alloc(ctx, n, LB);  // [S_{it+1} | P..P Q_it | P..P G_it (10 slots) | 0 0]
     Yb.alloc(ctx, n, ld);  // Afun_it(S_it), then Q_it in place
     T.alloc(ctx, n, ld);   // Rademacher columns before they enter the block
-    zero_cols(ctx, n, Bk.col(3 * mb), LB, LB - 3 * mb);
     auto rademacher_into = [&](int64_t base, double* dst) {
         KT_HIP(launch_rademacher(ld, (int)n, seed, base, nullptr, T.col(0), st));
         copy_cols(ctx, n, T.col(0), ld, dst, LB, mb);
     };
-    // round 1's S term alone: Y_1 = F(S_1)                                   :43-45
-    rademacher_into(0, Bk.col(0));
-    lanczos_columns_mixed(A, Bk.col(0), LB, mb, F.m, F.fun, nullptr, Yb.col(0), ld, mb, 16);
+    // S term of round itx: Y = F(P_{itx-1}..P_1 S_itx) into Yb (unprojected)
+    auto s_term = [&](int itx) {
+        rademacher_into((int64_t)(itx - 1) * 2 * mb, Bk.col(0));
+        for (int k = (int)Qs.size() - 1; k >= 0; --k) project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(0), LB, mb);
+        lanczos_columns_split(A, Bk.col(0), LB, mb, mb, mb, F.m, F.fun, nullptr, Yb.col(0), ld, 16);
+    };
+    s_term(1);                                                             // :43-45
     std::vector<double> q(3 * mb);
+    double gprev = INFINITY;  // |trace(G' Afun G)/m| of the previous round
+    // KT_MC_AHEAD (tests): 1 always compute the next S term ahead, 0 never
+    // (each round starts with its own), unset: the guess above
+    const char* ae = getenv("KT_MC_AHEAD");
+    const int ahead_mode = ae ? (ae[0] == '1' ? 1 : 0) : -1;
     int it = 0;
     for (it = 1; it <= K; ++it) {
         const int64_t base = (int64_t)(it - 1) * 2 * mb;
@@ -628,14 +646,20 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
         for (int c = sh.rank; c < mb; c += sh.world) copy_cols(ctx, n, T.col(c), ld, Bk.col(2 * mb + ng++), LB, 1);
         for (int k = (int)Qs.size() - 1; k >= 0 && ng > 0; --k)
             project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(2 * mb), LB, ng);
-        // next round's S term input: P_it..P_1 S_{it+1}
-        const bool next = it < K;
-        if (next) {
+        // next round's S term input: P_it..P_1 S_{it+1}, unless this round is
+        // expected to stop
+        const bool ahead = it < K && (ahead_mode == 1 || (ahead_mode < 0 && (it == 1 || !(gprev < tol * std::fabs(tr_new)))));
+        if (ahead) {
             rademacher_into(base + 2 * mb, Bk.col(0));
             for (int k = (int)Qs.size() - 1; k >= 0; --k) project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(0), LB, mb);
-            lanczos_columns_mixed(A, Bk.col(0), LB, 2 * mb + ng, F.m, F.fun, q.data(), Yb.col(0), ld, mb, LB);
+            // one explicit 32-wide sweep [S | Q | G]: per nonzero one 256-B row
+            // gather and one CSR pass for the three Afun calls
+            lanczos_columns_split(A, Bk.col(0), LB, 3 * mb, mb, 3 * mb, F.m, F.fun, q.data(), Yb.col(0), ld, LB);
         } else {
-            lanczos_columns_mixed(A, Bk.col(mb), LB, mb + ng, F.m, F.fun, q.data() + mb, nullptr, 0, 0, LB);
+            // no S term: Q by the explicit sweep (16 wide; its columns start
+            // near the deflated operator's top eigenvectors, where the y-form's
+            // cancellation guard trips), G (random probes) by y-form sweeps
+            lanczos_columns_split(A, Bk.col(mb), LB, 2 * mb, 0, mb, F.m, F.fun, q.data() + mb, nullptr, 0, 16);
         }
         std::vector<double> qv(mb, 0.0);
         for (int c = sh.rank, t = 0; c < mb; c += sh.world, ++t) qv[c] = q[2 * mb + t];
@@ -646,11 +670,15 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
         for (double v : qv) gsum += v;
         tr += qsum;
         tr_new = tr + gsum / mb;                                           // :49
+        gprev = std::fabs(gsum / mb);
         res = std::fabs(tr_new - tr_old) / std::max(std::fabs(tr_new), std::fabs(tr_old));  // :50
         if (res < tol) break;                                              // :54-56
         tr_old = tr_new;
-        if (next)  // Y_{it+1} = P_1..P_it F(P_it..P_1 S_{it+1})              :45, :48
+        if (it < K) {
+            if (!ahead) s_term(it + 1);  // the guess was wrong: the S term now
+            // Y_{it+1} = P_1..P_it F(P_it..P_1 S_{it+1})                     :45, :48
             for (size_t k = 0; k < Qs.size(); ++k) project_ld(ctx, n, Qs[k].col(0), ld, mb, Yb.col(0), ld, mb);
+        }
     }
     if (it > K) it = K;
     *tr_out = tr_new;

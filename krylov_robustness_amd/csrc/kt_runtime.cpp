@@ -385,6 +385,7 @@ int kt_context_destroy(kt_context_t ctx) {
     if (w.comb_ev) (void)hipEventDestroy(w.comb_ev);
     if (w.qrfac_ev) (void)hipEventDestroy(w.qrfac_ev);
     if (w.qrm_ev) (void)hipEventDestroy(w.qrm_ev);
+    if (w.colsplit_ev) (void)hipEventDestroy(w.colsplit_ev);
     for (auto& b : w.host_trec) b.release();
     for (auto& pd : w.slq_pend)
         for (auto& e : pd.done)

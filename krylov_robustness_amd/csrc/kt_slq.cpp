@@ -233,6 +233,74 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     KT_HIP(hipMemcpyAsync(rec_host, trec, sizeof(double) * rec, hipMemcpyDeviceToHost, st));
 }
 
+// y-form sweep seeded by a given device block (the quadrature-only columns
+// of mc_trace's Lanczos Afun, kt_mctrace.cpp): x (n x ldx, ncols columns, in
+// M's row order, squared norms norms2) is normalised into the gathered table
+// v_0 (zero columns stay zero), the pass in start mode forms y_0 = A v_0 with
+// (g, a, b) = (1, 0, 0), then the same passes as the RNG-seeded sweep.
+// rec_host (pinned, or the call waits for the copy) receives [alpha | up |
+// low][m][P] followed by guard[P].  No basis: quadratic forms only.
+void lanczos_sweep_y_block(kt_matrix_s* A, const DevCSR& M, int P, int m, const double* x, int ldx, int ncols,
+                           const double* norms2, double* rec_host, int lane) {
+    kt_context_s* ctx = A->ctx;
+    const int n = (int)A->n;
+    if (lane < 0 || lane > 3) fail(KT_ERR_ARG, "sweep lane out of range");
+    if (ncols < 1 || ncols > P) fail(KT_ERR_ARG, "y-form block sweep: 1 <= ncols <= P");
+    if (lane && !ctx->aux_stream[lane - 1])
+        KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[lane - 1], hipStreamNonBlocking));
+    hipStream_t st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
+    const int grid = spmm_grid(n, P, ctx->num_cu * 4);
+    const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
+    const int grid1 = grid + lblocks;
+    SweepBufs& w = ctx->ws.sweep[lane];
+    const size_t blk_bytes = sizeof(double) * (size_t)n * P;
+    w.X0.ensure(blk_bytes);
+    w.X1.ensure(blk_bytes);
+    w.Y.ensure(blk_bytes);
+    w.partial.ensure(sizeof(double) * (size_t)3 * P * grid1);
+    w.coef.ensure(sizeof(double) * 9 * P);
+    const size_t rec = (size_t)3 * m * P + P;
+    w.trec.ensure(sizeof(double) * rec);
+    double* part = w.partial.as<double>();
+    double* ys = w.coef.as<double>();
+    double* trec = w.trec.as<double>();
+    double* guard = trec + (size_t)3 * m * P;
+    auto rec_at = [&](int row, int j) { return trec + (size_t)(row * m + j) * P; };
+    int flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
+    if (blk_bytes >= ((size_t)1 << 31)) flags &= ~16;
+    // ys: [1/||x_c|| (P) | 0 (5P) | start pass (g, a, b) = (1, 0, 0) (3P)]
+    PinnedBuf& hb = ctx->ws.pin_ycoef[lane];
+    hb.ensure(sizeof(double) * 9 * P);
+    double* h = hb.as<double>();
+    KT_HIP(hipStreamSynchronize(st));  // the lane's previous upload out of hb is done
+    std::fill(h, h + 9 * P, 0.0);
+    for (int c = 0; c < ncols; ++c)
+        if (norms2[c] > 0.0) h[c] = 1.0 / std::sqrt(norms2[c]);
+    for (int c = 0; c < P; ++c) h[6 * P + c] = 1.0;
+    KT_HIP(hipMemcpyAsync(ys, h, sizeof(double) * 9 * P, hipMemcpyHostToDevice, st));
+    double* V0 = w.X1.as<double>();  // the start pass's gathered table v_0
+    KT_HIP(hipMemsetAsync(V0, 0, blk_bytes, st));
+    KT_HIP(launch_weighted_sum(n, 1, P, ncols, x, ldx, 0, ys, V0, P, st));
+    double* Xc = w.Y.as<double>();   // y_j
+    double* Yo = nullptr;            // y_{j-1}
+    double* Ot = w.X0.as<double>();  // y_{j+1}
+    KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, V0, nullptr, Xc, ys + 6 * P, part,
+                               M.long_rows, M.n_long, A->long_thresh, lblocks, st, nullptr));
+    KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, 1.0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0), guard, st));
+    for (int j = 0; j + 1 < m; ++j) {
+        const bool last = j + 2 == m;
+        KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
+                                   last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long, A->long_thresh,
+                                   lblocks, st, nullptr));
+        KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1),
+                            rec_at(2, j + 1), guard, st));
+        Yo = Xc;
+        Xc = Ot;
+        Ot = Yo;
+    }
+    KT_HIP(hipMemcpyAsync(rec_host, trec, sizeof(double) * rec, hipMemcpyDeviceToHost, st));
+}
+
 // A y-form probe is accepted when every used beta_k^2 kept at least this
 // fraction of ||y_{k-1}||^2 (its Gram-identity cancellation then costs at most
 // ~1e4 ulp); otherwise its sweep is recomputed by the explicit CGS2 sweep.
@@ -256,20 +324,32 @@ int record_tridiag(const double* R, int m, int P, int c, double* al, double* off
 
 void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m, int fun,
                      double* quad, double* Y, int ldy) {
-    lanczos_columns_mixed(A, X, ldx, ncols, m, fun, quad, Y, ldy, Y ? ncols : 0, 16);
+    // every column by the explicit sweep (P = pow2 >= ncols, <= 16)
+    lanczos_columns_split(A, X, ldx, ncols, Y ? ncols : 0, ncols, m, fun, quad, Y, ldy, 0);
 }
 
-void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, int m, int fun,
-                           double* quad, double* Y, int ldy, int ny, int pmax) {
+// Widths of the y-form sweeps for `cols` quadrature-only columns: sweeps of
+// 16, the last zero-padded.  At config 4 the final mc_trace round's 10 G
+// columns as one padded 16-wide sweep beside the Q sweep: 52.0 ms per
+// trace_exp, vs 54.5 as 8 + 2 and 57.0 with every column in one explicit
+// 32-wide sweep (profiles/r05/mc_layout_ab/) -- a narrow pass costs about
+// what a 16-wide one does (its gathers are latency, not bytes).
+static std::vector<int> quad_plan(int cols) {
+    std::vector<int> wv;
+    for (int left = cols; left > 0; left -= 16) wv.push_back(16);
+    return wv;
+}
+
+void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, int ny, int ne, int m, int fun,
+                           double* quad, double* Y, int ldy, int px) {
     kt_context_s* ctx = A->ctx;
     const int64_t n = A->n;
     if (!Y) ny = 0;
+    if (ny < 0 || ny > ne || ne > ncols) fail(KT_ERR_ARG, "lanczos_columns_split: 0 <= ny <= ne <= ncols");
     std::vector<double> nrm2;
     gram(ctx, n, X, ldx, ncols, X, ldx, ncols, nrm2);
     std::vector<double> norms2(ncols);
     for (int c = 0; c < ncols; ++c) norms2[c] = nrm2[c + (size_t)c * ncols];
-    int P = 1;
-    while (P < ncols && P < pmax) P <<= 1;
     // The sweeps run on the hubs-first CSR (equal-length neighbouring rows,
     // adjacent hub segments: the explicit K1 at P = 16 on the bench graph 264
     // -> ~210 us): the block is permuted into that row order on the way in
@@ -295,28 +375,93 @@ void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, 
             ldys = ny;
         }
     }
-    for (int c0 = 0; c0 < ncols; c0 += P) {
-        const int nc = std::min(P, ncols - c0);
-        const int nyc = std::max(0, std::min(nc, ny - c0));  // columns of this sweep that need f(A) x
-        std::vector<double> rec((size_t)3 * m * P);
-        DevMat basis;
-        std::vector<double> hist;
-        // the basis keeps only the nyc columns whose f(A) x is wanted (slot j
-        // = an n x nyc block at basis.col(0) + j n nyc): a 30-column sweep
-        // with 10 such columns stores and re-reads a third of the bytes
-        if (nyc) basis.alloc(ctx, n, m * nyc, false);  // every slot is written by the sweep
-        lanczos_sweep(A, M, P, m, 0, 0, Xs + c0, ldxs, nc, norms2.data() + c0, rec.data(),
-                      nyc ? &basis : nullptr, nyc ? &hist : nullptr, 0, nyc);
+    // Sweeps: columns [0, ne) by the explicit CGS2 sweep (P = px, or pow2 >=
+    // ne capped at 16), the basis kept for the ny f(A)x columns among them, on
+    // lane 0; columns [ne, ncols) -- quadratic forms only -- by y-form sweeps
+    // (no K2, no basis; widths quad_plan) on lanes 1..3.  All queued before the
+    // host waits, so the device runs them side by side.
+    struct Sw {
+        int c0, nc, P, lane;
+        bool yform;
+    };
+    std::vector<Sw> sw;
+    const char* ye = getenv("KT_LC_YFORM");  // 0: every column by the explicit sweep
+    if (ye && ye[0] == '0') ne = ncols;
+    int Pe = 1;
+    while (Pe < ne && Pe < 16) Pe <<= 1;
+    if (px > 0) Pe = px;
+    for (int c0 = 0; c0 < ne; c0 += Pe) sw.push_back({c0, std::min(Pe, ne - c0), Pe, 0, false});
+    {
+        int c0 = ne, k = 0;
+        for (int P : quad_plan(ncols - ne)) {
+            sw.push_back({c0, std::min(P, ncols - c0), P, 1 + (k++ % 3), true});
+            c0 += P;
+        }
+    }
+    const size_t rec_max = (size_t)3 * m * 32 + 32;
+    PinnedBuf& hr = ctx->ws.pin_colrec;
+    hr.ensure(sizeof(double) * rec_max * sw.size());
+    // the aux lanes read the permuted block written on ctx->stream
+    hipEvent_t ready = ctx->ws.colsplit_ev;
+    if (!ready) {
+        KT_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        ctx->ws.colsplit_ev = ready;
+    }
+    KT_HIP(hipEventRecord(ready, ctx->stream));
+    bool used[4] = {false, false, false, false};
+    for (size_t i = 0; i < sw.size(); ++i) {
+        const Sw& q = sw[i];
+        if (!q.yform) continue;
+        if (!used[q.lane]) {
+            hipStream_t& as = ctx->aux_stream[q.lane - 1];
+            if (!as) KT_HIP(hipStreamCreateWithFlags(&as, hipStreamNonBlocking));
+            KT_HIP(hipStreamWaitEvent(as, ready, 0));
+            used[q.lane] = true;
+        }
+        lanczos_sweep_y_block(A, M, q.P, m, Xs + q.c0, ldxs, q.nc, norms2.data() + q.c0,
+                              hr.as<double>() + rec_max * i, q.lane);
+    }
+    // the explicit sweeps (lane 0) with their bases
+    std::vector<DevMat> bases(sw.size());
+    std::vector<std::vector<double>> hists(sw.size());
+    for (size_t i = 0; i < sw.size(); ++i) {
+        const Sw& q = sw[i];
+        if (q.yform) continue;
+        const int nyc = std::max(0, std::min(q.nc, ny - q.c0));
+        if (nyc) bases[i].alloc(ctx, n, m * nyc, false);  // every slot is written by the sweep
+        lanczos_sweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, norms2.data() + q.c0,
+                      hr.as<double>() + rec_max * i, nyc ? &bases[i] : nullptr, nyc ? &hists[i] : nullptr, 0, nyc);
+    }
+    KT_HIP(hipStreamSynchronize(ctx->stream));
+    for (int l = 1; l < 4; ++l)
+        if (used[l]) KT_HIP(hipStreamSynchronize(ctx->aux_stream[l - 1]));
+    // a y-form sweep whose live column tripped the cancellation guard (or a
+    // lucky breakdown) is redone by the explicit CGS2 sweep (kt_slq_collect's rule)
+    for (size_t i = 0; i < sw.size(); ++i) {
+        const Sw& q = sw[i];
+        if (!q.yform) continue;
+        const double* g = hr.as<double>() + rec_max * i + (size_t)3 * m * q.P;
+        bool bad = false;
+        for (int c = 0; c < q.nc; ++c) bad |= norms2[q.c0 + c] > 0.0 && !(g[c] >= kYformGuard);
+        if (!bad) continue;
+        lanczos_sweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, norms2.data() + q.c0, hr.as<double>() + rec_max * i,
+                      nullptr, nullptr, 0);
         KT_HIP(hipStreamSynchronize(ctx->stream));
+        ctx->yform_redone += 1;
+    }
+    for (size_t i = 0; i < sw.size(); ++i) {
+        const Sw& q = sw[i];
+        const double* R = hr.as<double>() + rec_max * i;
+        const int nyc = q.yform ? 0 : std::max(0, std::min(q.nc, ny - q.c0));
         std::vector<double> W((size_t)m * std::max(nyc, 1), 0.0);  // weights for Y = sum_j u_j w_j, [j * nyc + c]
-        for (int c = 0; c < nc; ++c) {
+        for (int c = 0; c < q.nc; ++c) {
             std::vector<double> al(m), off(m);
-            const int steps = record_tridiag(rec.data(), m, P, c, al.data(), off.data());
-            if (norms2[c0 + c] == 0.0) {
-                if (quad) quad[c0 + c] = 0.0;
+            const int steps = record_tridiag(R, m, q.P, c, al.data(), off.data());
+            if (norms2[q.c0 + c] == 0.0) {
+                if (quad) quad[q.c0 + c] = 0.0;
                 continue;
             }
-            if (quad) quad[c0 + c] = norms2[c0 + c] * tridiag_quadrature(steps, al.data(), off.data(), fun);
+            if (quad) quad[q.c0 + c] = norms2[q.c0 + c] * tridiag_quadrature(steps, al.data(), off.data(), fun);
             if (c < nyc) {
                 // f(T) e1 = Z f(theta) Z(0,:)'
                 std::vector<double> T((size_t)steps * steps, 0.0), th(steps), Z((size_t)steps * steps);
@@ -324,22 +469,21 @@ void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, 
                 for (int j = 0; j + 1 < steps; ++j)
                     T[j + 1 + (size_t)j * steps] = T[j + (size_t)(j + 1) * steps] = off[j];
                 sym_eig_host(steps, T.data(), th.data(), Z.data());
-                const double nx = std::sqrt(norms2[c0 + c]);
+                const double nx = std::sqrt(norms2[q.c0 + c]);
                 for (int j = 0; j < steps; ++j) {
                     double cj = 0.0;
                     for (int k = 0; k < steps; ++k)
                         cj += Z[j + (size_t)k * steps] * fscalar(fun, th[k]) * Z[(size_t)k * steps];
-                    W[(size_t)j * nyc + c] = nx * hist[(size_t)j * P + c] * cj;  // v_j = s_j u_j
+                    W[(size_t)j * nyc + c] = nx * hists[i][(size_t)j * q.P + c] * cj;  // v_j = s_j u_j
                 }
             }
         }
         if (nyc) {
             DevBuf& dw = ctx->ws.small2;
             dw.ensure(sizeof(double) * W.size());
-            KT_HIP(hipMemcpyAsync(dw.ptr, W.data(), sizeof(double) * W.size(), hipMemcpyHostToDevice,
-                                  ctx->stream));
-            KT_HIP(launch_weighted_sum((int)n, m, nyc, nyc, basis.col(0), nyc, (int64_t)n * nyc,
-                                       dw.as<double>(), Ys + c0, ldys, ctx->stream));
+            KT_HIP(hipMemcpyAsync(dw.ptr, W.data(), sizeof(double) * W.size(), hipMemcpyHostToDevice, ctx->stream));
+            KT_HIP(launch_weighted_sum((int)n, m, nyc, nyc, bases[i].col(0), nyc, (int64_t)n * nyc, dw.as<double>(),
+                                       Ys + q.c0, ldys, ctx->stream));
             KT_HIP(hipStreamSynchronize(ctx->stream));
         }
     }

@@ -25,10 +25,20 @@ void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m,
                      double* quad, double* Y, int ldy);
 
 // lanczos_columns for a block whose first ny columns need f(A) x (into Y)
-// and every column its quadratic form: sweeps of up to pmax (power of two
-// <= 128) columns, the basis kept only for sweeps holding Y columns.  Lets
-// several Afun calls of mc_trace share one sweep (kt_mctrace.cpp).
-void lanczos_columns_mixed(kt_matrix_s* A, const double* X, int ldx, int ncols, int m, int fun,
-                           double* quad, double* Y, int ldy, int ny, int pmax);
+// and every column its quadratic form: columns [0, ne) by the explicit CGS2
+// sweep (sweeps of px columns, or pow2 >= ne capped at 16 when px = 0), the
+// basis kept for the ny f(A)x columns; columns [ne, ncols) -- quadratic
+// forms only -- by y-form sweeps (one pass per step, no K2, no basis) on the
+// extra sweep lanes, all queued together.  A column's form depends only on
+// the widths of the sweeps, which depend only on (ncols, ny, ne, px) -- not
+// on the values (zero columns included).  The y-form suits random probes;
+// columns that start close to an invariant subspace (mc_trace's Q) trip its
+// cancellation guard and belong in [0, ne).
+void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, int ny, int ne, int m, int fun,
+                           double* quad, double* Y, int ldy, int px = 0);
+
+// y-form sweep seeded by a device block (see kt_slq.cpp)
+void lanczos_sweep_y_block(kt_matrix_s* A, const DevCSR& M, int P, int m, const double* x, int ldx, int ncols,
+                           const double* norms2, double* rec_host, int lane);
 
 }  // namespace kt

@@ -269,3 +269,43 @@ def test_mc_trace_batched_rounds_match_per_call(kra, gpu_ctx, monkeypatch, name)
     if name != "oregon_A6":  # the numpy restatement at n = 10,860 x 5 rounds is slow
         tro, _, ito = ko.trace_exp_lanczos(A, m=20, tol=1e-8, maxit=150, seed=5)
         assert b[2] == ito and b[0] == pytest.approx(tro, rel=1e-10)
+
+
+@pytest.mark.parametrize("name", ["oregon_A0", "rome"])
+def test_mc_trace_next_s_term_guess_is_bit_identical(kra, gpu_ctx, monkeypatch, name):
+    """The Lanczos-Afun mc_trace computes the next round's S term ahead unless
+    the round is expected to stop (kt_mctrace.cpp mc_trace_batched); always
+    ahead (KT_MC_AHEAD=1), never ahead (0) and the guess give the same round
+    count and the estimate to rounding (a round with its S term ahead runs Q
+    and G in one 32-wide explicit sweep, one without runs Q 16 wide and G by
+    y-form sweeps: other reduction widths), over several rounds and a last
+    round it == K (tol = 0)."""
+    A = load_graph(name)
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    for tol, maxit in ((1e-8, 150), (0.0, 90)):
+        args = dict(n=A.shape[0], tol=tol, maxit=maxit, isAreal=1, seed=5, m=20)
+        monkeypatch.delenv("KT_MC_AHEAD", raising=False)
+        g = kra.mc_trace("lanczos", A=D, ctx=gpu_ctx, **args)
+        monkeypatch.setenv("KT_MC_AHEAD", "1")
+        a = kra.mc_trace("lanczos", A=D, ctx=gpu_ctx, **args)
+        monkeypatch.setenv("KT_MC_AHEAD", "0")
+        z = kra.mc_trace("lanczos", A=D, ctx=gpu_ctx, **args)
+        assert g[2] == a[2] == z[2] and g[2] > 1
+        assert a[0] == pytest.approx(g[0], rel=1e-12) and z[0] == pytest.approx(g[0], rel=1e-12)
+        if tol == 0.0:
+            assert g[2] == 3
+
+
+def test_mc_trace_quadrature_columns_yform_vs_explicit(kra, gpu_ctx, monkeypatch):
+    """The Q and G columns' forms by the y-form sweep (default) and by the
+    explicit CGS2 sweep (KT_LC_YFORM=0) agree to rounding (a y-form sweep
+    whose deflated column trips the cancellation guard is redone by the
+    explicit sweep, as kt_slq_collect does)."""
+    A = load_graph("oregon_A6")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    args = dict(n=A.shape[0], tol=1e-8, maxit=150, isAreal=1, seed=2, m=20)
+    y = kra.mc_trace("lanczos", A=D, ctx=gpu_ctx, **args)
+    monkeypatch.setenv("KT_LC_YFORM", "0")
+    x = kra.mc_trace("lanczos", A=D, ctx=gpu_ctx, **args)
+    assert y[2] == x[2]
+    assert y[0] == pytest.approx(x[0], rel=1e-11)
