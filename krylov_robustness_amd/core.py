@@ -22,7 +22,7 @@ class Context:
     def __init__(self, device: Optional[int] = None):
         lib = _lib.load()
         if device is None:
-            device = int(os.environ.get("KT_DEVICE", "0"))
+            device = 0
         h = C.c_void_p()
         _lib.check(lib.kt_context_create(int(device), C.byref(h)))
         self._h = h

@@ -102,23 +102,12 @@ void DevMat::release() {
     ctx = nullptr;
 }
 
-// KT_PINNED_STAGING=0: gram / combine / the thin QR move their small blocks
-// through pageable host memory with a sync each (the A/B switch)
-static bool pinned_staging() {
-    static const bool on = !(getenv("KT_PINNED_STAGING") && getenv("KT_PINNED_STAGING")[0] == '0');
-    return on;
-}
 
 void gram(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* Y,
           int ldy, int py, std::vector<double>& G) {
     G.assign((size_t)px * py, 0.0);
     if (px == 0 || py == 0 || n == 0) return;
     const double* d = gram_device(ctx, n, X, ldx, px, Y, ldy, py);
-    if (!pinned_staging()) {
-        KT_HIP(hipMemcpyAsync(G.data(), d, sizeof(double) * G.size(), hipMemcpyDeviceToHost, ctx->stream));
-        KT_HIP(hipStreamSynchronize(ctx->stream));
-        return;
-    }
     PinnedBuf& pb = ctx->ws.pin_gram;
     pb.ensure(sizeof(double) * G.size());
     KT_HIP(hipMemcpyAsync(pb.ptr, d, sizeof(double) * G.size(), hipMemcpyDeviceToHost, ctx->stream));
@@ -127,16 +116,11 @@ void gram(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const 
 }
 
 // gram / combine go through kt_gemm_ts.hip for tall blocks and through
-// rocBLAS dgemm below KT_GEMM_TS_MIN_N rows (default 8192): on India (n =
-// 3,228) the pipelined fun_update with the ts kernels stalled 20-30 ms at the
-// first stream operation of every call (profiles/r03_fg_exp_stall.txt), with
-// rocBLAS not.  KT_GEMM_ROCBLAS=1 forces rocBLAS for every n (A/B); read per call
+// rocBLAS dgemm below 8,192 rows: on India (n = 3,228) the pipelined
+// fun_update with the ts kernels stalled 20-30 ms at the first stream
+// operation of every call (profiles/r03_fg_exp_stall.txt), with rocBLAS not
 static bool rocblas_gemm_path(int64_t n) {
-    const char* e = getenv("KT_GEMM_ROCBLAS");
-    if (e && e[0] == '1') return true;
-    const char* m = getenv("KT_GEMM_TS_MIN_N");
-    const int64_t min_n = m ? std::atoll(m) : 8192;
-    return n < min_n;
+    return n < 8192;
 }
 
 const double* gram_device(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px, const double* Y,
@@ -211,15 +195,6 @@ void combine(kt_context_s* ctx, int64_t n, const double* X, int ldx, int px,
     // and the stream is not drained; the staging buffer is only rewritten once
     // the previous upload out of it has completed (event)
     const double one = 1.0;
-    if (!pinned_staging()) {
-        d.ensure(bytes);
-        KT_HIP(hipMemcpyAsync(d.ptr, C.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
-        rb(rocblas_dgemm(blas(ctx), rocblas_operation_transpose, rocblas_operation_none, q,
-                         (rocblas_int)n, px, &one, d.as<double>(), px, X, ldx, &beta, Y, ldy),
-           "rocblas_dgemm(combine)");
-        KT_HIP(hipStreamSynchronize(ctx->stream));  // the caller may free C right after
-        return;
-    }
     Workspace& ws = ctx->ws;
     if (ws.comb_pending) KT_HIP(hipEventSynchronize(ws.comb_ev));
     ws.comb_pending = false;
@@ -483,7 +458,7 @@ namespace kt {
 // 1e4), or whose scale is at a breakdown, takes householder_qr on the
 // untouched W: rank-deficient blocks keep LAPACK's reflectors and tau = 0
 // completions, which decide the reference's continuation.
-// KT_QR_CHOL=0 always takes householder_qr.
+
 static void apply_rinv(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, const std::vector<double>& R) {
     std::vector<double> Ri((size_t)bs * bs);
     tri_upper_inv(R.data(), bs, Ri.data());
@@ -564,8 +539,7 @@ static bool shifted_cholqr3(kt_context_s* ctx, int64_t n, double* W, int ld, int
 }
 
 void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R, bool allow_shifted) {
-    const char* e = std::getenv("KT_QR_CHOL");
-    if ((e && e[0] == '0') || n < 4 * (int64_t)bs || bs < 1) {
+    if (n < 4 * (int64_t)bs || bs < 1) {
         householder_qr(ctx, n, W, ld, bs, R);
         return;
     }
@@ -578,7 +552,7 @@ void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vect
         dmin = std::min(dmin, R1[k + (size_t)k * bs]);
     }
     if (!ok || !(dmin >= 1e-4 * dmax) || !(dmax > 1e-6)) {
-        // block Arnoldi (allow_shifted; KT_QR_SHIFTED=0 disables): an
+        // block Arnoldi (allow_shifted): an
         // ill-conditioned block that is not at a breakdown takes shifted
         // CholeskyQR3 (Fukaya et al.: Q orthonormal to O(eps) up to kappa ~
         // 1/eps) -- 3 Gram / combine passes instead of 2 bs + 3 Householder
@@ -593,17 +567,8 @@ void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vect
         // A block whose first plain Cholesky fails is left to Householder: on
         // Hawaii those blocks are exactly dependent, and both the shifted form
         // and a two-shift variant fail there and fall back, at +0.7-1 ms per
-        // call (profiles/r03_qr_paths.txt).  KT_QR_LOG=1 logs every block that
-        // leaves CholeskyQR2.
-        const char* se = std::getenv("KT_QR_SHIFTED");
-        static const bool qlog = std::getenv("KT_QR_LOG") != nullptr;
-        if (allow_shifted && !(se && se[0] == '0') && dmax > 1e-6 && shifted_cholqr3(ctx, n, W, ld, bs, R)) {
-            if (qlog) fprintf(stderr, "[kt qr] shifted cholqr3 bs %d\n", bs);
-            return;
-        }
-        if (qlog)
-            fprintf(stderr, "[kt qr] householder bs %d (%s, chol %s, dmin/dmax %.2e)\n", bs,
-                    allow_shifted ? "block Arnoldi" : "block Lanczos", ok ? "ok" : "failed", ok ? dmin / dmax : 0.0);
+        // call (profiles/r03_qr_paths.txt).
+        if (allow_shifted && dmax > 1e-6 && shifted_cholqr3(ctx, n, W, ld, bs, R)) return;
         householder_qr(ctx, n, W, ld, bs, R);
         return;
     }
@@ -642,14 +607,10 @@ void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std
     double* taus = sums + BP;
     double* Md = taus + BP;
     KT_HIP(hipMemsetAsync(V, 0, sizeof(double) * (size_t)n * BP, ctx->stream));
-    // the reflector sweep: two launches per column; KT_TSQR_PERSIST=1 runs it as
-    // one persistent launch (k_ts_qr, bit-identical) where the row blocks fit
-    // LDS -- measured slower (config 3 fun_and_grad 17.9 vs 17.0 ms: two grid
-    // barriers per column cost more than the two launches, profiles/r02_tsqr_persistent.txt)
-    const char* pe = std::getenv("KT_TSQR_PERSIST");
-    const int pgrid = (pe && pe[0] == '1') ? ts_qr_grid((int)n, BP, ctx->num_cu) : 0;
-    int rpw_q1 = 0;
-    const int qgrid1 = (pe && pe[0] == '2') ? ts_qr1_grid((int)n, BP, ctx->num_cu, &rpw_q1) : 0;
+    // the reflector sweep: two launches per column (the persistent forms with
+    // one or two grid barriers per column measured slower, config 3
+    // fun_and_grad 17.9 vs 17.0 ms, profiles/r02_tsqr_persistent.txt, and
+    // were dropped in round 5).
     // KT_TSQR_STEP1=1: one launch per column (k_ts_step1) where its grid fits
     // (n <= 49,152) -- measured equal to the two-launch form (config 3: 13.05
     // us per column launch vs 8.43 + 5.01 us, fun_and_grad 9.6-10.0 vs
@@ -658,44 +619,28 @@ void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std
     // inside one launch, so it stays opt-in
     const char* s1e = std::getenv("KT_TSQR_STEP1");
     int rpw1 = 0;
-    const int g1 = (pgrid == 0 && qgrid1 == 0 && s1e && s1e[0] == '1') ? ts_step1_grid((int)n, &rpw1) : 0;
-    if (qgrid1 > 0) {
-        ws.ts_pub.ensure(sizeof(double) * ts_qr1_pub_doubles((int)n, BP, ctx->num_cu));
-        ws.ts_bar.ensure(ts_qr_bar_bytes());
-        KT_HIP(launch_ts_qr1((int)n, bs, BP, ctx->num_cu, W, ld, V, ws.ts_pub.as<double>(), taus, ws.ts_bar.ptr,
-                             ctx->stream));
-    } else if (g1 > 0) {
+    const int g1 = (s1e && s1e[0] == '1') ? ts_step1_grid((int)n, &rpw1) : 0;
+    if (g1 > 0) {
         ws.ts_part.ensure(sizeof(double) * ((size_t)2 * BP * g1 + 2 * (size_t)BP));
         double* part1 = ws.ts_part.as<double>();
         KT_HIP(launch_ts_reflectors1((int)n, bs, BP, W, ld, V, part1, part1 + (size_t)2 * BP * g1, taus,
                                      ctx->stream));
-    } else if (pgrid > 0) {
-        ws.ts_pub.ensure(sizeof(double) * ts_qr_pub_doubles((int)n, BP, ctx->num_cu));
-        ws.ts_bar.ensure(ts_qr_bar_bytes());
-        KT_HIP(launch_ts_qr((int)n, bs, BP, ctx->num_cu, W, ld, V, ws.ts_pub.as<double>(), taus, ws.ts_bar.ptr,
-                            ctx->stream));
     } else {
         KT_HIP(launch_ts_reflectors((int)n, bs, BP, W, ld, V, pivot, sums, ws.ts_part.as<double>(), taus,
                                     ctx->num_cu, ctx->stream));
     }
     // R's rows, V's top block and the taus come back through pinned staging
     // (asynchronous); gram's synchronisation covers them
-    ws.pin_qr.ensure(sizeof(double) * ((size_t)bs * bs + (size_t)bs * BP + bs + 1));
+    ws.pin_qr.ensure(sizeof(double) * ((size_t)bs * bs + (size_t)bs * BP + bs));
     double* ptop = ws.pin_qr.as<double>();
     double* pV1 = ptop + (size_t)bs * bs;
     double* ptau = pV1 + (size_t)bs * BP;
-    unsigned* ptmo = reinterpret_cast<unsigned*>(ptau + bs);
-    *ptmo = 0;
-    if (pgrid > 0 || qgrid1 > 0)
-        KT_HIP(hipMemcpyAsync(ptmo, static_cast<char*>(ws.ts_bar.ptr) + ts_qr_tmo_offset(), sizeof(unsigned),
-                              hipMemcpyDeviceToHost, ctx->stream));
     KT_HIP(hipMemcpy2DAsync(ptop, sizeof(double) * bs, W, sizeof(double) * ld, sizeof(double) * bs, (size_t)bs,
                             hipMemcpyDeviceToHost, ctx->stream));
     KT_HIP(hipMemcpyAsync(pV1, V, sizeof(double) * (size_t)bs * BP, hipMemcpyDeviceToHost, ctx->stream));
     KT_HIP(hipMemcpyAsync(ptau, taus, sizeof(double) * bs, hipMemcpyDeviceToHost, ctx->stream));
     std::vector<double> G;  // V' V (bs x bs), gram synchronises the stream
     gram(ctx, n, V, BP, bs, V, BP, bs, G);
-    if (*ptmo) fail(KT_ERR_HIP, "thin QR: a grid barrier of the persistent reflector sweep timed out");
     const std::vector<double> top(ptop, ptop + (size_t)bs * bs), V1(pV1, pV1 + (size_t)bs * BP),
         tau(ptau, ptau + bs);
     for (int i = 0; i < bs; ++i)

@@ -96,7 +96,7 @@ bool cholqr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector
 void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R);
 // block-Krylov thin QR: CholeskyQR2 where well conditioned, else householder_qr
 // allow_shifted: an ill-conditioned block may take shifted CholeskyQR3 instead
-// of the Householder sweep (block Arnoldi; KT_QR_SHIFTED=0 disables, kt_block.cpp)
+// of the Householder sweep (block Arnoldi, kt_block.cpp)
 void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R,
               bool allow_shifted = false);
 

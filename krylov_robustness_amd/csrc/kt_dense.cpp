@@ -395,11 +395,7 @@ constexpr int kColTridiagMinN = 96;
 
 void sym_eig_host(int n, const double* A, double* w, double* V /* nullable */) {
     if (n <= 0) return;
-    static const bool col_ok = [] {
-        const char* c = std::getenv("KT_EIG_COLTRIDIAG");
-        return !(c && c[0] == '0');
-    }();
-    if (!V && col_ok && n >= kColTridiagMinN) {
+    if (!V && n >= kColTridiagMinN) {
         std::vector<double> a(A, A + (size_t)n * n), e(n), v(n), p(n);
         static const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
         if (avx2) tridiag_lower_cols_avx2(n, a.data(), w, e.data(), v.data(), p.data());

@@ -85,7 +85,7 @@ void run_pair_batch(kt_matrix_s* A, int C, const int64_t* ei, const int64_t* ej,
     const int64_t n = A->n;
     const int cols = 2 * C;
     using clk = std::chrono::steady_clock;
-    static const bool timing = getenv("KT_PAIRS_TIMING") != nullptr;
+    constexpr bool timing = KT_DIAG != 0;
     double t_setup = 0, t_gpu = 0, t_host = 0;
     auto t0 = clk::now();
     auto lap = [&](double& acc) {
@@ -418,7 +418,7 @@ static void run_pairs_range(kt_matrix_s* A, const std::vector<int64_t>& pairs, s
                             const int64_t* ei, const int64_t* ej, const double* B, double tol, int it,
                             int fun, double* Xm, int* iter, int* lucky) {
     {
-        static const bool timing = getenv("KT_PAIRS_TIMING") != nullptr;
+        constexpr bool timing = KT_DIAG != 0;
         const auto t0 = std::chrono::steady_clock::now();
         (void)natural_csr_ordered(A);  // candidate kernels run on ctx->stream (side-stream work waits on its events)
         if (timing)
@@ -525,7 +525,7 @@ namespace {
 int64_t miobi_select(kt_matrix_s* A, std::vector<int64_t>& Ei, std::vector<int64_t>& Ej, int64_t m,
                      const double* B, double sg, double tol, int it, int make, std::vector<double>& xm,
                      double* value) {
-    static const bool timing = getenv("KT_PAIRS_TIMING") != nullptr;
+    constexpr bool timing = KT_DIAG != 0;
     using clk = std::chrono::steady_clock;
     xm.assign(m, 0.0);
     const auto t0 = clk::now();

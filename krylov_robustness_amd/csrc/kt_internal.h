@@ -11,6 +11,13 @@
 
 struct kt_matrix_s;
 
+// KT_DIAG (compile time, `make EXTRA=-DKT_DIAG=1`): the host-side phase
+// clocks of the block-Krylov, eigensolver and greedy drivers print to stderr
+// (2: every eigensolve too).  0 in every product build.
+#ifndef KT_DIAG
+#define KT_DIAG 0
+#endif
+
 namespace kt {
 
 void set_error(const std::string& msg);
@@ -127,7 +134,6 @@ enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_START = 2, PROF_NSLOTS = 3 };
 // run on two streams.
 struct SweepBufs {
     DevBuf X0, X1, Y, partial, coef, scales, k2s, trec;
-    DevBuf tick;  // arrival tickets of the fused coefficient step (zeroed when allocated)
 };
 
 // one host int the device may store to at system scope (fine-grained,
@@ -198,7 +204,6 @@ struct Workspace {
     DevBuf pair_hist, pair_state, pair_scratch, pair_active;  // device-mode candidate state
     PinnedBuf pair_active_host;
     DevBuf ts_V, ts_part, ts_small;  // tall-skinny Householder QR (kt_tsqr.hip)
-    DevBuf ts_pub, ts_bar;           // its persistent form (k_ts_qr): hand-off slots, barrier words
     // lanczos_columns_split (kt_slq.cpp): pinned sweep records, the y-form
     // start scales per lane, the permuted block's ready event for the aux lanes
     PinnedBuf pin_colrec, pin_ycoef[4];
@@ -213,16 +218,16 @@ struct kt_context_s {
     hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};  // extra probe-sweep lanes (lazy)
     int num_cu = 256;
     bool profile = false;
-    // KT_K1_FLAGS: bit 0 = non-temporal CSR streams in K1, bit 2 = deep gather
-    // issue, bit 3 = non-temporal y store (default: profiles/r01_sweep_nt.txt)
+    // K1 flags: bit 3 = non-temporal y store (bit 0 non-temporal CSR streams
+    // and bit 2 deep gather issue measured no better, profiles/r01_sweep_nt.txt)
     int k1_flags = 8;
-    bool k2_nt = true;  // KT_K2_NT=0 disables: K2 loads y and u_prev non-temporal
+    bool k2_nt = true;  // K2 loads y and u_prev non-temporal
     int64_t yform_redone = 0;  // y-form sweeps recomputed by the explicit sweep (guard)
     int64_t fu_dense = 0;      // fun_update calls that took the dense fallback (fun_update.m:85-90)
     int64_t fu_last_cols = 0;  // projected size of the last fun_update (n when dense)
     int64_t expmv_calls = 0;   // expmv_device calls (kt_expmv and the expmv Afun of mc_trace)
     int64_t expmv_terms = 0;   // Taylor terms those calls executed (one A b product each, expmv.m:75)
-    int ky_flags = 8;   // KT_KY_FLAGS: y-form pass flags (8 = nontemporal store of y_{j+1}, +0.3 %)
+    int ky_flags = 8;   // y-form pass flags (8 = nontemporal store of y_{j+1}, +0.3 %)
     bool yform = true;  // KT_SLQ_YFORM=0: the hot path runs the explicit K1/K2 sweep
     void* blas = nullptr;  // rocblas_handle, created on first block-Krylov use
     // a second context on the same device (own stream, rocBLAS handle and

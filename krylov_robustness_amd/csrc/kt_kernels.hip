@@ -89,10 +89,7 @@ template <int P> using GeoB = GeoW<P, (P >= 16) ? KT_BLK_VW : (P >= 2) ? 2 : 1>;
 // with sc1), which drops the line from the XCD's L2 instead of keeping it
 // (MI355X_MICROARCH.md: plain / nt stores keep the line), leaving L2 to the
 // gathered table.
-// FLAGS bit 5 (persistent expmv, k_expmv_run): the gathered block is loaded
-// write-through-coherent (sc1, bypassing this CU's L1), so a grid barrier needs
-// no acquire fence (cdna_hip_programming.md Guideline 16, R1 consume form).
-enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4, KF_NTY = 8, KF_SC1 = 16, KF_LDSC1 = 32 };
+enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4, KF_NTY = 8, KF_SC1 = 16 };
 
 // KT_KY_DIAG (diagnostic builds of the y-form pass only, tools/ky_diag.sh; their
 // results are wrong): 1 = gathers + own row, 2 = gathers only, 3 = row streams only
@@ -204,28 +201,10 @@ template <int FLAGS, class T> __device__ __forceinline__ T ld_stream(const T* p)
     else return *p;
 }
 
-typedef __attribute__((address_space(1))) unsigned long long kt_gu64_t;
-// one double, agent-scope relaxed (a global load with sc1: past this CU's L1)
-__device__ __forceinline__ double ld_sc1d(const double* p) {
-    return __longlong_as_double((long long)__hip_atomic_load((kt_gu64_t*)p, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st_sc1d(double* p, double v) {
-    __hip_atomic_store((kt_gu64_t*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-// VEC doubles of the gathered block: plain, or sc1 (KF_LDSC1)
+// VEC doubles of the gathered block
 template <int FLAGS, int VEC>
 __device__ __forceinline__ typename VecT<VEC>::T ld_gather(const double* p) {
-    if constexpr (FLAGS & KF_LDSC1) {
-        if constexpr (VEC == 1) return ld_sc1d(p);
-        else if constexpr (VEC == 2) return double2(ld_sc1d(p), ld_sc1d(p + 1));
-        else if constexpr (VEC == 4) return Dbl4{double2(ld_sc1d(p), ld_sc1d(p + 1)), double2(ld_sc1d(p + 2), ld_sc1d(p + 3))};
-        else return Dbl8{Dbl4{double2(ld_sc1d(p), ld_sc1d(p + 1)), double2(ld_sc1d(p + 2), ld_sc1d(p + 3))},
-                         Dbl4{double2(ld_sc1d(p + 4), ld_sc1d(p + 5)), double2(ld_sc1d(p + 6), ld_sc1d(p + 7))}};
-    } else {
-        return VecT<VEC>::load(p);
-    }
+    return VecT<VEC>::load(p);
 }
 
 // ---------------------------------------------------------------------------
@@ -460,7 +439,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
 }
 
 // One probe's coefficient step from the pass's three sums d0 = X.t,
-// d1 = X.Out, d2 = Out.Out (shared by k_ycoef and the fused pass tail).
+// d1 = X.Out, d2 = Out.Out.
 __device__ __forceinline__ void ycoef_probe(int p, int P, double d0, double d1, double d2, int start,
                                             int last, double s0, double* __restrict__ ys,
                                             double* __restrict__ t_alpha, double* __restrict__ t_up,
@@ -505,115 +484,6 @@ __device__ __forceinline__ void ycoef_probe(int p, int P, double d0, double d1, 
     ys[6 * P + p] = inv;
     ys[7 * P + p] = an * inv;
     ys[8 * P + p] = bn * inv;
-}
-
-// ---------------------------------------------------------------------------
-// Fused coefficient step (the default y-form path): the pass's workgroups
-// hand their 3P partial sums to the pass's LAST arriving workgroup, which
-// runs k_ycoef's recurrence itself -- no separate launch, so the next pass
-// of the sweep is not queued behind another lane's workgroups for CU slots
-// (26 us per k_ycoef under two lanes vs 4.5 us alone, profiles/r02_timeline).
-// Two levels keep the serial tail short: workgroups of a group of
-// kTickGroup consecutive ids -> the group's last arriver sums the group's
-// slabs in id order; group sums -> the last group reducer sums them in group
-// order.  Fixed orders: bitwise reproducible whatever the arrival order.
-// Hand-off (cdna_hip_programming.md Guideline 16, counter form with
-// write-through slabs): slab stores sc1 -> every storing wave drains vmcnt
-// -> barrier -> one lane takes a relaxed agent-scope ticket; the last
-// arriver acquires (agent) before loading.  No workgroup ever waits for
-// another (no spin), so residency cannot deadlock it.  Tickets are zeroed
-// once at allocation and reset by their reducer for the next launch.
-// ---------------------------------------------------------------------------
-constexpr int kTickGroup = 32;
-typedef __attribute__((address_space(1))) unsigned int kt_gu32;
-typedef __attribute__((address_space(1))) unsigned long long kt_gu64;
-
-struct YFuse {
-    double* slab;   // [grid][3P] per-workgroup sums
-    double* gpart;  // [groups][3P] per-group sums
-    int* tick;      // [groups + 1] arrival tickets
-    double* ys;
-    double *t_alpha, *t_up, *t_low, *guard;
-    int start, last;
-    double s0;
-};
-
-__device__ __forceinline__ void st_wt(double* p, double v) {  // write-through (sc1) 8-B store
-    __hip_atomic_store((kt_gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int P, int BLOCK>
-__device__ __forceinline__ void fused_ycoef_tail(double (*red)[3][P], const YFuse& f) {
-    constexpr int WAVES = BLOCK / 64, NS = 3 * P;
-    __shared__ int s_last;
-    __shared__ double s_sum[NS];
-    const int tid = threadIdx.x, b = blockIdx.x, nblk = gridDim.x;
-    const int g = b / kTickGroup, g0 = g * kTickGroup;
-    const int gn = (nblk - g0 < kTickGroup) ? nblk - g0 : kTickGroup;
-    const int ngroups = (nblk + kTickGroup - 1) / kTickGroup;
-    for (int t = tid; t < NS; t += BLOCK) {
-        double v = 0.0;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) v += red[w][t / P][t % P];
-        st_wt(f.slab + (int64_t)b * NS + t, v);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned old = __hip_atomic_fetch_add((kt_gu32*)(f.tick + g), 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (int)old == gn - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // group reducer: the group's slabs in id order
-    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int t = tid; t < NS; t += BLOCK) {
-        const double* col = f.slab + (int64_t)g0 * NS + t;
-        double s = 0.0;
-        for (int i0 = 0; i0 < gn; i0 += 8) {  // 8 loads in flight, added in id order
-            double x[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) x[i] = i0 + i < gn ? col[(int64_t)(i0 + i) * NS] : 0.0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) s += x[i];
-        }
-        st_wt(f.gpart + (int64_t)g * NS + t, s);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __hip_atomic_store((kt_gu32*)(f.tick + g), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned old = __hip_atomic_fetch_add((kt_gu32*)(f.tick + ngroups), 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (int)old == ngroups - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // final reducer: group sums in group order, then the recurrence
-    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int t = tid; t < NS; t += BLOCK) {
-        double s = 0.0;
-        for (int gg = 0; gg < ngroups; gg += 8) {
-            double x[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) x[i] = gg + i < ngroups ? f.gpart[(int64_t)(gg + i) * NS + t] : 0.0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) s += x[i];
-        }
-        s_sum[t] = s;
-    }
-    __syncthreads();
-    if (tid == 0)
-        __hip_atomic_store((kt_gu32*)(f.tick + ngroups), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int p = tid; p < P; p += BLOCK)
-        ycoef_probe(p, P, s_sum[p], s_sum[P + p], s_sum[2 * P + p], f.start, f.last, f.s0, f.ys,
-                    f.t_alpha, f.t_up, f.t_low, f.guard);
 }
 
 // ---------------------------------------------------------------------------
@@ -732,7 +602,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos_start(
     const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
     int n, const uint32_t* __restrict__ S, double s0, double* __restrict__ Out,
     double* __restrict__ partial, const int* __restrict__ long_rows, int n_long, int long_thresh,
-    int long_blocks, YFuse fz) {
+    int long_blocks) {
     using G = GeoKY<P>;
     using V = VecT<G::VEC>;
     constexpr int WAVES = BLOCK / 64;
@@ -809,10 +679,6 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos_start(
         }
     }
     __syncthreads();
-    if (fz.tick) {  // fused coefficient step (opt-in, KT_KY_FUSED=1; kt_slq.cpp)
-        fused_ycoef_tail<P, BLOCK>(red, fz);
-        return;
-    }
     for (int t = threadIdx.x; t < 3 * P; t += BLOCK) {
         const int q = t / P, p = t % P;
         double v = 0.0;
@@ -840,7 +706,7 @@ __global__ KT_KY_BOUNDS(BLOCK) void k_spmm_lanczos(
     const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
     int n, const double* __restrict__ X, const double* __restrict__ Yold, double* __restrict__ Out,
     const double* __restrict__ coef, double* __restrict__ partial,
-    const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks, YFuse fz) {
+    const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks) {
     using G = GeoKY<P>;
     constexpr int WAVES = BLOCK / 64;
     const int lane = threadIdx.x & 63;
@@ -930,10 +796,6 @@ __global__ KT_KY_BOUNDS(BLOCK) void k_spmm_lanczos(
         }
     }
     __syncthreads();
-    if (fz.tick) {  // fused coefficient step (opt-in, KT_KY_FUSED=1; kt_slq.cpp)
-        fused_ycoef_tail<P, BLOCK>(red, fz);
-        return;
-    }
     for (int t = threadIdx.x; t < 3 * P; t += BLOCK) {  // slot t = q * P + p
         const int q = t / P, p = t % P;
         double v = 0.0;
@@ -1520,7 +1382,7 @@ __global__ __launch_bounds__(256) void k_expmv_term(int n, int nc, double mu, do
 // bout = coef (A bin - mu bin), F = F + bout on one row (VEC columns from p0);
 // row sums of |bout| and |F| of those columns into sb, sf   (expmv.m:75-78)
 // The row's own F and b values are loaded before the gathers (expmv_row_prefetch).
-template <int VEC, bool SC1 = false>
+template <int VEC>
 __device__ __forceinline__ void expmv_row_prefetch(int row, int p0, int nc, int ld, double mu,
                                                    const double* __restrict__ bin,
                                                    const double* __restrict__ F, double* fo, double* bo) {
@@ -1528,16 +1390,11 @@ __device__ __forceinline__ void expmv_row_prefetch(int row, int p0, int nc, int 
     for (int e = 0; e < VEC; ++e) {
         const int c = p0 + e;
         const int64_t o = (int64_t)row * ld + c;
-        if constexpr (SC1) {
-            fo[e] = (c < nc) ? ld_sc1d(F + o) : 0.0;
-            bo[e] = (c < nc && mu != 0.0) ? ld_sc1d(bin + o) : 0.0;
-        } else {
-            fo[e] = (c < nc) ? F[o] : 0.0;
-            bo[e] = (c < nc && mu != 0.0) ? bin[o] : 0.0;
-        }
+        fo[e] = (c < nc) ? F[o] : 0.0;
+        bo[e] = (c < nc && mu != 0.0) ? bin[o] : 0.0;
     }
 }
-template <int VEC, bool SC1 = false>
+template <int VEC>
 __device__ __forceinline__ void expmv_row_update(int row, int p0, const double* s, const double* fo,
                                                  const double* bo, int nc, int ld, double mu, double coef,
                                                  double* __restrict__ bout, double* __restrict__ F,
@@ -1551,18 +1408,12 @@ __device__ __forceinline__ void expmv_row_update(int row, int p0, const double* 
             if (mu != 0.0) t = fma(-mu, bo[e], t);  // (A - mu I) b, as launch_axpby(-mu, b, 1, Ab)
             const double bn = fma(coef, t, 0.0);
             const double f = fma(1.0, bn, fo[e]);
-            if constexpr (SC1) {
-                st_sc1d(bout + o, bn);
-                st_sc1d(F + o, f);
-            } else {
-                bout[o] = bn;
-                F[o] = f;
-            }
+            bout[o] = bn;
+            F[o] = f;
             sb += fabs(bn);
             sf += fabs(f);
         } else {
-            if constexpr (SC1) st_sc1d(bout + o, 0.0);
-            else bout[o] = 0.0;
+            bout[o] = 0.0;
         }
     }
 }
@@ -1840,329 +1691,6 @@ __global__ __launch_bounds__(256) void k_expmv_check(const double* __restrict__ 
     }
 }
 
-// ---------------------------------------------------------------------------
-// expmv.m:73-92 as ONE persistent launch per expmv call: every stage and
-// every Taylor term of the call, with a grid barrier where the per-term
-// launches had a kernel boundary.  The per-term form queued all s * m terms
-// (config 1: 440 per call, ~130 of them no-ops after the stage's stop test,
-// 4.4 us each, real ones ~9 us); here the stop test ends the stage inside the
-// launch, so only the terms MATLAB executes cost anything.
-//
-// Work split: the G workgroups cycle over the same virtual blocks as
-// k_expmv_step (long rows: one block each; medium rows: one wave; short rows:
-// one row group), so every row's arithmetic -- gather order, fma sequence,
-// |.| row sums in column order -- is the per-term kernel's, bit for bit.  The
-// stage passes (c1 = norm(b, inf) at a stage start, f = eta f; b = f at a
-// stage end) use contiguous row ranges.  A workgroup writes only rows it owns
-// and gathers b of the previous term, so each term needs exactly one barrier.
-//
-// The stop test: every workgroup reads all G partial maxima after the barrier
-// and decides alone; max is exact, so all decide the same term.
-//
-// Barrier (cdna_hip_programming.md Guideline 16; MI355X_MICROARCH.md
-// barrier-xcd): every storing wave drains, lane 0 releases (agent) and adds
-// to its group counter (group = id % 8, one per XCD under round-robin
-// placement -- speed only); the last of a group adds to the top counter, the
-// last group stores the epoch into every group's generation word; pollers
-// read their group's word relaxed with s_sleep, then acquire (agent).
-// Counters are monotonic within a launch and zeroed before it.  Spins are
-// bounded: a workgroup that waits ~2 s raises `tmo`, every waiting workgroup
-// sees it and leaves, and the host reports the failure.
-// ---------------------------------------------------------------------------
-struct ExpmvBar {  // 128-B lines; hipMemsetAsync'd before every launch
-    unsigned grp[8][32];
-    unsigned top[32];
-    unsigned gen[8][32];
-    unsigned tmo[32];
-    int out[32];  // [0] Taylor terms executed (mv), [1] 1 = completed
-};
-
-struct ExpmvRunArgs {
-    const int* rp;
-    const int* ci;
-    const double* va;
-    int n;
-    const int* long_rows;
-    int n_long;
-    const int* med_rows;
-    int n_med;
-    int nc, ld;
-    double mu, t, tol, eta;
-    int s, m, nvb;
-    double* b0;    // stage input b (and the ping of the terms)
-    double* b1;    // pong
-    double* F;     // f
-    double* part;  // [2 slots][2][G] per-workgroup maxima
-    ExpmvBar* bar;
-    unsigned long long* prof;  // diagnostic (KT_EXPMV_PROF): [G][kProfEpochs][2] barrier enter / exit
-};
-constexpr int kProfEpochs = 512;
-
-// SC1: every handed-off byte is stored and loaded sc1 (R1), so neither the
-// release (an L2 write-back) nor the acquire (an L1 invalidate) is needed
-template <bool SC1>
-__device__ __forceinline__ bool expmv_grid_sync(ExpmvBar* B, unsigned e, int G, int g,
-                                                unsigned long long* prof = nullptr) {
-    __shared__ int s_ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (prof && e <= kProfEpochs) prof[((size_t)g * kProfEpochs + e - 1) * 2] = wall_clock64();
-        if constexpr (!SC1) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        const int grp = g & 7;
-        const int ngrp = G < 8 ? G : 8;
-        const unsigned gsz = (unsigned)((G - grp + 7) / 8);
-        const unsigned old = __hip_atomic_fetch_add((kt_gu32*)&B->grp[grp][0], 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        if (old == e * gsz - 1u) {  // last of its group in this epoch
-            const unsigned o2 = __hip_atomic_fetch_add((kt_gu32*)&B->top[0], 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-            if (o2 == e * (unsigned)ngrp - 1u)
-                for (int q = 0; q < ngrp; ++q)
-                    __hip_atomic_store((kt_gu32*)&B->gen[q][0], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        int ok = 1;
-        for (unsigned spins = 0;; ++spins) {
-            if (__hip_atomic_load((kt_gu32*)&B->gen[grp][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= e)
-                break;
-            if ((spins & 63u) == 63u &&
-                __hip_atomic_load((kt_gu32*)&B->tmo[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                ok = 0;
-                break;
-            }
-            if (spins > (1u << 22)) {  // >= ~2 s: give up, and tell everyone
-                __hip_atomic_store((kt_gu32*)&B->tmo[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if constexpr (SC1) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps loads below the poll
-        } else {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (prof && e <= kProfEpochs) prof[((size_t)g * kProfEpochs + e - 1) * 2 + 1] = wall_clock64();
-        s_ok = ok;
-    }
-    __syncthreads();
-    return s_ok != 0;
-}
-
-// workgroup max of (x, y) -> thread 0 stores them at slot[0][g], slot[1][g]
-__device__ __forceinline__ void expmv_publish_max(double x, double y, double* slot, int G, int g,
-                                                  double (*red)[4]) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        x = fmax(x, __shfl_xor(x, o, 64));
-        y = fmax(y, __shfl_xor(y, o, 64));
-    }
-    __syncthreads();
-    if (lane == 0) {
-        red[0][wave] = x;
-        red[1][wave] = y;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        st_sc1d(slot + g, fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3])));
-        st_sc1d(slot + G + g, fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3])));
-    }
-}
-
-// max over the G published values of slot[0][.] and slot[1][.] (after the
-// barrier's acquire), the same in every workgroup
-__device__ __forceinline__ void expmv_read_max(const double* slot, int G, double (*red)[4], double& x,
-                                               double& y) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    double a = 0.0, b = 0.0;
-    for (int i = threadIdx.x; i < G; i += 256) {
-        a = fmax(a, __longlong_as_double((long long)__hip_atomic_load(
-                        (kt_gu64*)(slot + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-        b = fmax(b, __longlong_as_double((long long)__hip_atomic_load(
-                        (kt_gu64*)(slot + G + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        a = fmax(a, __shfl_xor(a, o, 64));
-        b = fmax(b, __shfl_xor(b, o, 64));
-    }
-    __syncthreads();
-    if (lane == 0) {
-        red[0][wave] = a;
-        red[1][wave] = b;
-    }
-    __syncthreads();
-    x = fmax(fmax(red[0][0], red[0][1]), fmax(red[0][2], red[0][3]));
-    y = fmax(fmax(red[1][0], red[1][1]), fmax(red[1][2], red[1][3]));
-}
-
-// one virtual block of k_expmv_step's grid (its parts (2) and (4)): the
-// gathers, bout = coef (A bin - mu bin), F = F + bout on the block's rows,
-// and the running maxima of the row sums |bout|, |F| into mb, mf
-template <int P, int FLAGS>
-__device__ __forceinline__ void expmv_vblock(const ExpmvRunArgs& a, int vb, int med_blocks, double coef,
-                                             const double* __restrict__ bin, double* __restrict__ bout,
-                                             double (*lred)[P], double& mb, double& mf) {
-    constexpr int WAVES = 4;
-    using G = GeoW<P, (P >= 2) ? 2 : 1>;
-    using GL = GeoW<P, (P >= 4) ? 4 : (P >= 2) ? 2 : 1>;
-    constexpr bool SC1 = (FLAGS & KF_LDSC1) != 0;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int kind = (vb < a.n_long) ? 2 : (vb < a.n_long + med_blocks) ? 1 : 0;
-    const int subL = lane % GL::LPR, grpL = lane / GL::LPR, p0L = subL * GL::VEC;
-    const int sub = lane % G::LPR, grp = lane / G::LPR, p0 = sub * G::VEC;
-    double sl[GL::VEC], s[G::VEC], fo[GL::VEC], bo[GL::VEC];
-#pragma unroll
-    for (int e = 0; e < GL::VEC; ++e) sl[e] = fo[e] = bo[e] = 0.0;
-#pragma unroll
-    for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-    int row = -1;
-    bool mine = false;
-    if (kind == 2) {
-        row = a.long_rows[vb];
-        if (wave == 0 && grpL == 0) expmv_row_prefetch<GL::VEC, SC1>(row, p0L, a.nc, a.ld, a.mu, bin, a.F, fo, bo);
-        row_gather8<P, FLAGS, GL>(a.rp[row] + wave * GL::GPW + grpL, a.rp[row + 1], WAVES * GL::GPW, p0L,
-                                  a.ci, a.va, bin, sl, a.ld);
-    } else if (kind == 1) {
-        const int mi = (vb - a.n_long) * WAVES + wave;
-        if (mi < a.n_med) {
-            row = a.med_rows[mi];
-            if (grpL == 0) expmv_row_prefetch<GL::VEC, SC1>(row, p0L, a.nc, a.ld, a.mu, bin, a.F, fo, bo);
-            row_gather8<P, FLAGS, GL>(a.rp[row] + grpL, a.rp[row + 1], GL::GPW, p0L, a.ci, a.va, bin, sl, a.ld);
-            mine = grpL == 0;
-        }
-    } else {
-        row = ((vb - a.n_long - med_blocks) * WAVES + wave) * G::GPW + grp;
-        if (row < a.n) {
-            const int beg = a.rp[row], end = a.rp[row + 1];
-            if (end - beg <= kMedThresh) {
-                expmv_row_prefetch<G::VEC, SC1>(row, p0, a.nc, a.ld, a.mu, bin, a.F, fo, bo);
-                row_gather8<P, FLAGS, G>(beg, end, 1, p0, a.ci, a.va, bin, s, a.ld);
-                mine = true;
-            }
-        }
-    }
-    if (kind != 0) {
-#pragma unroll
-        for (int o = GL::LPR; o < 64; o <<= 1)
-#pragma unroll
-            for (int e = 0; e < GL::VEC; ++e) sl[e] += __shfl_xor(sl[e], o, 64);
-    }
-    if (kind == 2) {
-        if (grpL == 0)
-#pragma unroll
-            for (int e = 0; e < GL::VEC; ++e) lred[wave][p0L + e] = sl[e];
-        __syncthreads();
-        if (wave == 0 && grpL == 0) {
-#pragma unroll
-            for (int e = 0; e < GL::VEC; ++e)
-                sl[e] = lred[0][p0L + e] + lred[1][p0L + e] + lred[2][p0L + e] + lred[3][p0L + e];
-            mine = true;
-        }
-        __syncthreads();  // lred is reused by the next virtual block
-    }
-    double sb = 0.0, sf = 0.0;
-    if (kind == 0) {
-        if (mine) expmv_row_update<G::VEC, SC1>(row, p0, s, fo, bo, a.nc, a.ld, a.mu, coef, bout, a.F, sb, sf);
-#pragma unroll
-        for (int o = 1; o < G::LPR; o <<= 1) {
-            sb += __shfl_xor(sb, o, 64);
-            sf += __shfl_xor(sf, o, 64);
-        }
-    } else {
-        if (mine) expmv_row_update<GL::VEC, SC1>(row, p0L, sl, fo, bo, a.nc, a.ld, a.mu, coef, bout, a.F, sb, sf);
-#pragma unroll
-        for (int o = 1; o < GL::LPR; o <<= 1) {
-            sb += __shfl_xor(sb, o, 64);
-            sf += __shfl_xor(sf, o, 64);
-        }
-    }
-    mb = fmax(mb, sb);
-    mf = fmax(mf, sf);
-}
-
-template <int P, int FLAGS>
-__global__ __launch_bounds__(256) void k_expmv_run(ExpmvRunArgs a) {
-    constexpr bool SC1 = (FLAGS & KF_LDSC1) != 0;
-    __shared__ double lred[4][P];
-    __shared__ double red[2][4];
-    const int G = (int)gridDim.x, g = (int)blockIdx.x, tid = (int)threadIdx.x;
-    const int med_blocks = (a.n_med + 3) / 4;
-    const int r0 = (int)((int64_t)a.n * g / G), r1 = (int)((int64_t)a.n * (g + 1) / G);
-    unsigned epoch = 0;
-    int mv = 0;
-    bool ok = true;
-    for (int i = 0; i < a.s && ok; ++i) {
-        // stage start: (i > 0: the previous stage's f = eta f; b = f) and
-        // c1 = norm(b, inf)   (expmv.m:74, 91)
-        double mx = 0.0;
-        for (int r = r0 + tid; r < r1; r += 256) {
-            double sm = 0.0;
-            for (int c = 0; c < a.nc; ++c) {
-                const int64_t o = (int64_t)r * a.ld + c;
-                double v;
-                if (i == 0) {
-                    v = SC1 ? ld_sc1d(a.b0 + o) : a.b0[o];
-                } else {
-                    v = fma(a.eta, SC1 ? ld_sc1d(a.F + o) : a.F[o], 0.0);  // as launch_axpby(eta, F, 0, F)
-                    if constexpr (SC1) {
-                        st_sc1d(a.F + o, v);
-                        st_sc1d(a.b0 + o, v);
-                    } else {
-                        a.F[o] = v;
-                        a.b0[o] = v;
-                    }
-                }
-                sm += fabs(v);
-            }
-            mx = fmax(mx, sm);
-        }
-        double* slot = a.part + (size_t)((epoch + 1) & 1) * 2 * G;
-        expmv_publish_max(mx, 0.0, slot, G, g, red);
-        ok = expmv_grid_sync<SC1>(a.bar, ++epoch, G, g, a.prof);
-        if (!ok) break;
-        double c1, unused;
-        expmv_read_max(slot, G, red, c1, unused);
-        const double* bin = a.b0;
-        double* bout = a.b1;
-        for (int k = 1; k <= a.m; ++k) {  // expmv.m:75-90
-            const double coef = a.t / ((double)a.s * k);
-            double mb = 0.0, mf = 0.0;
-            for (int vb = g; vb < a.nvb; vb += G)
-                expmv_vblock<P, FLAGS>(a, vb, med_blocks, coef, bin, bout, lred, mb, mf);
-            slot = a.part + (size_t)((epoch + 1) & 1) * 2 * G;
-            expmv_publish_max(mb, mf, slot, G, g, red);
-            ok = expmv_grid_sync<SC1>(a.bar, ++epoch, G, g, a.prof);
-            if (!ok) break;
-            ++mv;
-            double c2, nf;
-            expmv_read_max(slot, G, red, c2, nf);
-            double* t = const_cast<double*>(bin);
-            bin = bout;
-            bout = t;
-            if (c1 + c2 <= a.tol * nf) break;  // :83-86
-            c1 = c2;
-        }
-    }
-    if (ok) {  // the last stage's f = eta f   (:91)
-        for (int r = r0 + tid; r < r1; r += 256)
-            for (int c = 0; c < a.nc; ++c) {
-                const int64_t o = (int64_t)r * a.ld + c;
-                if constexpr (SC1) st_sc1d(a.F + o, fma(a.eta, ld_sc1d(a.F + o), 0.0));
-                else a.F[o] = fma(a.eta, a.F[o], 0.0);
-            }
-    }
-    if (g == 0 && tid == 0) {
-        __hip_atomic_store((kt_gu32*)&a.bar->out[0], (unsigned)mv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((kt_gu32*)&a.bar->out[1], ok ? 1u : 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 }  // namespace kt
 
 // ---------------------------------------------------------------------------
@@ -2302,26 +1830,17 @@ hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, doub
     });
 }
 
-static YFuse to_fuse(const YFuseArgs* a) {
-    YFuse f{};
-    if (a) f = YFuse{a->slab, a->gpart, a->tick, a->ys, a->t_alpha, a->t_up, a->t_low, a->guard,
-                     a->start, a->last, a->s0};
-    return f;
-}
-
-int fuse_groups(int grid) { return (grid + kTickGroup - 1) / kTickGroup; }
 
 hipError_t launch_spmm_lanczos(int P, int flags, int grid, const int* rp, const int* ci,
                                const double* va, int n, const double* X, const double* Yold,
                                double* Out, const double* coef, double* partial,
                                const int* long_rows, int n_long, int long_thresh, int long_blocks,
-                               hipStream_t st, const YFuseArgs* fuse) {
-    const YFuse fz = to_fuse(fuse);
+                               hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
 #define KT_KY(F)                                                                                   \
     k_spmm_lanczos<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, X, Yold, Out, coef, partial, \
-                                                           long_rows, n_long, long_thresh, long_blocks, fz)
+                                                           long_rows, n_long, long_thresh, long_blocks)
         switch (flags & (KF_UNIT | KF_NTY | KF_SC1)) {
         case 0: KT_KY(0); break;
         case KF_UNIT: KT_KY(KF_UNIT); break;
@@ -2349,15 +1868,13 @@ hipError_t launch_rademacher_signs(int P, int n, uint64_t seed, int64_t probe_ba
 hipError_t launch_spmm_lanczos_start(int P, int flags, int grid, const int* rp, const int* ci,
                                      const double* va, int n, const uint32_t* S, double s0,
                                      double* Out, double* partial, const int* long_rows, int n_long,
-                                     int long_thresh, int long_blocks, hipStream_t st,
-                                     const YFuseArgs* fuse) {
-    const YFuse fz = to_fuse(fuse);
+                                     int long_thresh, int long_blocks, hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
 #define KT_KS(F)                                                                                 \
     k_spmm_lanczos_start<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, S, s0, Out, partial, \
                                                                  long_rows, n_long, long_thresh,  \
-                                                                 long_blocks, fz)
+                                                                 long_blocks)
         switch (flags & (KF_UNIT | KF_NTY | KF_SC1)) {
         case 0: KT_KS(0); break;
         case KF_UNIT: KT_KS(KF_UNIT); break;
@@ -2486,62 +2003,6 @@ hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_
 #undef KT_EXPMV_LAUNCH
     return hipGetLastError();
 }
-
-size_t expmv_run_bar_bytes() { return sizeof(ExpmvBar); }
-
-template <int P, int FLAGS>
-static int expmv_run_occ() {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_expmv_run<P, FLAGS>, 256, 0) != hipSuccess)
-        return 1;
-    return per_cu < 1 ? 1 : per_cu;
-}
-
-hipError_t launch_expmv_run(int P, bool unit, bool sc1, int grid, int num_cu, const CsrView& M,
-                            const int* med_rows, int n_med, int nc, int ld, double mu, double t, double tol,
-                            double eta, int s, int m, double* b0, double* b1, double* F, double* part,
-                            void* bar, hipStream_t st, unsigned long long* prof) {
-    ExpmvRunArgs a{M.rp, M.ci, M.va, M.n, M.long_rows, M.n_long, med_rows, n_med, nc, ld, mu, t, tol, eta,
-                   s, m, expmv_step_blocks(M.n, P, M.n_long, n_med, 4), b0, b1, F, part,
-                   static_cast<ExpmvBar*>(bar), prof};
-    hipError_t e = hipMemsetAsync(bar, 0, sizeof(ExpmvBar), st);
-    if (e != hipSuccess) return e;
-#define KT_EXPMV_RUN(PP)                                                                           \
-    {                                                                                              \
-        /* every workgroup must be resident (grid barrier): at most half the   */                  \
-        /* occupancy bound, leaving room for a twin context's run             */                   \
-        const int cap = expmv_run_occ<PP, KF_LDSC1>() * num_cu / 2;                                \
-        if (grid > cap) grid = cap;                                                                \
-        if (grid < 1) grid = 1;                                                                    \
-        if (sc1) {                                                                                 \
-            if (unit) k_expmv_run<PP, KF_UNIT | KF_LDSC1><<<grid, 256, 0, st>>>(a);                \
-            else k_expmv_run<PP, KF_LDSC1><<<grid, 256, 0, st>>>(a);                               \
-        } else {                                                                                   \
-            if (unit) k_expmv_run<PP, KF_UNIT><<<grid, 256, 0, st>>>(a);                           \
-            else k_expmv_run<PP, 0><<<grid, 256, 0, st>>>(a);                                      \
-        }                                                                                          \
-    }
-    switch (P) {
-    case 1: KT_EXPMV_RUN(1) break;
-    case 2: KT_EXPMV_RUN(2) break;
-    case 4: KT_EXPMV_RUN(4) break;
-    case 8: KT_EXPMV_RUN(8) break;
-    case 16: KT_EXPMV_RUN(16) break;
-    case 32: KT_EXPMV_RUN(32) break;
-    default: return hipErrorInvalidValue;
-    }
-#undef KT_EXPMV_RUN
-    return hipGetLastError();
-}
-
-int expmv_prof_epochs() { return kProfEpochs; }
-
-int expmv_run_read(const void* bar_host, int* mv) {
-    const ExpmvBar* b = static_cast<const ExpmvBar*>(bar_host);
-    *mv = b->out[0];
-    return b->out[1];
-}
-
 
 hipError_t launch_gather_rows(int nr, int cols, const double* D, int ldd, const int64_t* rows, double* out,
                               hipStream_t st) {

@@ -40,7 +40,7 @@ struct EigStats {
     double ms = 0.0;
     int maxn = 0;
     ~EigStats() {
-        if (getenv("KT_EIG_STATS"))
+        if (KT_DIAG)
             fprintf(stderr, "[kt eig] calls %lld (device %lld) max n %d total %.1f ms\n",
                     (long long)calls, (long long)dev_calls, maxn, ms);
     }
@@ -57,15 +57,12 @@ struct EigTimer {
     }
 };
 
-// KT_FG_TIMING=1: per-step wall-clock phases of fun_update / trace_fun_update
+// KT_DIAG builds: per-step wall-clock phases of fun_update / trace_fun_update
 // on stderr (host clock; each phase ends at a stream sync of its own)
 struct PhaseClock {
     bool on = false;
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-    PhaseClock() {
-        const char* e = getenv("KT_FG_TIMING");
-        on = e && e[0] == '1';
-    }
+    PhaseClock() { on = KT_DIAG != 0; }
     double lap() {  // ms since the previous lap
         const auto now = std::chrono::steady_clock::now();
         const double ms = std::chrono::duration<double, std::milli>(now - t).count();
@@ -77,7 +74,7 @@ struct PhaseClock {
 static void sym_eig_dispatch(kt_context_s* ctx, int n, const double* A, double* w, double* V);
 
 static void sym_eig(kt_context_s* ctx, int n, const double* A, double* w, double* V) {
-    static const bool log = getenv("KT_EIG_STATS") && getenv("KT_EIG_STATS")[0] == '2';
+    constexpr bool log = KT_DIAG >= 2;
     const auto t0 = std::chrono::steady_clock::now();
     {
         EigTimer tm;
@@ -494,12 +491,6 @@ static void add_UBUt(std::vector<double>& M, int64_t n, int r, const double* U, 
 // BlockLanczos: lanczos_krylov.m (start :30-58, extend :60-67,
 // add_inf_pole :73-101, CGS2 :109-115).  Window slots 0/1 of `win`.
 // ---------------------------------------------------------------------------
-// KT_GRAM_HOST=1: the CGS2 Gram blocks go through the host (one round trip
-// per pass) instead of staying on the device -- the A/B switch of that change
-static bool gram_host_path() {
-    static const bool host = getenv("KT_GRAM_HOST") && getenv("KT_GRAM_HOST")[0] == '1';
-    return host;
-}
 
 struct BlockLanczos {
     kt_matrix_s* A;
@@ -550,7 +541,7 @@ struct BlockLanczos {
         std::vector<double> h((size_t)2 * PB * bs, 0.0);
         const size_t cnt = (size_t)2 * PB * bs;
         double* hg = nullptr;
-        if (prev >= 0 && !gram_host_path()) {  // both slots live: Gram blocks stay on the device
+        if (prev >= 0) {  // both slots live: Gram blocks stay on the device
             PinnedBuf& hp = ctx->ws.pin_small;
             hp.ensure(sizeof(double) * 2 * cnt);
             hg = hp.as<double>();
@@ -674,7 +665,6 @@ struct BlockArnoldi {
         const int L = ld();
         const int pv = nb * PB;
         spmm(A, blk(last), L, W.col(0), PB, bs);  // w = A * w   :86
-        if (gram_host_path()) return;             // (the host-path A/B projects in add_inf_pole)
         const size_t cnt = (size_t)pv * bs;
         double* hg = ctx->ws.pin_arn.as<double>() + (size_t)par * slot_;
         for (int pass = 0; pass < 2; ++pass) {
@@ -689,7 +679,6 @@ struct BlockArnoldi {
         const int L = ld();
         const int pv = nblk * PB;
         const size_t cnt = (size_t)pv * bs;
-        const bool host_path = gram_host_path();
         // the spmm and the first two CGS2 passes of this step were queued at
         // the end of the previous one (pre_), while its last read-back drained
         if (!pre_) head(last, nblk, hpar_);
@@ -697,21 +686,10 @@ struct BlockArnoldi {
         double* hg = ctx->ws.pin_arn.as<double>() + (size_t)hpar_ * slot_;
         // w = w - V (V'w), the Gram block read back into hg + off
         auto project = [&](size_t off) {
-            if (host_path) {  // A/B: through the host, one round trip per pass
-                std::vector<double> g;
-                gram(ctx, n, V.col(0), L, pv, W.col(0), PB, bs, g);
-                std::vector<double> C(g.size());
-                for (size_t t = 0; t < g.size(); ++t) C[t] = -g[t];
-                combine(ctx, n, V.col(0), L, pv, C, bs, 1.0, W.col(0), PB);
-                std::copy(g.begin(), g.end(), hg + off);
-                return;
-            }
             const double* dG = gram_device(ctx, n, V.col(0), L, pv, W.col(0), PB, bs);
             KT_HIP(hipMemcpyAsync(hg + off, dG, sizeof(double) * cnt, hipMemcpyDeviceToHost, ctx->stream));
             combine_device(ctx, n, V.col(0), L, pv, dG, bs, -1.0, 1.0, W.col(0), PB);
         };
-        if (host_path)
-            for (int pass = 0; pass < 2; ++pass) project(pass * cnt);
         std::vector<double> r;
         block_qr(ctx, n, W.col(0), PB, bs, r, true);  // [w, r] = qr(w, 0)   :99
         lucky = norm2_small(bs, bs, r.data()) < 1e-12;  // :100-102
@@ -728,16 +706,15 @@ struct BlockArnoldi {
                 if (i % PB < bs) H[hrow(i) + (size_t)(c0 + j) * Hr] = h[i + (size_t)j * pv];  // :96
         // reorthogonalise :104-106
         project(2 * cnt);
-        if (!host_path) {  // the read-back of hh is complete at this event
-            if (!hh_ev_) KT_HIP(hipEventCreateWithFlags(&hh_ev_, hipEventDisableTiming));
-            KT_HIP(hipEventRecord(hh_ev_, ctx->stream));
-        }
+        // the read-back of hh is complete at this event
+        if (!hh_ev_) KT_HIP(hipEventCreateWithFlags(&hh_ev_, hipEventDisableTiming));
+        KT_HIP(hipEventRecord(hh_ev_, ctx->stream));
         copy_cols(ctx, n, W.col(0), PB, blk(nblk), L, PB);  // V = [V, w]   :110
         // queue the next step's spmm and first two passes (they read the block
         // just copied; stream order) before waiting for this read-back, so the
         // device keeps working through the host's turn-around.  When the run
         // stops here they are never used (W and the other slot only).
-        if (!host_path && nblk + 1 < maxblk && !lucky) {
+        if (nblk + 1 < maxblk && !lucky) {
             head(nblk, nblk + 1, hpar_ ^ 1);
             pre_ = true;
         }

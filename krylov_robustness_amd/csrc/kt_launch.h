@@ -67,33 +67,19 @@ hipError_t launch_update(int P, int grid, int n, const double* y, double* uprev,
                          bool nt = false, double* rec = nullptr, int bcols = 0);
 hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, double* scale_next,
                        double* t_low, hipStream_t st);
-// y-form probe Lanczos (one pass per step) and its per-probe coefficients.
-// With `fuse` the pass's last arriving workgroup runs the coefficient step
-// itself (k_ycoef's recurrence; slab [grid][3P], gpart [fuse_groups(grid)][3P],
-// tick [fuse_groups(grid) + 1] zeroed once); without, it writes slot-major
-// partials for launch_ycoef.
-struct YFuseArgs {
-    double* slab;
-    double* gpart;
-    int* tick;
-    double* ys;
-    double *t_alpha, *t_up, *t_low, *guard;
-    int start, last;
-    double s0;
-};
-int fuse_groups(int grid);
+// y-form probe Lanczos (one pass per step; slot-major partials [3P][grid]
+// for launch_ycoef, the per-probe coefficient step).
 hipError_t launch_spmm_lanczos(int P, int flags, int grid, const int* rp, const int* ci,
                                const double* va, int n, const double* X, const double* Yold,
                                double* Out, const double* coef, double* partial,
                                const int* long_rows, int n_long, int long_thresh, int long_blocks,
-                               hipStream_t st, const YFuseArgs* fuse = nullptr);
+                               hipStream_t st);
 hipError_t launch_rademacher_signs(int P, int n, uint64_t seed, int64_t probe_base,
                                   const int* perm, uint32_t* S, hipStream_t st);
 hipError_t launch_spmm_lanczos_start(int P, int flags, int grid, const int* rp, const int* ci,
                                      const double* va, int n, const uint32_t* S, double s0,
                                      double* Out, double* partial, const int* long_rows, int n_long,
-                                     int long_thresh, int long_blocks, hipStream_t st,
-                                     const YFuseArgs* fuse = nullptr);
+                                     int long_thresh, int long_blocks, hipStream_t st);
 hipError_t launch_ycoef(int P, const double* partial, int nblk, int start, int last, double s0,
                         double* ys, double* t_alpha, double* t_up, double* t_low, double* guard,
                         hipStream_t st);
@@ -152,28 +138,11 @@ int ts_nrb(int n, int num_cu);
 hipError_t launch_ts_reflectors(int n, int bs, int BP, double* W, int ld, double* V, double* pivot,
                                 double* sums, double* part, double* taus, int num_cu,
                                 hipStream_t st);
-// the reflector sweep as one persistent launch (k_ts_qr), bit-identical to
-// launch_ts_reflectors: ts_qr_grid > 0 when it applies; pub:
-// ts_qr_pub_doubles doubles; bar: ts_qr_bar_bytes() (zeroed by the launch);
-// the unsigned at bar + ts_qr_tmo_offset() is nonzero after the launch if a
-// grid barrier timed out
-size_t ts_qr_bar_bytes();
-size_t ts_qr_tmo_offset();
-int ts_qr_grid(int n, int BP, int num_cu);
-size_t ts_qr_pub_doubles(int n, int BP, int num_cu);
-hipError_t launch_ts_qr(int n, int bs, int BP, int num_cu, double* W, int ld, double* V, double* pub,
-                        double* taus, void* bar, hipStream_t st);
 // one launch per column (k_ts_step1): ts_step1_grid > 0 when it applies;
 // part: 2 * BP * grid doubles, piv: 2 * BP doubles
 int ts_step1_grid(int n, int* rows_per_wg);
 hipError_t launch_ts_reflectors1(int n, int bs, int BP, double* W, int ld, double* V, double* part, double* piv,
                                  double* taus, hipStream_t st);
-// one grid barrier per column (k_ts_qr1, KT_TSQR_PERSIST=2): ts_qr1_grid > 0
-// when it applies; pub: ts_qr1_pub_doubles doubles; bar as launch_ts_qr
-int ts_qr1_grid(int n, int BP, int num_cu, int* rows_per_wg);
-size_t ts_qr1_pub_doubles(int n, int BP, int num_cu);
-hipError_t launch_ts_qr1(int n, int bs, int BP, int num_cu, double* W, int ld, double* V, double* pub, double* taus,
-                         void* bar, hipStream_t st);
 hipError_t launch_ts_formq(int n, int bs, int BP, const double* V, const double* M, double* W,
                            int ld, hipStream_t st);
 hipError_t launch_sum_slabs(int count, int S, const double* part, double* G, hipStream_t st);
@@ -203,7 +172,7 @@ hipError_t launch_expmv_check(int n, const double* partial, double tol, void* st
 // one fused launch per Taylor term k (P = pow2 >= nc, P <= 32, ld >= P): the
 // check of term k-1, SpMM of the natural-order CSR (M), update, the maxima
 // of term k's row sums folded into the state (term_max slot k % 3)
-// waves: per block (0: the per-term kernel's; the persistent form uses 4)
+// waves: per block (0: the per-term kernel's)
 int expmv_step_blocks(int n, int P, int n_long, int n_med, int waves = 0);
 // the default form of launch_expmv_step for this shape (true: SPLIT, grids
 // above 1,024 workgroups); with split the host launches
@@ -214,20 +183,5 @@ hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_
                              int ld, double mu, double coef,
                              double tol, int k, const double* bin, double* bout, double* F,
                              void* state, hipStream_t st, bool split, int* hflag = nullptr, int stage = 0);
-// the whole expmv call (s stages x up to m terms, stop tests, f = eta f) in
-// ONE persistent launch of `grid` workgroups (capped so all are resident);
-// b0 / F hold the input block, b1 is scratch (n x ld each, zero padded);
-// part: 4 * grid doubles; bar: expmv_run_bar_bytes() (zeroed by the launch).
-// After the stream is synchronised, copy bar to the host and
-// expmv_run_read() gives the terms executed and 1 = completed (2 = a grid
-// barrier timed out).
-size_t expmv_run_bar_bytes();
-// sc1: the handed-off blocks are stored and loaded sc1, no fences at the barriers
-hipError_t launch_expmv_run(int P, bool unit, bool sc1, int grid, int num_cu, const CsrView& M,
-                            const int* med_rows, int n_med, int nc, int ld, double mu, double t, double tol,
-                            double eta, int s, int m, double* b0, double* b1, double* F, double* part,
-                            void* bar, hipStream_t st, unsigned long long* prof = nullptr);
-int expmv_prof_epochs();  // prof: [grid][expmv_prof_epochs()][2] wall clocks (100 MHz)
-int expmv_run_read(const void* bar_host, int* mv);
 
 }  // namespace kt

@@ -209,9 +209,7 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
     // shift + degree selection, cached per (A version, t, block width): the
     // reference recomputes them every call from the same inputs; the
     // selection's matrix products still count in mv, as expmv.m's mv does
-    const char* nc_env = std::getenv("KT_EXPMV_SEL_CACHE");
-    const bool use_cache = !(nc_env && nc_env[0] == '0');
-    if (use_cache && A->expmv_sel_ok && A->expmv_sel_version == A->version && A->expmv_sel_t == t &&
+    if (A->expmv_sel_ok && A->expmv_sel_version == A->version && A->expmv_sel_t == t &&
         A->expmv_sel_nc == nc) {
         r.s = A->expmv_sel_s;
         r.m = A->expmv_sel_m;
@@ -319,122 +317,19 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
     void* state = ctx->ws.expmv_state.ptr;
     KT_HIP(hipMemsetAsync(state, 0, expmv_state_bytes(), st));
     const int P = pow2_at_least(std::max(nc, 1));
-    const char* persist = std::getenv("KT_EXPMV_PERSIST");
-    if (P <= 32 && ld >= P && !std::getenv("KT_EXPMV_UNFUSED") && persist && persist[0] == '1') {
-        // KT_EXPMV_PERSIST=1: the whole call in ONE launch (k_expmv_run):
-        // stages, terms, stop tests and f = eta f, a grid barrier per term
-        // instead of a launch; the same per-row arithmetic as the per-term
-        // launches below (bit-identical).  Measured slower on config 1
-        // (25 vs 18.5 ms): the barrier is cheap (1.5 us, sc1 form) but a
-        // term's virtual blocks are chains of dependent loads (median 8.8 us,
-        // hub rows 14.7 us per term), which the per-term grid runs in
-        // parallel (profiles/r02_expmv_persistent.txt).
-        const DevCSR& M = natural_csr(A);
-        const CsrView V{M.rowptr, M.col, M.val, (int)n, M.long_rows, M.n_long, A->long_thresh,
-                        kSplitThresh, M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split};
-        const int nvb = expmv_step_blocks((int)n, P, M.n_long, M.n_med, 4);  // the persistent form's virtual blocks
-        int grid = std::min(nvb, ctx->num_cu);
-        if (const char* g = std::getenv("KT_EXPMV_GRID")) grid = std::max(1, std::atoi(g));
-        ctx->ws.norm_part.ensure(sizeof(double) * 4 * (size_t)std::max(grid, 1));
-        ctx->ws.expmv_state.ensure(std::max(expmv_state_bytes(), expmv_run_bar_bytes()));
-        // KT_EXPMV_PROF=1 (diagnostic): wall clocks at every barrier's entry
-        // and exit per workgroup, summarised on stderr
-        const char* pf = std::getenv("KT_EXPMV_PROF");
-        const bool prof = pf && pf[0] == '1';
-        const int pe = expmv_prof_epochs();
-        DevBuf pbuf;
-        if (prof) {
-            pbuf.ensure(sizeof(unsigned long long) * 2 * (size_t)pe * grid);
-            KT_HIP(hipMemsetAsync(pbuf.ptr, 0, sizeof(unsigned long long) * 2 * (size_t)pe * grid, st));
-        }
-        const char* sc1e = std::getenv("KT_EXPMV_SC1");
-        const bool sc1 = !(sc1e && sc1e[0] == '0');
-        KT_HIP(launch_expmv_run(P, A->unit_values, sc1, grid, ctx->num_cu, V, M.med_rows, M.n_med, nc, ld, mu, t,
-                                tol, eta, r.s, r.m, b.col(0), Ab.col(0), F, ctx->ws.norm_part.as<double>(),
-                                ctx->ws.expmv_state.ptr, st,
-                                prof ? static_cast<unsigned long long*>(pbuf.ptr) : nullptr));
-        std::vector<char> hb(expmv_run_bar_bytes());
-        KT_HIP(hipMemcpyAsync(hb.data(), ctx->ws.expmv_state.ptr, hb.size(), hipMemcpyDeviceToHost, st));
-        KT_HIP(hipStreamSynchronize(st));
-        int terms = 0;
-        if (expmv_run_read(hb.data(), &terms) != 1)
-            fail(KT_ERR_HIP, "expmv: a grid barrier of the persistent Taylor launch timed out");
-        if (prof) {
-            std::vector<unsigned long long> h(2 * (size_t)pe * grid);
-            KT_HIP(hipMemcpy(h.data(), pbuf.ptr, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
-            // per epoch: work = max over workgroups of (enter_e - exit_{e-1}),
-            // barrier = max exit_e - max enter_e (the last arrival to the last release)
-            double work = 0, bar = 0, skew = 0;
-            int ne = 0;
-            for (int e = 1; e < pe; ++e) {
-                unsigned long long me = 0, mx = 0, mn = ~0ull, w = 0;
-                bool any = false;
-                for (int g2 = 0; g2 < grid; ++g2) {
-                    const unsigned long long en = h[((size_t)g2 * pe + e) * 2], ex = h[((size_t)g2 * pe + e) * 2 + 1];
-                    const unsigned long long px = h[((size_t)g2 * pe + e - 1) * 2 + 1];
-                    if (!en || !ex || !px) continue;
-                    any = true;
-                    me = std::max(me, en);
-                    mn = std::min(mn, ex);
-                    mx = std::max(mx, ex);
-                    w = std::max(w, en - px);
-                }
-                if (!any) break;
-                ++ne;
-                work += (double)w;
-                bar += (double)(mx - me);
-                skew += (double)(mx - mn);
-            }
-            if (ne) {
-                std::fprintf(stderr, "[expmv prof] grid %d epochs %d: work %.2f us, last-arrival->last-exit %.2f us, exit skew %.2f us per epoch\n",
-                             grid, ne, work / ne / 100.0, bar / ne / 100.0, skew / ne / 100.0);
-                // per workgroup: mean work over the epochs (enter_e - exit_{e-1})
-                std::vector<std::pair<double, int>> wg(grid);
-                for (int g2 = 0; g2 < grid; ++g2) {
-                    double s = 0;
-                    for (int e = 1; e <= ne; ++e)
-                        s += (double)(h[((size_t)g2 * pe + e) * 2] - h[((size_t)g2 * pe + e - 1) * 2 + 1]);
-                    wg[g2] = {s / ne / 100.0, g2};
-                }
-                std::sort(wg.begin(), wg.end());
-                std::fprintf(stderr, "[expmv prof]   per-wg work: min %.2f median %.2f max %.2f us; top:", wg[0].first,
-                             wg[grid / 2].first, wg[grid - 1].first);
-                for (int q = grid - 1; q >= std::max(0, grid - 6); --q)
-                    std::fprintf(stderr, " wg%d %.2f", wg[q].second, wg[q].first);
-                std::fprintf(stderr, " (long rows %d, med rows %d, vblocks %d)\n", M.n_long, M.n_med, nvb);
-            }
-        }
-        r.mv += terms;
-        ctx->expmv_terms += terms;
-        return r;
-    }
     if (P <= 32 && ld >= P && !std::getenv("KT_EXPMV_UNFUSED")) {
         // One launch per term (k_expmv_step: the previous term's stop test,
         // SpMM, update, the term's norm maxima); b ping-pongs, the maxima
-        // rotate through three slots of the state.
-        // KT_EXPMV_HUB=1: run on the hubs-first CSR (as the Lanczos sweeps
-        // do): b and f are permuted into its row order on the way in and f
-        // back out; max row sums (the stop test) do not depend on the row
-        // order.  Read per call.  Opt-in: 7 % faster at config 4, but a row's
-        // gathers then sum in another order than the reference's A*b, which
-        // moved one stage's stop by a term there (seed 1: 3,573 vs 3,575
-        // terms, profiles/r04/expmv_c4/variants.json).
-        const char* hbe = std::getenv("KT_EXPMV_HUB");
-        const bool hub = hbe && hbe[0] == '1';
-        const DevCSR& M = hub ? hub_csr(A) : natural_csr(A);
+        // rotate through three slots of the state.  Natural row order: a
+        // row's gathers sum in the order of the reference's A*b (the
+        // hubs-first CSR ran 7 % faster at config 4 but moved one stage's
+        // stop by a term, profiles/r04/expmv_c4/variants.json).
+        const DevCSR& M = natural_csr(A);
         const CsrView V{M.rowptr, M.col, M.val, (int)n, M.long_rows, M.n_long, A->long_thresh,
                         kSplitThresh, M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split};
         // KT_EXPMV_SPLIT=0 / 1 forces the fused / split term form (read per call)
         const char* spe = std::getenv("KT_EXPMV_SPLIT");
         const bool split = spe ? spe[0] == '1' : expmv_split_check((int)n, P, M.n_long, M.n_med);
-        double* Fout = F;
-        DevMat Fh;
-        if (hub) {
-            Fh.alloc(ctx, n, ld);
-            KT_HIP(launch_perm_rows((int)n, nc, M.perm, 1, Bsrc, ld, b.col(0), ld, st));
-            KT_HIP(launch_perm_rows((int)n, nc, M.perm, 1, Bsrc, ld, Fh.col(0), ld, st));
-            F = Fh.col(0);
-        }
         // The launch that finds a stage's stop test satisfied also stores the
         // stage index into a coherent host flag; the host, which queues terms
         // only slightly ahead of the device here, stops queueing that stage's
@@ -449,12 +344,11 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
             hflag = ctx->ws.expmv_stop.dev;
         }
         // Split form (large grids, terms of ~0.4 ms): the host keeps at most
-        // KT_EXPMV_AHEAD (default 3; 0 = no limit) terms queued past the last
-        // finished one, so it sees a stage's stop flag before it has queued
-        // the stage's remaining terms (each a launch that returns at once,
-        // ~19 us with its check; ~2,000 of them per config-4 trace_exp).
-        const char* ae = std::getenv("KT_EXPMV_AHEAD");
-        const int ahead = (split && use_flag) ? (ae ? std::max(0, std::atoi(ae)) : 3) : 0;
+        // 3 terms queued past the last finished one, so it sees a stage's
+        // stop flag before it has queued the stage's remaining terms (each a
+        // launch that returns at once, ~19 us with its check; ~2,000 of them
+        // per config-4 trace_exp).
+        const int ahead = (split && use_flag) ? 3 : 0;
         std::vector<hipEvent_t> ring(ahead, nullptr);
         for (auto& e : ring) KT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         struct RingGuard {
@@ -483,7 +377,6 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
             KT_HIP(launch_axpby((int)n, nc, eta, F, ld, 0.0, F, ld, st));  // f = eta f
             copy_cols(ctx, n, F, ld, b.col(0), ld, nc);                    // b = f
         }
-        if (hub) KT_HIP(launch_perm_rows((int)n, nc, M.perm, 0, F, ld, Fout, ld, st));
         int hstate[2] = {0, 0};  // {active, mv}
         KT_HIP(hipMemcpyAsync(hstate, state, sizeof(hstate), hipMemcpyDeviceToHost, st));
         KT_HIP(hipStreamSynchronize(st));

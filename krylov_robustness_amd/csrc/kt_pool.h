@@ -1,7 +1,7 @@
 // kt_pool.h -- persistent host worker pool for small per-column / per-
 // candidate dense work between device steps (the greedy host-eig path,
 // the Frechet entries of hessianfcn); spawning threads every Krylov step
-// would cost more than the work.  Sized min(16, cores) or KT_HOST_THREADS.
+// would cost more than the work.  Sized min(16, cores).
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -56,7 +56,6 @@ class HostPool {
    private:
     HostPool() {
         int nt = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) - 1;
-        if (const char* e = getenv("KT_HOST_THREADS")) nt = std::max(0, atoi(e) - 1);
         for (int t = 0; t < nt; ++t) workers_.emplace_back([this] { loop(); });
     }
     void drain(const std::function<void(int)>& f, int count) {

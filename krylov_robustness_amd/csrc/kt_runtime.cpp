@@ -256,8 +256,6 @@ void refresh_device(kt_matrix_s* A) {
     A->nat.invalidate();
     A->version++;  // a twin copy (kt_krylov.cpp) is now stale
     A->unit_values = std::all_of(A->h_val.begin(), A->h_val.end(), [](double v) { return v == 1.0; });
-    const char* un = getenv("KT_UNIT");
-    if (un && un[0] == '0') A->unit_values = false;
 }
 
 // degree-relabelled CSR of the probe hot path, built on first use
@@ -265,13 +263,10 @@ const DevCSR& hub_csr(kt_matrix_s* A) {
     if (A->hub.built) return A->hub;
     const int64_t n = A->n;
     // degree-descending relabelling (stable, so ties keep original order)
-    const char* rl = getenv("KT_RELABEL");
-    const bool relabel = !(rl && rl[0] == '0');
     A->new2old.resize(n);
     A->old2new.resize(n);
     for (int64_t i = 0; i < n; ++i) A->new2old[i] = (int32_t)i;
-    if (relabel)
-        std::stable_sort(A->new2old.begin(), A->new2old.end(), [&](int32_t a, int32_t b) {
+    std::stable_sort(A->new2old.begin(), A->new2old.end(), [&](int32_t a, int32_t b) {
             return A->h_rowptr[a + 1] - A->h_rowptr[a] > A->h_rowptr[b + 1] - A->h_rowptr[b];
         });
     for (int64_t r = 0; r < n; ++r) A->old2new[A->new2old[r]] = (int32_t)r;
@@ -341,9 +336,6 @@ int kt_context_create(int device, kt_context_t* out) {
     hipDeviceProp_t prop;
     KT_HIP(hipGetDeviceProperties(&prop, device));
     ctx->num_cu = prop.multiProcessorCount;
-    if (const char* f = getenv("KT_K1_FLAGS")) ctx->k1_flags = atoi(f);
-    if (const char* f = getenv("KT_K2_NT")) ctx->k2_nt = f[0] == '1';
-    if (const char* f = getenv("KT_KY_FLAGS")) ctx->ky_flags = atoi(f);
     if (const char* f = getenv("KT_SLQ_YFORM")) ctx->yform = f[0] != '0';
     KT_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     *out = ctx;

@@ -151,11 +151,7 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     if (lane && !ctx->aux_stream[lane - 1])
         KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[lane - 1], hipStreamNonBlocking));
     hipStream_t st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
-    // KT_KY_BPC: row-group workgroups per CU of the pass (default 4), read per
-    // sweep like KT_SLQ_LANES
-    const char* bpc_env = getenv("KT_KY_BPC");
-    const int bpc = bpc_env ? std::max(1, std::min(16, atoi(bpc_env))) : 4;
-    const int grid = spmm_grid(n, P, ctx->num_cu * bpc);
+    const int grid = spmm_grid(n, P, ctx->num_cu * 4);  // 4 row-group workgroups per CU
     const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
     const int grid1 = grid + lblocks;
     SweepBufs& w = ctx->ws.sweep[lane];
@@ -163,16 +159,7 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     w.X0.ensure(blk_bytes);
     w.X1.ensure(blk_bytes);
     w.Y.ensure(blk_bytes);
-    // KT_KY_FUSED=1: the pass's last arriving workgroup runs the coefficient
-    // step instead of a k_ycoef launch per step (read per sweep).  Measured
-    // neutral with two lanes (+-0.3 %) and 2 % slower with one
-    // (profiles/r02_ab_fused.txt): its serial hand-off tail costs what the
-    // launch saved, so the separate launch stays the default.
-    const char* fe = getenv("KT_KY_FUSED");
-    const bool fused = fe && fe[0] == '1';
-    const int ngroups = fuse_groups(grid1);
-    // slabs [grid1][3P] + group sums [ngroups][3P] (fused) or slot-major [3P][grid1]
-    w.partial.ensure(sizeof(double) * (size_t)3 * P * (grid1 + ngroups));
+    w.partial.ensure(sizeof(double) * (size_t)3 * P * grid1);  // slot-major [3P][grid1]
     w.coef.ensure(sizeof(double) * 9 * P);
     const size_t rec = (size_t)3 * m * P + P;
     w.trec.ensure(sizeof(double) * rec);
@@ -181,22 +168,6 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     double* trec = w.trec.as<double>();
     double* guard = trec + (size_t)3 * m * P;
     auto rec_at = [&](int row, int j) { return trec + (size_t)(row * m + j) * P; };
-    const size_t tick_bytes = ((sizeof(int) * (size_t)(ngroups + 1) + 15) / 16) * 16;
-    if (w.tick.bytes < tick_bytes) {  // every reducer resets its ticket: zero once
-        w.tick.ensure(tick_bytes);
-        KT_HIP(hipMemsetAsync(w.tick.ptr, 0, w.tick.bytes, st));
-    }
-    YFuseArgs fz{part, part + (size_t)3 * P * grid1, w.tick.as<int>(), ys, nullptr, nullptr, nullptr,
-                 guard, 0, 0, 0.0};
-    auto fuse_at = [&](int j, int start, int last, double s) {
-        fz.t_alpha = rec_at(0, j);
-        fz.t_up = rec_at(1, j);
-        fz.t_low = rec_at(2, j);
-        fz.start = start;
-        fz.last = last;
-        fz.s0 = s;
-        return fused ? &fz : nullptr;
-    };
     int flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
     if (blk_bytes >= ((size_t)1 << 31)) flags &= ~16;  // sc1 buffer stores take 32-bit offsets
     const double s0 = 1.0 / std::sqrt((double)n);  // v_0 = z / ||z||, ||z||^2 = n
@@ -210,22 +181,18 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     double* Ot = w.X0.as<double>();  // y_{j+1}
     prof_begin(ctx, PROF_START, st);
     KT_HIP(launch_spmm_lanczos_start(P, flags, grid1, M.rowptr, M.col, M.val, n, Z, s0, Xc, part,
-                                     M.long_rows, M.n_long, A->long_thresh, lblocks, st,
-                                     fuse_at(0, 1, m == 1, s0)));
+                                     M.long_rows, M.n_long, A->long_thresh, lblocks, st));
     prof_end(ctx, PROF_START, st);
-    if (!fused)
-        KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, s0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0),
-                            guard, st));
+    KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, s0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0), guard, st));
     for (int j = 0; j + 1 < m; ++j) {
         prof_begin(ctx, PROF_SPMM, st);
         const bool last = j + 2 == m;  // y_{m} is never used: alpha_{m-1} needs only X.t
         KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
                                    last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long,
-                                   A->long_thresh, lblocks, st, fuse_at(j + 1, 0, last, 0.0)));
+                                   A->long_thresh, lblocks, st));
         prof_end(ctx, PROF_SPMM, st);
-        if (!fused)
-            KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1),
-                                rec_at(2, j + 1), guard, st));
+        KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1),
+                            rec_at(2, j + 1), guard, st));
         Yo = Xc;  // y_{j+1} overwrites y_{j-1} from the next pass on
         Xc = Ot;
         Ot = Yo;
@@ -285,13 +252,13 @@ void lanczos_sweep_y_block(kt_matrix_s* A, const DevCSR& M, int P, int m, const 
     double* Yo = nullptr;            // y_{j-1}
     double* Ot = w.X0.as<double>();  // y_{j+1}
     KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, V0, nullptr, Xc, ys + 6 * P, part,
-                               M.long_rows, M.n_long, A->long_thresh, lblocks, st, nullptr));
+                               M.long_rows, M.n_long, A->long_thresh, lblocks, st));
     KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, 1.0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0), guard, st));
     for (int j = 0; j + 1 < m; ++j) {
         const bool last = j + 2 == m;
         KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
                                    last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long, A->long_thresh,
-                                   lblocks, st, nullptr));
+                                   lblocks, st));
         KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1),
                             rec_at(2, j + 1), guard, st));
         Yo = Xc;
@@ -354,11 +321,8 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     // adjacent hub segments: the explicit K1 at P = 16 on the bench graph 264
     // -> ~210 us): the block is permuted into that row order on the way in
     // and f(A) x back out; quadratic forms are permutation invariant.
-    // KT_LC_HUB=0: natural row order.
-    const char* he = getenv("KT_LC_HUB");
-    const bool hub = !(he && he[0] == '0');
-    const DevCSR& M = hub ? hub_csr(A) : natural_csr(A);
-    const int* perm = hub ? M.perm : nullptr;
+    const DevCSR& M = hub_csr(A);
+    const int* perm = M.perm;
     DevMat Xh, Yh;
     const double* Xs = X;
     int ldxs = ldx;
@@ -598,14 +562,8 @@ static void slq_collect(kt_matrix_s* A, int ticket, double* sum_q, double* sum_q
     const int m = pd.m, P = pd.P, fun = pd.fun;
     const size_t rec = pd.rec;
     double* htrec = w.host_trec[slot].as<double>();
-    // KT_SLQ_PHASES=1 (diagnostic): host-side phase times of the call on stderr
-    const char* phe = getenv("KT_SLQ_PHASES");
-    const bool phases = phe && phe[0] == '1';
-    auto clk = [] { return std::chrono::steady_clock::now(); };
-    const auto t_in = clk();
     KT_HIP(hipSetDevice(ctx->device));
     for (int l = 0; l < pd.lanes; ++l) KT_HIP(hipEventSynchronize(pd.done[l]));
-    const auto t_synced = clk();
 #if !defined(KT_KY_DIAG) || KT_KY_DIAG == 0  // (diagnostic builds time the pass alone: no redo)
     if (ctx->yform) {  // sweeps with a guarded probe are redone by the explicit CGS2 sweep
         const DevCSR& H = hub_csr(A);
@@ -636,13 +594,6 @@ static void slq_collect(kt_matrix_s* A, int ticket, double* sum_q, double* sum_q
             qv[p] = (double)n * tridiag_quadrature(steps, al.data(), off.data(), fun);
         }
     }, 4);
-    if (phases) {
-        auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
-            return std::chrono::duration<double, std::micro>(b - a).count();
-        };
-        std::fprintf(stderr, "[kt slq] wait %.1f us, redo + quadrature %.1f us (%lld probes)\n", us(t_in, t_synced),
-                     us(t_synced, clk()), (long long)nprobes);
-    }
     double s1 = 0.0, s2 = 0.0;
     for (int64_t p = 0; p < nprobes; ++p) {
         s1 += qv[p];

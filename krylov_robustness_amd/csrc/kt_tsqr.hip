@@ -268,381 +268,6 @@ __global__ __launch_bounds__(kTsBlock) void k_ts_formq(int n, int bs, int BP,
     }
 }
 
-// ---------------------------------------------------------------------------
-// The reflector sweep as ONE persistent launch (k_ts_qr): workgroup g keeps
-// its row slice of W in LDS for the whole factorisation and per column k runs
-// k_ts_step's arithmetic on it (apply H_k, write v_k, accumulate the next
-// column's sums); the per-column reduce launch becomes a grid barrier after
-// which every workgroup sums the G per-workgroup partials itself, in
-// workgroup order (the same sums, so the same coefficients, everywhere).
-// Partials and the pivot row move write-through (sc1) and are read sc1, so
-// the barrier needs no fences (cdna_hip_programming.md Guideline 16, R1).
-// 2 bs launches -> 1; the reduction tree differs from the two-launch form's
-// (per-workgroup slices of rpb rows, then G partials), i.e. rounding-level
-// differences.  Only for n * BP * 8 small enough that the slices fit LDS.
-// ---------------------------------------------------------------------------
-struct TsBar {  // 128-B lines, zeroed before every launch
-    unsigned grp[8][32];
-    unsigned top[32];
-    unsigned gen[8][32];
-    unsigned tmo[32];
-};
-typedef __attribute__((address_space(1))) unsigned int ts_gu32;
-typedef __attribute__((address_space(1))) unsigned long long ts_gu64;
-
-__device__ __forceinline__ double ts_ld(const double* p) {
-    return __longlong_as_double((long long)__hip_atomic_load((ts_gu64*)p, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void ts_st(double* p, double v) {
-    __hip_atomic_store((ts_gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// grid barrier (per-group counters -> top counter -> per-group generation
-// words); every handed-off byte is sc1, so no release / acquire fences.
-// Bounded spin: ~2 s, then tmo is raised and every waiter leaves.
-__device__ __forceinline__ bool ts_grid_sync(TsBar* B, unsigned e, int G, int g) {
-    __shared__ int s_ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int grp = g & 7;
-        const int ngrp = G < 8 ? G : 8;
-        const unsigned gsz = (unsigned)((G - grp + 7) / 8);
-        const unsigned old = __hip_atomic_fetch_add((ts_gu32*)&B->grp[grp][0], 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        if (old == e * gsz - 1u) {
-            const unsigned o2 = __hip_atomic_fetch_add((ts_gu32*)&B->top[0], 1u, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-            if (o2 == e * (unsigned)ngrp - 1u)
-                for (int q = 0; q < ngrp; ++q)
-                    __hip_atomic_store((ts_gu32*)&B->gen[q][0], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        int ok = 1;
-        for (unsigned spins = 0;; ++spins) {
-            if (__hip_atomic_load((ts_gu32*)&B->gen[grp][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= e) break;
-            if ((spins & 63u) == 63u &&
-                __hip_atomic_load((ts_gu32*)&B->tmo[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                ok = 0;
-                break;
-            }
-            if (spins > (1u << 22)) {
-                __hip_atomic_store((ts_gu32*)&B->tmo[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: loads stay below the poll
-        s_ok = ok;
-    }
-    __syncthreads();
-    return s_ok != 0;
-}
-
-// Workgroup g owns blocks [g bpw, (g+1) bpw) of the two-launch form's row
-// blocks (rpb rows each, nrb in all) and keeps their rows in LDS.  Per column
-// k: the update and each block's partial sums exactly as k_ts_step computes
-// them (block by block) -> barrier -> workgroups 0 .. ceil((bs-kn)/4)-1 sum
-// the partials one wave per column exactly as k_ts_reduce does -> barrier ->
-// every workgroup reads the sums and the pivot row.  So every value equals
-// the two-launch form's, bit for bit.
-// pub: [2 slots][BP * nrb partials (column-major, as `part`) | BP sums | BP pivot]
-__global__ __launch_bounds__(kTsBlock) void k_ts_qr(int n, int bs, int BP, int rpb, int nrb, int bpw,
-                                                    double* __restrict__ W, int ld, double* __restrict__ V,
-                                                    double* __restrict__ pub, double* __restrict__ taus,
-                                                    TsBar* bar) {
-    extern __shared__ double lw[];  // [rows of the workgroup's blocks][BP]
-    __shared__ double red[kTsBlock];
-    __shared__ double s_sums[128], s_piv[128];
-    const int G = (int)gridDim.x, g = (int)blockIdx.x, tid = (int)threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int c = tid % BP, sub = tid / BP, rpi = kTsBlock / BP;
-    const int b0 = g * bpw, b1 = min(nrb, b0 + bpw);
-    const int r0 = min(n, b0 * rpb), r1 = min(n, b1 * rpb);
-    const int nr = r1 - r0;
-    const size_t slot_sz = (size_t)BP * nrb + 2 * BP;
-    for (int t = tid; t < nr * BP; t += kTsBlock) {
-        const int rr = t / BP, cc = t % BP;
-        lw[t] = cc < bs ? W[(int64_t)(r0 + rr) * ld + cc] : 0.0;
-    }
-    __syncthreads();
-    unsigned epoch = 0;
-    bool ok = true;
-    for (int k = -1; k < bs && ok; ++k) {
-        const int kn = k + 1;
-        double beta = 0.0, tau = 0.0, scal = 1.0, tc = 0.0, tn = 0.0;
-        if (k >= 0) {  // as k_ts_step
-            ts_larfg(s_piv[k], s_sums[k], beta, tau, scal);
-            if (c > k && c < bs) tc = s_piv[c] + scal * s_sums[c];
-            if (kn < bs) tn = s_piv[kn] + scal * s_sums[kn];
-            if (g == 0 && tid == 0) taus[k] = tau;
-        }
-        double* slot = pub + (size_t)((epoch + 1) & 1) * slot_sz;
-        for (int b = b0; b < b1; ++b) {  // k_ts_step's block b
-            const int rb0 = b * rpb, rb1 = min(n, rb0 + rpb);
-            const int rstart = max(rb0, k < 0 ? 0 : k);
-            double acc = 0.0;
-            for (int base = rstart; base < rb1; base += rpi) {  // uniform trip count (barrier inside)
-                const int r = base + sub;
-                const bool live = r < rb1 && c < bs;
-                double* row = lw + (size_t)(r - r0) * BP;
-                double wk = 0.0, wn = 0.0, wc = 0.0;
-                if (live) {
-                    if (k >= 0) wk = row[k];
-                    if (kn < bs) wn = row[kn];
-                    wc = row[c];
-                }
-                __syncthreads();  // every read of this row block before any write
-                if (live) {
-                    double v = 0.0;
-                    if (k >= 0) {
-                        v = (r == k) ? 1.0 : wk * scal;
-                        if (c == k) {
-                            V[(int64_t)r * BP + k] = v;
-                            if (r == k) row[k] = beta;
-                        } else if (c > k) {
-                            wc -= tau * v * tc;
-                            row[c] = wc;
-                        }
-                    }
-                    if (kn < bs && c >= kn && r > kn) {
-                        const double wn_new = k >= 0 ? wn - tau * v * tn : wn;
-                        acc = fma(wn_new, wc, acc);
-                    }
-                }
-            }
-            if (kn < bs) {
-                red[tid] = acc;
-                __syncthreads();
-                if (tid < BP) {
-                    double s = 0.0;
-                    for (int q = 0; q < rpi; ++q) s += red[q * BP + tid];
-                    ts_st(slot + (size_t)tid * nrb + b, s);
-                }
-                __syncthreads();
-            }
-        }
-        if (kn >= bs) break;
-        if (kn >= r0 && kn < r1 && tid < BP)  // the next pivot row, W(kn, :) after H_k
-            ts_st(slot + (size_t)BP * nrb + BP + tid, tid < bs ? lw[(size_t)(kn - r0) * BP + tid] : 0.0);
-        ok = ts_grid_sync(bar, ++epoch, G, g);
-        if (!ok) break;
-        // k_ts_reduce: one wave per column j >= kn, lanes strided over the blocks
-        {
-            const int j = kn + g * 4 + wave;
-            if (j < bs) {
-                const double* p = slot + (size_t)j * nrb;
-                double s = 0.0;
-                for (int i = lane; i < nrb; i += 64) s += ts_ld(p + i);
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-                if (lane == 0) ts_st(slot + (size_t)BP * nrb + j, s);
-            }
-        }
-        ok = ts_grid_sync(bar, ++epoch, G, g);
-        if (!ok) break;
-        if (tid < BP) {
-            s_sums[tid] = (tid >= kn && tid < bs) ? ts_ld(slot + (size_t)BP * nrb + tid) : 0.0;
-            s_piv[tid] = ts_ld(slot + (size_t)BP * nrb + BP + tid);
-        }
-        __syncthreads();
-    }
-    // R: rows 0..bs-1 of W back to memory (Q is formed from V afterwards)
-    for (int t = tid; t < nr * BP; t += kTsBlock) {
-        const int rr = t / BP, cc = t % BP;
-        if (r0 + rr < bs && cc < bs) W[(int64_t)(r0 + rr) * ld + cc] = lw[t];
-    }
-}
-
-size_t ts_qr_bar_bytes() { return sizeof(TsBar); }
-size_t ts_qr_tmo_offset() { return offsetof(TsBar, tmo); }
-
-// ---------------------------------------------------------------------------
-// The persistent sweep with ONE grid barrier per column (k_ts_qr1,
-// KT_TSQR_PERSIST=2): every workgroup keeps its row slice in LDS (1024
-// threads), publishes one partial per column (its rows summed) and the next
-// pivot row write-through (sc1), and after the barrier sums the G partials
-// itself in one fixed order -- identical coefficients in every workgroup, no
-// second barrier for a reduce.  Rounding-level differences from the
-// two-launch form (reductions grouped by workgroup).
-// pub: 2 slots x [BP x G partials | BP pivot].
-// ---------------------------------------------------------------------------
-constexpr int kTsQ1Block = 1024;
-constexpr size_t kTsQ1Lds = 136 * 1024;  // the row slice; + 8 KB reduce + 2 KB coefficients
-
-__global__ __launch_bounds__(kTsQ1Block) void k_ts_qr1(int n, int bs, int BP, int rpw, double* __restrict__ W, int ld,
-                                                       double* __restrict__ V, double* __restrict__ pub,
-                                                       double* __restrict__ taus, TsBar* bar) {
-    extern __shared__ double lw[];  // [rows of this workgroup][BP]
-    __shared__ double red[kTsQ1Block];
-    __shared__ double s_sums[128], s_piv[128];
-    const int G = (int)gridDim.x, g = (int)blockIdx.x, tid = (int)threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int c = tid % BP, sub = tid / BP, rpi = kTsQ1Block / BP;
-    const int r0 = min(n, g * rpw), r1 = min(n, r0 + rpw);
-    const int nr = r1 - r0;
-    const size_t slot_sz = (size_t)BP * G + BP;
-    for (int t = tid; t < nr * BP; t += kTsQ1Block) {
-        const int rr = t / BP, cc = t % BP;
-        lw[t] = cc < bs ? W[(int64_t)(r0 + rr) * ld + cc] : 0.0;
-    }
-    __syncthreads();
-    unsigned epoch = 0;
-    bool ok = true;
-    for (int k = -1; k < bs && ok; ++k) {
-        const int kn = k + 1;
-        double beta = 0.0, tau = 0.0, scal = 1.0, tc = 0.0, tn = 0.0;
-        if (k >= 0) {
-            ts_larfg(s_piv[k], s_sums[k], beta, tau, scal);
-            if (c > k && c < bs) tc = s_piv[c] + scal * s_sums[c];
-            if (kn < bs) tn = s_piv[kn] + scal * s_sums[kn];
-            if (g == 0 && tid == 0) taus[k] = tau;
-        }
-        double* slot = pub + (size_t)((epoch + 1) & 1) * slot_sz;
-        const int rstart = max(r0, k < 0 ? 0 : k);
-        double acc = 0.0;
-        for (int base = rstart; base < r1; base += rpi) {  // uniform trip count (barrier inside)
-            const int r = base + sub;
-            const bool live = r < r1 && c < bs;
-            double* row = lw + (size_t)(r - r0) * BP;
-            double wk = 0.0, wn = 0.0, wc = 0.0;
-            if (live) {
-                if (k >= 0) wk = row[k];
-                if (kn < bs) wn = row[kn];
-                wc = row[c];
-            }
-            __syncthreads();  // every read of this row slot before any write
-            if (live) {
-                double v = 0.0;
-                if (k >= 0) {
-                    v = (r == k) ? 1.0 : wk * scal;
-                    if (c == k) {
-                        V[(int64_t)r * BP + k] = v;
-                        if (r == k) row[k] = beta;
-                    } else if (c > k) {
-                        wc -= tau * v * tc;
-                        row[c] = wc;
-                    }
-                }
-                if (kn < bs && c >= kn && r > kn) {
-                    const double wn_new = k >= 0 ? wn - tau * v * tn : wn;
-                    acc = fma(wn_new, wc, acc);
-                }
-            }
-        }
-        if (kn >= bs) break;
-        red[tid] = acc;
-        __syncthreads();
-        if (tid < BP) {
-            double sm = 0.0;
-            for (int q = 0; q < rpi; ++q) sm += red[q * BP + tid];
-            ts_st(slot + (size_t)tid * G + g, sm);
-        }
-        if (kn >= r0 && kn < r1 && tid < BP)  // the next pivot row, W(kn, :) after H_k
-            ts_st(slot + (size_t)BP * G + tid, tid < bs ? lw[(size_t)(kn - r0) * BP + tid] : 0.0);
-        ok = ts_grid_sync(bar, ++epoch, G, g);
-        if (!ok) break;
-        // every workgroup: sums[j], j in [kn, bs), one wave per column, lanes
-        // over the G partials, a fixed xor tree
-        for (int j = kn + wave; j < bs; j += kTsQ1Block / 64) {
-            double sm = 0.0;
-            for (int i = lane; i < G; i += 64) sm += ts_ld(slot + (size_t)j * G + i);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
-            if (lane == 0) s_sums[j] = sm;
-        }
-        if (tid < BP) s_piv[tid] = ts_ld(slot + (size_t)BP * G + tid);
-        __syncthreads();
-    }
-    // R: rows 0..bs-1 of W back to memory (Q is formed from V afterwards)
-    for (int t = tid; t < nr * BP; t += kTsQ1Block) {
-        const int rr = t / BP, cc = t % BP;
-        if (r0 + rr < bs && cc < bs) W[(int64_t)(r0 + rr) * ld + cc] = lw[t];
-    }
-}
-
-// grid of k_ts_qr1 (0 when it does not apply): rows per workgroup from the LDS
-// budget, at most a quarter of the CUs (one workgroup per CU, co-resident
-// next to another context's work)
-int ts_qr1_grid(int n, int BP, int num_cu, int* rows_per_wg) {
-    const int rpw_max = (int)(kTsQ1Lds / (sizeof(double) * (size_t)BP));
-    int G = (n + rpw_max - 1) / rpw_max;
-    const int floor_g = std::min(16, num_cu / 4);  // spread small problems over a few CUs
-    G = std::max(G, std::min(floor_g, (n + 63) / 64));
-    if (G < 1 || G > num_cu / 4 || BP > 128) return 0;
-    *rows_per_wg = (n + G - 1) / G;
-    if ((size_t)*rows_per_wg * BP * sizeof(double) > kTsQ1Lds) return 0;
-    return G;
-}
-
-size_t ts_qr1_pub_doubles(int n, int BP, int num_cu) {
-    int rpw = 0;
-    const int G = ts_qr1_grid(n, BP, num_cu, &rpw);
-    return 2 * ((size_t)BP * std::max(G, 1) + BP);
-}
-
-hipError_t launch_ts_qr1(int n, int bs, int BP, int num_cu, double* W, int ld, double* V, double* pub, double* taus,
-                         void* bar, hipStream_t st) {
-    int rpw = 0;
-    const int G = ts_qr1_grid(n, BP, num_cu, &rpw);
-    if (!G) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(bar, 0, sizeof(TsBar), st);
-    if (e != hipSuccess) return e;
-    k_ts_qr1<<<G, kTsQ1Block, sizeof(double) * (size_t)rpw * BP, st>>>(n, bs, BP, rpw, W, ld, V, pub, taus,
-                                                                     static_cast<TsBar*>(bar));
-    return hipGetLastError();
-}
-
-static int ts_rows_per_blk(int n, int num_cu);
-
-// blocks per workgroup of the persistent sweep (the two-launch form's blocks,
-// ~192 rows per workgroup), 0 when the rows would not fit LDS, the grid would
-// not stay resident next to a twin context's run, or the reduce needs more
-// workgroups than the grid has
-static int ts_qr_bpw(int n, int BP, int num_cu, int* grid) {
-    const int rpb = ts_rows_per_blk(n, num_cu);
-    const int nrb = (n + rpb - 1) / rpb;
-    const size_t lds_rows = (size_t)(144 * 1024) / (sizeof(double) * BP);
-    if ((size_t)rpb > lds_rows) return 0;
-    int bpw = (192 + rpb - 1) / rpb;
-    if ((size_t)bpw * rpb > lds_rows) bpw = (int)(lds_rows / rpb);
-    const int G = (nrb + bpw - 1) / bpw;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessorWithFlags(&per_cu, k_ts_qr, kTsBlock,
-                                                              sizeof(double) * (size_t)bpw * rpb * BP, 0) !=
-            hipSuccess ||
-        per_cu < 1 || G > per_cu * num_cu / 2 || 4 * G < BP)
-        return 0;
-    *grid = G;
-    return bpw;
-}
-
-int ts_qr_grid(int n, int BP, int num_cu) {
-    int G = 0;
-    return ts_qr_bpw(n, BP, num_cu, &G) ? G : 0;
-}
-
-size_t ts_qr_pub_doubles(int n, int BP, int num_cu) {
-    const int rpb = ts_rows_per_blk(n, num_cu);
-    const int nrb = (n + rpb - 1) / rpb;
-    return 2 * ((size_t)BP * nrb + 2 * BP);
-}
-
-hipError_t launch_ts_qr(int n, int bs, int BP, int num_cu, double* W, int ld, double* V, double* pub,
-                        double* taus, void* bar, hipStream_t st) {
-    int G = 0;
-    const int bpw = ts_qr_bpw(n, BP, num_cu, &G);
-    if (!bpw) return hipErrorInvalidValue;
-    const int rpb = ts_rows_per_blk(n, num_cu);
-    const int nrb = (n + rpb - 1) / rpb;
-    hipError_t e = hipMemsetAsync(bar, 0, sizeof(TsBar), st);
-    if (e != hipSuccess) return e;
-    k_ts_qr<<<G, kTsBlock, sizeof(double) * (size_t)bpw * rpb * BP, st>>>(n, bs, BP, rpb, nrb, bpw, W, ld, V, pub,
-                                                                         taus, static_cast<TsBar*>(bar));
-    return hipGetLastError();
-}
 
 static int ts_rows_per_blk(int n, int num_cu) {
     int want = 2 * num_cu;

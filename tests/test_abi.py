@@ -86,6 +86,22 @@ def test_missing_library_raises(monkeypatch, tmp_path):
         _lib.load()
 
 
+def test_kt_lib_selects_the_library_and_fails_loudly(tmp_path):
+    """KT_LIB names another build of the library (the A/B of compile-time
+    variants); a missing one raises KrylovLibraryError naming it -- no
+    fallback."""
+    import subprocess
+    import sys
+    bad = str(tmp_path / "libkrylov_other.so")
+    code = ("import krylov_robustness_amd as k, krylov_robustness_amd._lib as L\n"
+            "assert k.LIB_PATH == %r\n"
+            "try:\n    L.load()\nexcept L.KrylovLibraryError as e:\n    print('raised', e)\n" % bad)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT,
+                       env=dict(os.environ, KT_LIB=bad))
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("raised") and bad in r.stdout
+
+
 def test_every_entry_point_rejects_null_handles():
     """Every compute entry point reports KT_ERR_ARG (or another status) for a
     NULL matrix / context and NULL buffers -- never a crash -- and leaves a

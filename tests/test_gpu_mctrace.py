@@ -58,9 +58,7 @@ def test_expmv_split_check_form(kra, gpu_ctx, monkeypatch, graph):
     workgroups at 10 columns, split by default) and on oregon_A6 (340, fused
     by default) both forms (KT_EXPMV_SPLIT=0 / 1) give the same F, s, m, mv
     bit for bit, and agree with the oracle; the first column alone (P = 1:
-    391 / 43 workgroups) too.  Both row orders (KT_EXPMV_HUB: natural CSR or
-    the opt-in hubs-first CSR) agree with the oracle (equal s,
-    m, mv)."""
+    391 / 43 workgroups) too."""
     from krylov_robustness_amd import graphs
     A = graphs.erdos_renyi(100_000, 500_000, seed=0) if graph == "er100k" else load_graph(graph)
     D = kra.DeviceMatrix(A, gpu_ctx)
@@ -77,25 +75,12 @@ def test_expmv_split_check_form(kra, gpu_ctx, monkeypatch, graph):
         Fo, *ro = ko.expmv(1.0, A, B)
         assert tuple(outs[0][1:]) == tuple(ro)
         np.testing.assert_allclose(outs[0][0], Fo, rtol=1e-11, atol=1e-13 * np.abs(Fo).max())
-        # the other row order (KT_EXPMV_HUB=1: the hubs-first CSR)
-        for v in ("0", "1"):
-            monkeypatch.setenv("KT_EXPMV_HUB", v)
-            Fh, *rh = kra.expmv(1.0, D, B, ctx=gpu_ctx)
-            assert tuple(rh) == tuple(ro)
-            np.testing.assert_allclose(Fh, Fo, rtol=1e-11, atol=1e-13 * np.abs(Fo).max())
-        monkeypatch.delenv("KT_EXPMV_HUB")
 
 
 @pytest.mark.parametrize("name,loops", [("oregon_A6", False), ("oregon_A0", True), ("anaheim", False)])
-def test_expmv_persistent_launch_is_bit_identical(kra, gpu_ctx, monkeypatch, name, loops):
-    """KT_EXPMV_PERSIST=1: the whole expmv call as ONE persistent launch
-    (k_expmv_run: a grid barrier per Taylor term, the stop test inside the
-    launch) runs the per-term kernel's row arithmetic: F, s, m and mv equal
-    the per-term launches (the default, 4-wave blocks) bit for bit -- in both barrier forms
-    (sc1 hand-off without fences, and plain stores + agent release/acquire,
-    KT_EXPMV_SC1=0), for the default grid, a grid of one workgroup (every
-    virtual block on one workgroup) and a grid of 7 (a partial XCD group);
-    self loops exercise mu != 0."""
+def test_expmv_per_term_launches_match_oracle(kra, gpu_ctx, name, loops):
+    """The per-term launches (k_expmv_step) give the oracle's F with equal s,
+    m and mv; self loops exercise mu != 0."""
     from test_normest1 import looped
     A = load_graph(name)
     if loops:
@@ -106,14 +91,6 @@ def test_expmv_persistent_launch_is_bit_identical(kra, gpu_ctx, monkeypatch, nam
     Fo, *ro = ko.expmv(1.0, A, b)
     assert tuple(ref[1:]) == tuple(ro)
     np.testing.assert_allclose(ref[0], Fo, rtol=1e-11, atol=1e-13 * np.abs(Fo).max())
-    monkeypatch.setenv("KT_EXPMV_PERSIST", "1")
-    for sc1, grid in (("1", None), ("0", None), ("1", "1"), ("1", "7"), ("0", "7")):
-        monkeypatch.setenv("KT_EXPMV_SC1", sc1)
-        if grid:
-            monkeypatch.setenv("KT_EXPMV_GRID", grid)
-        out = kra.expmv(1.0, D, b, ctx=gpu_ctx)
-        assert tuple(out[1:]) == tuple(ref[1:])
-        np.testing.assert_array_equal(out[0], ref[0])
 
 
 def test_expmv_host_stop_flag_is_exact(kra, gpu_ctx, monkeypatch):

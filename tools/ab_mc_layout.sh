@@ -10,7 +10,7 @@ run() {  # name, env...
   env "$@" timeout -k 10 200 python bench.py --estimator mc_trace --steps 8 --cpu-seconds 0 --ref-cpu-seconds 0 \
     > gpurun_out/ab1/bench_$name.json 2> gpurun_out/ab1/bench_$name.err
 }
-run default || exit 1
+run layout_default || exit 1
 run ahead1 KT_MC_AHEAD=1 || exit 1
 run explicit KT_LC_YFORM=0 || exit 1
 timeout -k 10 400 python bench.py > gpurun_out/ab1/bench_default.json 2> gpurun_out/ab1/bench_default.err || exit 1
