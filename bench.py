@@ -320,9 +320,13 @@ def main():
     D = kra.DeviceMatrix(A, ctx)
     off, cnt = kdist.probe_shard(N, rank, world)
     counts = [kdist.probe_shard(N, r, world)[1] for r in range(world)]
-    # --bitstable plans the sweep width on the GLOBAL probe count, so every
-    # world size runs each probe in a sweep of the same width
+    # --bitstable plans the sweep width on the GLOBAL probe count and deals
+    # whole sweeps to the ranks, so every world size runs each probe in the
+    # same sweep (a guard redo recomputes a whole sweep)
     P = args.block or kra.slq_plan(D, N if args.bitstable else cnt, ctx=ctx)
+    if args.bitstable:
+        off, cnt = kdist.probe_shard_aligned(N, P, rank, world)
+        counts = [kdist.probe_shard_aligned(N, P, r, world)[1] for r in range(world)]
     ref = reference_trace(args.config, args.weighted) if m >= 20 else None
 
     def submit(seed):

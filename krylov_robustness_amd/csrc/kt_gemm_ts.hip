@@ -243,8 +243,16 @@ __global__ __launch_bounds__(256) void k_combine_ts(int64_t n, const double* X, 
 hipError_t launch_combine_ts(int64_t n, const double* X, int ldx, int px, const double* C, int q, double alpha,
                              double beta, double* Y, int ldy, hipStream_t st) {
     if (n <= 0 || q <= 0) return hipSuccess;
-    // in place only within one y-block (see k_combine_ts)
-    if (X == Y && q > 32) return hipErrorInvalidValue;
+    // in place only within one y-block (see k_combine_ts): with more than one
+    // y-block any overlap of X's and Y's address ranges would race, exact
+    // aliasing or a Y offset into X's block alike
+    if (q > 32) {
+        const char* x0 = reinterpret_cast<const char*>(X);
+        const char* x1 = reinterpret_cast<const char*>(X + (n - 1) * (int64_t)ldx + px);
+        const char* y0 = reinterpret_cast<const char*>(Y);
+        const char* y1 = reinterpret_cast<const char*>(Y + (n - 1) * (int64_t)ldy + q);
+        if (x0 < y1 && y0 < x1) return hipErrorInvalidValue;
+    }
     dim3 grid((unsigned)((n + kCombRows - 1) / kCombRows), (q + 31) / 32);
     k_combine_ts<<<grid, 256, 0, st>>>(n, X, ldx, px, C, q, alpha, beta, Y, ldy);
     return hipGetLastError();

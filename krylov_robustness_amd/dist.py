@@ -18,6 +18,20 @@ def probe_shard(nprobes: int, rank: int, world: int):
     return offset, count
 
 
+def probe_shard_aligned(nprobes: int, block: int, rank: int, world: int):
+    """Shard [offset, offset+count) whose boundaries are multiples of the
+    sweep width `block`: whole sweeps are dealt (balanced) over the ranks, so
+    every probe sits in the same sweep -- same neighbours, same width -- at
+    any world size.  Then even a sweep the y-form guard sends back to the
+    explicit CGS2 sweep (which recomputes the whole sweep) gives each probe
+    the same form everywhere (bench.py --bitstable)."""
+    nprobes, block = int(nprobes), max(1, int(block))
+    sweeps = (nprobes + block - 1) // block
+    s_off, s_cnt = probe_shard(sweeps, rank, world)
+    off = min(nprobes, s_off * block)
+    return off, min(nprobes, (s_off + s_cnt) * block) - off
+
+
 def env_rank():
     return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
             int(os.environ.get("LOCAL_RANK", "0")))

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from conftest import load_graph
-from krylov_robustness_amd.dist import probe_shard
+from krylov_robustness_amd.dist import probe_shard, probe_shard_aligned
 
 
 def test_probe_shard_covers_range():
@@ -20,6 +20,22 @@ def test_probe_shard_covers_range():
                 o, c = probe_shard(N, r, W)
                 seen.extend(range(o, o + c))
             assert seen == list(range(N))
+
+
+def test_probe_shard_aligned_deals_whole_sweeps():
+    """--bitstable's shards: contiguous, covering, and every boundary a
+    multiple of the sweep width, so a probe's sweep (its neighbours and the
+    sweep's width) is the same at every world size."""
+    for N in [0, 1, 7, 128, 1000, 1024]:
+        for P in [1, 16, 64]:
+            for W in [1, 2, 3, 4, 8]:
+                seen = []
+                for r in range(W):
+                    o, c = probe_shard_aligned(N, P, r, W)
+                    assert c >= 0 and (c == 0 or o % P == 0)
+                    assert c == 0 or (o + c) % P == 0 or o + c == N
+                    seen.extend(range(o, o + c))
+                assert seen == list(range(N))
 
 
 def _free_port():
