@@ -696,17 +696,17 @@ def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev,
         l1, ms1 = ctx.profile_read(0)
         l2, ms2 = ctx.profile_read(1)
         if l1:
-            # mc_trace_batched: round 1's S term is one 16-wide sweep (m K1
-            # launches), every round after it one 32-wide sweep (the round's Q
-            # and G terms and the next S term); the K1 launches of the pass are
-            # charged their own width's bytes
+            # mc_trace_batched: round 1's S term and a final round's Q term are
+            # 16-wide explicit sweeps, a round with the next S term ahead one
+            # 32-wide sweep (the G columns of a final round run as y-form
+            # passes, not K1); each K1 launch is charged its own width's bytes
             unit = bool(A.nnz) and bool(np.all(A.data == 1.0))
             per_nnz = 4 if unit else 12
 
             def kb(P):
                 return per_nnz * nnz + 4 * (n + 1) + 16 * n * P
-            l16 = min(m, l1)
-            l32 = l1 - l16
+            l16, ms16 = ctx.profile_read_width(0, 16)
+            l32, ms32 = ctx.profile_read_width(0, 32)
             bytes_total = l16 * kb(16) + l32 * kb(32)
             us = ms1 / l1 * 1e3
             gbs = bytes_total / (ms1 * 1e-3) / 1e9
@@ -717,14 +717,17 @@ def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev,
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                                "traffic": traffic, "avg_launch_us": round(us, 2), "launches": l1,
                                "launches_by_width": {"16": l16, "32": l32},
+                               "avg_launch_us_by_width": {"16": round(ms16 / l16 * 1e3, 2) if l16 else None,
+                                                          "32": round(ms32 / l32 * 1e3, 2) if l32 else None},
                                "algorithmic_bytes_per_launch": round(bytes_total / l1),
                                "algorithmic_bytes_basis": f"{per_nnz} nnz + 4 (n+1) + 16 n P per launch (the "
-                                                          "CSR, u_j gathered once, y = A u_j written), P = 16 "
-                                                          "for round 1's S sweep, 32 for the rest; mean",
+                                                          "CSR, u_j gathered once, y = A u_j written), each "
+                                                          "launch at its sweep's width P (16 or 32); mean",
                                "k2_update_avg_us": round(ms2 / l2 * 1e3, 2) if l2 else None,
                                "serial_eval_ms": round(serial_ms, 2),
-                               "measured": "HIP events around every K1 launch of one serial trace_exp "
-                                           "(KT_TWIN=0: all Afun calls on one stream) after the timed region"}
+                               "measured": "HIP events around every K1 launch of one trace_exp after the timed "
+                                           "region (a final round's G y-form sweep runs beside its Q sweep on a "
+                                           "second lane, so those K1 times include that overlap)"}
             if traffic:
                 out["roofline"]["traffic_GBs"] = round(traffic * l1 / (ms1 * 1e-3) / 1e9, 1)
     return out

@@ -313,6 +313,9 @@ int kt_eigs_leading(kt_matrix_t A, double tol, int maxit, double* lambda, double
 int kt_profile_enable(kt_context_t ctx, int enable);
 int kt_profile_read(kt_context_t ctx, int kernel, int64_t* launches, double* total_ms);
 int kt_profile_reset(kt_context_t ctx);
+/* The same totals restricted to launches of sweep width `width` (the probe
+ * block P of the sweep that launched them). */
+int kt_profile_read_width(kt_context_t ctx, int kernel, int width, int64_t* launches, double* total_ms);
 /* Wall time during which at least one launch of `kernel` was in flight (the
  * union of the launches' event intervals, on whichever sweep-lane stream
  * each ran): with several lanes overlapping, summed per-launch durations

@@ -56,6 +56,13 @@ class Context:
         _lib.check(_lib.load().kt_profile_read(self._h, kernel, C.byref(n), C.byref(ms)))
         return int(n.value), float(ms.value)
 
+    def profile_read_width(self, kernel: int, width: int):
+        """(launches, milliseconds) of `kernel` in sweeps of width P = width."""
+        n = C.c_int64()
+        ms = C.c_double()
+        _lib.check(_lib.load().kt_profile_read_width(self._h, kernel, int(width), C.byref(n), C.byref(ms)))
+        return int(n.value), float(ms.value)
+
     def profile_busy(self, kernel: int) -> float:
         """Milliseconds during which at least one profiled launch of `kernel`
         was in flight (union over the sweep lanes' streams)."""

@@ -126,6 +126,10 @@ struct ProfSlot {
     std::vector<std::pair<double, double>> iv;
     hipEvent_t anchor = nullptr;
     bool anchored = false;
+    // a tag per recorded launch not folded in yet (the sweep width P), and
+    // the folded launches / milliseconds per tag
+    std::vector<int> tags;
+    std::vector<std::pair<int, std::pair<int64_t, double>>> by_tag;
 };
 
 enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_START = 2, PROF_NSLOTS = 3 };
@@ -324,7 +328,7 @@ void refresh_device(kt_matrix_s* A);
 const DevCSR& hub_csr(kt_matrix_s* A);
 
 // profiling helpers (no-ops unless ctx->profile)
-void prof_begin(kt_context_s* ctx, int slot, hipStream_t st = nullptr);
+void prof_begin(kt_context_s* ctx, int slot, hipStream_t st = nullptr, int tag = 0);
 void prof_end(kt_context_s* ctx, int slot, hipStream_t st = nullptr);
 // fold recorded events into the totals: all of them (every one complete:
 // after a stream sync, or waited for here when `wait`), or, with `upto`,

@@ -23,7 +23,7 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 // order everything the host reads)
 static constexpr unsigned kProfEventFlags = hipEventDisableSystemFence;
 
-void prof_begin(kt_context_s* ctx, int slot, hipStream_t st) {
+void prof_begin(kt_context_s* ctx, int slot, hipStream_t st, int tag) {
     if (!ctx->profile) return;
     ProfSlot& s = ctx->prof[slot];
     if (s.used + 2 > s.ev.size()) {
@@ -39,6 +39,7 @@ void prof_begin(kt_context_s* ctx, int slot, hipStream_t st) {
         s.anchored = true;
     }
     KT_HIP(hipEventRecord(s.ev[s.used], st ? st : ctx->stream));
+    s.tags.push_back(tag);
 }
 
 void prof_end(kt_context_s* ctx, int slot, hipStream_t st) {
@@ -71,7 +72,15 @@ void prof_collect(kt_context_s* ctx, const size_t* upto, bool wait) {
             s.iv.push_back({a, b});
             s.total_ms += ms;
             s.launches += 1;
+            const int tag = s.tags[(i - s.done) / 2];
+            auto it = std::find_if(s.by_tag.begin(), s.by_tag.end(), [&](const auto& e) { return e.first == tag; });
+            if (it == s.by_tag.end()) s.by_tag.push_back({tag, {1, (double)ms}});
+            else {
+                it->second.first += 1;
+                it->second.second += ms;
+            }
         }
+        s.tags.erase(s.tags.begin(), s.tags.begin() + (std::ptrdiff_t)((end - s.done) / 2));
         s.done = end;
     }
 }
@@ -535,6 +544,8 @@ int kt_profile_reset(kt_context_t ctx) {
         s.total_ms = 0.0;
         s.iv.clear();
         s.anchored = false;
+        s.tags.clear();
+        s.by_tag.clear();
         s.used = 0;
         s.done = 0;
     }
@@ -549,6 +560,23 @@ int kt_debug_delay(kt_context_t ctx, int lane, double microseconds) {
     if (lane && !ctx->aux_stream[lane - 1])
         KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[lane - 1], hipStreamNonBlocking));
     KT_HIP(launch_delay(microseconds, lane ? ctx->aux_stream[lane - 1] : ctx->stream));
+    KT_GUARD_END
+}
+
+int kt_profile_read_width(kt_context_t ctx, int kernel, int width, int64_t* launches, double* total_ms) {
+    KT_GUARD_BEGIN
+    if (!ctx || kernel < 0 || kernel >= PROF_NSLOTS) fail(KT_ERR_ARG, "bad profile query");
+    KT_HIP(hipSetDevice(ctx->device));
+    prof_collect(ctx, nullptr, true);
+    int64_t l = 0;
+    double ms = 0.0;
+    for (const auto& e : ctx->prof[kernel].by_tag)
+        if (e.first == width) {
+            l = e.second.first;
+            ms = e.second.second;
+        }
+    if (launches) *launches = l;
+    if (total_ms) *total_ms = ms;
     KT_GUARD_END
 }
 

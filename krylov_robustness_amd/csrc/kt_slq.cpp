@@ -115,14 +115,14 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
             KT_HIP(hipMemcpyAsync(hist_dev->as<double>() + (size_t)j * P, sc, sizeof(double) * P,
                                   hipMemcpyDeviceToDevice, st));
         }
-        prof_begin(ctx, PROF_SPMM, st);
+        prof_begin(ctx, PROF_SPMM, st, P);
         KT_HIP(launch_spmm_dot(P, ctx->k1_flags | (A->unit_values ? 2 : 0), grid1, M.rowptr, M.col,
                                M.val, n, ucur, sc, w.Y.as<double>(), part1, M.long_rows, M.n_long,
                                A->long_thresh, lblocks, st));
         prof_end(ctx, PROF_SPMM, st);
         KT_HIP(launch_coef_cgs2(P, part1, grid1, first, k2s, sc, sp, coef,
                                 trec + (size_t)(0 * m + j) * P, trec + (size_t)(1 * m + j) * P, st));
-        prof_begin(ctx, PROF_UPDATE, st);
+        prof_begin(ctx, PROF_UPDATE, st, P);
         double* rec = (basis && j + 1 < m) ? bbase + (size_t)(j + 1) * n * bcols : nullptr;
         KT_HIP(launch_update(P, grid, n, w.Y.as<double>(), uprev, ucur, sc, sp, coef, first, part2,
                              st, ctx->k2_nt, rec, bcols));
@@ -179,13 +179,13 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
     double* Xc = w.Y.as<double>();   // y_j
     double* Yo = nullptr;            // y_{j-1} (none at j = 0)
     double* Ot = w.X0.as<double>();  // y_{j+1}
-    prof_begin(ctx, PROF_START, st);
+    prof_begin(ctx, PROF_START, st, P);
     KT_HIP(launch_spmm_lanczos_start(P, flags, grid1, M.rowptr, M.col, M.val, n, Z, s0, Xc, part,
                                      M.long_rows, M.n_long, A->long_thresh, lblocks, st));
     prof_end(ctx, PROF_START, st);
     KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, s0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0), guard, st));
     for (int j = 0; j + 1 < m; ++j) {
-        prof_begin(ctx, PROF_SPMM, st);
+        prof_begin(ctx, PROF_SPMM, st, P);
         const bool last = j + 2 == m;  // y_{m} is never used: alpha_{m-1} needs only X.t
         KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
                                    last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long,

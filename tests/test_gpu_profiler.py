@@ -78,6 +78,10 @@ def test_pipelined_union_counts_overlap_once(kra, monkeypatch):
     busy = ctx.profile_busy(0)
     assert launches == 6 * 4 * 29
     assert busy <= wall_ms and busy <= summed + 1e-4 * launches
+    # every launch carries its sweep's width
+    assert ctx.profile_read_width(0, 16) == (launches, summed)
+    assert ctx.profile_read_width(0, 32) == (0, 0.0)
+    assert ctx.profile_read_width(2, 16)[0] == 6 * 4  # one start pass per sweep
 
 
 def test_destroyed_matrix_ticket_fails_cleanly(kra):
