@@ -13,6 +13,7 @@
 #            config-1/3/5 drivers under rocprofv3
 #   timeline rocprofv3 kernel trace of the er100k bench, per-evaluation
 #            breakdown (tools/eval_timeline.py)
+#   rehearse `python bench.py --gpus 2` (self-launched ranks) on one GPU, gloo
 #   pmc      FETCH_SIZE / WRITE_SIZE passes (separate runs) of `bench.py
 #            --steps 1 --lanes 1 [extra]` -> traffic.json section
 #            (SECTION env, default sf1m)
@@ -65,6 +66,12 @@ secondary)
         gzip -f $(find $O/st_$s -name "*kernel_trace.csv")
         echo "== $s"; cut -c1-300 $O/$s.json
     done ;;
+rehearse)
+    # the driver's N = 2 command as it may run it (no torchrun: bench.py starts
+    # the ranks itself), both ranks on GPU 0 over gloo, default config
+    KT_BENCH_ONE_DEVICE=1 timeout -k 10 500 python -u bench.py --gpus 2 --dist-backend gloo "$@" \
+        > $O/bench_2ranks_self_launch.json 2> $O/bench_2ranks_self_launch.err || { tail -20 $O/bench_2ranks_self_launch.err; exit 1; }
+    cut -c1-400 $O/bench_2ranks_self_launch.json ;;
 pmc)
     SEC=${SECTION:-sf1m}
     B="$GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --cpu-seconds 0 --lanes 1 --mc-steps 1 --no-profile $*"
