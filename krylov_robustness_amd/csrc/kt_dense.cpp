@@ -27,9 +27,27 @@ double fscalar(int fun, double x) {
     }
 }
 
+// Radius of a plane rotation: sqrt(f^2 + g^2), rescaled through hypot only
+// when the squares could leave the double range.  (glibc's hypot is a libm
+// call of ~20 ns; the QL sweep below is a serial chain of ~m^2 rotations, so
+// at m = 30 hypot alone was 40% of a column's quadrature.)
+static inline double rot_radius(double f, double g) {
+    const double af = std::fabs(f), ag = std::fabs(g);
+    const double mx = af > ag ? af : ag;
+    if (mx > 1e150 || (mx < 1e-150 && mx > 0.0)) return std::hypot(f, g);
+    return std::sqrt(f * f + g * g);
+}
+
+struct Rot {
+    int i;
+    double s, c;
+};
+
 // Symmetric tridiagonal (d[0..m-1], e[0..m-2]) -> eigenvalues in d and the
-// first eigenvector components in z.
-static void ql_first_row(int m, double* d, double* e, double* z) {
+// first eigenvector components in z (implicit-shift QL rotating only the first
+// row of the eigenvector matrix Z).  With `log`, every rotation applied to z
+// is recorded in order: Z = R_1 R_2 ... R_k, R_j acting on columns (i, i+1).
+static void ql_first_row(int m, double* d, double* e, double* z, std::vector<Rot>* log = nullptr) {
     e[m - 1] = 0.0;
     for (int i = 0; i < m; ++i) z[i] = (i == 0) ? 1.0 : 0.0;
     for (int l = 0; l < m; ++l) {
@@ -42,13 +60,13 @@ static void ql_first_row(int m, double* d, double* e, double* z) {
             }
             if (mm == l || iter++ == 100) break;
             double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
-            double r = std::hypot(g, 1.0);
+            double r = rot_radius(g, 1.0);
             g = d[mm] - d[l] + e[l] / (g + std::copysign(r, g));
             double s = 1.0, c = 1.0, p = 0.0;
             bool deflated = false;
             for (int i = mm - 1; i >= l; --i) {
                 const double f = s * e[i], b = c * e[i];
-                r = std::hypot(f, g);
+                r = rot_radius(f, g);
                 e[i + 1] = r;
                 if (r == 0.0) {
                     d[i + 1] -= p;
@@ -66,6 +84,7 @@ static void ql_first_row(int m, double* d, double* e, double* z) {
                 const double zf = z[i + 1];
                 z[i + 1] = s * z[i] + c * zf;
                 z[i] = c * z[i] - s * zf;
+                if (log) log->push_back({i, s, c});
             }
             if (deflated) continue;
             d[l] -= p;
@@ -82,6 +101,32 @@ double tridiag_quadrature(int m, const double* alpha, const double* off, int fun
     ql_first_row(m, d.data(), e.data(), z.data());
     double q = 0.0;
     for (int i = 0; i < m; ++i) q += z[i] * z[i] * fscalar(fun, d[i]);
+    return q;
+}
+
+// The quadrature and f(T) e1 = Z f(Theta) Z' e1 from one QL pass: Z' e1 = z
+// (the rotated first row), and Z v = R_1 (R_2 (... R_k v)) replays the logged
+// rotations backwards on the one vector v = f(theta) .* z -- O(rotations),
+// where forming Z (tred2 + tql2 with vectors) costs m times that.
+double tridiag_fun_e1(int m, const double* alpha, const double* off, int fun, double* fe1) {
+    if (m <= 0) return 0.0;
+    std::vector<double> d(alpha, alpha + m), e(m, 0.0), z(m);
+    for (int i = 0; i + 1 < m; ++i) e[i] = off[i];
+    std::vector<Rot> log;
+    log.reserve((size_t)4 * m * m);
+    ql_first_row(m, d.data(), e.data(), z.data(), &log);
+    double q = 0.0;
+    for (int k = 0; k < m; ++k) {
+        const double fk = fscalar(fun, d[k]);
+        q += z[k] * z[k] * fk;
+        fe1[k] = fk * z[k];
+    }
+    for (size_t j = log.size(); j-- > 0;) {
+        const Rot& R = log[j];
+        const double a = fe1[R.i], b = fe1[R.i + 1];
+        fe1[R.i] = R.c * a + R.s * b;
+        fe1[R.i + 1] = R.c * b - R.s * a;
+    }
     return q;
 }
 
@@ -204,14 +249,14 @@ static void tql2(int n, double* d, double* e, double* z /* nullable */) {
             }
             if (m == l || iter++ == 200) break;
             double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
-            double r = std::hypot(g, 1.0);
+            double r = rot_radius(g, 1.0);
             g = d[m] - d[l] + e[l] / (g + std::copysign(r, g));
             double s = 1.0, c = 1.0, p = 0.0;
             bool deflated = false;
             for (int i = m - 1; i >= l; --i) {
                 double f = s * e[i];
                 const double b = c * e[i];
-                r = std::hypot(f, g);
+                r = rot_radius(f, g);
                 e[i + 1] = r;
                 if (r == 0.0) {
                     d[i + 1] -= p;
@@ -335,18 +380,10 @@ static void tridiag_lower_cols_base(int n, double* a, double* d, double* e, doub
     tridiag_lower_cols<0>(n, a, d, e, v, p);
 }
 
-// tql2 without eigenvectors for the column path: the rotations' radii by
-// sqrt(f^2 + g^2) instead of hypot (a libm call per rotation), rescaled when
-// the squares could leave the double range
+// tql2 without eigenvectors for the column path
 static void tql_values(int n, double* d, double* e) {
     for (int i = 1; i < n; ++i) e[i - 1] = e[i];
     e[n - 1] = 0.0;
-    auto rad = [](double f, double g) {
-        const double af = std::fabs(f), ag = std::fabs(g);
-        const double mx = af > ag ? af : ag;
-        if (mx > 1e150 || (mx < 1e-150 && mx > 0.0)) return std::hypot(f, g);
-        return std::sqrt(f * f + g * g);
-    };
     for (int l = 0; l < n; ++l) {
         int iter = 0;
         for (;;) {
@@ -357,14 +394,14 @@ static void tql_values(int n, double* d, double* e) {
             }
             if (m == l || iter++ == 200) break;
             double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
-            double r = rad(g, 1.0);
+            double r = rot_radius(g, 1.0);
             g = d[m] - d[l] + e[l] / (g + std::copysign(r, g));
             double s = 1.0, c = 1.0, p = 0.0;
             bool deflated = false;
             for (int i = m - 1; i >= l; --i) {
                 const double f = s * e[i];
                 const double b = c * e[i];
-                r = rad(f, g);
+                r = rot_radius(f, g);
                 e[i + 1] = r;
                 if (r == 0.0) {
                     d[i + 1] -= p;

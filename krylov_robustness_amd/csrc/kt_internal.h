@@ -210,7 +210,8 @@ struct Workspace {
     DevBuf ts_V, ts_part, ts_small;  // tall-skinny Householder QR (kt_tsqr.hip)
     // lanczos_columns_split (kt_slq.cpp): pinned sweep records, the y-form
     // start scales per lane, the permuted block's ready event for the aux lanes
-    PinnedBuf pin_colrec, pin_ycoef[4];
+    PinnedBuf pin_colrec;
+    DevBuf colnorm;  // the block's squared column norms (device)
     hipEvent_t colsplit_ev = nullptr;
 };
 
@@ -344,6 +345,8 @@ double prof_busy(const ProfSlot& s);
 double fscalar(int fun, double x);
 // Gauss quadrature e1' f(T) e1 for symmetric tridiagonal T (m x m).
 double tridiag_quadrature(int m, const double* alpha, const double* off, int fun);
+// The same quadrature, and f(T) e1 into fe1[0..m-1], from one QL pass.
+double tridiag_fun_e1(int m, const double* alpha, const double* off, int fun, double* fe1);
 bool chol_upper(double* G, int n);
 void tri_upper_inv(const double* R, int n, double* X);
 void sym_eig_host(int n, const double* A, double* w, double* V);

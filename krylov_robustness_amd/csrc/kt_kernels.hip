@@ -2040,6 +2040,42 @@ hipError_t launch_absmax_idx(int n, const double* Z, double* pval, int* pidx, hi
     return hipGetLastError();
 }
 
+// Start scales of a sweep seeded by a device block, from the columns'
+// squared norms n2 (device, nc of them; zero norm: a zero column):
+//   mode 0 (explicit sweep): a = sc[P] = 1/||x_c||, b = k2s[P] = ||x_c||^2;
+//   mode 1 (y-form sweep):   a = ys[9P] = [1/||x_c|| | 0 (5P) | 1 (P) | 0 (2P)]
+// so the sweep is queued without the host reading the norms first.
+__global__ __launch_bounds__(256) void k_sweep_scales(const double* __restrict__ n2, int nc, int P, int mode,
+                                                      double* __restrict__ a, double* __restrict__ b) {
+    for (int t = threadIdx.x; t < (mode ? 9 * P : P); t += blockDim.x) {
+        const int c = t % P, q = t / P;
+        const double v = c < nc ? n2[c] : 0.0;
+        const double s = v > 0.0 ? 1.0 / sqrt(v) : 0.0;
+        if (mode == 0) {
+            a[t] = s;
+            b[t] = v > 0.0 ? v : 0.0;
+        } else {
+            a[t] = q == 0 ? s : (q == 6 ? 1.0 : 0.0);
+        }
+    }
+}
+
+// n2[c] = G[c + c ld] (the diagonal of a Gram block)
+__global__ __launch_bounds__(64) void k_gram_diag(const double* __restrict__ G, int ld, int nc,
+                                                  double* __restrict__ n2) {
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) n2[c] = G[c + (int64_t)c * ld];
+}
+
+hipError_t launch_sweep_scales(const double* n2, int nc, int P, int mode, double* a, double* b, hipStream_t st) {
+    k_sweep_scales<<<1, 256, 0, st>>>(n2, nc, P, mode, a, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_gram_diag(const double* G, int ld, int nc, double* n2, hipStream_t st) {
+    k_gram_diag<<<1, 64, 0, st>>>(G, ld, nc, n2);
+    return hipGetLastError();
+}
+
 // test hook (kt_debug_delay): one wave that waits `ticks` of the 100 MHz
 // constant clock, so a stream is busy for a known time; every wave exits
 __global__ __launch_bounds__(64) void k_delay(long long ticks) {

@@ -85,6 +85,10 @@ hipError_t launch_ycoef(int P, const double* partial, int nblk, int start, int l
                         hipStream_t st);
 hipError_t launch_fill(double* x, int count, double v, hipStream_t st);
 hipError_t launch_delay(double microseconds, hipStream_t st);
+// sweep start scales from device column norms (kt_slq.cpp; mode 0 explicit: sc,
+// k2s; mode 1 y-form: the 9P coefficient block) and a Gram block's diagonal
+hipError_t launch_sweep_scales(const double* n2, int nc, int P, int mode, double* a, double* b, hipStream_t st);
+hipError_t launch_gram_diag(const double* G, int ld, int nc, double* n2, hipStream_t st);
 // out[i] = D[off[i]], i < count
 // tall-skinny Gram / combine (kt_gemm_ts.hip)
 int gram_ts_chunks(int64_t n);

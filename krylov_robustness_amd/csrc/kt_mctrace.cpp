@@ -450,21 +450,19 @@ struct Shard {
     void* user = nullptr;
 };
 
-// X <- X - Q (Q' X)  on nc columns (the deflation aux of mc_trace.m:47)
-static void project(kt_context_s* ctx, int64_t n, const double* Q, int ld, int nq, double* X, int nc) {
-    std::vector<double> G;
-    gram(ctx, n, Q, ld, nq, X, ld, nc, G);
-    for (double& g : G) g = -g;
-    combine(ctx, n, Q, ld, nq, G, nc, 1.0, X, ld);
-}
-
-// X <- X - Q (Q' X) with separate leading dimensions for Q and X
+// X <- X - Q (Q' X) with separate leading dimensions for Q and X (the
+// deflation aux of mc_trace.m:47): the Gram block stays on the device and
+// the combine reads it in stream order -- no host round trip per projection
 static void project_ld(kt_context_s* ctx, int64_t n, const double* Q, int ldq, int nq, double* X, int ldx,
                        int nc) {
-    std::vector<double> G;
-    gram(ctx, n, Q, ldq, nq, X, ldx, nc, G);
-    for (double& g : G) g = -g;
-    combine(ctx, n, Q, ldq, nq, G, nc, 1.0, X, ldx);
+    if (nc <= 0 || nq <= 0) return;
+    const double* dG = gram_device(ctx, n, Q, ldq, nq, X, ldx, nc);
+    combine_device(ctx, n, Q, ldq, nq, dG, nc, -1.0, 1.0, X, ldx);
+}
+
+// X <- X - Q (Q' X)  on nc columns, one leading dimension
+static void project(kt_context_s* ctx, int64_t n, const double* Q, int ld, int nq, double* X, int nc) {
+    project_ld(ctx, n, Q, ld, nq, X, ld, nc);
 }
 
 // mc_trace.m:42-58 with the Lanczos-f Afun, one batch of sweeps per round.
@@ -536,7 +534,12 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
         // G term input: P_it..P_1 G_it, this rank's columns c % world == rank  :44, :49
         KT_HIP(launch_rademacher(ld, (int)n, seed, base + mb, nullptr, T.col(0), st));
         int ng = 0;
-        for (int c = sh.rank; c < mb; c += sh.world) copy_cols(ctx, n, T.col(c), ld, Bk.col(2 * mb + ng++), LB, 1);
+        if (sh.world == 1) {  // every G column: one block copy
+            copy_cols(ctx, n, T.col(0), ld, Bk.col(2 * mb), LB, mb);
+            ng = mb;
+        } else {
+            for (int c = sh.rank; c < mb; c += sh.world) copy_cols(ctx, n, T.col(c), ld, Bk.col(2 * mb + ng++), LB, 1);
+        }
         for (int k = (int)Qs.size() - 1; k >= 0 && ng > 0; --k)
             project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(2 * mb), LB, ng);
         // next round's S term input: P_it..P_1 S_{it+1}, unless this round is

@@ -42,9 +42,10 @@ int slq_auto_block(int64_t n, int64_t nprobes) {
 
 // Run one sweep.  rec_host receives [alpha | up | low][m][P].
 // init: if seeded by RNG, `x` == nullptr; else x (device, n x ldx, ncols
-// columns, original-column norms^2 in norms2) is copied into the sweep block.
+// columns, their squared norms in the DEVICE array dnorms2) is copied into
+// the sweep block.
 void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base,
-                   const double* x, int ldx, int ncols, const double* norms2, double* rec_host,
+                   const double* x, int ldx, int ncols, const double* dnorms2, double* rec_host,
                    DevMat* basis, std::vector<double>* scale_hist, int lane, int bcols) {
     if (bcols <= 0 || bcols > P) bcols = P;
     kt_context_s* ctx = A->ctx;
@@ -86,15 +87,8 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
         KT_HIP(hipMemsetAsync(ucur, 0, blk_bytes, st));
         KT_HIP(hipMemcpy2DAsync(ucur, sizeof(double) * P, x, sizeof(double) * ldx,
                                 sizeof(double) * ncols, (size_t)n, hipMemcpyDeviceToDevice, st));
-        std::vector<double> s0(P, 0.0), q0(P, 0.0);
-        for (int c = 0; c < ncols; ++c)
-            if (norms2[c] > 0.0) {
-                s0[c] = 1.0 / std::sqrt(norms2[c]);
-                q0[c] = norms2[c];
-            }
-        KT_HIP(hipMemcpyAsync(sc, s0.data(), sizeof(double) * P, hipMemcpyHostToDevice, st));
-        KT_HIP(hipMemcpyAsync(k2s, q0.data(), sizeof(double) * P, hipMemcpyHostToDevice, st));
-        KT_HIP(hipStreamSynchronize(st));  // s0/q0 are stack temporaries
+        // s_0 = 1/||x_c||, ||x_c||^2 from the device norms: no host round trip
+        KT_HIP(launch_sweep_scales(dnorms2, ncols, P, 0, sc, k2s, st));
     }
     if (scale_hist) scale_hist->assign((size_t)m * P, 0.0);
     DevBuf* hist_dev = nullptr;
@@ -202,13 +196,13 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
 
 // y-form sweep seeded by a given device block (the quadrature-only columns
 // of mc_trace's Lanczos Afun, kt_mctrace.cpp): x (n x ldx, ncols columns, in
-// M's row order, squared norms norms2) is normalised into the gathered table
+// M's row order, squared norms in the device array dnorms2) is normalised into the gathered table
 // v_0 (zero columns stay zero), the pass in start mode forms y_0 = A v_0 with
 // (g, a, b) = (1, 0, 0), then the same passes as the RNG-seeded sweep.
 // rec_host (pinned, or the call waits for the copy) receives [alpha | up |
 // low][m][P] followed by guard[P].  No basis: quadratic forms only.
 void lanczos_sweep_y_block(kt_matrix_s* A, const DevCSR& M, int P, int m, const double* x, int ldx, int ncols,
-                           const double* norms2, double* rec_host, int lane) {
+                           const double* dnorms2, double* rec_host, int lane) {
     kt_context_s* ctx = A->ctx;
     const int n = (int)A->n;
     if (lane < 0 || lane > 3) fail(KT_ERR_ARG, "sweep lane out of range");
@@ -235,16 +229,9 @@ void lanczos_sweep_y_block(kt_matrix_s* A, const DevCSR& M, int P, int m, const 
     auto rec_at = [&](int row, int j) { return trec + (size_t)(row * m + j) * P; };
     int flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
     if (blk_bytes >= ((size_t)1 << 31)) flags &= ~16;
-    // ys: [1/||x_c|| (P) | 0 (5P) | start pass (g, a, b) = (1, 0, 0) (3P)]
-    PinnedBuf& hb = ctx->ws.pin_ycoef[lane];
-    hb.ensure(sizeof(double) * 9 * P);
-    double* h = hb.as<double>();
-    KT_HIP(hipStreamSynchronize(st));  // the lane's previous upload out of hb is done
-    std::fill(h, h + 9 * P, 0.0);
-    for (int c = 0; c < ncols; ++c)
-        if (norms2[c] > 0.0) h[c] = 1.0 / std::sqrt(norms2[c]);
-    for (int c = 0; c < P; ++c) h[6 * P + c] = 1.0;
-    KT_HIP(hipMemcpyAsync(ys, h, sizeof(double) * 9 * P, hipMemcpyHostToDevice, st));
+    // ys: [1/||x_c|| (P) | 0 (5P) | start pass (g, a, b) = (1, 0, 0) (3P)], from
+    // the device norms (no host round trip)
+    KT_HIP(launch_sweep_scales(dnorms2, ncols, P, 1, ys, nullptr, st));
     double* V0 = w.X1.as<double>();  // the start pass's gathered table v_0
     KT_HIP(hipMemsetAsync(V0, 0, blk_bytes, st));
     KT_HIP(launch_weighted_sum(n, 1, P, ncols, x, ldx, 0, ys, V0, P, st));
@@ -313,10 +300,11 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     const int64_t n = A->n;
     if (!Y) ny = 0;
     if (ny < 0 || ny > ne || ne > ncols) fail(KT_ERR_ARG, "lanczos_columns_split: 0 <= ny <= ne <= ncols");
-    std::vector<double> nrm2;
-    gram(ctx, n, X, ldx, ncols, X, ldx, ncols, nrm2);
-    std::vector<double> norms2(ncols);
-    for (int c = 0; c < ncols; ++c) norms2[c] = nrm2[c + (size_t)c * ncols];
+    // squared column norms on the device (the sweeps' start scales are formed
+    // from them there); the host reads them with the sweep records
+    ctx->ws.colnorm.ensure(sizeof(double) * ncols);
+    double* dn2 = ctx->ws.colnorm.as<double>();
+    KT_HIP(launch_gram_diag(gram_device(ctx, n, X, ldx, ncols, X, ldx, ncols), ncols, ncols, dn2, ctx->stream));
     // The sweeps run on the hubs-first CSR (equal-length neighbouring rows,
     // adjacent hub segments: the explicit K1 at P = 16 on the bench graph 264
     // -> ~210 us): the block is permuted into that row order on the way in
@@ -364,7 +352,9 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     }
     const size_t rec_max = (size_t)3 * m * 32 + 32;
     PinnedBuf& hr = ctx->ws.pin_colrec;
-    hr.ensure(sizeof(double) * rec_max * sw.size());
+    hr.ensure(sizeof(double) * (rec_max * sw.size() + ncols));
+    double* hn2 = hr.as<double>() + rec_max * sw.size();  // the norms, read after the sweeps
+    KT_HIP(hipMemcpyAsync(hn2, dn2, sizeof(double) * ncols, hipMemcpyDeviceToHost, ctx->stream));
     // the aux lanes read the permuted block written on ctx->stream
     hipEvent_t ready = ctx->ws.colsplit_ev;
     if (!ready) {
@@ -382,8 +372,8 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
             KT_HIP(hipStreamWaitEvent(as, ready, 0));
             used[q.lane] = true;
         }
-        lanczos_sweep_y_block(A, M, q.P, m, Xs + q.c0, ldxs, q.nc, norms2.data() + q.c0,
-                              hr.as<double>() + rec_max * i, q.lane);
+        lanczos_sweep_y_block(A, M, q.P, m, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, hr.as<double>() + rec_max * i,
+                              q.lane);
     }
     // the explicit sweeps (lane 0) with their bases
     std::vector<DevMat> bases(sw.size());
@@ -393,12 +383,13 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
         if (q.yform) continue;
         const int nyc = std::max(0, std::min(q.nc, ny - q.c0));
         if (nyc) bases[i].alloc(ctx, n, m * nyc, false);  // every slot is written by the sweep
-        lanczos_sweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, norms2.data() + q.c0,
-                      hr.as<double>() + rec_max * i, nyc ? &bases[i] : nullptr, nyc ? &hists[i] : nullptr, 0, nyc);
+        lanczos_sweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, hr.as<double>() + rec_max * i,
+                      nyc ? &bases[i] : nullptr, nyc ? &hists[i] : nullptr, 0, nyc);
     }
     KT_HIP(hipStreamSynchronize(ctx->stream));
     for (int l = 1; l < 4; ++l)
         if (used[l]) KT_HIP(hipStreamSynchronize(ctx->aux_stream[l - 1]));
+    const std::vector<double> norms2(hn2, hn2 + ncols);
     // a y-form sweep whose live column tripped the cancellation guard (or a
     // lucky breakdown) is redone by the explicit CGS2 sweep (kt_slq_collect's rule)
     for (size_t i = 0; i < sw.size(); ++i) {
@@ -408,40 +399,48 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
         bool bad = false;
         for (int c = 0; c < q.nc; ++c) bad |= norms2[q.c0 + c] > 0.0 && !(g[c] >= kYformGuard);
         if (!bad) continue;
-        lanczos_sweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, norms2.data() + q.c0, hr.as<double>() + rec_max * i,
+        lanczos_sweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, hr.as<double>() + rec_max * i,
                       nullptr, nullptr, 0);
         KT_HIP(hipStreamSynchronize(ctx->stream));
         ctx->yform_redone += 1;
     }
+    // per column (one QL pass each, on the host pool): the quadrature and,
+    // for the f(A) x columns, f(T) e1 -> the basis weights
+    std::vector<int> nycs(sw.size()), col_sw, col_c;
+    std::vector<std::vector<double>> Ws(sw.size());  // Y = sum_j u_j w_j, [j * nyc + c]
     for (size_t i = 0; i < sw.size(); ++i) {
         const Sw& q = sw[i];
-        const double* R = hr.as<double>() + rec_max * i;
-        const int nyc = q.yform ? 0 : std::max(0, std::min(q.nc, ny - q.c0));
-        std::vector<double> W((size_t)m * std::max(nyc, 1), 0.0);  // weights for Y = sum_j u_j w_j, [j * nyc + c]
+        nycs[i] = q.yform ? 0 : std::max(0, std::min(q.nc, ny - q.c0));
+        Ws[i].assign((size_t)m * std::max(nycs[i], 1), 0.0);
         for (int c = 0; c < q.nc; ++c) {
-            std::vector<double> al(m), off(m);
-            const int steps = record_tridiag(R, m, q.P, c, al.data(), off.data());
-            if (norms2[q.c0 + c] == 0.0) {
-                if (quad) quad[q.c0 + c] = 0.0;
-                continue;
-            }
-            if (quad) quad[q.c0 + c] = norms2[q.c0 + c] * tridiag_quadrature(steps, al.data(), off.data(), fun);
-            if (c < nyc) {
-                // f(T) e1 = Z f(theta) Z(0,:)'
-                std::vector<double> T((size_t)steps * steps, 0.0), th(steps), Z((size_t)steps * steps);
-                for (int j = 0; j < steps; ++j) T[j + (size_t)j * steps] = al[j];
-                for (int j = 0; j + 1 < steps; ++j)
-                    T[j + 1 + (size_t)j * steps] = T[j + (size_t)(j + 1) * steps] = off[j];
-                sym_eig_host(steps, T.data(), th.data(), Z.data());
-                const double nx = std::sqrt(norms2[q.c0 + c]);
-                for (int j = 0; j < steps; ++j) {
-                    double cj = 0.0;
-                    for (int k = 0; k < steps; ++k)
-                        cj += Z[j + (size_t)k * steps] * fscalar(fun, th[k]) * Z[(size_t)k * steps];
-                    W[(size_t)j * nyc + c] = nx * hists[i][(size_t)j * q.P + c] * cj;  // v_j = s_j u_j
-                }
-            }
+            col_sw.push_back((int)i);
+            col_c.push_back(c);
         }
+    }
+    HostPool::get().run((int)col_sw.size(), [&](int t) {
+        const int i = col_sw[t], c = col_c[t], nyc = nycs[i];
+        const Sw& q = sw[i];
+        const double* R = hr.as<double>() + rec_max * i;
+        std::vector<double> al(m), off(m), fe1(m);
+        const int steps = record_tridiag(R, m, q.P, c, al.data(), off.data());
+        if (norms2[q.c0 + c] == 0.0) {
+            if (quad) quad[q.c0 + c] = 0.0;
+            return;
+        }
+        if (c >= nyc) {
+            if (quad) quad[q.c0 + c] = norms2[q.c0 + c] * tridiag_quadrature(steps, al.data(), off.data(), fun);
+            return;
+        }
+        const double qd = tridiag_fun_e1(steps, al.data(), off.data(), fun, fe1.data());
+        if (quad) quad[q.c0 + c] = norms2[q.c0 + c] * qd;
+        const double nx = std::sqrt(norms2[q.c0 + c]);
+        for (int j = 0; j < steps; ++j)
+            Ws[i][(size_t)j * nyc + c] = nx * hists[i][(size_t)j * q.P + c] * fe1[j];  // v_j = s_j u_j
+    }, 4);
+    for (size_t i = 0; i < sw.size(); ++i) {
+        const Sw& q = sw[i];
+        const int nyc = nycs[i];
+        const std::vector<double>& W = Ws[i];
         if (nyc) {
             DevBuf& dw = ctx->ws.small2;
             dw.ensure(sizeof(double) * W.size());

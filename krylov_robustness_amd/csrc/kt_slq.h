@@ -13,7 +13,7 @@ int slq_auto_block(int64_t n, int64_t nprobes);
 // basis (optional, >= n m bcols doubles): slot j = u_j's first bcols columns
 // as an n x bcols row-major block at basis->col(0) + j n bcols.
 void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base,
-                   const double* x, int ldx, int ncols, const double* norms2, double* rec_host,
+                   const double* x, int ldx, int ncols, const double* dnorms2, double* rec_host,
                    DevMat* basis, std::vector<double>* scale_hist, int lane = 0, int bcols = 0);
 
 int record_tridiag(const double* R, int m, int P, int c, double* al, double* off);
@@ -39,6 +39,6 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
 
 // y-form sweep seeded by a device block (see kt_slq.cpp)
 void lanczos_sweep_y_block(kt_matrix_s* A, const DevCSR& M, int P, int m, const double* x, int ldx, int ncols,
-                           const double* norms2, double* rec_host, int lane);
+                           const double* dnorms2, double* rec_host, int lane);
 
 }  // namespace kt

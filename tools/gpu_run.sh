@@ -13,6 +13,8 @@
 #            config-1/3/5 drivers under rocprofv3
 #   timeline rocprofv3 kernel trace of the er100k bench, per-evaluation
 #            breakdown (tools/eval_timeline.py)
+#   mctl     kernel trace of the mc_trace leg, per-evaluation breakdown
+#            (tools/mc_timeline.py)
 #   rehearse `python bench.py --gpus 2` (self-launched ranks) on one GPU, gloo
 #   pmc      FETCH_SIZE / WRITE_SIZE passes (separate runs) of `bench.py
 #            --steps 1 --lanes 1 [extra]` -> traffic.json section
@@ -66,6 +68,13 @@ secondary)
         gzip -f $(find $O/st_$s -name "*kernel_trace.csv")
         echo "== $s"; cut -c1-300 $O/$s.json
     done ;;
+mctl)
+    # kernel trace of the mc_trace leg (trace_exp, Lanczos-exp Afun), evaluation by evaluation
+    ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/mctl -o mctl \
+        -- python3 $GRAFT_REPO_ROOT/bench.py --estimator mc_trace --steps 10 --cpu-seconds 0 --ref-cpu-seconds 0 \
+        --no-profile "$@" > $O/bench_mc_traced.json 2> $O/mctl.err ) || { tail -20 $O/mctl.err; exit 1; }
+    python3 tools/mc_timeline.py $(find $O/mctl -name "*kernel_trace.csv") 10 $O/mc_timeline.json || exit 1
+    gzip -f $(find $O/mctl -name "*kernel_trace.csv") ;;
 rehearse)
     # the driver's N = 2 command as it may run it (no torchrun: bench.py starts
     # the ranks itself), both ranks on GPU 0 over gloo, default config
