@@ -477,10 +477,9 @@ static void project(kt_context_s* ctx, int64_t n, const double* Q, int ld, int n
 // is expected to stop the loop: |trace(G' Afun G)/m| of the previous round
 // below tol |tr_new| (the deflated remainder is already below the stopping
 // tolerance; on the config-4 graph, rank one to 1e-23, round 2 always
-// stops).  Such a round runs only its Q and G terms: Q by a 16-wide explicit
-// sweep, G -- quadratic forms of random probes, mc_trace.m:49 -- by y-form
-// sweeps (one pass per Lanczos step, no K2 stream) beside it on another
-// lane.  A wrong guess moves the S term to the start of the next round;
+// stops).  Such a round runs only its Q and G terms (:46, :49), quadratic
+// forms both, by y-form sweeps (one pass per Lanczos step, no K2 stream) on
+// two lanes.  A wrong guess moves the S term to the start of the next round;
 // mc_trace never stops in round 1 (tr_old = 0), so round 2's S term is always
 // computed ahead.
 //
@@ -552,10 +551,13 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
             // gather and one CSR pass for the three Afun calls
             lanczos_columns_split(A, Bk.col(0), LB, 3 * mb, mb, 3 * mb, F.m, F.fun, q.data(), Yb.col(0), ld, LB);
         } else {
-            // no S term: Q by the explicit sweep (16 wide; its columns start
-            // near the deflated operator's top eigenvectors, where the y-form's
-            // cancellation guard trips), G (random probes) by y-form sweeps
-            lanczos_columns_split(A, Bk.col(mb), LB, 2 * mb, 0, mb, F.m, F.fun, q.data() + mb, nullptr, 0, 16);
+            // no S term: the Q and G columns need quadratic forms only, so
+            // both go through y-form sweeps (no K2, no basis), 16 wide on two
+            // lanes.  (Round 1's Q_1 column 0 is the top eigenvector to
+            // rounding -- a lucky breakdown at step 1 that the y-form guard
+            // sends to the explicit redo -- but round 1 always computes the
+            // S term ahead, so its Q columns ride the explicit 32-wide sweep.)
+            lanczos_columns_split(A, Bk.col(mb), LB, 2 * mb, 0, 0, F.m, F.fun, q.data() + mb, nullptr, 0, 16);
         }
         std::vector<double> qv(mb, 0.0);
         for (int c = sh.rank, t = 0; c < mb; c += sh.world, ++t) qv[c] = q[2 * mb + t];

@@ -390,18 +390,25 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     for (int l = 1; l < 4; ++l)
         if (used[l]) KT_HIP(hipStreamSynchronize(ctx->aux_stream[l - 1]));
     const std::vector<double> norms2(hn2, hn2 + ncols);
-    // a y-form sweep whose live column tripped the cancellation guard (or a
-    // lucky breakdown) is redone by the explicit CGS2 sweep (kt_slq_collect's rule)
+    // a y-form column that tripped the cancellation guard (or broke down) is
+    // redone by the explicit CGS2 sweep at the same width; only the tripped
+    // columns take the redo's records, so a column's form never depends on
+    // which columns share its sweep (mc_trace's world-size bit identity)
+    std::vector<double> redo;
     for (size_t i = 0; i < sw.size(); ++i) {
         const Sw& q = sw[i];
         if (!q.yform) continue;
-        const double* g = hr.as<double>() + rec_max * i + (size_t)3 * m * q.P;
-        bool bad = false;
-        for (int c = 0; c < q.nc; ++c) bad |= norms2[q.c0 + c] > 0.0 && !(g[c] >= kYformGuard);
-        if (!bad) continue;
-        lanczos_sweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, hr.as<double>() + rec_max * i,
-                      nullptr, nullptr, 0);
+        double* R = hr.as<double>() + rec_max * i;
+        const double* g = R + (size_t)3 * m * q.P;
+        std::vector<int> bad;
+        for (int c = 0; c < q.nc; ++c)
+            if (norms2[q.c0 + c] > 0.0 && !(g[c] >= kYformGuard)) bad.push_back(c);
+        if (bad.empty()) continue;
+        redo.assign((size_t)3 * m * q.P, 0.0);
+        lanczos_sweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, redo.data(), nullptr, nullptr, 0);
         KT_HIP(hipStreamSynchronize(ctx->stream));
+        for (int c : bad)
+            for (int row = 0; row < 3 * m; ++row) R[(size_t)row * q.P + c] = redo[(size_t)row * q.P + c];
         ctx->yform_redone += 1;
     }
     // per column (one QL pass each, on the host pool): the quadrature and,

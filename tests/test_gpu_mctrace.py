@@ -254,9 +254,9 @@ def test_mc_trace_next_s_term_guess_is_bit_identical(kra, gpu_ctx, monkeypatch, 
     the round is expected to stop (kt_mctrace.cpp mc_trace_batched); always
     ahead (KT_MC_AHEAD=1), never ahead (0) and the guess give the same round
     count and the estimate to rounding (a round with its S term ahead runs Q
-    and G in one 32-wide explicit sweep, one without runs Q 16 wide and G by
-    y-form sweeps: other reduction widths), over several rounds and a last
-    round it == K (tol = 0)."""
+    and G in one 32-wide explicit sweep, one without runs them by y-form
+    sweeps: other reduction widths), over several rounds and a last round
+    it == K (tol = 0)."""
     A = load_graph(name)
     D = kra.DeviceMatrix(A, gpu_ctx)
     for tol, maxit in ((1e-8, 150), (0.0, 90)):
@@ -275,9 +275,8 @@ def test_mc_trace_next_s_term_guess_is_bit_identical(kra, gpu_ctx, monkeypatch, 
 
 def test_mc_trace_quadrature_columns_yform_vs_explicit(kra, gpu_ctx, monkeypatch):
     """The Q and G columns' forms by the y-form sweep (default) and by the
-    explicit CGS2 sweep (KT_LC_YFORM=0) agree to rounding (a y-form sweep
-    whose deflated column trips the cancellation guard is redone by the
-    explicit sweep, as kt_slq_collect does)."""
+    explicit CGS2 sweep (KT_LC_YFORM=0) agree to rounding (a y-form column
+    that trips the cancellation guard takes the explicit redo's records)."""
     A = load_graph("oregon_A6")
     D = kra.DeviceMatrix(A, gpu_ctx)
     args = dict(n=A.shape[0], tol=1e-8, maxit=150, isAreal=1, seed=2, m=20)

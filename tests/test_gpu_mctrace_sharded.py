@@ -113,6 +113,26 @@ def test_threads_world_matches_single(kra, gpu_ctx, world, tol, maxit):
 
 
 @pytest.mark.parametrize("world", [2, 3])
+def test_threads_world_guard_redo_bit_identical(kra, gpu_ctx, monkeypatch, world):
+    """Never computing the S term ahead (KT_MC_AHEAD=0) sends round 1's Q
+    columns through y-form sweeps; Q_1's first column is the top eigenvector
+    to rounding (exp(A) of this graph is near rank one), a lucky breakdown at
+    step 1 that trips the y-form guard.  Only the tripped column takes the
+    explicit redo's records, so the replicated Q forms and the G slots stay
+    world-independent: bit for bit at every world size, redo included."""
+    monkeypatch.setenv("KT_MC_AHEAD", "0")
+    A = load_graph("oregon_A0")
+    kw = dict(tol=0.0, maxit=60, isAreal=1, seed=3, fun="exp", m=20)
+    before = gpu_ctx.stat(0)
+    ref = kra.mc_trace("lanczos", None, A=kra.DeviceMatrix(A, gpu_ctx), ctx=gpu_ctx, **kw)
+    assert gpu_ctx.stat(0) > before  # the guard redo ran
+    out, calls = _run_world(kra, A, world, "lanczos", **kw)
+    for r in out:
+        assert r == ref
+    assert calls == ref[2]
+
+
+@pytest.mark.parametrize("world", [2, 3])
 def test_threads_world_per_call_form(kra, gpu_ctx, monkeypatch, world):
     monkeypatch.setenv("KT_MC_BATCH", "0")
     A = load_graph("oregon_A0")
