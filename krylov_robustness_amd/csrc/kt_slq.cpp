@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cmath>
 #include <cstdlib>
+#include <memory>
 #include <thread>
 
 #include "kt_launch.h"
@@ -43,22 +44,27 @@ int slq_auto_block(int64_t n, int64_t nprobes) {
 // Run one sweep.  rec_host receives [alpha | up | low][m][P].
 // init: if seeded by RNG, `x` == nullptr; else x (device, n x ldx, ncols
 // columns, their squared norms in the DEVICE array dnorms2) is copied into
-// the sweep block.
-void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base,
-                   const double* x, int ldx, int ncols, const double* dnorms2, double* rec_host,
-                   DevMat* basis, std::vector<double>* scale_hist, int lane, int bcols) {
+// the sweep block.  ExplicitSweep enqueues it step by step, so sweeps on
+// different lanes can be queued launch by launch (the runtime throttles a
+// long enqueue burst to ~58 us per call once the host runs ~1 ms ahead, so
+// a second lane queued after a whole first sweep would start ms late).
+ExplicitSweep::ExplicitSweep(kt_matrix_s* A_, const DevCSR& M_, int P_, int m_, uint64_t seed_, int64_t probe_base_,
+                             const double* x_, int ldx_, int ncols_, const double* dnorms2_, double* rec_host_,
+                             DevMat* basis_, std::vector<double>* scale_hist_, int lane_, int bcols_)
+    : A(A_), M(M_), P(P_), m(m_), seed(seed_), probe_base(probe_base_), x(x_), ldx(ldx_), ncols(ncols_),
+      dnorms2(dnorms2_), rec_host(rec_host_), basis(basis_), scale_hist(scale_hist_), lane(lane_), bcols(bcols_) {
     if (bcols <= 0 || bcols > P) bcols = P;
     kt_context_s* ctx = A->ctx;
-    const int n = (int)A->n;
+    n = (int)A->n;
     if (lane < 0 || lane > 3) fail(KT_ERR_ARG, "sweep lane out of range");
     if (lane && !ctx->aux_stream[lane - 1])
         KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[lane - 1], hipStreamNonBlocking));
-    hipStream_t st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
-    const int grid = spmm_grid(n, P, ctx->num_cu * 4);  // K2 / short rows
-    const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
-    const int grid1 = grid + lblocks;                    // K1 total
+    st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
+    grid = spmm_grid(n, P, ctx->num_cu * 4);  // K2 / short rows
+    lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
+    grid1 = grid + lblocks;                    // K1 total
     SweepBufs& w = ctx->ws.sweep[lane];
-    const size_t blk_bytes = sizeof(double) * (size_t)n * P;
+    blk_bytes = sizeof(double) * (size_t)n * P;
     w.X0.ensure(blk_bytes);
     w.X1.ensure(blk_bytes);
     w.Y.ensure(blk_bytes);
@@ -66,72 +72,86 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
     w.k2s.ensure(sizeof(double) * 4 * P);
     w.coef.ensure(sizeof(double) * 2 * P);
     w.scales.ensure(sizeof(double) * 3 * P);
-    const size_t rec = (size_t)3 * m * P;
-    w.trec.ensure(sizeof(double) * rec);
-    double* part1 = w.partial.as<double>();
-    double* part2 = part1 + (size_t)grid1 * P;
-    double* k2s = w.k2s.as<double>();
-    double* coef = w.coef.as<double>();
-    double* trec = w.trec.as<double>();
+    w.trec.ensure(sizeof(double) * (size_t)3 * m * P);
+    part1 = w.partial.as<double>();
+    part2 = part1 + (size_t)grid1 * P;
+    k2s = w.k2s.as<double>();
+    coef = w.coef.as<double>();
+    trec = w.trec.as<double>();
+    Yb = w.Y.as<double>();
+    ucur = w.X1.as<double>();
+    uprev = w.X0.as<double>();
+    sc = w.scales.as<double>();
+    sp = sc + P;
+    sn = sc + 2 * P;
+}
 
-    double* ucur = w.X1.as<double>();
-    double* uprev = w.X0.as<double>();
-    double* sc = w.scales.as<double>();
-    double* sp = sc + P;
-    double* sn = sc + 2 * P;
+void ExplicitSweep::start() {
+    kt_context_s* ctx = A->ctx;
     if (!x) {
         KT_HIP(launch_rademacher(P, n, seed, probe_base, M.perm, ucur, st));
         KT_HIP(launch_fill(sc, P, 1.0 / std::sqrt((double)n), st));
         KT_HIP(launch_fill(k2s, P, (double)n, st));  // ||z||^2 = n
     } else {
         KT_HIP(hipMemsetAsync(ucur, 0, blk_bytes, st));
-        KT_HIP(hipMemcpy2DAsync(ucur, sizeof(double) * P, x, sizeof(double) * ldx,
-                                sizeof(double) * ncols, (size_t)n, hipMemcpyDeviceToDevice, st));
+        KT_HIP(hipMemcpy2DAsync(ucur, sizeof(double) * P, x, sizeof(double) * ldx, sizeof(double) * ncols, (size_t)n,
+                                hipMemcpyDeviceToDevice, st));
         // s_0 = 1/||x_c||, ||x_c||^2 from the device norms: no host round trip
         KT_HIP(launch_sweep_scales(dnorms2, ncols, P, 0, sc, k2s, st));
     }
-    if (scale_hist) scale_hist->assign((size_t)m * P, 0.0);
-    DevBuf* hist_dev = nullptr;
     if (scale_hist) {
+        scale_hist->assign((size_t)m * P, 0.0);
         hist_dev = &ctx->ws.hist;
         hist_dev->ensure(sizeof(double) * (size_t)m * P);
     }
     // basis slot j (u_j's first bcols columns, n x bcols row-major) at
     // bbase + j n bcols: slot 0 copied from the start block, slot j + 1
     // stored by step j's K2 as it forms u_{j+1} (no copy pass per step)
-    double* bbase = basis ? basis->col(0) : nullptr;
-    for (int j = 0; j < m; ++j) {
-        const int first = (j == 0);
-        if (basis) {  // record s_j (v_j = s_j u_j); u_0 into slot 0
-            if (first)
-                KT_HIP(hipMemcpy2DAsync(bbase, sizeof(double) * bcols, ucur, sizeof(double) * P,
-                                        sizeof(double) * bcols, (size_t)n, hipMemcpyDeviceToDevice, st));
-            KT_HIP(hipMemcpyAsync(hist_dev->as<double>() + (size_t)j * P, sc, sizeof(double) * P,
-                                  hipMemcpyDeviceToDevice, st));
-        }
-        prof_begin(ctx, PROF_SPMM, st, P);
-        KT_HIP(launch_spmm_dot(P, ctx->k1_flags | (A->unit_values ? 2 : 0), grid1, M.rowptr, M.col,
-                               M.val, n, ucur, sc, w.Y.as<double>(), part1, M.long_rows, M.n_long,
-                               A->long_thresh, lblocks, st));
-        prof_end(ctx, PROF_SPMM, st);
-        KT_HIP(launch_coef_cgs2(P, part1, grid1, first, k2s, sc, sp, coef,
-                                trec + (size_t)(0 * m + j) * P, trec + (size_t)(1 * m + j) * P, st));
-        prof_begin(ctx, PROF_UPDATE, st, P);
-        double* rec = (basis && j + 1 < m) ? bbase + (size_t)(j + 1) * n * bcols : nullptr;
-        KT_HIP(launch_update(P, grid, n, w.Y.as<double>(), uprev, ucur, sc, sp, coef, first, part2,
-                             st, ctx->k2_nt, rec, bcols));
-        prof_end(ctx, PROF_UPDATE, st);
-        KT_HIP(launch_norm(P, part2, grid, k2s, sn, trec + (size_t)(2 * m + j) * P, st));
-        std::swap(ucur, uprev);  // uprev now holds u_{j+1}
-        double* t = sp;
-        sp = sc;
-        sc = sn;
-        sn = t;
+    bbase = basis ? basis->col(0) : nullptr;
+}
+
+void ExplicitSweep::step(int j) {
+    kt_context_s* ctx = A->ctx;
+    const int first = (j == 0);
+    if (basis) {  // record s_j (v_j = s_j u_j); u_0 into slot 0
+        if (first)
+            KT_HIP(hipMemcpy2DAsync(bbase, sizeof(double) * bcols, ucur, sizeof(double) * P, sizeof(double) * bcols,
+                                    (size_t)n, hipMemcpyDeviceToDevice, st));
+        KT_HIP(hipMemcpyAsync(hist_dev->as<double>() + (size_t)j * P, sc, sizeof(double) * P,
+                              hipMemcpyDeviceToDevice, st));
     }
-    KT_HIP(hipMemcpyAsync(rec_host, trec, sizeof(double) * rec, hipMemcpyDeviceToHost, st));
+    prof_begin(ctx, PROF_SPMM, st, P);
+    KT_HIP(launch_spmm_dot(P, ctx->k1_flags | (A->unit_values ? 2 : 0), grid1, M.rowptr, M.col, M.val, n, ucur, sc, Yb,
+                           part1, M.long_rows, M.n_long, A->long_thresh, lblocks, st));
+    prof_end(ctx, PROF_SPMM, st);
+    KT_HIP(launch_coef_cgs2(P, part1, grid1, first, k2s, sc, sp, coef, trec + (size_t)(0 * m + j) * P,
+                            trec + (size_t)(1 * m + j) * P, st));
+    prof_begin(ctx, PROF_UPDATE, st, P);
+    double* rec = (basis && j + 1 < m) ? bbase + (size_t)(j + 1) * n * bcols : nullptr;
+    KT_HIP(launch_update(P, grid, n, Yb, uprev, ucur, sc, sp, coef, first, part2, st, ctx->k2_nt, rec, bcols));
+    prof_end(ctx, PROF_UPDATE, st);
+    KT_HIP(launch_norm(P, part2, grid, k2s, sn, trec + (size_t)(2 * m + j) * P, st));
+    std::swap(ucur, uprev);  // uprev now holds u_{j+1}
+    double* t = sp;
+    sp = sc;
+    sc = sn;
+    sn = t;
+}
+
+void ExplicitSweep::finish() {
+    KT_HIP(hipMemcpyAsync(rec_host, trec, sizeof(double) * (size_t)3 * m * P, hipMemcpyDeviceToHost, st));
     if (scale_hist)
         KT_HIP(hipMemcpyAsync(scale_hist->data(), hist_dev->ptr, sizeof(double) * (size_t)m * P,
                               hipMemcpyDeviceToHost, st));
+}
+
+void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base,
+                   const double* x, int ldx, int ncols, const double* dnorms2, double* rec_host,
+                   DevMat* basis, std::vector<double>* scale_hist, int lane, int bcols) {
+    ExplicitSweep s(A, M, P, m, seed, probe_base, x, ldx, ncols, dnorms2, rec_host, basis, scale_hist, lane, bcols);
+    s.start();
+    for (int j = 0; j < m; ++j) s.step(j);
+    s.finish();
 }
 
 // y-form sweep (RNG-seeded probes only): one fused pass + one coefficient
@@ -198,61 +218,77 @@ void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t see
 // of mc_trace's Lanczos Afun, kt_mctrace.cpp): x (n x ldx, ncols columns, in
 // M's row order, squared norms in the device array dnorms2) is normalised into the gathered table
 // v_0 (zero columns stay zero), the pass in start mode forms y_0 = A v_0 with
-// (g, a, b) = (1, 0, 0), then the same passes as the RNG-seeded sweep.
-// rec_host (pinned, or the call waits for the copy) receives [alpha | up |
-// low][m][P] followed by guard[P].  No basis: quadratic forms only.
-void lanczos_sweep_y_block(kt_matrix_s* A, const DevCSR& M, int P, int m, const double* x, int ldx, int ncols,
-                           const double* dnorms2, double* rec_host, int lane) {
+// (g, a, b) = (1, 0, 0), then the same passes as the RNG-seeded sweep
+// (steps 0 .. m-2).  rec_host (pinned, or the call waits for the copy)
+// receives [alpha | up | low][m][P] followed by guard[P].  No basis:
+// quadratic forms only.
+YBlockSweep::YBlockSweep(kt_matrix_s* A_, const DevCSR& M_, int P_, int m_, const double* x_, int ldx_, int ncols_,
+                         const double* dnorms2_, double* rec_host_, int lane_)
+    : A(A_), M(M_), P(P_), m(m_), x(x_), ldx(ldx_), ncols(ncols_), dnorms2(dnorms2_), rec_host(rec_host_),
+      lane(lane_) {
     kt_context_s* ctx = A->ctx;
-    const int n = (int)A->n;
+    n = (int)A->n;
     if (lane < 0 || lane > 3) fail(KT_ERR_ARG, "sweep lane out of range");
     if (ncols < 1 || ncols > P) fail(KT_ERR_ARG, "y-form block sweep: 1 <= ncols <= P");
     if (lane && !ctx->aux_stream[lane - 1])
         KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[lane - 1], hipStreamNonBlocking));
-    hipStream_t st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
-    const int grid = spmm_grid(n, P, ctx->num_cu * 4);
-    const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
-    const int grid1 = grid + lblocks;
+    st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
+    grid = spmm_grid(n, P, ctx->num_cu * 4);
+    lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
+    grid1 = grid + lblocks;
     SweepBufs& w = ctx->ws.sweep[lane];
-    const size_t blk_bytes = sizeof(double) * (size_t)n * P;
+    blk_bytes = sizeof(double) * (size_t)n * P;
     w.X0.ensure(blk_bytes);
     w.X1.ensure(blk_bytes);
     w.Y.ensure(blk_bytes);
     w.partial.ensure(sizeof(double) * (size_t)3 * P * grid1);
     w.coef.ensure(sizeof(double) * 9 * P);
-    const size_t rec = (size_t)3 * m * P + P;
-    w.trec.ensure(sizeof(double) * rec);
-    double* part = w.partial.as<double>();
-    double* ys = w.coef.as<double>();
-    double* trec = w.trec.as<double>();
-    double* guard = trec + (size_t)3 * m * P;
-    auto rec_at = [&](int row, int j) { return trec + (size_t)(row * m + j) * P; };
-    int flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
-    if (blk_bytes >= ((size_t)1 << 31)) flags &= ~16;
+    w.trec.ensure(sizeof(double) * ((size_t)3 * m * P + P));
+    part = w.partial.as<double>();
+    ys = w.coef.as<double>();
+    trec = w.trec.as<double>();
+    guard = trec + (size_t)3 * m * P;
+    flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
+    if (blk_bytes >= ((size_t)1 << 31)) flags &= ~16;  // sc1 buffer stores take 32-bit offsets
+    V0 = w.X1.as<double>();  // the start pass's gathered table v_0
+    Xc = w.Y.as<double>();   // y_j
+    Yo = nullptr;            // y_{j-1}
+    Ot = w.X0.as<double>();  // y_{j+1}
+}
+
+void YBlockSweep::start() {
     // ys: [1/||x_c|| (P) | 0 (5P) | start pass (g, a, b) = (1, 0, 0) (3P)], from
     // the device norms (no host round trip)
     KT_HIP(launch_sweep_scales(dnorms2, ncols, P, 1, ys, nullptr, st));
-    double* V0 = w.X1.as<double>();  // the start pass's gathered table v_0
     KT_HIP(hipMemsetAsync(V0, 0, blk_bytes, st));
     KT_HIP(launch_weighted_sum(n, 1, P, ncols, x, ldx, 0, ys, V0, P, st));
-    double* Xc = w.Y.as<double>();   // y_j
-    double* Yo = nullptr;            // y_{j-1}
-    double* Ot = w.X0.as<double>();  // y_{j+1}
     KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, V0, nullptr, Xc, ys + 6 * P, part,
                                M.long_rows, M.n_long, A->long_thresh, lblocks, st));
     KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, 1.0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0), guard, st));
-    for (int j = 0; j + 1 < m; ++j) {
-        const bool last = j + 2 == m;
-        KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
-                                   last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long, A->long_thresh,
-                                   lblocks, st));
-        KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1),
-                            rec_at(2, j + 1), guard, st));
-        Yo = Xc;
-        Xc = Ot;
-        Ot = Yo;
-    }
-    KT_HIP(hipMemcpyAsync(rec_host, trec, sizeof(double) * rec, hipMemcpyDeviceToHost, st));
+}
+
+void YBlockSweep::step(int j) {
+    const bool last = j + 2 == m;
+    KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
+                               last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long, A->long_thresh, lblocks,
+                               st));
+    KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1), rec_at(2, j + 1), guard,
+                        st));
+    Yo = Xc;
+    Xc = Ot;
+    Ot = Yo;
+}
+
+void YBlockSweep::finish() {
+    KT_HIP(hipMemcpyAsync(rec_host, trec, sizeof(double) * ((size_t)3 * m * P + P), hipMemcpyDeviceToHost, st));
+}
+
+void lanczos_sweep_y_block(kt_matrix_s* A, const DevCSR& M, int P, int m, const double* x, int ldx, int ncols,
+                           const double* dnorms2, double* rec_host, int lane) {
+    YBlockSweep s(A, M, P, m, x, ldx, ncols, dnorms2, rec_host, lane);
+    s.start();
+    for (int j = 0; j + 1 < m; ++j) s.step(j);
+    s.finish();
 }
 
 // A y-form probe is accepted when every used beta_k^2 kept at least this
@@ -365,17 +401,13 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     bool used[4] = {false, false, false, false};
     for (size_t i = 0; i < sw.size(); ++i) {
         const Sw& q = sw[i];
-        if (!q.yform) continue;
-        if (!used[q.lane]) {
-            hipStream_t& as = ctx->aux_stream[q.lane - 1];
-            if (!as) KT_HIP(hipStreamCreateWithFlags(&as, hipStreamNonBlocking));
-            KT_HIP(hipStreamWaitEvent(as, ready, 0));
-            used[q.lane] = true;
-        }
-        lanczos_sweep_y_block(A, M, q.P, m, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, hr.as<double>() + rec_max * i,
-                              q.lane);
+        if (!q.yform || used[q.lane]) continue;
+        hipStream_t& as = ctx->aux_stream[q.lane - 1];
+        if (!as) KT_HIP(hipStreamCreateWithFlags(&as, hipStreamNonBlocking));
+        KT_HIP(hipStreamWaitEvent(as, ready, 0));
+        used[q.lane] = true;
     }
-    // the explicit sweeps (lane 0) with their bases
+    // the explicit sweeps (lane 0) keep their bases
     std::vector<DevMat> bases(sw.size());
     std::vector<std::vector<double>> hists(sw.size());
     for (size_t i = 0; i < sw.size(); ++i) {
@@ -383,8 +415,38 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
         if (q.yform) continue;
         const int nyc = std::max(0, std::min(q.nc, ny - q.c0));
         if (nyc) bases[i].alloc(ctx, n, m * nyc, false);  // every slot is written by the sweep
-        lanczos_sweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, hr.as<double>() + rec_max * i,
-                      nyc ? &bases[i] : nullptr, nyc ? &hists[i] : nullptr, 0, nyc);
+    }
+    // Queue the sweeps launch by launch across lanes (one sweep per lane at a
+    // time: a lane's sweeps share its buffers), so every lane starts at once
+    std::vector<int> next(4, 0);  // per lane: index into its sweeps
+    std::vector<std::vector<int>> by_lane(4);
+    for (size_t i = 0; i < sw.size(); ++i) by_lane[sw[i].lane].push_back((int)i);
+    for (;;) {
+        std::vector<std::unique_ptr<ExplicitSweep>> ex;
+        std::vector<std::unique_ptr<YBlockSweep>> yb;
+        for (int l = 0; l < 4; ++l) {
+            if (next[l] >= (int)by_lane[l].size()) continue;
+            const int i = by_lane[l][next[l]++];
+            const Sw& q = sw[i];
+            double* R = hr.as<double>() + rec_max * i;
+            if (q.yform) {
+                yb.emplace_back(new YBlockSweep(A, M, q.P, m, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, R, q.lane));
+            } else {
+                const int nyc = std::max(0, std::min(q.nc, ny - q.c0));
+                ex.emplace_back(new ExplicitSweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, R,
+                                                  nyc ? &bases[i] : nullptr, nyc ? &hists[i] : nullptr, 0, nyc));
+            }
+        }
+        if (ex.empty() && yb.empty()) break;
+        for (auto& y : yb) y->start();
+        for (auto& e : ex) e->start();
+        for (int j = 0; j < m; ++j) {
+            for (auto& y : yb)
+                if (j + 1 < m) y->step(j);
+            for (auto& e : ex) e->step(j);
+        }
+        for (auto& y : yb) y->finish();
+        for (auto& e : ex) e->finish();
     }
     KT_HIP(hipStreamSynchronize(ctx->stream));
     for (int l = 1; l < 4; ++l)

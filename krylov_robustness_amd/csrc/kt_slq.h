@@ -16,6 +16,66 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
                    const double* x, int ldx, int ncols, const double* dnorms2, double* rec_host,
                    DevMat* basis, std::vector<double>* scale_hist, int lane = 0, int bcols = 0);
 
+// lanczos_sweep enqueued step by step: start(), step(j) for j < m, finish().
+// Sweeps on different lanes may be interleaved step by step; two sweeps on
+// one lane may not (they share the lane's buffers).
+class ExplicitSweep {
+   public:
+    ExplicitSweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base, const double* x,
+                  int ldx, int ncols, const double* dnorms2, double* rec_host, DevMat* basis,
+                  std::vector<double>* scale_hist, int lane, int bcols);
+    void start();
+    void step(int j);
+    void finish();
+
+   private:
+    kt_matrix_s* A;
+    const DevCSR& M;
+    int P, m;
+    uint64_t seed;
+    int64_t probe_base;
+    const double* x;
+    int ldx, ncols;
+    const double* dnorms2;
+    double* rec_host;
+    DevMat* basis;
+    std::vector<double>* scale_hist;
+    int lane, bcols;
+    int n = 0, grid = 0, lblocks = 0, grid1 = 0;
+    size_t blk_bytes = 0;
+    hipStream_t st = nullptr;
+    double *part1 = nullptr, *part2 = nullptr, *k2s = nullptr, *coef = nullptr, *trec = nullptr, *Yb = nullptr;
+    double *ucur = nullptr, *uprev = nullptr, *sc = nullptr, *sp = nullptr, *sn = nullptr, *bbase = nullptr;
+    DevBuf* hist_dev = nullptr;
+};
+
+// lanczos_sweep_y_block enqueued step by step: start(), step(j) for j < m - 1,
+// finish(); same interleaving rule as ExplicitSweep.
+class YBlockSweep {
+   public:
+    YBlockSweep(kt_matrix_s* A, const DevCSR& M, int P, int m, const double* x, int ldx, int ncols,
+                const double* dnorms2, double* rec_host, int lane);
+    void start();
+    void step(int j);
+    void finish();
+
+   private:
+    double* rec_at(int row, int j) { return trec + (size_t)(row * m + j) * P; }
+    kt_matrix_s* A;
+    const DevCSR& M;
+    int P, m;
+    const double* x;
+    int ldx, ncols;
+    const double* dnorms2;
+    double* rec_host;
+    int lane;
+    int n = 0, grid = 0, lblocks = 0, grid1 = 0, flags = 0;
+    size_t blk_bytes = 0;
+    hipStream_t st = nullptr;
+    double *part = nullptr, *ys = nullptr, *trec = nullptr, *guard = nullptr;
+    double *V0 = nullptr, *Xc = nullptr, *Yo = nullptr, *Ot = nullptr;
+};
+
 int record_tridiag(const double* R, int m, int P, int c, double* al, double* off);
 
 // For the ncols columns of the device block X (n x ldx, natural row order):
