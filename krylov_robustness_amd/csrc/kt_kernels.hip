@@ -1145,8 +1145,20 @@ __global__ __launch_bounds__(256) void k_weighted_sum(int n, int m, int P, int n
          t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = t / nc;
         const int c = (int)(t % nc);
+        const double* u = U + r * ldu + c;
         double s = 0.0;
-        for (int j = 0; j < m; ++j) s = fma(U[r * ldu + (int64_t)j * sstride + c], W[j * P + c], s);
+        // the slots' loads of a group of 8 issue together (one memory round
+        // trip), then the fma chain in slot order: the sum is bit-identical
+        // to the one-slot loop's
+        constexpr int kG = 8;
+        for (int j0 = 0; j0 < m; j0 += kG) {
+            double v[kG];
+#pragma unroll
+            for (int g = 0; g < kG; ++g) v[g] = (j0 + g < m) ? __builtin_nontemporal_load(u + (int64_t)(j0 + g) * sstride) : 0.0;
+#pragma unroll
+            for (int g = 0; g < kG; ++g)
+                if (j0 + g < m) s = fma(v[g], W[(j0 + g) * P + c], s);
+        }
         Y[r * ldy + c] = s;
     }
 }
