@@ -698,8 +698,8 @@ def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev,
         if l1:
             # mc_trace_batched: round 1's S term and a final round's Q term are
             # 16-wide explicit sweeps, a round with the next S term ahead one
-            # 32-wide sweep (the G columns of a final round run as y-form
-            # passes, not K1); each K1 launch is charged its own width's bytes
+            # 32-wide sweep (the Q and G columns of a final round run as
+            # y-form passes, not K1); each K1 launch is charged its own width's bytes
             unit = bool(A.nnz) and bool(np.all(A.data == 1.0))
             per_nnz = 4 if unit else 12
 
@@ -726,8 +726,8 @@ def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev,
                                "k2_update_avg_us": round(ms2 / l2 * 1e3, 2) if l2 else None,
                                "serial_eval_ms": round(serial_ms, 2),
                                "measured": "HIP events around every K1 launch of one trace_exp after the timed "
-                                           "region (a final round's G y-form sweep runs beside its Q sweep on a "
-                                           "second lane, so those K1 times include that overlap)"}
+                                           "region (the K1 sweeps run alone on their lane; a final round's y-form "
+                                           "sweeps launch no K1)"}
             if traffic:
                 out["roofline"]["traffic_GBs"] = round(traffic * l1 / (ms1 * 1e-3) / 1e9, 1)
     return out

@@ -46,7 +46,8 @@ def test_bench_single_process_line():
     # (the union is formed over every launch of the timed region at once, so
     # pipelined evaluations' overlapping launches are not counted twice)
     assert roof["timed_region_busy_ms"] <= roof["timed_region_ms"] + 1e-3
-    assert roof["timed_region_ms"] <= d["steps"] * d["ms_per_step"] * 1.001
+    # (both printed to 3 decimals: half a unit of rounding per step)
+    assert roof["timed_region_ms"] <= d["steps"] * (d["ms_per_step"] + 5e-4) * 1.001 + 5e-4
     assert roof["isolated_pass"]["avg_launch_us"] > 0 and roof["isolated_pass"]["launches"] > 0
     # unit-weight graph: the roofline is priced on the bytes the kernel must
     # move (4 B per nonzero, values never read), SURVEY's 12 B figure beside it

@@ -11,7 +11,14 @@ def main(trace_csv, bench_json, out_json):
     b = json.loads(open(bench_json).read().strip().splitlines()[-1])
     roof = b["roofline"]
     kname = roof["kernel"].rstrip(">")  # e.g. k_spmm_lanczos<16
-    rows = [r for r in csv.DictReader(open(trace_csv)) if f"kt::{kname}," in r["Kernel_Name"]]
+    allrows = list(csv.DictReader(open(trace_csv)))
+    # the headline's launches end where the mc_trace leg starts: its first
+    # explicit K1 (k_spmm_dot) launch (the leg's y-form sweeps launch the
+    # headline kernel too)
+    k1 = [int(r["Start_Timestamp"]) for r in allrows if "kt::k_spmm_dot<" in r["Kernel_Name"]]
+    cut = min(k1) if k1 else None
+    rows = [r for r in allrows if f"kt::{kname}," in r["Kernel_Name"]
+            and (cut is None or int(r["Start_Timestamp"]) < cut)]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]  # us
     iso = (roof.get("isolated_pass") or {}).get("launches", roof["launches"])
@@ -49,13 +56,14 @@ def main(trace_csv, bench_json, out_json):
                                  "share the chip"},
         "_doc": "rocprofv3 kernel trace of the default bench command split into the timed region "
                 "(the steps x sweeps x (m-1) launches before the isolated pass) and the isolated "
-                "single-lane roofline pass (the last `launches` launches)",
+                "single-lane roofline pass (the last `launches` launches before the mc_trace leg's "
+                "first k_spmm_dot launch)",
     }
     mc = (b.get("mc_trace") or {}).get("roofline")
     if mc:
         # the mc_trace leg's serial roofline pass: its K1 launches (16- and
         # 32-wide) are the last `launches` k_spmm_dot launches of the run
-        allk = [r for r in csv.DictReader(open(trace_csv))
+        allk = [r for r in allrows
                 if "kt::k_spmm_dot<16," in r["Kernel_Name"] or "kt::k_spmm_dot<32," in r["Kernel_Name"]]
         allk.sort(key=lambda r: int(r["Start_Timestamp"]))
         last = allk[-mc["launches"]:]
