@@ -1,4 +1,4 @@
-"""CPU: the N>1 path -- probe sharding + one all-reduce -- with world_size 2
+"""CPU: the N>1 path -- probe sharding + one all-reduce -- with world_size 2 (and 8)
 over gloo.  Each rank evaluates its shard with the C oracle (the device call
 stands behind the same interface on the GPU box); the reduced estimate must
 equal the single-process one."""
@@ -63,13 +63,15 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_matches_single():
+@pytest.mark.parametrize("world", [2, 8])
+def test_gloo_world_matches_single(world):
+    """world 8 = the driver's 8-GPU node (50 probes: shards of 7, 7, 6 x 6)"""
     import torch.multiprocessing as mp
     from oracle import slq_ref
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     s = q.get(timeout=120)
@@ -235,7 +237,7 @@ def _bitstable_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_gloo_bitstable_sums_identical_across_world_sizes(world):
     """Bit-identical (==, not approx) estimate on every rank and equal to the
     single-process ordered sum of the same forms (SURVEY.md §8e option); the
