@@ -693,13 +693,16 @@ def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev,
             os.environ.pop("KT_TWIN")
         else:
             os.environ["KT_TWIN"] = prev
-        l1, ms1 = ctx.profile_read(0)
+        l1, ms1_sum = ctx.profile_read(0)
         l2, ms2 = ctx.profile_read(1)
         if l1:
-            # mc_trace_batched: round 1's S term and a final round's Q term are
-            # 16-wide explicit sweeps, a round with the next S term ahead one
-            # 32-wide sweep (the Q and G columns of a final round run as
-            # y-form passes, not K1); each K1 launch is charged its own width's bytes
+            # mc_trace_batched: round 1's S term is a 16-wide explicit sweep, a
+            # round with the next S term ahead two 16-wide explicit sweeps on
+            # two lanes (the Q and G columns of a final round run as y-form
+            # passes, not K1); each K1 launch is charged its own width's bytes,
+            # and the K1 time is the union of the launches' intervals (two
+            # lanes' K1 launches overlap, counted once), as the headline's
+            ms1 = ctx.profile_busy(0)
             unit = bool(A.nnz) and bool(np.all(A.data == 1.0))
             per_nnz = 4 if unit else 12
 
@@ -724,10 +727,12 @@ def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev,
                                                           "CSR, u_j gathered once, y = A u_j written), each "
                                                           "launch at its sweep's width P (16 or 32); mean",
                                "k2_update_avg_us": round(ms2 / l2 * 1e3, 2) if l2 else None,
+                               "avg_launch_us_overlapped": round(ms1_sum / l1 * 1e3, 2),
                                "serial_eval_ms": round(serial_ms, 2),
                                "measured": "HIP events around every K1 launch of one trace_exp after the timed "
-                                           "region (the K1 sweeps run alone on their lane; a final round's y-form "
-                                           "sweeps launch no K1)"}
+                                           "region; avg_launch_us = union of their intervals (time with >= 1 K1 "
+                                           "in flight, two lanes' overlap counted once) / launches; a final "
+                                           "round's y-form sweeps launch no K1"}
             if traffic:
                 out["roofline"]["traffic_GBs"] = round(traffic * l1 / (ms1 * 1e-3) / 1e9, 1)
     return out

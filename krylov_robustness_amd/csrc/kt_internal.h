@@ -137,7 +137,7 @@ enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_START = 2, PROF_NSLOTS = 3 };
 // Buffers of one probe-sweep lane (kt_slq.cpp); two lanes let two sweeps
 // run on two streams.
 struct SweepBufs {
-    DevBuf X0, X1, Y, partial, coef, scales, k2s, trec;
+    DevBuf X0, X1, Y, partial, coef, scales, k2s, trec, hist;  // hist: the explicit sweep's scale history
 };
 
 // one host int the device may store to at system scope (fine-grained,
@@ -186,7 +186,7 @@ struct Workspace {
     DevBuf small, small2, qrtmp, qrkeep, qrfac, eigA, eigW, eigInfo;  // block-Krylov scratch
     DevBuf expm;                                       // batched device expm (6 x batch x n^2)
     DevBuf ck_part;                                    // block SpMM hub-row chunk partials
-    DevBuf hist, norm_part;                             // sweep scale history, inf-norm partials
+    DevBuf norm_part;                                   // inf-norm partials
     DevBuf expmv_state;                                 // expmv stage stop state (device)
     PinnedBuf host_trec[2];  // sweep records of the (at most two) submitted kt_slq calls
     SlqPending slq_pend[2];

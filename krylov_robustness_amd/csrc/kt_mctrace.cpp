@@ -468,10 +468,11 @@ static void project(kt_context_s* ctx, int64_t n, const double* Q, int ld, int n
 // mc_trace.m:42-58 with the Lanczos-f Afun, one batch of sweeps per round.
 // The round's Q term (:46), its G term (:49) and the NEXT round's S term
 // (:43-45, which needs only Q_1..Q_it) are independent Afun calls, so their
-// 30 columns share one explicit 32-wide sweep (per nonzero one 256-B probe-row
-// gather and one CSR pass instead of three 128-B gathers and three CSR
-// passes), the basis kept for the 10 S columns whose f(A) x feeds the next
-// qr (:45).  Round 1's S term runs alone.
+// 30 columns are queued together as two 16-wide explicit sweeps on two lanes
+// (config 4: 45.0-45.3 ms per trace_exp vs 46.6 as one 32-wide sweep, whose
+// 256 MB gathered table fills the Infinity Cache; profiles/r05/mc_ahead_ab),
+// the basis kept for the 10 S columns whose f(A) x feeds the next qr (:45).
+// Round 1's S term runs alone.
 //
 // The next round's S term is computed ahead in round `it` unless the round
 // is expected to stop the loop: |trace(G' Afun G)/m| of the previous round
@@ -547,16 +548,15 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
         if (ahead) {
             rademacher_into(base + 2 * mb, Bk.col(0));
             for (int k = (int)Qs.size() - 1; k >= 0; --k) project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(0), LB, mb);
-            // one explicit 32-wide sweep [S | Q | G]: per nonzero one 256-B row
-            // gather and one CSR pass for the three Afun calls
-            lanczos_columns_split(A, Bk.col(0), LB, 3 * mb, mb, 3 * mb, F.m, F.fun, q.data(), Yb.col(0), ld, LB);
+            // [S | Q | G] as two 16-wide explicit sweeps on two lanes
+            lanczos_columns_split(A, Bk.col(0), LB, 3 * mb, mb, 3 * mb, F.m, F.fun, q.data(), Yb.col(0), ld, 16);
         } else {
             // no S term: the Q and G columns need quadratic forms only, so
             // both go through y-form sweeps (no K2, no basis), 16 wide on two
             // lanes.  (Round 1's Q_1 column 0 is the top eigenvector to
             // rounding -- a lucky breakdown at step 1 that the y-form guard
             // sends to the explicit redo -- but round 1 always computes the
-            // S term ahead, so its Q columns ride the explicit 32-wide sweep.)
+            // S term ahead, so its Q columns ride the explicit sweeps.)
             lanczos_columns_split(A, Bk.col(mb), LB, 2 * mb, 0, 0, F.m, F.fun, q.data() + mb, nullptr, 0, 16);
         }
         std::vector<double> qv(mb, 0.0);

@@ -376,11 +376,11 @@ int kt_context_destroy(kt_context_t ctx) {
     Workspace& w = ctx->ws;
     for (auto& b : w.sweep) {
         b.X0.release(); b.X1.release(); b.Y.release(); b.partial.release();
-        b.coef.release(); b.scales.release(); b.k2s.release(); b.trec.release();
+        b.coef.release(); b.scales.release(); b.k2s.release(); b.trec.release(); b.hist.release();
     }
     w.small.release(); w.small2.release(); w.qrtmp.release();
     w.eigA.release(); w.eigW.release(); w.eigInfo.release();
-    w.hist.release(); w.norm_part.release();
+    w.norm_part.release();
     ctx->pool.clear();
     if (ctx->blas) rocblas_destroy_handle(static_cast<rocblas_handle>(ctx->blas));
     if (w.comb_ev) (void)hipEventDestroy(w.comb_ev);

@@ -101,7 +101,7 @@ void ExplicitSweep::start() {
     }
     if (scale_hist) {
         scale_hist->assign((size_t)m * P, 0.0);
-        hist_dev = &ctx->ws.hist;
+        hist_dev = &ctx->ws.sweep[lane].hist;
         hist_dev->ensure(sizeof(double) * (size_t)m * P);
     }
     // basis slot j (u_j's first bcols columns, n x bcols row-major) at
@@ -364,10 +364,10 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
         }
     }
     // Sweeps: columns [0, ne) by the explicit CGS2 sweep (P = px, or pow2 >=
-    // ne capped at 16), the basis kept for the ny f(A)x columns among them, on
-    // lane 0; columns [ne, ncols) -- quadratic forms only -- by y-form sweeps
-    // (no K2, no basis; widths quad_plan) on lanes 1..3.  All queued before the
-    // host waits, so the device runs them side by side.
+    // ne capped at 16), the basis kept for the ny f(A)x columns among them;
+    // columns [ne, ncols) -- quadratic forms only -- by y-form sweeps (no K2,
+    // no basis; widths quad_plan).  All queued before the host waits, dealt
+    // over the four lanes, so the device runs them side by side.
     struct Sw {
         int c0, nc, P, lane;
         bool yform;
@@ -378,11 +378,14 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     int Pe = 1;
     while (Pe < ne && Pe < 16) Pe <<= 1;
     if (px > 0) Pe = px;
-    for (int c0 = 0; c0 < ne; c0 += Pe) sw.push_back({c0, std::min(Pe, ne - c0), Pe, 0, false});
+    // sweeps dealt over the four lanes in order (explicit first), so up to
+    // four run side by side; a lane's later sweeps follow its earlier ones
+    int k = 0;
+    for (int c0 = 0; c0 < ne; c0 += Pe) sw.push_back({c0, std::min(Pe, ne - c0), Pe, k++ % 4, false});
     {
-        int c0 = ne, k = 0;
+        int c0 = ne;
         for (int P : quad_plan(ncols - ne)) {
-            sw.push_back({c0, std::min(P, ncols - c0), P, 1 + (k++ % 3), true});
+            sw.push_back({c0, std::min(P, ncols - c0), P, k++ % 4, true});
             c0 += P;
         }
     }
@@ -398,16 +401,16 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
         ctx->ws.colsplit_ev = ready;
     }
     KT_HIP(hipEventRecord(ready, ctx->stream));
-    bool used[4] = {false, false, false, false};
+    bool used[4] = {true, false, false, false};
     for (size_t i = 0; i < sw.size(); ++i) {
         const Sw& q = sw[i];
-        if (!q.yform || used[q.lane]) continue;
+        if (used[q.lane]) continue;
         hipStream_t& as = ctx->aux_stream[q.lane - 1];
         if (!as) KT_HIP(hipStreamCreateWithFlags(&as, hipStreamNonBlocking));
         KT_HIP(hipStreamWaitEvent(as, ready, 0));
         used[q.lane] = true;
     }
-    // the explicit sweeps (lane 0) keep their bases
+    // the explicit sweeps keep their bases
     std::vector<DevMat> bases(sw.size());
     std::vector<std::vector<double>> hists(sw.size());
     for (size_t i = 0; i < sw.size(); ++i) {
@@ -434,7 +437,8 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
             } else {
                 const int nyc = std::max(0, std::min(q.nc, ny - q.c0));
                 ex.emplace_back(new ExplicitSweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, R,
-                                                  nyc ? &bases[i] : nullptr, nyc ? &hists[i] : nullptr, 0, nyc));
+                                                  nyc ? &bases[i] : nullptr, nyc ? &hists[i] : nullptr, q.lane,
+                                                  nyc));
             }
         }
         if (ex.empty() && yb.empty()) break;

@@ -254,8 +254,8 @@ def test_mc_trace_next_s_term_guess_is_bit_identical(kra, gpu_ctx, monkeypatch, 
     the round is expected to stop (kt_mctrace.cpp mc_trace_batched); always
     ahead (KT_MC_AHEAD=1), never ahead (0) and the guess give the same round
     count and the estimate to rounding (a round with its S term ahead runs Q
-    and G in one 32-wide explicit sweep, one without runs them by y-form
-    sweeps: other reduction widths), over several rounds and a last round
+    and G in explicit sweeps beside S, one without runs them by y-form
+    sweeps: other reduction forms), over several rounds and a last round
     it == K (tol = 0)."""
     A = load_graph(name)
     D = kra.DeviceMatrix(A, gpu_ctx)

@@ -5,10 +5,11 @@ their quadratic forms all-reduced once per round.
 world = 1 must equal kt_mc_trace bit for bit.  world = 2, 3 are run in one
 process by one host thread per rank, each with its own context on the same
 GPU, joined by an in-process all-reduce.  With the Lanczos Afun each round
-is one 32-wide probe sweep (kt_mctrace.cpp mc_trace_batched: the round's Q
-and G terms and the next S term); a rank's G columns sit in that sweep
-beside the replicated columns, and a column's form does not depend on its
-neighbours, so every world size returns the world-1 estimate BIT FOR BIT.
+queues its Afun columns together (kt_mctrace.cpp mc_trace_batched: the
+round's Q and G terms and the next S term, as 16-wide sweeps on several
+lanes); a rank's G columns sit in fixed slots beside the replicated columns,
+and a column's form does not depend on its neighbours, so every world size
+returns the world-1 estimate BIT FOR BIT.
 The per-call form (KT_MC_BATCH=0) runs a rank's G columns as a narrower
 block (P = 8 or 4 instead of 16), whose reductions round differently: there
 the estimate agrees to 1e-12 relative with the same round count.  The expmv

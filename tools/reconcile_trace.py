@@ -7,6 +7,18 @@ import json
 import sys
 
 
+def _union(iv):
+    tot, cs, ce = 0, None, None
+    for a, e in sorted(iv):
+        if ce is None or a > ce:
+            if ce is not None:
+                tot += ce - cs
+            cs, ce = a, e
+        else:
+            ce = max(ce, e)
+    return tot + ((ce - cs) if ce is not None else 0)
+
+
 def main(trace_csv, bench_json, out_json):
     b = json.loads(open(bench_json).read().strip().splitlines()[-1])
     roof = b["roofline"]
@@ -26,16 +38,7 @@ def main(trace_csv, bench_json, out_json):
         (b["config"]["lanczos_m"] - 1)
     t_iso, t_timed = dur[-iso:], dur[-iso - timed:-iso]
     # union of the timed region's launch intervals (lane overlap counted once)
-    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows[-iso - timed:-iso])
-    union, cs, ce = 0, None, None
-    for a, e in iv:
-        if ce is None or a > ce:
-            if ce is not None:
-                union += ce - cs
-            cs, ce = a, e
-        else:
-            ce = max(ce, e)
-    union += ce - cs
+    union = _union([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows[-iso - timed:-iso]])
     out = {
         "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py (default command)",
         "kernel": kname,
@@ -70,7 +73,11 @@ def main(trace_csv, bench_json, out_json):
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in last]
         out["mc_trace_serial_pass"] = {"kernel": mc["kernel"], "launches": len(d),
                                        "rocprof_avg_us": round(sum(d) / len(d), 2),
-                                       "bench_avg_launch_us": mc["avg_launch_us"]}
+                                       "rocprof_union_us_per_launch": round(
+                                           _union([(int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                                                   for r in last]) / 1e3 / len(d), 2),
+                                       "bench_avg_launch_us": mc["avg_launch_us"],
+                                       "bench_avg_launch_us_overlapped": mc.get("avg_launch_us_overlapped")}
     json.dump(out, open(out_json, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
