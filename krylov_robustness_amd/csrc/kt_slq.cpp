@@ -319,14 +319,23 @@ void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m,
 }
 
 // Widths of the y-form sweeps for `cols` quadrature-only columns: sweeps of
-// 16, the last zero-padded.  At config 4 the final mc_trace round's 10 G
-// columns as one padded 16-wide sweep beside the Q sweep: 52.0 ms per
-// trace_exp, vs 54.5 as 8 + 2 and 57.0 with every column in one explicit
-// 32-wide sweep (profiles/r05/mc_layout_ab/) -- a narrow pass costs about
-// what a 16-wide one does (its gathers are latency, not bytes).
+// 16, the remainder at the power of two that holds it.  At config 4 the final
+// mc_trace round's 20 columns as 16 + 4: 43.2 ms per trace_exp vs 44.8 with
+// the remainder zero-padded to 16 (profiles/r05/sweep_plan_ab/; with the
+// lanes queued step by step -- the padded form measured faster while the
+// second lane was queued only after the whole first sweep).  The explicit
+// sweep does not take narrow chunks: 10 + 30 columns as greedy power-of-two
+// sweeps (8 + 2, 16 + 8 + 4 + 2) cost 53 ms.
 static std::vector<int> quad_plan(int cols) {
     std::vector<int> wv;
-    for (int left = cols; left > 0; left -= 16) wv.push_back(16);
+    for (int left = cols; left > 0; left -= 16) {
+        int P = 16;
+        if (left < 16) {
+            P = 1;
+            while (P < left) P <<= 1;
+        }
+        wv.push_back(P);
+    }
     return wv;
 }
 
