@@ -468,11 +468,16 @@ static void project(kt_context_s* ctx, int64_t n, const double* Q, int ld, int n
 // mc_trace.m:42-58 with the Lanczos-f Afun, one batch of sweeps per round.
 // The round's Q term (:46), its G term (:49) and the NEXT round's S term
 // (:43-45, which needs only Q_1..Q_it) are independent Afun calls, so their
-// 30 columns are queued together as two 16-wide explicit sweeps on two lanes
-// (config 4: 45.0-45.3 ms per trace_exp vs 46.6 as one 32-wide sweep, whose
-// 256 MB gathered table fills the Infinity Cache; profiles/r05/mc_ahead_ab),
-// the basis kept for the 10 S columns whose f(A) x feeds the next qr (:45).
-// Round 1's S term runs alone.
+// 30 columns are queued together on two lanes: the 10 S columns, whose
+// f(A) x feeds the next qr (:45), by the explicit sweep with its basis, 16
+// wide, its 6 spare slots taking Q's leading columns (Q_1's first column is
+// the top eigenvector to rounding: a lucky breakdown the y-form's guard
+// would send to a redo); Q's other 4 columns and G -- quadratic forms only --
+// by a 16-wide y-form sweep beside it.  Config 4: 41.8 ms per trace_exp vs
+// 43.1 with all 30 columns in two explicit sweeps and 46.6 in one 32-wide
+// explicit sweep, whose 256 MB gathered table fills the Infinity Cache
+// (profiles/r05/mc_ahead_ab, profiles/r05/sweep_plan_ab).  Round 1's S term
+// runs alone.
 //
 // The next round's S term is computed ahead in round `it` unless the round
 // is expected to stop the loop: |trace(G' Afun G)/m| of the previous round
@@ -548,8 +553,9 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
         if (ahead) {
             rademacher_into(base + 2 * mb, Bk.col(0));
             for (int k = (int)Qs.size() - 1; k >= 0; --k) project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(0), LB, mb);
-            // [S | Q | G] as two 16-wide explicit sweeps on two lanes
-            lanczos_columns_split(A, Bk.col(0), LB, 3 * mb, mb, 3 * mb, F.m, F.fun, q.data(), Yb.col(0), ld, 16);
+            // [S | Q_0..5] explicit (16 wide, the basis for S) beside
+            // [Q_6..9 | G] as a y-form sweep on a second lane
+            lanczos_columns_split(A, Bk.col(0), LB, 3 * mb, mb, 16, F.m, F.fun, q.data(), Yb.col(0), ld, 16);
         } else {
             // no S term: the Q and G columns need quadratic forms only, so
             // both go through y-form sweeps (no K2, no basis), 16 wide on two
