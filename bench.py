@@ -693,48 +693,58 @@ def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev,
             os.environ.pop("KT_TWIN")
         else:
             os.environ["KT_TWIN"] = prev
-        l1, ms1_sum = ctx.profile_read(0)
-        l2, ms2 = ctx.profile_read(1)
-        if l1:
-            # mc_trace_batched: round 1's S term is a 16-wide explicit sweep, a
-            # round with the next S term ahead two 16-wide explicit sweeps on
-            # two lanes (the Q and G columns of a final round run as y-form
-            # passes, not K1); each K1 launch is charged its own width's bytes,
-            # and the K1 time is the union of the launches' intervals (two
-            # lanes' K1 launches overlap, counted once), as the headline's
-            ms1 = ctx.profile_busy(0)
-            unit = bool(A.nnz) and bool(np.all(A.data == 1.0))
-            per_nnz = 4 if unit else 12
-
-            def kb(P):
-                return per_nnz * nnz + 4 * (n + 1) + 16 * n * P
-            l16, ms16 = ctx.profile_read_width(0, 16)
-            l32, ms32 = ctx.profile_read_width(0, 32)
-            bytes_total = l16 * kb(16) + l32 * kb(32)
-            us = ms1 / l1 * 1e3
-            gbs = bytes_total / (ms1 * 1e-3) / 1e9
-            t16 = _pmc_traffic("k_spmm_dot", 16, args.config, args.weighted)
-            t32 = _pmc_traffic("k_spmm_dot", 32, args.config, args.weighted)
-            traffic = (l16 * t16 + l32 * t32) / l1 if (t16 and t32) else None
-            out["roofline"] = {"bound": "hbm", "kernel": "k_spmm_dot<16|32>", "achieved": round(gbs, 1),
-                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                               "traffic": traffic, "avg_launch_us": round(us, 2), "launches": l1,
-                               "launches_by_width": {"16": l16, "32": l32},
-                               "avg_launch_us_by_width": {"16": round(ms16 / l16 * 1e3, 2) if l16 else None,
-                                                          "32": round(ms32 / l32 * 1e3, 2) if l32 else None},
-                               "algorithmic_bytes_per_launch": round(bytes_total / l1),
-                               "algorithmic_bytes_basis": f"{per_nnz} nnz + 4 (n+1) + 16 n P per launch (the "
-                                                          "CSR, u_j gathered once, y = A u_j written), each "
-                                                          "launch at its sweep's width P (16 or 32); mean",
-                               "k2_update_avg_us": round(ms2 / l2 * 1e3, 2) if l2 else None,
-                               "avg_launch_us_overlapped": round(ms1_sum / l1 * 1e3, 2),
-                               "serial_eval_ms": round(serial_ms, 2),
-                               "measured": "HIP events around every K1 launch of one trace_exp after the timed "
-                                           "region; avg_launch_us = union of their intervals (time with >= 1 K1 "
-                                           "in flight, two lanes' overlap counted once) / launches; a final "
-                                           "round's y-form sweeps launch no K1"}
+        unit = bool(A.nnz) and bool(np.all(A.data == 1.0))
+        per_nnz = 4 if unit else 12
+        # mc_trace_batched's sweep passes (kt_mctrace.cpp): round 1's S term
+        # and a round with the next S term ahead run the explicit sweep (K1 =
+        # k_spmm_dot, slot 0), 16 wide; a round's quadrature-only columns run
+        # y-form passes of block-seeded sweeps (k_spmm_lanczos, slot 3), 16
+        # wide and at the power of two of a remainder.  Each launch is charged
+        # its own width's algorithmic bytes; a kernel's time is the union of
+        # its launches' HIP-event intervals (overlapping lanes counted once).
+        kinds = {
+            "k_spmm_dot": (0, lambda P: per_nnz * nnz + 4 * (n + 1) + 16 * n * P,
+                           f"{per_nnz} nnz + 4 (n+1) + 16 n P (the CSR, u_j gathered once, y = A u_j written)"),
+            "k_spmm_lanczos": (3, lambda P: per_nnz * nnz + 4 * (n + 1) + 24 * n * P,
+                               f"{per_nnz} nnz + 4 (n+1) + 24 n P (the CSR, y_j gathered once, y_j and "
+                               "y_(j-1) own rows read, y_(j+1) written)"),
+        }
+        rf = {}
+        for name, (slot, kb, basis) in kinds.items():
+            nl, ms_sum = ctx.profile_read(slot)
+            if not nl:
+                continue
+            busy = ctx.profile_busy(slot)
+            widths = {P: ctx.profile_read_width(slot, P) for P in (1, 2, 4, 8, 16, 32)}
+            widths = {P: v for P, v in widths.items() if v[0]}
+            bytes_total = sum(v[0] * kb(P) for P, v in widths.items())
+            gbs = bytes_total / (busy * 1e-3) / 1e9
+            tr = {P: _pmc_traffic(name, P, args.config, args.weighted) for P in widths}
+            traffic = (sum(widths[P][0] * tr[P] for P in widths) / nl) if all(tr.values()) else None
+            e = {"bound": "hbm", "kernel": f"{name}<{'|'.join(str(P) for P in sorted(widths))}>",
+                 "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                 "avg_launch_us": round(busy / nl * 1e3, 2), "launches": nl, "busy_ms": round(busy, 3),
+                 "launches_by_width": {str(P): v[0] for P, v in widths.items()},
+                 "avg_launch_us_by_width": {str(P): round(v[1] / v[0] * 1e3, 2) for P, v in widths.items()},
+                 "avg_launch_us_overlapped": round(ms_sum / nl * 1e3, 2),
+                 "algorithmic_bytes_per_launch": round(bytes_total / nl),
+                 "algorithmic_bytes_basis": basis + " per launch, at the launch's sweep width P; mean"}
             if traffic:
-                out["roofline"]["traffic_GBs"] = round(traffic * l1 / (ms1 * 1e-3) / 1e9, 1)
+                e["traffic_GBs"] = round(traffic * nl / (busy * 1e-3) / 1e9, 1)
+            rf[name] = e
+        if rf:
+            main_k = max(rf, key=lambda k: rf[k]["busy_ms"])  # the dominant kernel: most time in flight
+            out["roofline"] = dict(rf[main_k])
+            out["roofline"]["other_kernels"] = {k: v for k, v in rf.items() if k != main_k}
+            l2, ms2 = ctx.profile_read(1)
+            out["roofline"]["k2_update_avg_us"] = round(ms2 / l2 * 1e3, 2) if l2 else None
+            out["roofline"]["serial_eval_ms"] = round(serial_ms, 2)
+            out["roofline"]["measured"] = (
+                "HIP events around every sweep pass of one trace_exp after the timed region; avg_launch_us = "
+                "union of the kernel's launch intervals (time with >= 1 launch in flight) / launches; the "
+                "explicit and y-form sweeps of a round run side by side on two lanes, so each kernel's "
+                "launches share the chip with the other's")
     return out
 
 

@@ -262,16 +262,21 @@ void YBlockSweep::start() {
     KT_HIP(launch_sweep_scales(dnorms2, ncols, P, 1, ys, nullptr, st));
     KT_HIP(hipMemsetAsync(V0, 0, blk_bytes, st));
     KT_HIP(launch_weighted_sum(n, 1, P, ncols, x, ldx, 0, ys, V0, P, st));
+    kt_context_s* ctx = A->ctx;
+    prof_begin(ctx, PROF_YBLOCK, st, P);
     KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, V0, nullptr, Xc, ys + 6 * P, part,
                                M.long_rows, M.n_long, A->long_thresh, lblocks, st));
+    prof_end(ctx, PROF_YBLOCK, st);
     KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, 1.0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0), guard, st));
 }
 
 void YBlockSweep::step(int j) {
     const bool last = j + 2 == m;
+    prof_begin(A->ctx, PROF_YBLOCK, st, P);
     KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
                                last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long, A->long_thresh, lblocks,
                                st));
+    prof_end(A->ctx, PROF_YBLOCK, st);
     KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1), rec_at(2, j + 1), guard,
                         st));
     Yo = Xc;

@@ -64,10 +64,13 @@ def main(trace_csv, bench_json, out_json):
     }
     mc = (b.get("mc_trace") or {}).get("roofline")
     if mc:
-        # the mc_trace leg's serial roofline pass: its K1 launches (16- and
-        # 32-wide) are the last `launches` k_spmm_dot launches of the run
-        allk = [r for r in allrows
-                if "kt::k_spmm_dot<16," in r["Kernel_Name"] or "kt::k_spmm_dot<32," in r["Kernel_Name"]]
+        # the mc_trace leg's serial roofline pass: the dominant kernel's
+        # launches (every width it ran at) are the last `launches` launches of
+        # that kernel in the run (the reference-composition leg after it runs
+        # expmv kernels only)
+        base = mc["kernel"].split("<")[0]
+        widths = list(mc.get("launches_by_width", {}))
+        allk = [r for r in allrows if any(f"kt::{base}<{P}," in r["Kernel_Name"] for P in widths)]
         allk.sort(key=lambda r: int(r["Start_Timestamp"]))
         last = allk[-mc["launches"]:]
         d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in last]
