@@ -222,6 +222,16 @@ int kt_householder_qr(kt_context_t ctx, int64_t n, int64_t bs, const double* W, 
  * Pure host code (no device needed). */
 int kt_host_sym_eig(int n, const double* A, double* w, double* V);
 
+/* Host Gauss quadrature of one probe's m x m symmetric tridiagonal T
+ * (alpha: m diagonal entries, off: m - 1 off-diagonal ones), the per-probe
+ * step after every sweep (trace_fun_update.m:78-84 restated for a single
+ * vector: e1' f(T) e1 = sum_k tau_k^2 f(theta_k)): one implicit-shift QL pass
+ * rotating the first row of the eigenvector matrix.  q: e1' f(T) e1; fe1
+ * (m, nullable): f(T) e1, from the same pass by replaying its rotations (the
+ * weights of the Lanczos-f Afun, f(A) x = ||x|| V f(T) e1).  fun: KT_FUN_*.
+ * Pure host code (no device needed). */
+int kt_host_tridiag_quad(int m, const double* alpha, const double* off, int fun, double* q, double* fe1);
+
 /* ---- greedy edge selection (krylov_miobi.m / greedy_krylov.m) ---------- */
 
 /* Batched trace_fun_update over candidate edges, the inner loop of

@@ -97,6 +97,7 @@ SIGNATURES = [
                                                C.c_int, _dp, _ip]),
     ("kt_householder_qr", C.c_int, [_ctx_p, C.c_int64, C.c_int64, _dp, _dp, _dp]),
     ("kt_host_sym_eig", C.c_int, [C.c_int, _dp, _dp, _dp]),
+    ("kt_host_tridiag_quad", C.c_int, [C.c_int, _dp, _dp, C.c_int, _dp, _dp]),
     ("kt_frechet_entries", C.c_int, [_mat_p, C.c_int64, _i64p, _i64p, C.c_int, C.c_double, C.c_int,
                                      C.c_int64, _i64p, _i64p, _dp, _ip]),
     ("kt_hessianfcn", C.c_int, [_mat_p, C.c_int64, _dp, _dp, C.c_int, C.c_double, C.c_int, _dp]),

@@ -464,6 +464,16 @@ void sym_fun_from_eig(int n, const double* w, const double* V, int fun, double* 
 
 }  // namespace kt
 
+extern "C" int kt_host_tridiag_quad(int m, const double* alpha, const double* off, int fun, double* q,
+                                    double* fe1) {
+    if (m < 1 || !alpha || (m > 1 && !off) || !q || fun < KT_FUN_EXP || fun > KT_FUN_SQRT) {
+        kt::set_error("kt_host_tridiag_quad: bad argument");
+        return KT_ERR_ARG;
+    }
+    *q = fe1 ? kt::tridiag_fun_e1(m, alpha, off, fun, fe1) : kt::tridiag_quadrature(m, alpha, off, fun);
+    return KT_OK;
+}
+
 extern "C" int kt_host_sym_eig(int n, const double* A, double* w, double* V) {
     if (n < 0 || (n > 0 && (!A || !w))) {
         kt::set_error("kt_host_sym_eig: bad argument");
