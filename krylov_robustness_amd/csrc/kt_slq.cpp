@@ -156,62 +156,71 @@ void lanczos_sweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
 
 // y-form sweep (RNG-seeded probes only): one fused pass + one coefficient
 // launch per Lanczos step (kt_kernels.hip, k_spmm_lanczos / k_ycoef).
-// rec_host receives [alpha | up | low][m][P] followed by guard[P].
-void lanczos_sweep_y(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed,
-                     int64_t probe_base, double* rec_host, int lane) {
+// rec_host receives [alpha | up | low][m][P] followed by guard[P].  Enqueued
+// step by step (start(), step(j) for j < m - 1, finish()), so sweeps on
+// different lanes are queued launch by launch.
+YSweep::YSweep(kt_matrix_s* A_, const DevCSR& M_, int P_, int m_, uint64_t seed_, int64_t probe_base_,
+               double* rec_host_, int lane_)
+    : A(A_), M(M_), P(P_), m(m_), seed(seed_), probe_base(probe_base_), rec_host(rec_host_), lane(lane_) {
     kt_context_s* ctx = A->ctx;
-    const int n = (int)A->n;
+    n = (int)A->n;
     if (lane < 0 || lane > 3) fail(KT_ERR_ARG, "sweep lane out of range");
     if (lane && !ctx->aux_stream[lane - 1])
         KT_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[lane - 1], hipStreamNonBlocking));
-    hipStream_t st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
-    const int grid = spmm_grid(n, P, ctx->num_cu * 4);  // 4 row-group workgroups per CU
-    const int lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
-    const int grid1 = grid + lblocks;
+    st = lane ? ctx->aux_stream[lane - 1] : ctx->stream;
+    grid = spmm_grid(n, P, ctx->num_cu * 4);  // 4 row-group workgroups per CU
+    lblocks = long_blocks_for(M.n_long, ctx->num_cu * 2);
+    grid1 = grid + lblocks;
     SweepBufs& w = ctx->ws.sweep[lane];
-    const size_t blk_bytes = sizeof(double) * (size_t)n * P;
+    blk_bytes = sizeof(double) * (size_t)n * P;
     w.X0.ensure(blk_bytes);
     w.X1.ensure(blk_bytes);
     w.Y.ensure(blk_bytes);
     w.partial.ensure(sizeof(double) * (size_t)3 * P * grid1);  // slot-major [3P][grid1]
     w.coef.ensure(sizeof(double) * 9 * P);
-    const size_t rec = (size_t)3 * m * P + P;
-    w.trec.ensure(sizeof(double) * rec);
-    double* part = w.partial.as<double>();
-    double* ys = w.coef.as<double>();
-    double* trec = w.trec.as<double>();
-    double* guard = trec + (size_t)3 * m * P;
-    auto rec_at = [&](int row, int j) { return trec + (size_t)(row * m + j) * P; };
-    int flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
+    w.trec.ensure(sizeof(double) * ((size_t)3 * m * P + P));
+    part = w.partial.as<double>();
+    ys = w.coef.as<double>();
+    trec = w.trec.as<double>();
+    guard = trec + (size_t)3 * m * P;
+    flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
     if (blk_bytes >= ((size_t)1 << 31)) flags &= ~16;  // sc1 buffer stores take 32-bit offsets
-    const double s0 = 1.0 / std::sqrt((double)n);  // v_0 = z / ||z||, ||z||^2 = n
+    Z = w.X1.as<uint32_t>();
+    Xc = w.Y.as<double>();   // y_j
+    Yo = nullptr;            // y_{j-1} (none at j = 0)
+    Ot = w.X0.as<double>();  // y_{j+1}
+}
 
+void YSweep::start() {
+    kt_context_s* ctx = A->ctx;
+    const double s0 = 1.0 / std::sqrt((double)n);  // v_0 = z / ||z||, ||z||^2 = n
     // probes as a packed sign table (n x ceil(P/32) words), gathered by the
     // start pass instead of an 8nP-byte fp64 block
-    uint32_t* Z = w.X1.as<uint32_t>();
     KT_HIP(launch_rademacher_signs(P, n, seed, probe_base, M.perm, Z, st));
-    double* Xc = w.Y.as<double>();   // y_j
-    double* Yo = nullptr;            // y_{j-1} (none at j = 0)
-    double* Ot = w.X0.as<double>();  // y_{j+1}
     prof_begin(ctx, PROF_START, st, P);
-    KT_HIP(launch_spmm_lanczos_start(P, flags, grid1, M.rowptr, M.col, M.val, n, Z, s0, Xc, part,
-                                     M.long_rows, M.n_long, A->long_thresh, lblocks, st));
+    KT_HIP(launch_spmm_lanczos_start(P, flags, grid1, M.rowptr, M.col, M.val, n, Z, s0, Xc, part, M.long_rows,
+                                     M.n_long, A->long_thresh, lblocks, st));
     prof_end(ctx, PROF_START, st);
     KT_HIP(launch_ycoef(P, part, grid1, 1, m == 1, s0, ys, rec_at(0, 0), rec_at(1, 0), rec_at(2, 0), guard, st));
-    for (int j = 0; j + 1 < m; ++j) {
-        prof_begin(ctx, PROF_SPMM, st, P);
-        const bool last = j + 2 == m;  // y_{m} is never used: alpha_{m-1} needs only X.t
-        KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
-                                   last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long,
-                                   A->long_thresh, lblocks, st));
-        prof_end(ctx, PROF_SPMM, st);
-        KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1),
-                            rec_at(2, j + 1), guard, st));
-        Yo = Xc;  // y_{j+1} overwrites y_{j-1} from the next pass on
-        Xc = Ot;
-        Ot = Yo;
-    }
-    KT_HIP(hipMemcpyAsync(rec_host, trec, sizeof(double) * rec, hipMemcpyDeviceToHost, st));
+}
+
+void YSweep::step(int j) {
+    kt_context_s* ctx = A->ctx;
+    prof_begin(ctx, PROF_SPMM, st, P);
+    const bool last = j + 2 == m;  // y_{m} is never used: alpha_{m-1} needs only X.t
+    KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
+                               last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long, A->long_thresh,
+                               lblocks, st));
+    prof_end(ctx, PROF_SPMM, st);
+    KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1), rec_at(2, j + 1),
+                        guard, st));
+    Yo = Xc;  // y_{j+1} overwrites y_{j-1} from the next pass on
+    Xc = Ot;
+    Ot = Yo;
+}
+
+void YSweep::finish() {
+    KT_HIP(hipMemcpyAsync(rec_host, trec, sizeof(double) * ((size_t)3 * m * P + P), hipMemcpyDeviceToHost, st));
 }
 
 // y-form sweep seeded by a given device block (the quadrature-only columns
@@ -603,13 +612,30 @@ static int slq_submit(kt_matrix_s* A, int fun, int m, uint64_t seed, int64_t pro
         prof_recycle(ctx);
         size_t prev_events[PROF_NSLOTS];
         for (int k = 0; k < PROF_NSLOTS; ++k) prev_events[k] = ctx->prof[k].used;
-        for (int64_t sw = 0; sw < pd.nsweeps; ++sw) {
-            if (ctx->yform)
-                lanczos_sweep_y(A, H, pd.P, m, seed, probe_offset + sw * pd.P, htrec + pd.rec * sw,
-                                (int)(sw % pd.lanes));
-            else
-                lanczos_sweep(A, H, pd.P, m, seed, probe_offset + sw * pd.P, nullptr, 0, 0, nullptr,
-                              htrec + pd.rec * sw, nullptr, nullptr, (int)(sw % pd.lanes));
+        // one sweep per lane at a time, the lanes' sweeps queued step by step
+        // (launch by launch across the lanes, so every lane starts at once)
+        for (int64_t s0 = 0; s0 < pd.nsweeps; s0 += pd.lanes) {
+            const int g = (int)std::min<int64_t>(pd.lanes, pd.nsweeps - s0);
+            if (ctx->yform) {
+                std::vector<std::unique_ptr<YSweep>> grp;
+                for (int l = 0; l < g; ++l)
+                    grp.emplace_back(new YSweep(A, H, pd.P, m, seed, probe_offset + (s0 + l) * pd.P,
+                                                htrec + pd.rec * (s0 + l), l));
+                for (auto& y : grp) y->start();
+                for (int j = 0; j + 1 < m; ++j)
+                    for (auto& y : grp) y->step(j);
+                for (auto& y : grp) y->finish();
+            } else {
+                std::vector<std::unique_ptr<ExplicitSweep>> grp;
+                for (int l = 0; l < g; ++l)
+                    grp.emplace_back(new ExplicitSweep(A, H, pd.P, m, seed, probe_offset + (s0 + l) * pd.P, nullptr,
+                                                       0, 0, nullptr, htrec + pd.rec * (s0 + l), nullptr, nullptr,
+                                                       l, 0));
+                for (auto& e : grp) e->start();
+                for (int j = 0; j < m; ++j)
+                    for (auto& e : grp) e->step(j);
+                for (auto& e : grp) e->finish();
+            }
         }
         for (int l = 0; l < pd.lanes; ++l) {
             if (!pd.done[l]) KT_HIP(hipEventCreateWithFlags(&pd.done[l], hipEventDisableTiming));

@@ -49,6 +49,33 @@ class ExplicitSweep {
     DevBuf* hist_dev = nullptr;
 };
 
+// lanczos_sweep_y (the RNG-seeded y-form sweep of the Hutchinson hot path)
+// enqueued step by step: start(), step(j) for j < m - 1, finish().
+class YSweep {
+   public:
+    YSweep(kt_matrix_s* A, const DevCSR& M, int P, int m, uint64_t seed, int64_t probe_base, double* rec_host,
+           int lane);
+    void start();
+    void step(int j);
+    void finish();
+
+   private:
+    double* rec_at(int row, int j) { return trec + (size_t)(row * m + j) * P; }
+    kt_matrix_s* A;
+    const DevCSR& M;
+    int P, m;
+    uint64_t seed;
+    int64_t probe_base;
+    double* rec_host;
+    int lane;
+    int n = 0, grid = 0, lblocks = 0, grid1 = 0, flags = 0;
+    size_t blk_bytes = 0;
+    hipStream_t st = nullptr;
+    double *part = nullptr, *ys = nullptr, *trec = nullptr, *guard = nullptr;
+    uint32_t* Z = nullptr;
+    double *Xc = nullptr, *Yo = nullptr, *Ot = nullptr;
+};
+
 // lanczos_sweep_y_block enqueued step by step: start(), step(j) for j < m - 1,
 // finish(); same interleaving rule as ExplicitSweep.
 class YBlockSweep {
