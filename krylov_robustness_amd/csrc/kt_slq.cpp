@@ -401,6 +401,7 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     int Pe = 1;
     while (Pe < ne && Pe < 16) Pe <<= 1;
     if (px > 0) Pe = px;
+    if (Pe > 32 || (Pe & (Pe - 1))) fail(KT_ERR_ARG, "lanczos_columns_split: sweep width must be a power of two <= 32");
     // sweeps dealt over the four lanes in order (explicit first), so up to
     // four run side by side; a lane's later sweeps follow its earlier ones
     int k = 0;
