@@ -968,12 +968,14 @@ __global__ __launch_bounds__(256) void k_coef_cgs2(const double* __restrict__ pa
                                                     const double* __restrict__ scale_prev,
                                                     double* __restrict__ coef,
                                                     double* __restrict__ t_alpha,
-                                                    double* __restrict__ t_up) {
+                                                    double* __restrict__ t_up,
+                                                    double* __restrict__ hist) {
     const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (p >= P) return;
     const double g1 = wave_reduce_slot(partial, nblk, p);
     if ((threadIdx.x & 63) == 0) {
         const double sc = scale_cur[p];
+        if (hist) hist[p] = sc;  // the basis sweep's scale history: v_j = s_j u_j
         const double G11 = sc * sc * k2s[0 * P + p];
         double g0 = 0.0, G00 = 0.0, G01 = 0.0;
         if (!first) {
@@ -1812,11 +1814,11 @@ hipError_t launch_spmm_block(int P, int flags, int grid, const CsrView& M, const
 
 hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, const double* k2s,
                             const double* sc, const double* sp, double* coef, double* t_alpha,
-                            double* t_up, hipStream_t st) {
+                            double* t_up, double* hist, hipStream_t st) {
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
         k_coef_cgs2<PP><<<(PP + 3) / 4, 256, 0, st>>>(partial, nblk, first, k2s, sc, sp, coef,
-                                                      t_alpha, t_up);
+                                                      t_alpha, t_up, hist);
     });
 }
 

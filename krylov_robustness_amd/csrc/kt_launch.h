@@ -57,9 +57,10 @@ hipError_t launch_greedy_edit(int C, const double* state, int* Ti, int* Tj, int 
 hipError_t launch_spmm_block(int P, int flags, int grid, const CsrView& M, const double* X, int ldx,
                              double* Y, int ldy, int long_blocks, int chunk_blocks, double* ck_part,
                              hipStream_t st, int slices = 1, const int* skip = nullptr);
+// hist (nullable): P doubles receiving the step's scale s_j (sc)
 hipError_t launch_coef_cgs2(int P, const double* partial, int nblk, int first, const double* k2s,
                             const double* sc, const double* sp, double* coef, double* t_alpha,
-                            double* t_up, hipStream_t st);
+                            double* t_up, double* hist, hipStream_t st);
 // rec (optional): u_next's first bcols columns also to rec[row * bcols + c]
 hipError_t launch_update(int P, int grid, int n, const double* y, double* uprev,
                          const double* ucur, const double* sc, const double* sp,

@@ -113,19 +113,17 @@ void ExplicitSweep::start() {
 void ExplicitSweep::step(int j) {
     kt_context_s* ctx = A->ctx;
     const int first = (j == 0);
-    if (basis) {  // record s_j (v_j = s_j u_j); u_0 into slot 0
-        if (first)
-            KT_HIP(hipMemcpy2DAsync(bbase, sizeof(double) * bcols, ucur, sizeof(double) * P, sizeof(double) * bcols,
-                                    (size_t)n, hipMemcpyDeviceToDevice, st));
-        KT_HIP(hipMemcpyAsync(hist_dev->as<double>() + (size_t)j * P, sc, sizeof(double) * P,
-                              hipMemcpyDeviceToDevice, st));
-    }
+    if (basis && first)  // u_0 into slot 0
+        KT_HIP(hipMemcpy2DAsync(bbase, sizeof(double) * bcols, ucur, sizeof(double) * P, sizeof(double) * bcols,
+                                (size_t)n, hipMemcpyDeviceToDevice, st));
     prof_begin(ctx, PROF_SPMM, st, P);
     KT_HIP(launch_spmm_dot(P, ctx->k1_flags | (A->unit_values ? 2 : 0), grid1, M.rowptr, M.col, M.val, n, ucur, sc, Yb,
                            part1, M.long_rows, M.n_long, A->long_thresh, lblocks, st));
     prof_end(ctx, PROF_SPMM, st);
+    // the coefficient launch also records s_j (v_j = s_j u_j) for a basis sweep
     KT_HIP(launch_coef_cgs2(P, part1, grid1, first, k2s, sc, sp, coef, trec + (size_t)(0 * m + j) * P,
-                            trec + (size_t)(1 * m + j) * P, st));
+                            trec + (size_t)(1 * m + j) * P, hist_dev ? hist_dev->as<double>() + (size_t)j * P : nullptr,
+                            st));
     prof_begin(ctx, PROF_UPDATE, st, P);
     double* rec = (basis && j + 1 < m) ? bbase + (size_t)(j + 1) * n * bcols : nullptr;
     KT_HIP(launch_update(P, grid, n, Yb, uprev, ucur, sc, sp, coef, first, part2, st, ctx->k2_nt, rec, bcols));
