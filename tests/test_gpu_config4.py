@@ -3,9 +3,9 @@ graphs.chung_lu(1e6, 1e7, 2.5, seed=0)), pinned by tests/golden/
 config4_values.json (tests/golden/make_config4_fixture.py):
 
   * every one of the 1,024 per-probe forms of one evaluation at the bench's
-    first timed seed (0) equals the C oracle's (oracle/slq_ref.c) to 1e-8
-    relative (the tolerance of test_gpu_slq.py: the device forms CGS2 from a
-    Gram identity and sums in another order), and the 1,024-probe Hutchinson
+    first timed seed (0) equals the C oracle's (oracle/slq_ref.c) to 1e-11
+    relative (measured 3.7e-13: the device forms its coefficients from Gram
+    identities and sums in another order), and the 1,024-probe Hutchinson
     estimate lies within 3 standard errors of tr(exp(A)) from the spectrum;
   * trace_exp (trace_exp.m:5-6: mc_trace(Afun, n, 1e-4, 1000, 1), the
     mc_trace.m:42-58 deflated structure, Lanczos-exp Afun m = 30) equals the
@@ -30,7 +30,9 @@ import pytest
 from conftest import GOLDEN, ROOT
 
 pytestmark = pytest.mark.gpu
-RTOL_PROBE = 1e-8
+# per-probe forms vs the C oracle: measured max 3.7e-13 relative (median
+# 6e-14) on the final round-5 build; held at 1e-11
+RTOL_PROBE = 1e-11
 RTOL_MC = 1e-10
 
 
