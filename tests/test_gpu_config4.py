@@ -9,11 +9,11 @@ config4_values.json (tests/golden/make_config4_fixture.py):
     estimate lies within 3 standard errors of tr(exp(A)) from the spectrum;
   * trace_exp (trace_exp.m:5-6: mc_trace(Afun, n, 1e-4, 1000, 1), the
     mc_trace.m:42-58 deflated structure, Lanczos-exp Afun m = 30) equals the
-    spectral value to 1e-10 relative -- exp(A) is rank one to exp(lambda2 -
+    spectral value to 1e-12 relative -- exp(A) is rank one to exp(lambda2 -
     lambda1) = 1e-23 here, so the first round's Q captures the top
     eigenvector and the estimator is exact up to the Lanczos and eigsh
     rounding (the fixture's own tail bound is 3e-20) -- and the numpy
-    restatement's value to 1e-10, in the same 2 rounds;
+    restatement's value to 1e-13, in the same 2 rounds;
   * the weighted variant (graphs.symmetric_weights(A, seed=1), bench.py
     --weighted: values read, 12 B per nonzero) the same way on its own
     spectrum and 8 oracle probes;
@@ -33,7 +33,11 @@ pytestmark = pytest.mark.gpu
 # per-probe forms vs the C oracle: measured max 3.7e-13 relative (median
 # 6e-14) on the final round-5 build; held at 1e-11
 RTOL_PROBE = 1e-11
-RTOL_MC = 1e-10
+# trace_exp (mc_trace, Lanczos-exp Afun): measured 1.6e-13 from the spectral
+# value (the Lanczos and eigsh rounding) and 1.7e-15 from the numpy
+# restatement of the same algorithm
+RTOL_MC = 1e-12
+RTOL_MC_ORACLE = 1e-13
 
 
 @pytest.fixture(scope="module")
@@ -79,7 +83,7 @@ def test_config4_trace_exp_mc_trace_exact(fx, dev, gpu_ctx):
                                m=o["m"], A=dev, ctx=gpu_ctx)
     spec = fx["spectrum"]["tr_exp_topk"]
     assert abs(tr - spec) <= RTOL_MC * spec, (tr, spec)
-    assert abs(tr - o["tr"]) <= RTOL_MC * abs(o["tr"])
+    assert abs(tr - o["tr"]) <= RTOL_MC_ORACLE * abs(o["tr"])
     assert it == o["it"] == 2 and res < 1e-4
     # trace_exp (the drop-in's C entry) is the same call
     assert kra.trace_exp(dev, "lanczos", m=o["m"], seed=o["seed"], ctx=gpu_ctx) == tr
