@@ -230,6 +230,24 @@ __global__ __launch_bounds__(256) void k_rademacher(int n, uint64_t seed, int64_
     }
 }
 
+// The same probes written as ncols (<= 64) columns of a wider row-major block
+// (X[r * ldx + c] = probe probe_base + c of row r, natural row order): the
+// Rademacher columns of mc_trace.m:43-44 straight into their slots of the
+// round's probe block, without a staging block and a strided copy.
+__global__ __launch_bounds__(256) void k_rademacher_cols(int n, int ncols, uint64_t seed, int64_t probe_base,
+                                                         double* __restrict__ X, int ldx) {
+    __shared__ uint64_t keys[64];
+    for (int p = threadIdx.x; p < ncols; p += blockDim.x) keys[p] = sm64(sm64(seed) + (uint64_t)(probe_base + p));
+    __syncthreads();
+    const int64_t total = (int64_t)n * ncols;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = t / ncols;
+        const int p = (int)(t % ncols);
+        X[r * ldx + p] = (sm64(keys[p] + (uint64_t)r) >> 63) ? -1.0 : 1.0;
+    }
+}
+
 // Packed form of the same probe block for the y-form start pass: bit p of
 // S[r * W + p / 32] (W = ceil(P / 32) words per row) is set where X[r, p] = -1.
 // n x 4W bytes (2 MB at n = 1M, P = 16) instead of the 8nP-byte fp64 block.
@@ -1756,6 +1774,17 @@ hipError_t launch_rademacher(int P, int n, uint64_t seed, int64_t probe_base, co
     return dispatch_p(P, [&](auto c) {
         k_rademacher<decltype(c)::value><<<grid, 256, 0, st>>>(n, seed, probe_base, perm, X);
     });
+}
+
+hipError_t launch_rademacher_cols(int n, int ncols, uint64_t seed, int64_t probe_base, double* X, int ldx,
+                                  hipStream_t st) {
+    if (ncols < 1 || ncols > 64 || ldx < ncols) return hipErrorInvalidValue;
+    int64_t total = (int64_t)n * ncols;
+    int grid = (int)((total + 255) / 256);
+    if (grid > 8192) grid = 8192;
+    if (grid < 1) grid = 1;
+    k_rademacher_cols<<<grid, 256, 0, st>>>(n, ncols, seed, probe_base, X, ldx);
+    return hipGetLastError();
 }
 
 hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int* ci,

@@ -10,6 +10,10 @@ int long_blocks_for(int n_long, int max_blocks);
 
 hipError_t launch_rademacher(int P, int n, uint64_t seed, int64_t probe_base, const int* perm,
                              double* X, hipStream_t st);
+// probes probe_base .. probe_base + ncols - 1 as ncols (<= 64) columns of a
+// row-major block with row stride ldx (natural row order)
+hipError_t launch_rademacher_cols(int n, int ncols, uint64_t seed, int64_t probe_base, double* X, int ldx,
+                                  hipStream_t st);
 hipError_t launch_spmm_dot(int P, int flags, int grid, const int* rp, const int* ci,
                            const double* va, int n, const double* ucur, const double* sc,
                            double* y, double* partial, const int* long_rows, int n_long,

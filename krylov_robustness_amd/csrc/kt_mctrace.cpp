@@ -507,10 +507,9 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
     DevMat Bk, Yb, T;
     Bk.alloc(ctx, n, LB);  // [S_{it+1} | P..P Q_it | P..P G_it (10 slots) | 0 0]
     Yb.alloc(ctx, n, ld);  // Afun_it(S_it), then Q_it in place
-    T.alloc(ctx, n, ld);   // Rademacher columns before they enter the block
-    auto rademacher_into = [&](int64_t base, double* dst) {
-        KT_HIP(launch_rademacher(ld, (int)n, seed, base, nullptr, T.col(0), st));
-        copy_cols(ctx, n, T.col(0), ld, dst, LB, mb);
+    if (sh.world > 1) T.alloc(ctx, n, ld);  // a rank's G columns before they enter their slots
+    auto rademacher_into = [&](int64_t base, double* dst) {  // probes base .. base + 9 into their slots
+        KT_HIP(launch_rademacher_cols((int)n, mb, seed, base, dst, LB, st));
     };
     // S term of round itx: Y = F(P_{itx-1}..P_1 S_itx) into Yb (unprojected)
     auto s_term = [&](int itx) {
@@ -537,12 +536,12 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
         Qs.back().alloc(ctx, n, ld);
         copy_cols(ctx, n, Yb.col(0), ld, Qs.back().col(0), ld, mb);
         // G term input: P_it..P_1 G_it, this rank's columns c % world == rank  :44, :49
-        KT_HIP(launch_rademacher(ld, (int)n, seed, base + mb, nullptr, T.col(0), st));
         int ng = 0;
-        if (sh.world == 1) {  // every G column: one block copy
-            copy_cols(ctx, n, T.col(0), ld, Bk.col(2 * mb), LB, mb);
+        if (sh.world == 1) {  // every G column, straight into its slot
+            rademacher_into(base + mb, Bk.col(2 * mb));
             ng = mb;
         } else {
+            KT_HIP(launch_rademacher(ld, (int)n, seed, base + mb, nullptr, T.col(0), st));
             for (int c = sh.rank; c < mb; c += sh.world) copy_cols(ctx, n, T.col(c), ld, Bk.col(2 * mb + ng++), LB, 1);
         }
         for (int k = (int)Qs.size() - 1; k >= 0 && ng > 0; --k)
