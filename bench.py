@@ -745,6 +745,17 @@ def _mc_trace_leg(args, kra, kdist, D, ctx, m, steps, use_pg, barrier, coll_dev,
                 "union of the kernel's launch intervals (time with >= 1 launch in flight) / launches; the "
                 "explicit and y-form sweeps of a round run side by side on two lanes, so each kernel's "
                 "launches share the chip with the other's")
+            # the whole evaluation: every sweep pass's algorithmic bytes (K1,
+            # K2 with its basis stores, y-form passes) over the evaluation's
+            # wall time, the two lanes' concurrency included
+            k2_bytes = sum(ctx.profile_read_width(1, P)[0] * 32 * n * P for P in (1, 2, 4, 8, 16, 32))
+            sweep_bytes = sum(rf[k]["algorithmic_bytes_per_launch"] * rf[k]["launches"] for k in rf) + k2_bytes
+            eb = sweep_bytes / (serial_ms * 1e-3) / 1e9
+            out["eval_roofline"] = {"sweep_bytes_per_eval": int(sweep_bytes), "eval_ms": round(serial_ms, 2),
+                                    "achieved_GBs": round(eb, 1), "frac": round(eb / HBM_PEAK_GBS, 4),
+                                    "basis": "sum over the evaluation's sweep launches of their algorithmic "
+                                             "bytes (K1 and y-form passes as in roofline; K2 32 n P, its basis "
+                                             "stores not counted) / the serial evaluation's wall time"}
     return out
 
 
