@@ -119,6 +119,22 @@ def test_lanczos_fmv_matches_oracle(kra, gpu_ctx):
     np.testing.assert_allclose(Y, Yo, rtol=1e-8, atol=1e-10 * np.abs(Yo).max())
 
 
+def test_lanczos_fmv_many_columns_over_lanes(kra, gpu_ctx):
+    """40 columns: three 16-wide explicit sweeps (the last zero-padded) queued
+    step by step on three sweep lanes (kt_slq.cpp lanczos_columns_split).
+    Every column matches the oracle, and a column's f(A) x is bit-identical
+    to the same column computed in a call of its own sweep alone (its form
+    depends only on its sweep's width, not on the lanes beside it)."""
+    A = load_graph("rome")
+    X = np.random.default_rng(5).normal(size=(A.shape[0], 40))
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    Y = kra.lanczos_fmv(D, X, m=20, fun="exp", ctx=gpu_ctx)
+    Yo = ko.lanczos_fmv(A, X, 20, "exp")
+    np.testing.assert_allclose(Y, Yo, rtol=1e-8, atol=1e-10 * np.abs(Yo).max())
+    Y16 = kra.lanczos_fmv(D, np.ascontiguousarray(X[:, 16:32]), m=20, fun="exp", ctx=gpu_ctx)
+    np.testing.assert_array_equal(Y[:, 16:32], Y16)
+
+
 @pytest.mark.parametrize("name", ["denmark", "anaheim"])
 def test_mc_trace_matrix_afun(kra, gpu_ctx, name):
     """mc_trace.m:32-34 (Afun is a matrix), 3 rounds of nested deflation."""
