@@ -351,6 +351,14 @@ int kt_debug_delay(kt_context_t ctx, int lane, double microseconds);
  * creation. */
 int kt_context_stat(kt_context_t ctx, int stat, int64_t* value);
 
+/* Threads of the process-wide host pool (the per-column / per-candidate
+ * host work between device steps: Gauss quadratures, the greedy host
+ * eigenproblems), the calling thread included: min(16, the CPUs this
+ * process may use -- its affinity mask capped by the cgroup CPU quota --
+ * divided by LOCAL_WORLD_SIZE, the ranks torchrun started on this node),
+ * at least 1; KT_HOST_THREADS overrides.  Fixed at the pool's first use. */
+int kt_host_threads(void);
+
 #ifdef __cplusplus
 }
 #endif

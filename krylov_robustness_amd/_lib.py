@@ -109,6 +109,7 @@ SIGNATURES = [
     ("kt_debug_delay", C.c_int, [_ctx_p, C.c_int, C.c_double]),
     ("kt_profile_read_width", C.c_int, [_ctx_p, C.c_int, C.c_int, _i64p, _dp]),
     ("kt_context_stat", C.c_int, [_ctx_p, C.c_int, _i64p]),
+    ("kt_host_threads", C.c_int, []),
 ]
 
 _lib = None

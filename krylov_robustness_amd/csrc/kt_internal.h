@@ -257,8 +257,15 @@ struct DevCSR {
     double* val = nullptr;
     int* long_rows = nullptr;  // rows with degree > long_thresh, heaviest first
     int n_long = 0;
+    int n_heavy = 0;           // the first n_heavy long rows have degree > kExpmvCoopThresh
     int* med_rows = nullptr;   // rows with kMedThresh < degree <= long_thresh (expmv terms)
     int n_med = 0;
+    // natural order only (the row-blocked expmv term): rows of degree <=
+    // min(kMedThresh, long_thresh) as {row, beg, end, 0}, degree-descending
+    // within windows of consecutive rows (kt_runtime.cpp build_csr)
+    int* short_tasks = nullptr;
+    int n_short = 0;
+    int* med_tasks = nullptr;  // natural order only: med_rows as {row, beg, end, 0}
     int* perm = nullptr;       // device row -> original row (nullptr: identity)
     // hub rows (degree > kSplitThresh) cut into kChunkNnz-nonzero chunks for
     // the block SpMM: chunk c = nonzeros [ck_beg[c], ck_end[c]); split row i =

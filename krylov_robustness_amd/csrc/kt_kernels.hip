@@ -34,6 +34,8 @@
 #include "kt_launch.h"
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include <type_traits>
 
 namespace kt {
@@ -89,7 +91,9 @@ template <int P> using GeoB = GeoW<P, (P >= 16) ? KT_BLK_VW : (P >= 2) ? 2 : 1>;
 // with sc1), which drops the line from the XCD's L2 instead of keeping it
 // (MI355X_MICROARCH.md: plain / nt stores keep the line), leaving L2 to the
 // gathered table.
-enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4, KF_NTY = 8, KF_SC1 = 16 };
+// FLAGS bit 5 (expmv terms): mu = 0 (no self loops: trace(A) = 0), so a row's
+// own b is never read and (A - mu I) b is A b.
+enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4, KF_NTY = 8, KF_SC1 = 16, KF_MU0 = 32 };
 
 // KT_KY_DIAG (diagnostic builds of the y-form pass only, tools/ky_diag.sh; their
 // results are wrong): 1 = gathers + own row, 2 = gathers only, 3 = row streams only
@@ -318,35 +322,35 @@ __device__ __forceinline__ void row_gather(int k0, int end, int stride, int p0,
     }
 }
 
-// Same sum as row_gather, issued 8 deep: the 8 column indices of a chunk are
-// loaded together, then the 8 row gathers (a tail entry re-reads the chunk's
-// first row with weight 0, so no lane branches), then the 8 FMAs.
-template <int P, int FLAGS, class G = Geo<P>>
+// Same sum as row_gather, issued D deep (default 8): the D column indices of
+// a chunk are loaded together, then the D row gathers (a tail entry re-reads
+// the chunk's first row with weight 0, so no lane branches), then the D FMAs.
+template <int P, int FLAGS, class G = Geo<P>, int D = 8>
 __device__ __forceinline__ void row_gather8(int k0, int end, int stride, int p0,
                                             const int* __restrict__ col,
                                             const double* __restrict__ val,
                                             const double* __restrict__ ucur, double* s,
                                             int ld = P) {
     using V = VecT<G::VEC>;
-    for (int k = k0; k < end; k += 8 * stride) {
-        int c[8];
-        double a[8];
+    for (int k = k0; k < end; k += D * stride) {
+        int c[D];
+        double a[D];
         const int c0 = ld_stream<FLAGS>(col + k);
         c[0] = c0;
         a[0] = (FLAGS & KF_UNIT) ? 1.0 : ld_stream<FLAGS>(val + k);
 #pragma unroll
-        for (int i = 1; i < 8; ++i) {
+        for (int i = 1; i < D; ++i) {
             const int idx = k + i * stride;
             const bool ok = idx < end;
             c[i] = ok ? ld_stream<FLAGS>(col + idx) : c0;
             if constexpr (FLAGS & KF_UNIT) a[i] = ok ? 1.0 : 0.0;
             else a[i] = ok ? ld_stream<FLAGS>(val + idx) : 0.0;
         }
-        typename V::T x[8];
+        typename V::T x[D];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = ld_gather<FLAGS, G::VEC>(ucur + (int64_t)c[i] * ld + p0);
+        for (int i = 0; i < D; ++i) x[i] = ld_gather<FLAGS, G::VEC>(ucur + (int64_t)c[i] * ld + p0);
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < D; ++i)
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = fma(a[i], V::get(x[i], e), s[e]);
     }
@@ -1667,6 +1671,397 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
     }
 }
 
+// ROW-BLOCKED form of the SPLIT term (round 6; large grids, the default there).
+// The split kernel above launches one workgroup per long row, one per four
+// medium rows and one per 32 short rows: 66k workgroups at config 4 (12.6k
+// rows of degree > 64, 90k of 17-64), each paying an `active` read behind a
+// barrier, an LDS reduction, a barrier and two atomics for one gather round
+// trip.  Here resident workgroups stride over the rows with WAVES as the unit
+// of work, as the probe passes do (k_spmm_lanczos):
+//   long rows  (degree > long_thresh, heaviest first): one wave per row;
+//   medium rows (kMedThresh < degree <= long_thresh): one wave per row;
+//   short rows: row blocks of GPW (= 8 at P = 16) consecutive rows per wave,
+//               one row group of 16 B per lane per row, the next block's
+//               row_ptr loaded while this block gathers.
+// Every row's sum is formed in exactly the order of the split / fused
+// kernels, so F, s, m and mv are bit-identical to them:
+//   short:  one sequential chain over the row in CSR order (row_gather8, stride 1);
+//   medium: 16 chains k = beg + g + 16 i (g < 16), each in i order, summed by
+//           the xor butterfly over g (g ^ 1, g ^ 2, g ^ 4, g ^ 8);
+//   long:   the fused kernel's 4 waves x 16 chains k = beg + 16 w + g + 64 i,
+//           here the 4 chain sets w taken in turn by one wave, each
+//           butterflied over g, then ((t0 + t1) + t2) + t3 as the fused
+//           kernel's LDS sum.
+// The row sums of |b| and |F| and their maxima are the split kernel's too
+// (the same lane geometry per row class; max is exact in any order).
+// 4 waves per workgroup: 92 VGPRs = 5 waves per SIMD (8-wave workgroups
+// would fit only 2 per CU, 4 waves per SIMD)
+#ifndef KT_XR_WAVES
+#define KT_XR_WAVES 4
+#endif
+#ifndef KT_XR_WPE
+#define KT_XR_WPE 0
+#endif
+#ifndef KT_XR_SD
+#define KT_XR_SD 8
+#endif
+#ifndef KT_XR_TASKS
+#define KT_XR_TASKS 1
+#endif
+#ifndef KT_XR_FPS
+#define KT_XR_FPS 1
+#endif
+#ifndef KT_XR_FPM
+#define KT_XR_FPM 1
+#endif
+#ifndef KT_XR_MD
+#define KT_XR_MD 4
+#endif
+#ifndef KT_XR_LD
+#define KT_XR_LD 4
+#endif
+constexpr int kExpmvRowsWaves = KT_XR_WAVES;
+template <int P, int FLAGS>
+__global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
+    const int* __restrict__ rp, const int* __restrict__ ci, const double* __restrict__ va, int n,
+    const int* __restrict__ long_rows, int n_long, int n_heavy, const int4* __restrict__ med_tasks, int n_med,
+    const int4* __restrict__ short_tasks, int n_short,
+    int nc, int ld, double mu, double coef, int k, const double* __restrict__ bin,
+    double* __restrict__ bout, double* __restrict__ F, ExpmvState* st) {
+    constexpr int WAVES = kExpmvRowsWaves;
+    constexpr int VW = 4;                                          // the fused kernel's waves per long row
+    using G = GeoW<P, (P >= 2) ? 2 : 1>;                          // short rows
+    using GL = GeoW<P, (P >= 4) ? 4 : (P >= 2) ? 2 : 1>;          // medium / long rows
+    constexpr bool MU0 = (FLAGS & KF_MU0) != 0;
+    if constexpr (MU0) mu = 0.0;  // folds every own-b load and (A - mu I) away
+    __shared__ int decide;
+    __shared__ double red[2][WAVES];
+    __shared__ double lsum[WAVES][P];  // a heavy row's chain-set sums
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) decide = st->active;
+    __syncthreads();
+    if (!decide) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->mv += 1;
+#ifdef KT_XR_SKIP  // resource-usage probes only: drop row classes
+    if (KT_XR_SKIP & 1) n_long = n_heavy = 0;
+    if (KT_XR_SKIP & 2) n_med = 0;
+    if (KT_XR_SKIP & 4) n_short = 0;
+#endif
+    const int gw = blockIdx.x * WAVES + wave, TW = gridDim.x * WAVES;
+    __builtin_assume(gw >= 0);
+    __builtin_assume(TW > 0);
+    const int subL = lane % GL::LPR, grpL = lane / GL::LPR, p0L = subL * GL::VEC;
+    const int sub = lane % G::LPR, grp = lane / G::LPR, p0 = sub * G::VEC;
+    double mb = 0.0, mf = 0.0;  // running maxima of this lane's row sums
+    auto fold = [&](double sb, double sf, int lpr) {
+        for (int o = 1; o < lpr; o <<= 1) {
+            sb += __shfl_xor(sb, o, 64);
+            sf += __shfl_xor(sf, o, 64);
+        }
+        mb = fmax(mb, sb);
+        mf = fmax(mf, sf);
+    };
+    // (0) the heaviest long rows (degree > kExpmvCoopThresh, the first n_heavy
+    //     of the heaviest-first list): one WORKGROUP per row, wave w running
+    //     chain set w -- the fused kernel's own structure and LDS sum -- so a
+    //     hub's 4 x 16 chains (49 entries each at degree 3,122) run side by
+    //     side instead of one wave's 4 sets in turn (the tail of the launch)
+    static_assert(WAVES == VW, "one wave per chain set");
+    for (int hi = blockIdx.x; hi < n_heavy; hi += gridDim.x) {
+        const int row = long_rows[hi];
+        double acc[GL::VEC];
+#pragma unroll
+        for (int e = 0; e < GL::VEC; ++e) acc[e] = 0.0;
+        row_gather8<P, FLAGS, GL, KT_XR_LD>(rp[row] + wave * GL::GPW + grpL, rp[row + 1], VW * GL::GPW, p0L, ci, va,
+                                           bin, acc, ld);
+#pragma unroll
+        for (int o = GL::LPR; o < 64; o <<= 1)
+#pragma unroll
+            for (int e = 0; e < GL::VEC; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
+        if (grpL == 0)
+#pragma unroll
+            for (int e = 0; e < GL::VEC; ++e) lsum[wave][p0L + e] = acc[e];
+        __syncthreads();
+        double sb = 0.0, sf = 0.0;
+        if (wave == 0) {
+            if (grpL == 0) {
+                double t[GL::VEC], fo[GL::VEC], bo[GL::VEC];
+#pragma unroll
+                for (int e = 0; e < GL::VEC; ++e) {
+                    t[e] = lsum[0][p0L + e];
+#pragma unroll
+                    for (int w = 1; w < VW; ++w) t[e] += lsum[w][p0L + e];
+                }
+                expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
+                expmv_row_update<GL::VEC>(row, p0L, t, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+            }
+            fold(sb, sf, GL::LPR);
+        }
+        __syncthreads();  // lsum is rewritten by the next heavy row
+    }
+    // (1) the other long rows: the fused kernel's 4 waves as 4 chain sets in
+    //     turn in one wave (4 deep: the first chain entry of every set is
+    //     issued before the butterfly of the previous one is needed)
+    for (int li = n_heavy + gw; li < n_long; li += TW) {
+        const int row = long_rows[li];
+        const int beg = rp[row], end = rp[row + 1];
+        double s[GL::VEC];
+#pragma unroll 1
+        for (int w = 0; w < VW; ++w) {
+            double acc[GL::VEC];
+#pragma unroll
+            for (int e = 0; e < GL::VEC; ++e) acc[e] = 0.0;
+            row_gather8<P, FLAGS, GL, KT_XR_LD>(beg + w * GL::GPW + grpL, end, VW * GL::GPW, p0L, ci, va, bin, acc, ld);
+#pragma unroll
+            for (int o = GL::LPR; o < 64; o <<= 1)
+#pragma unroll
+                for (int e = 0; e < GL::VEC; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
+#pragma unroll
+            for (int e = 0; e < GL::VEC; ++e) s[e] = w == 0 ? acc[e] : s[e] + acc[e];
+        }
+        double sb = 0.0, sf = 0.0;
+        if (grpL == 0) {
+            double fo[GL::VEC], bo[GL::VEC];
+            expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
+            expmv_row_update<GL::VEC>(row, p0L, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+        }
+        fold(sb, sf, GL::LPR);
+    }
+    // (2) medium rows: one wave per row (16 chains; with MD = 4 a row of
+    //     degree <= 64 is one round), pipelined: while row mi gathers, the
+    //     chain columns of row mi + TW and the task of row mi + 2 TW are in
+    //     flight
+    constexpr int MD = KT_XR_MD;
+    auto load_mtask = [&](int ii, int& r, int& bg, int& en) {
+        r = -1;
+        bg = en = 0;
+        if (ii < n_med) {
+            const int4 v = med_tasks[ii];
+            r = v.x;
+            bg = v.y;
+            en = v.z;
+        }
+    };
+    auto load_mchunk = [&](int bg, int en, int* c) {  // this lane group's first MD chain entries
+        const int k0 = bg + grpL;
+        const int c0 = k0 < en ? ld_stream<FLAGS>(ci + k0) : 0;
+        c[0] = c0;
+#pragma unroll
+        for (int i = 1; i < MD; ++i) c[i] = (k0 + i * GL::GPW < en) ? ld_stream<FLAGS>(ci + k0 + i * GL::GPW) : c0;
+    };
+    {
+        // mu = 0: the row's own f is loaded one row ahead too (lane group 0)
+        auto load_mf = [&](int r, double* f) {
+#pragma unroll
+            for (int e = 0; e < GL::VEC; ++e) {
+                const int c = p0L + e;
+                f[e] = (MU0 && KT_XR_FPM && grpL == 0 && r >= 0 && c < nc) ? F[(int64_t)r * ld + c] : 0.0;
+            }
+        };
+        int mi = gw;
+        int row, beg, end, nrow, nbeg, nend;
+        load_mtask(mi, row, beg, end);
+        int mc[MD];
+        load_mchunk(beg, end, mc);
+        double mfc[GL::VEC];
+        load_mf(row, mfc);
+        load_mtask(mi + TW, nrow, nbeg, nend);
+        for (; mi < n_med; mi += TW) {
+            int nnrow, nnbeg, nnend;
+            load_mtask(mi + 2 * TW, nnrow, nnbeg, nnend);
+            int mn[MD];
+            load_mchunk(nbeg, nend, mn);
+            double mfn[GL::VEC];
+            load_mf(nrow, mfn);
+            using VL = VecT<GL::VEC>;
+            double s[GL::VEC];
+#pragma unroll
+            for (int e = 0; e < GL::VEC; ++e) s[e] = 0.0;
+            const int k0 = beg + grpL;
+            {
+                double a[(FLAGS & KF_UNIT) ? 1 : MD];
+                if constexpr (!(FLAGS & KF_UNIT)) {
+#pragma unroll
+                    for (int i = 0; i < MD; ++i)
+                        a[i] = (k0 + i * GL::GPW < end) ? ld_stream<FLAGS>(va + k0 + i * GL::GPW) : 0.0;
+                }
+                typename VL::T x[MD];
+#pragma unroll
+                for (int i = 0; i < MD; ++i) x[i] = VL::load(bin + (int64_t)mc[i] * ld + p0L);
+#pragma unroll
+                for (int i = 0; i < MD; ++i)
+#pragma unroll
+                    for (int e = 0; e < GL::VEC; ++e) {
+                        if constexpr (FLAGS & KF_UNIT)
+                            s[e] = (k0 + i * GL::GPW < end) ? s[e] + VL::get(x[i], e) : s[e];
+                        else s[e] = fma(a[i], VL::get(x[i], e), s[e]);
+                    }
+            }
+            // (rows longer than 16 MD: the rest of each chain, same order)
+            row_gather8<P, FLAGS, GL, MD>(k0 + MD * GL::GPW, end, GL::GPW, p0L, ci, va, bin, s, ld);
+#pragma unroll
+            for (int o = GL::LPR; o < 64; o <<= 1)
+#pragma unroll
+                for (int e = 0; e < GL::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
+            double sb = 0.0, sf = 0.0;
+            if (grpL == 0) {
+                double fo[GL::VEC], bo[GL::VEC];
+                if constexpr (MU0 && KT_XR_FPM) {
+#pragma unroll
+                    for (int e = 0; e < GL::VEC; ++e) fo[e] = mfc[e];
+                } else {
+                    expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
+                }
+                expmv_row_update<GL::VEC>(row, p0L, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+            }
+            fold(sb, sf, GL::LPR);
+#pragma unroll
+            for (int e = 0; e < GL::VEC; ++e) mfc[e] = mfn[e];
+            row = nrow;
+            beg = nbeg;
+            end = nend;
+            nrow = nnrow;
+            nbeg = nnbeg;
+            nend = nnend;
+#pragma unroll
+            for (int i = 0; i < MD; ++i) mc[i] = mn[i];
+        }
+    }
+    constexpr int SD = KT_XR_SD;  // short rows: gathers in flight per row group
+    // (3) short rows, in the task list's order (degree-descending, so the
+    //     GPW rows of a wave take the same number of gather rounds), GPW
+    //     tasks per wave, software-pipelined: while block b gathers, the
+    //     first SD column indices of block b + TW and the tasks of block
+    //     b + 2 TW are in flight
+#if KT_XR_TASKS
+    const int nblk = (n_short + G::GPW - 1) / G::GPW;
+    auto load_task = [&](int bb, int& r, int& bg, int& en) {
+        const int t = bb * G::GPW + grp;
+        r = -1;
+        bg = en = 0;
+        if (bb < nblk && t < n_short) {
+            const int4 v = short_tasks[t];
+            r = v.x;
+            bg = v.y;
+            en = v.z;
+        }
+    };
+#else  // natural row blocks from row_ptr (medium / long rows skipped)
+    const int nblk = (n + G::GPW - 1) / G::GPW;
+    auto load_task = [&](int bb, int& r, int& bg, int& en) {
+        const int t = bb * G::GPW + grp;
+        r = -1;
+        bg = en = 0;
+        if (bb < nblk && t < n) {
+            bg = ld_stream<FLAGS>(rp + t);
+            en = ld_stream<FLAGS>(rp + t + 1);
+            if (en - bg <= kMedThresh) r = t;
+            else en = bg;
+        }
+    };
+#endif
+    auto load_chunk = [&](int bg, int en, int* c) {  // a row's first SD columns (tail: its first)
+        const int c0 = bg < en ? ld_stream<FLAGS>(ci + bg) : 0;
+        c[0] = c0;
+#pragma unroll
+        for (int i = 1; i < SD; ++i) c[i] = (bg + i < en) ? ld_stream<FLAGS>(ci + bg + i) : c0;
+    };
+    // mu = 0: the rows' own f is loaded one block ahead too
+    auto load_f = [&](int r, double* f) {
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) {
+            const int c = p0 + e;
+            f[e] = (MU0 && KT_XR_FPS && r >= 0 && c < nc) ? F[(int64_t)r * ld + c] : 0.0;
+        }
+    };
+    int b = gw;
+    int row, beg, end, nrow, nbeg, nend;
+    load_task(b, row, beg, end);
+    int cc[SD];
+    load_chunk(beg, end, cc);
+    double fc[G::VEC];
+    load_f(row, fc);
+    load_task(b + TW, nrow, nbeg, nend);
+    for (; b < nblk; b += TW) {
+        int nnrow, nnbeg, nnend;
+        load_task(b + 2 * TW, nnrow, nnbeg, nnend);
+        int cn[SD];
+        load_chunk(nbeg, nend, cn);
+        double fn[G::VEC];
+        load_f(nrow, fn);
+        double sb = 0.0, sf = 0.0;
+        if (row >= 0) {
+            using VV = VecT<G::VEC>;
+            double s[G::VEC], fo[G::VEC], bo[G::VEC];
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
+            {   // first chunk (the prefetched columns), then the rest as row_gather8
+                // unit weights: fma(1, x, s) = s + x and fma(0, x, s) = s (a
+                // masked tail entry), so the weights are predicates, not registers
+                double a[(FLAGS & KF_UNIT) ? 1 : SD];
+                if constexpr (!(FLAGS & KF_UNIT)) {
+#pragma unroll
+                    for (int i = 0; i < SD; ++i) a[i] = (beg + i < end) ? ld_stream<FLAGS>(va + beg + i) : 0.0;
+                }
+                typename VV::T x[SD];
+#pragma unroll
+                for (int i = 0; i < SD; ++i) x[i] = VV::load(bin + (int64_t)cc[i] * ld + p0);
+#pragma unroll
+                for (int i = 0; i < SD; ++i)
+#pragma unroll
+                    for (int e = 0; e < G::VEC; ++e) {
+                        if constexpr (FLAGS & KF_UNIT) s[e] = (beg + i < end) ? s[e] + VV::get(x[i], e) : s[e];
+                        else s[e] = fma(a[i], VV::get(x[i], e), s[e]);
+                    }
+            }
+            row_gather8<P, FLAGS, G, SD>(beg + SD, end, 1, p0, ci, va, bin, s, ld);
+            if constexpr (MU0 && KT_XR_FPS) {
+#pragma unroll
+                for (int e = 0; e < G::VEC; ++e) fo[e] = fc[e];
+            } else {
+                expmv_row_prefetch<G::VEC>(row, p0, nc, ld, mu, bin, F, fo, bo);
+            }
+            expmv_row_update<G::VEC>(row, p0, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+        }
+        fold(sb, sf, G::LPR);
+#pragma unroll
+        for (int e = 0; e < G::VEC; ++e) fc[e] = fn[e];
+        row = nrow;
+        beg = nbeg;
+        end = nend;
+        nrow = nnrow;
+        nbeg = nnbeg;
+        nend = nnend;
+#pragma unroll
+        for (int i = 0; i < SD; ++i) cc[i] = cn[i];
+    }
+    // (4) this workgroup's maxima into slot blockIdx % 64 of set k % 3
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mb = fmax(mb, __shfl_xor(mb, o, 64));
+        mf = fmax(mf, __shfl_xor(mf, o, 64));
+    }
+    if (lane == 0) {
+        red[0][wave] = mb;
+        red[1][wave] = mf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double x = red[0][0], y = red[1][0];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) {
+            x = fmax(x, red[0][w]);
+            y = fmax(y, red[1][w]);
+        }
+        unsigned long long* slot = st->term_max[k % 3][blockIdx.x % kTermSlots];
+        __hip_atomic_fetch_max(slot, (unsigned long long)__double_as_longlong(x), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(slot + 1, (unsigned long long)__double_as_longlong(y), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // The check of term k (expmv.m:79-82) for the SPLIT term kernel, one wave:
 // c2 / nf = the maxima in the 64 slots of set k % 3, c1 = st->c1s[k & 1];
 // stop: active = 0 (and the host flag); else c1s[(k + 1) & 1] = c2.  Zeroes
@@ -2015,12 +2410,70 @@ hipError_t launch_expmv_slot_check(void* state, int k, double tol, hipStream_t s
     return hipGetLastError();
 }
 
+// form: 0 fused, 1 split (a workgroup per long row / 4 medium rows / 32 short
+// rows), 2 row-blocked split (k_expmv_rows, resident workgroups)
+static int expmv_rows_grid(int n_tasks_hint) {
+    static int per_cu = 0, cus = 0;
+    if (!per_cu) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        int occ = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_expmv_rows<16, KF_UNIT | KF_MU0>,
+                                                           64 * kExpmvRowsWaves, 0);
+        per_cu = occ > 0 ? occ : 2;
+        if (cus <= 0) cus = 256;
+    }
+    int g = per_cu * cus;
+    if (g > n_tasks_hint) g = n_tasks_hint;
+    return g < 1 ? 1 : g;
+}
+
 hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_rows, int n_med, int nc,
                              int ld, double mu, double coef, double tol, int k, const double* bin,
-                             double* bout, double* F, void* state, hipStream_t st, bool split, int* hflag,
+                             double* bout, double* F, void* state, hipStream_t st, int form, int* hflag,
                              int stage) {
-    const int grid = expmv_step_blocks(M.n, P, M.n_long, n_med);
     ExpmvState* s = static_cast<ExpmvState*>(state);
+    if (form == 2 && !(M.short_tasks && M.med_tasks)) form = 1;  // no task lists: the split kernel
+    if (form == 2) {
+        // KT_EXPMV_CLASSES (timing diagnostics only; the results are WRONG):
+        // bit mask of the row classes the term processes, 1 long, 2 medium, 4 short
+        static const int classes = [] {
+            const char* e = std::getenv("KT_EXPMV_CLASSES");
+            return e ? std::atoi(e) : 7;
+        }();
+        const int nl = (classes & 1) ? M.n_long : 0, nh = (classes & 1) ? M.n_heavy : 0, nm = (classes & 2) ? n_med : 0,
+                  ns = (classes & 4) ? M.n_short : 0;
+        // no more waves than tasks (long rows, medium rows, blocks of 8 short rows)
+        const int tasks = nl + nm + (ns + 7) / 8;
+        const int grid = expmv_rows_grid((tasks + kExpmvRowsWaves - 1) / kExpmvRowsWaves);
+#define KT_EXPMV_ROWS(PP, F_)                                                                      \
+    k_expmv_rows<PP, F_><<<grid, 64 * kExpmvRowsWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, nl, nh, \
+        reinterpret_cast<const int4*>(M.med_tasks), nm, reinterpret_cast<const int4*>(M.short_tasks), ns, \
+        nc, ld, mu, coef, k, bin, bout, F, s)
+#define KT_EXPMV_ROWS_P(PP)                                                                        \
+    if (mu == 0.0) {                                                                               \
+        if (unit) KT_EXPMV_ROWS(PP, KF_UNIT | KF_MU0);                                             \
+        else KT_EXPMV_ROWS(PP, KF_MU0);                                                            \
+    } else {                                                                                       \
+        if (unit) KT_EXPMV_ROWS(PP, KF_UNIT);                                                      \
+        else KT_EXPMV_ROWS(PP, 0);                                                                 \
+    }
+        switch (P) {
+        case 1: KT_EXPMV_ROWS_P(1) break;
+        case 2: KT_EXPMV_ROWS_P(2) break;
+        case 4: KT_EXPMV_ROWS_P(4) break;
+        case 8: KT_EXPMV_ROWS_P(8) break;
+        case 16: KT_EXPMV_ROWS_P(16) break;
+        case 32: KT_EXPMV_ROWS_P(32) break;
+        default: return hipErrorInvalidValue;
+        }
+#undef KT_EXPMV_ROWS_P
+#undef KT_EXPMV_ROWS
+        return hipGetLastError();
+    }
+    const bool split = form == 1;
+    const int grid = expmv_step_blocks(M.n, P, M.n_long, n_med);
 #define KT_EXPMV_LAUNCH(PP, F_, SP)                                                                \
     k_expmv_step<PP, F_, SP><<<grid, 64 * kExpmvWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, \
                                                                M.n_long, med_rows, n_med, nc, ld, mu, \

@@ -32,7 +32,16 @@ struct CsrView {
     const int* sp_rows;
     const int* sp_first;
     int n_split;
+    // natural CSR only: rows of degree <= kMedThresh as {row, beg, end, 0},
+    // degree-descending (the row-blocked expmv term; nullptr elsewhere)
+    const int* short_tasks = nullptr;
+    int n_short = 0;
+    // natural CSR only: the medium rows (med_rows) as {row, beg, end, 0}
+    const int* med_tasks = nullptr;
+    // the first n_heavy long rows have degree > kExpmvCoopThresh
+    int n_heavy = 0;
 };
+constexpr int kExpmvCoopThresh = 256;  // expmv terms: a long row this heavy takes a whole workgroup
 constexpr int kChunkNnz = 32;      // nonzeros per hub-row chunk
 constexpr int kSplitThresh = 64;   // rows longer than this are chunked (block SpMM)
 constexpr int kMedThresh = 16;     // expmv terms: rows longer than this get a wave (or a workgroup)
@@ -185,12 +194,14 @@ hipError_t launch_expmv_check(int n, const double* partial, double tol, void* st
 int expmv_step_blocks(int n, int P, int n_long, int n_med, int waves = 0);
 // the default form of launch_expmv_step for this shape (true: SPLIT, grids
 // above 1,024 workgroups); with split the host launches
-// launch_expmv_slot_check after every term but a stage's last
+// launch_expmv_slot_check after every term but a stage's last.
+// launch_expmv_step form: 0 fused, 1 split (a workgroup per row class unit),
+// 2 split, row-blocked (k_expmv_rows: resident workgroups; the default split form)
 bool expmv_split_check(int n, int P, int n_long, int n_med);
 hipError_t launch_expmv_slot_check(void* state, int k, double tol, hipStream_t st, int* hflag, int stage);
 hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_rows, int n_med, int nc,
                              int ld, double mu, double coef,
                              double tol, int k, const double* bin, double* bout, double* F,
-                             void* state, hipStream_t st, bool split, int* hflag = nullptr, int stage = 0);
+                             void* state, hipStream_t st, int form, int* hflag = nullptr, int stage = 0);
 
 }  // namespace kt

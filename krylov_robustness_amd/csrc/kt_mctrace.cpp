@@ -320,16 +320,23 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
     if (P <= 32 && ld >= P && !std::getenv("KT_EXPMV_UNFUSED")) {
         // One launch per term (k_expmv_step: the previous term's stop test,
         // SpMM, update, the term's norm maxima); b ping-pongs, the maxima
-        // rotate through three slots of the state.  Natural row order: a
-        // row's gathers sum in the order of the reference's A*b (the
-        // hubs-first CSR ran 7 % faster at config 4 but moved one stage's
-        // stop by a term, profiles/r04/expmv_c4/variants.json).
-        const DevCSR& M = natural_csr(A);
-        const CsrView V{M.rowptr, M.col, M.val, (int)n, M.long_rows, M.n_long, A->long_thresh,
-                        kSplitThresh, M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split};
+        // rotate through three slots of the state.  Every row sums its
+        // gathers in the order of the reference's A*b (natural CSR order).
+        const DevCSR& M0 = natural_csr(A);
         // KT_EXPMV_SPLIT=0 / 1 forces the fused / split term form (read per call)
         const char* spe = std::getenv("KT_EXPMV_SPLIT");
-        const bool split = spe ? spe[0] == '1' : expmv_split_check((int)n, P, M.n_long, M.n_med);
+        const bool split = spe ? spe[0] == '1' : expmv_split_check((int)n, P, M0.n_long, M0.n_med);
+        // the split form runs row-blocked (k_expmv_rows, resident workgroups);
+        // KT_EXPMV_ROWS=0 selects the workgroup-per-row-class split kernel (A/B)
+        const char* rwe = std::getenv("KT_EXPMV_ROWS");
+        const int form = !split ? 0 : (rwe && rwe[0] == '0') ? 1 : 2;
+        // (Measured and dropped, round 6: the Taylor loop on hubs-first copies
+        // of b and f with each row in natural column order -- bit-identical --
+        // ran 16 % slower than the natural table, profiles/r06/expmv_rows_ab.)
+        const DevCSR& M = M0;
+        const CsrView V{M.rowptr, M.col, M.val, (int)n, M.long_rows, M.n_long, A->long_thresh,
+                        kSplitThresh, M.ck_beg, M.ck_end, M.n_chunks, M.sp_rows, M.sp_first, M.n_split,
+                        M.short_tasks, M.n_short, M.med_tasks, M.n_heavy};
         // The launch that finds a stage's stop test satisfied also stores the
         // stage index into a coherent host flag; the host, which queues terms
         // only slightly ahead of the device here, stops queueing that stage's
@@ -368,7 +375,7 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
                 if (ahead && queued >= ahead) KT_HIP(hipEventSynchronize(ring[queued % ahead]));
                 if (use_flag && k > 2 && __atomic_load_n(ctx->ws.expmv_stop.host, __ATOMIC_ACQUIRE) >= i) break;
                 KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu,
-                                         t / ((double)r.s * k), tol, k, cur, nxt, F, state, st, split, hflag, i));
+                                         t / ((double)r.s * k), tol, k, cur, nxt, F, state, st, form, hflag, i));
                 if (split && k < r.m) KT_HIP(launch_expmv_slot_check(state, k, tol, st, hflag, i));
                 if (ahead) KT_HIP(hipEventRecord(ring[queued % ahead], st));
                 ++queued;

@@ -1,17 +1,66 @@
 // kt_pool.h -- persistent host worker pool for small per-column / per-
 // candidate dense work between device steps (the greedy host-eig path,
 // the Frechet entries of hessianfcn); spawning threads every Krylov step
-// would cost more than the work.  Sized min(16, cores).
+// would cost more than the work.  Sized by host_pool_threads().
 #pragma once
+#include <sched.h>
+
+#include <algorithm>
 #include <atomic>
+#include <cmath>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <functional>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
 namespace kt {
+
+// CPUs this process may use: the affinity mask capped by the cgroup CPU
+// quota (v2 cpu.max, v1 cfs_quota_us / cfs_period_us), as bench.py cpu_share
+inline int process_cpus() {
+    int aff = 0;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) aff = CPU_COUNT(&set);
+    if (aff <= 0) aff = (int)std::max(1u, std::thread::hardware_concurrency());
+    double quota = -1.0;
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long per = 100000;
+        if (std::fscanf(f, "%31s %ld", q, &per) >= 1 && std::string(q) != "max" && per > 0)
+            quota = std::atof(q) / (double)per;
+        std::fclose(f);
+    } else if (FILE* g = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+        long q = -1, per = 100000;
+        if (std::fscanf(g, "%ld", &q) == 1 && q > 0) {
+            if (FILE* h = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+                if (std::fscanf(h, "%ld", &per) != 1 || per <= 0) per = 100000;
+                std::fclose(h);
+            }
+            quota = (double)q / (double)per;
+        }
+        std::fclose(g);
+    }
+    if (quota > 0.0) aff = std::max(1, std::min(aff, (int)std::floor(quota + 1e-9)));
+    return aff;
+}
+
+// The pool's threads (caller included): min(16, process_cpus() /
+// LOCAL_WORLD_SIZE), >= 1 -- torchrun's ranks on one node share its CPUs;
+// KT_HOST_THREADS overrides
+inline int host_pool_threads() {
+    if (const char* e = std::getenv("KT_HOST_THREADS")) {
+        const int v = std::atoi(e);
+        if (v > 0) return std::min(v, 256);
+    }
+    int lws = 1;
+    if (const char* e = std::getenv("LOCAL_WORLD_SIZE")) lws = std::max(1, std::atoi(e));
+    return std::max(1, std::min(16, process_cpus() / lws));
+}
 
 class HostPool {
    public:
@@ -43,6 +92,7 @@ class HostPool {
         done_cv_.wait(lk, [&] { return pending_ == 0; });
         job_ = nullptr;
     }
+    int threads() const { return (int)workers_.size() + 1; }
     ~HostPool() {
         {
             std::lock_guard<std::mutex> lk(m_);
@@ -55,7 +105,7 @@ class HostPool {
 
    private:
     HostPool() {
-        int nt = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) - 1;
+        const int nt = host_pool_threads() - 1;
         for (int t = 0; t < nt; ++t) workers_.emplace_back([this] { loop(); });
     }
     void drain(const std::function<void(int)>& f, int count) {

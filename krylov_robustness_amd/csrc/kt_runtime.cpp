@@ -11,6 +11,7 @@
 
 #include "kt_internal.h"
 #include "kt_launch.h"
+#include "kt_pool.h"
 
 namespace kt {
 
@@ -127,16 +128,17 @@ void DevCSR::release() {
     if (blob) (void)hipFree(blob);
     blob = nullptr;
     blob_bytes = 0;
-    rowptr = col = long_rows = perm = med_rows = nullptr;
+    rowptr = col = long_rows = perm = med_rows = short_tasks = med_tasks = nullptr;
     ck_beg = ck_end = sp_rows = sp_first = nullptr;
     val = nullptr;
-    n_long = n_med = n_chunks = n_split = 0;
+    n_long = n_heavy = n_med = n_short = n_chunks = n_split = 0;
     built = false;
 }
 
 void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out, bool sync) {
     const int64_t n = A->n, nnz = A->nnz;
     const bool ident = new2old.empty();
+    const bool tasks = ident;  // the expmv term's task lists: natural order only
     auto orig = [&](int64_t r) -> int64_t { return ident ? r : new2old[r]; };
     std::vector<int32_t> rp32(n + 1), c32(std::max<int64_t>(nnz, 1));
     std::vector<double> v64(std::max<int64_t>(nnz, 1));
@@ -179,6 +181,47 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out,
         const int32_t d = rp32[r + 1] - rp32[r];
         if (d > kMedThresh && d <= A->long_thresh) mr.push_back((int32_t)r);
     }
+    // short-row task list of the row-blocked expmv term (natural order only):
+    // rows of degree <= kMedThresh (and not long) as {row, beg, end, 0},
+    // counting-sorted by degree (descending; rows in order within a degree)
+    // inside each window of consecutive rows
+    std::vector<int32_t> st4;
+    if (tasks) {
+        const int dmax = std::min(kMedThresh, A->long_thresh);
+        // sorted within windows of 4,096 consecutive rows: a wave's rows take
+        // the same number of gather rounds while the F / b rows a launch
+        // touches at one time stay as local as in natural order (config-4
+        // expmv trace_exp, same box: natural 1,453 ms, whole-matrix sort
+        // 1,432, windows of 4,096 1,401; profiles/r06/expmv_rows_ab).
+        // KT_EXPMV_SORTWIN (A/B) sets the window (0: the whole matrix).
+        const char* sw = std::getenv("KT_EXPMV_SORTWIN");
+        const int64_t win = sw ? std::max<int64_t>(0, std::atoll(sw)) : 4096;
+        const int64_t W = win > 0 ? win : n;
+        std::vector<int64_t> cnt(dmax + 2);
+        size_t ns = 0;
+        for (int64_t r = 0; r < n; ++r) ns += (rp32[r + 1] - rp32[r] <= dmax);
+        st4.assign(4 * ns, 0);
+        int64_t t0 = 0;
+        for (int64_t w0 = 0; w0 < n; w0 += W) {
+            const int64_t w1 = std::min(n, w0 + W);
+            std::fill(cnt.begin(), cnt.end(), 0);
+            for (int64_t r = w0; r < w1; ++r) {
+                const int32_t d = rp32[r + 1] - rp32[r];
+                if (d <= dmax) cnt[dmax - d + 1]++;
+            }
+            cnt[0] = t0;
+            for (int i = 1; i <= dmax + 1; ++i) cnt[i] += cnt[i - 1];
+            t0 = cnt[dmax + 1];
+            for (int64_t r = w0; r < w1; ++r) {
+                const int32_t d = rp32[r + 1] - rp32[r];
+                if (d > dmax) continue;
+                const int64_t t = cnt[dmax - d]++;
+                st4[4 * t] = (int32_t)r;
+                st4[4 * t + 1] = rp32[r];
+                st4[4 * t + 2] = rp32[r + 1];
+            }
+        }
+    }
     // hub-row chunk table (block SpMM)
     std::vector<int32_t> ckb, cke, spr, spf(1, 0);
     for (int32_t r : lr) {  // heaviest first
@@ -209,6 +252,17 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out,
     add(out.val, v64.data(), sizeof(double) * v64.size());
     add(out.long_rows, lr.data(), sizeof(int) * lr.size());
     add(out.med_rows, mr.data(), sizeof(int) * mr.size());
+    add(out.short_tasks, st4.data(), sizeof(int) * st4.size());
+    std::vector<int32_t> mt4;
+    if (tasks) {
+        mt4.assign(4 * mr.size(), 0);
+        for (size_t i = 0; i < mr.size(); ++i) {
+            mt4[4 * i] = mr[i];
+            mt4[4 * i + 1] = rp32[mr[i]];
+            mt4[4 * i + 2] = rp32[mr[i] + 1];
+        }
+    }
+    add(out.med_tasks, mt4.data(), sizeof(int) * mt4.size());
     if (!spr.empty()) {
         add(out.ck_beg, ckb.data(), sizeof(int) * ckb.size());
         add(out.ck_end, cke.data(), sizeof(int) * cke.size());
@@ -237,6 +291,7 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out,
         size_t off = 0;
         out.ck_beg = out.ck_end = out.sp_rows = out.sp_first = nullptr;
         out.perm = nullptr;
+        out.short_tasks = out.med_tasks = nullptr;
         for (const Seg& g : segs) {
             if (g.bytes) std::memcpy(h + off, g.src, g.bytes);
             *g.dst = out.blob + off;
@@ -248,7 +303,12 @@ void build_csr(kt_matrix_s* A, const std::vector<int32_t>& new2old, DevCSR& out,
         // staging buffer is not rewritten before the next build's sync above)
         if (sync) KT_HIP(hipStreamSynchronize(A->ctx->stream));
         out.n_long = (int)lr.size();
+        out.n_heavy = 0;
+        while (out.n_heavy < out.n_long &&
+               rp32[lr[out.n_heavy] + 1] - rp32[lr[out.n_heavy]] > kExpmvCoopThresh) ++out.n_heavy;
         out.n_med = (int)mr.size();
+        out.n_short = (int)(st4.size() / 4);
+        if (!tasks) out.short_tasks = out.med_tasks = nullptr;
         out.n_split = (int)spr.size();
         out.n_chunks = (int)ckb.size();
     } catch (...) {
@@ -532,6 +592,8 @@ int kt_context_stat(kt_context_t ctx, int stat, int64_t* value) {
     *value = v[stat];
     KT_GUARD_END
 }
+
+int kt_host_threads(void) { return kt::HostPool::get().threads(); }
 
 int kt_profile_reset(kt_context_t ctx) {
     KT_GUARD_BEGIN

@@ -659,13 +659,16 @@ static void slq_collect(kt_matrix_s* A, int ticket, double* sum_q, double* sum_q
         fail(KT_ERR_ARG, "kt_slq_collect: tickets must be collected once each, in submission order");
     SlqPending& pd = w.slq_pend[w.slq_collected & 1];
     const uint64_t slot = w.slq_collected & 1;
+    // the record's n, CSR (guard redo) and lanes belong to the submitting
+    // matrix: a call with another matrix is refused BEFORE the ticket is
+    // consumed, so the caller can collect it with the right one; a ticket
+    // whose matrix was destroyed (its sweeps drained) is consumed
+    if (pd.live && pd.A && pd.A != A)
+        fail(KT_ERR_ARG, "kt_slq_collect: the ticket was submitted with another matrix");
     ++w.slq_collected;
     if (!pd.live) fail(KT_ERR_ARG, "kt_slq_collect: the submission failed");
     pd.live = false;
-    // the record's n, CSR (guard redo) and lanes belong to the submitting matrix
-    if (pd.A != A)
-        fail(KT_ERR_ARG, pd.A ? "kt_slq_collect: the ticket was submitted with another matrix"
-                              : "kt_slq_collect: the submitting matrix was destroyed");
+    if (pd.A != A) fail(KT_ERR_ARG, "kt_slq_collect: the submitting matrix was destroyed");
     if (sum_q) *sum_q = 0.0;
     if (sum_q2) *sum_q2 = 0.0;
     if (pd.nprobes == 0) return;

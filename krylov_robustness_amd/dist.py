@@ -1,9 +1,11 @@
 """Multi-GPU plumbing: probes shard across ranks (one process per GPU), one
-all-reduce of the partial sums.
+collective per evaluation.
 
 The probe RNG is keyed by the GLOBAL probe index, so the estimate does not
-depend on the number of ranks; the only collective is a 2-double sum
-(sum q, sum q^2) over RCCL ("nccl" backend) or gloo on CPU.
+depend on the number of ranks; the only collective of a Hutchinson
+evaluation is one all-gather of each rank's (count, sum, centred second
+moment) -- 24 bytes per rank -- over RCCL ("nccl" backend) or gloo on CPU,
+combined on every rank in rank order (moment_sums).
 """
 from __future__ import annotations
 
@@ -104,11 +106,10 @@ def ordered_sums(q):
 
 
 def centred_sums(q, nprobes, device=None, force=False):
-    """Hutchinson reduction over the ranks' probe shards: sum q by one
-    all-reduce, then every rank centres its forms on the global mean and a
-    second all-reduce sums (q - mean)^2.  Returns (sum q, sum (q - mean)^2);
-    the result differs from the single-process value only by the order the
-    shards' partial sums are added (rounding, not cancellation)."""
+    """Hutchinson reduction in two all-reduces (rounds 1-5; kept for
+    comparison): sum q, then every rank centres its forms on the global mean
+    and a second all-reduce sums (q - mean)^2.  Returns (sum q, sum (q -
+    mean)^2).  bench.py uses moment_sums (one collective)."""
     s_loc = 0.0
     for v in q:
         s_loc += float(v)
@@ -118,6 +119,75 @@ def centred_sums(q, nprobes, device=None, force=False):
     for v in q:
         m2_loc += (float(v) - mu) * (float(v) - mu)
     return s1, allreduce_sums([m2_loc], device=device, force=force)[0]
+
+
+def local_moments(q):
+    """(count, sum q, sum (q - local mean)^2) of one rank's forms, in index
+    order (ordered_sums' two passes)."""
+    s, m2 = ordered_sums(q)
+    return float(len(q)), s, m2
+
+
+def chan_combine(parts):
+    """Combine per-rank (count, sum, M2) triples in the order given (rank
+    order) with the pairwise update of Chan, Golub & LeVeque (1979):
+    M2_ab = M2_a + M2_b + delta^2 n_a n_b / (n_a + n_b), delta = mean_b -
+    mean_a; the sums are added in the same order.  Returns (sum q, M2) --
+    the same quantities as ordered_sums over the concatenated forms, equal
+    to rounding (bit-equal for a single part)."""
+    n, s, m2 = 0.0, 0.0, 0.0
+    for nb, sb, m2b in parts:
+        nb, sb, m2b = float(nb), float(sb), float(m2b)
+        if nb <= 0:
+            continue
+        if n <= 0:
+            n, s, m2 = nb, sb, m2b
+            continue
+        delta = sb / nb - s / n
+        tot = n + nb
+        m2 = m2 + m2b + delta * delta * (n * nb / tot)
+        s = s + sb
+        n = tot
+    return s, m2
+
+
+def moment_sums(q, device=None, force=False, stats=None):
+    """Hutchinson reduction over the ranks' probe shards with ONE collective:
+    every rank forms (count, sum, M2) of its own forms (local_moments),
+    all-gathers the triples (24 bytes per rank) and combines them in rank
+    order (chan_combine), so every rank holds the same (sum q, sum (q -
+    mean)^2).  Without a process group (or at world 1 without `force`) no
+    collective runs and the local triple is the answer.  `stats` (a dict)
+    collects the collective's calls and host-side microseconds."""
+    import time
+    trip = local_moments(q)
+    if not _group_ready(force):
+        return trip[1], trip[2]
+    import torch
+    import torch.distributed as dist
+    t0 = time.perf_counter()
+    world = dist.get_world_size()
+    t = torch.tensor(list(trip), dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    rows = torch.stack(parts).cpu().tolist()
+    if stats is not None:
+        stats["calls"] = stats.get("calls", 0) + 1
+        stats.setdefault("us", []).append((time.perf_counter() - t0) * 1e6)
+    return chan_combine(rows)
+
+
+def allgather_floats(vals, device=None):
+    """Every rank's list of floats (same length), in rank order; the local
+    list alone without a process group."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return [[float(v) for v in vals]]
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return torch.stack(parts).cpu().tolist()
 
 
 def bitstable_sums(q, counts, group=None):

@@ -126,3 +126,30 @@ def test_every_entry_point_rejects_null_handles():
         st = getattr(lib, name)(*vals)
         assert st != _lib.KT_OK, name
         assert lib.kt_last_error(), name
+
+
+def _host_threads_in_child(env):
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from krylov_robustness_amd import _lib; "
+            "print(_lib.load().kt_host_threads())" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return int(r.stdout.strip().splitlines()[-1])
+
+
+def test_host_pool_sized_from_cpu_share_and_local_world():
+    """kt_host_threads: min(16, affinity capped by the cgroup quota /
+    LOCAL_WORLD_SIZE), >= 1 -- each of torchrun's ranks on a node takes its
+    share of the CPUs instead of hardware_concurrency(); KT_HOST_THREADS
+    overrides.  (Host-only: no GPU needed.)"""
+    import os
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    cpus = bench.cpu_share()[0]
+    base = {k: v for k, v in os.environ.items() if k not in ("KT_HOST_THREADS", "LOCAL_WORLD_SIZE")}
+    for lws in (1, 2, 8):
+        got = _host_threads_in_child(dict(base, LOCAL_WORLD_SIZE=str(lws)))
+        assert got == max(1, min(16, cpus // lws))
+    assert _host_threads_in_child(dict(base, KT_HOST_THREADS="3", LOCAL_WORLD_SIZE="8")) == 3

@@ -223,7 +223,7 @@ def _bitstable_worker(rank, world, port, out):
     in global probe order."""
     import torch.distributed as dist
     from oracle import slq_ref
-    from krylov_robustness_amd.dist import bitstable_sums, centred_sums
+    from krylov_robustness_amd.dist import bitstable_sums, centred_sums, moment_sums
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -232,7 +232,9 @@ def _bitstable_worker(rank, world, port, out):
     counts = [probe_shard(N, r, world)[1] for r in range(world)]
     off, cnt = probe_shard(N, rank, world)
     _, q = slq_ref.slq_trace(A, cnt, 15, seed=3, probe_offset=off, nthreads=1)
-    out.put((rank, (bitstable_sums(q[:cnt], counts), centred_sums(q[:cnt], N))))
+    stats = {}
+    ms = moment_sums(q[:cnt], stats=stats)
+    out.put((rank, (bitstable_sums(q[:cnt], counts), centred_sums(q[:cnt], N), ms, stats["calls"])))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -241,7 +243,10 @@ def _bitstable_worker(rank, world, port, out):
 def test_gloo_bitstable_sums_identical_across_world_sizes(world):
     """Bit-identical (==, not approx) estimate on every rank and equal to the
     single-process ordered sum of the same forms (SURVEY.md §8e option); the
-    default two-all-reduce centred form agrees to rounding."""
+    default one-collective form (moment_sums: all-gather of (count, sum, M2),
+    Chan's pairwise combination in rank order; ONE collective per
+    evaluation) and the two-all-reduce centred form agree to rounding, and
+    every rank's moment_sums result is the same bits."""
     import torch.multiprocessing as mp
     from oracle import slq_ref
     from krylov_robustness_amd.dist import bitstable_sums, ordered_sums
@@ -261,6 +266,11 @@ def test_gloo_bitstable_sums_identical_across_world_sizes(world):
     assert single == ordered_sums(q1)
     for r in range(world):
         assert got[r][0] == single
-        # the all-reduce form (bench.py default): the same to rounding
+        # the two-all-reduce form: the same to rounding
         assert got[r][1][0] == pytest.approx(single[0], rel=1e-14)
         assert got[r][1][1] == pytest.approx(single[1], rel=1e-12)
+        # bench.py's default: one all-gather, Chan's combination
+        assert got[r][3] == 1
+        assert got[r][2] == got[0][2]
+        assert got[r][2][0] == pytest.approx(single[0], rel=1e-14)
+        assert got[r][2][1] == pytest.approx(single[1], rel=1e-12)

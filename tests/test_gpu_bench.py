@@ -67,6 +67,7 @@ def test_bench_single_process_line():
     assert cpu["affinity_cpus"] >= cpu["cores"]
     assert d["yform_redone_sweeps"] == 0
     assert d["collective"] is None  # single process, no torchrun: no process group
+    assert roof["busy_within_timed_region"] is True
 
 
 def _single_line(*extra):
@@ -88,8 +89,13 @@ def _ranks_line(world, port, *extra):
     lines = _json_lines(r.stdout)
     assert len(lines) == 1  # rank 0 only
     d = lines[0]
-    assert d["n_gpus"] == world and d["config"]["parallelism"] == f"probes sharded x{world}"
+    # a one-device rehearsal counts one GPU; the ranks are the process group's
+    assert d["n_gpus"] == 1 and d["launch"]["process_group_world_size"] == world
+    assert d["launch"]["one_device_rehearsal"] is True
+    assert d["config"]["parallelism"] == f"probes sharded x{world}"
     assert d["cpu_baseline"] is None and d["value"] > 0
+    assert d["per_rank_timed_ms"]["ranks"] == world
+    assert d["per_rank_timed_ms"]["min"] <= d["per_rank_timed_ms"]["max"]
     return d
 
 
@@ -100,7 +106,10 @@ def test_bench_two_ranks_one_gpu_gloo():
     over the ranks; S, Q replicated)."""
     d1 = _single_line("--mc-steps", "1")
     d = _ranks_line(2, 29531, "--mc-steps", "1")
-    assert d["collective"].startswith("gloo all_reduce")
+    # one collective per evaluation (all-gather of count, sum, M2; Chan's combination)
+    c = d["collective"]
+    assert c["backend"] == "gloo" and c["op"].startswith("all_gather of each rank's")
+    assert c["calls_per_eval"] == 1 and c["us_per_call_mean"] > 0
     assert d["trace_estimate"] == pytest.approx(d1["trace_estimate"], rel=1e-12)
     assert d["trace_stderr"] == pytest.approx(d1["trace_stderr"], rel=1e-12)
     for a, b in zip(d["evaluations"]["estimates"], d1["evaluations"]["estimates"]):
@@ -123,7 +132,7 @@ def test_bench_bitstable_identical_over_1_2_4_ranks():
     d1 = _single_line("--mc-steps", "0", "--bitstable")
     d2 = _ranks_line(2, 29539, "--mc-steps", "0", "--bitstable")
     d4 = _ranks_line(4, 29541, "--mc-steps", "0", "--bitstable")
-    assert d2["collective"].startswith("gloo all_gather")
+    assert d2["collective"]["op"].startswith("all_gather of the per-probe forms")
     for d in (d2, d4):
         assert d["trace_estimate"] == d1["trace_estimate"]
         assert d["trace_stderr"] == d1["trace_stderr"]
@@ -136,7 +145,7 @@ def test_bench_bitstable_identical_over_1_2_4_ranks():
 def test_bench_world1_torchrun_rccl():
     """torchrun with ONE rank and the nccl (RCCL) backend: the process group is
     initialised (device_id bound before any library call) and the per-evaluation
-    all-reduce of (sum q, sum q^2) and the max-over-ranks time run through RCCL
+    all-gather of (count, sum q, M2) and the max-over-ranks time run through RCCL
     at world 1 -- RCCL init coexisting with libkrylov_hip.so's streams, the
     launch the driver uses at N > 1 minus the peers."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
@@ -148,7 +157,8 @@ def test_bench_world1_torchrun_rccl():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
     d = lines[0]
-    assert d["n_gpus"] == 1 and d["collective"].startswith("RCCL all_reduce")
+    assert d["n_gpus"] == 1 and d["collective"]["backend"] == "RCCL"
+    assert d["collective"]["calls_per_eval"] == 1
     assert d["value"] > 0 and d["roofline"]["avg_launch_us"] > 0
     # same probes, same estimate as the single-process line (the collective is a sum of one)
     d1 = _single_line()
@@ -175,9 +185,10 @@ def test_mc_trace_sharded_rccl_world1():
 def test_bench_gpus2_self_launches_two_ranks():
     """`python3 bench.py --gpus 2` with no torchrun environment (the way the
     driver may invoke it) starts the two ranks itself as a torchrun child
-    process: the line reports n_gpus 2 from the process group's own world
-    size, and the estimate equals the single-process line's to rounding.
-    Rehearsed on one card: both ranks share GPU 0 over gloo."""
+    process: the process group's world size is 2 (n_gpus counts distinct
+    devices: 1 in this one-card rehearsal), and the estimate equals the
+    single-process line's to rounding.  Rehearsed on one card: both ranks
+    share GPU 0 over gloo."""
     d1 = _single_line("--mc-steps", "0")
     env = dict(os.environ, KT_BENCH_ONE_DEVICE="1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID"):
@@ -189,7 +200,7 @@ def test_bench_gpus2_self_launches_two_ranks():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1  # rank 0's line, relayed
     d = lines[0]
-    assert d["n_gpus"] == 2 and d["launch"]["process_group_world_size"] == 2
+    assert d["n_gpus"] == 1 and d["launch"]["process_group_world_size"] == 2
     assert d["launch"]["launcher"] == "torchrun" and d["config"]["parallelism"] == "probes sharded x2"
     assert d["trace_estimate"] == pytest.approx(d1["trace_estimate"], rel=1e-12)
     assert d["trace_stderr"] == pytest.approx(d1["trace_stderr"], rel=1e-12)

@@ -50,25 +50,58 @@ def test_expmv_wide_block_and_unfused_form(kra, gpu_ctx, monkeypatch):
     np.testing.assert_allclose(Fu, Ff, rtol=1e-13, atol=1e-15 * np.abs(Ff).max())
 
 
-@pytest.mark.parametrize("graph", ["oregon_A6", "er100k"])
-def test_expmv_split_check_form(kra, gpu_ctx, monkeypatch, graph):
-    """Grids above 1,024 workgroups run the SPLIT term kernel (the stop test
-    in its own one-wave launch after each term, a stopped term returning
-    before its gathers) instead of the fused one.  On ER n = 100k (3,125
-    workgroups at 10 columns, split by default) and on oregon_A6 (340, fused
-    by default) both forms (KT_EXPMV_SPLIT=0 / 1) give the same F, s, m, mv
-    bit for bit, and agree with the oracle; the first column alone (P = 1:
-    391 / 43 workgroups) too."""
+def _expmv_graph(graph):
     from krylov_robustness_amd import graphs
-    A = graphs.erdos_renyi(100_000, 500_000, seed=0) if graph == "er100k" else load_graph(graph)
-    D = kra.DeviceMatrix(A, gpu_ctx)
+    if graph == "er100k":
+        return graphs.erdos_renyi(100_000, 500_000, seed=0)
+    if graph.startswith("chunglu200k"):
+        # scale-free: 17-64-degree rows (one wave each in the split forms) and
+        # rows of degree > 64 (a workgroup each in the split kernel, four
+        # chain sets of one wave in the row-blocked one); "_w": fp64 weights
+        A = graphs.chung_lu(200_000, 2_000_000, gamma=2.5, seed=3)
+        if graph.endswith("_w"):
+            import scipy.sparse as sp
+            U = sp.triu(A, 1).tocoo()
+            w = np.random.default_rng(4).uniform(0.5, 1.5, size=U.nnz)
+            W = sp.coo_matrix((w, (U.row, U.col)), shape=A.shape)
+            A = (W + W.T).tocsr()
+            A.sort_indices()
+        return A
+    return load_graph(graph)
+
+
+@pytest.mark.parametrize("graph", ["oregon_A6", "er100k", "chunglu200k", "chunglu200k_w"])
+def test_expmv_split_check_form(kra, gpu_ctx, monkeypatch, graph):
+    """Grids above 1,024 workgroups run the SPLIT term (the stop test in its
+    own one-wave launch after each term, a stopped term returning before its
+    gathers) instead of the fused one; the split term runs row-blocked
+    (k_expmv_rows, resident workgroups, round 6) unless KT_EXPMV_ROWS=0
+    selects the workgroup-per-row-class split kernel; KT_EXPMV_SORTWIN sets
+    the short-row order (a row-build option: the matrix is rebuilt per
+    form below).  On oregon_A6 (340 workgroups, fused by default), ER
+    n = 100k (3,125, split) and Chung-Lu n = 200k (medium and long rows; unit
+    and fp64 weights) all four forms give the same F, s, m, mv bit for bit,
+    and agree with the oracle; the first column alone (P = 1) too."""
+    A = _expmv_graph(graph)
     b = np.random.default_rng(7).normal(size=(A.shape[0], 10))
+    # (KT_EXPMV_SPLIT, KT_EXPMV_ROWS, KT_EXPMV_SORTWIN): fused; split;
+    # row-blocked (short rows degree-sorted in windows of 4,096 rows, the
+    # default); row-blocked with the whole matrix's short rows degree-sorted
+    forms = (("0", None, None), ("1", "0", None), ("1", None, None), ("1", None, "0"))
+    keys = ("KT_EXPMV_SPLIT", "KT_EXPMV_ROWS", "KT_EXPMV_SORTWIN")
     for B in (b, b[:, :1]):
         outs = []
-        for v in ("0", "1"):
-            monkeypatch.setenv("KT_EXPMV_SPLIT", v)
-            outs.append(kra.expmv(1.0, D, B, ctx=gpu_ctx))
-        monkeypatch.delenv("KT_EXPMV_SPLIT")
+        for f in forms:
+            for k, v in zip(keys, f):
+                if v is None:
+                    monkeypatch.delenv(k, raising=False)
+                else:
+                    monkeypatch.setenv(k, v)
+            Df = kra.DeviceMatrix(A, gpu_ctx)  # the natural CSR (and its task lists) built under f
+            outs.append(kra.expmv(1.0, Df, B, ctx=gpu_ctx))
+            Df.close()
+        for k in keys:
+            monkeypatch.delenv(k, raising=False)
         for o in outs[1:]:
             assert tuple(outs[0][1:]) == tuple(o[1:])
             assert np.array_equal(outs[0][0], o[0])

@@ -87,7 +87,8 @@ def test_pipelined_union_counts_overlap_once(kra, monkeypatch):
 def test_destroyed_matrix_ticket_fails_cleanly(kra):
     """kt_matrix_destroy drains every lane before releasing the CSR; a ticket
     of the destroyed matrix then fails to collect instead of reading it, and
-    a ticket collected with another matrix is refused."""
+    a ticket collected with another matrix is refused without being consumed
+    (collected with its own matrix afterwards, it gives the sweeps' forms)."""
     from krylov_robustness_amd import _lib, graphs
     A = graphs.chung_lu(50_000, 500_000, seed=1)
     ctx = kra.Context(0)
@@ -96,6 +97,8 @@ def test_destroyed_matrix_ticket_fails_cleanly(kra):
     p = kra.slq_submit(D1, 32, 20, seed=1, block=16, ctx=ctx)
     with pytest.raises(_lib.KrylovError, match="another matrix"):
         _lib.check(_lib.load().kt_slq_collect(D2.handle, p[1], None, None, None))
+    q1 = kra.slq_collect(p)[2]  # the right matrix: still collectable
+    assert np.array_equal(q1, kra.slq_quadforms(D1, 32, 20, seed=1, block=16, ctx=ctx)[2])
     p = kra.slq_submit(D1, 32, 20, seed=1, block=16, ctx=ctx)
     D1.close()
     with pytest.raises(_lib.KrylovError, match="destroyed"):

@@ -90,6 +90,29 @@ pmc)
     ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$R" -d $O/pmc_hit -o h --output-format csv -- python3 $B > $O/pmc_hit.log 2>&1 ) || { tail -20 $O/pmc_hit.log; exit 1; }
     python3 tools/pmc_traffic.py $(find $O/pmc_fetch -name "*counter_collection.csv") $(find $O/pmc_write -name "*counter_collection.csv") $O/traffic.json $SEC \
         $(find $O/pmc_hit -name "*counter_collection.csv") || exit 1 ;;
+expmv)
+    # the reference composition at config 4 (tools/expmv_c4.py): kernel trace
+    # of the default term kernel and of the KT_EXPMV_ROWS=0 split kernel
+    # (per-term statistics, tools/expmv_terms.py), then FETCH / WRITE / hit
+    # passes of the default term kernel (tools/pmc_traffic.py, section expmv_c4)
+    for v in rows split; do
+        E=""; [ $v = split ] && E="KT_EXPMV_ROWS=0"
+        ( cd /tmp && env $E timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tr_$v -o c4 \
+            -- python3 $GRAFT_REPO_ROOT/tools/expmv_c4.py 1 > $O/c4_$v.jsonl 2> $O/c4_$v.err ) || { tail -20 $O/c4_$v.err; exit 1; }
+        cp $(find $O/tr_$v -name "*kernel_stats.csv") $O/kernel_stats_$v.csv
+        python3 tools/expmv_terms.py $(find $O/tr_$v -name "*kernel_trace.csv") $O/terms_$v.json || exit 1
+        rm -f $(find $O/tr_$v -name "*kernel_trace.csv")
+        cat $O/c4_$v.jsonl
+    done
+    B="$GRAFT_REPO_ROOT/tools/expmv_c4.py 1"
+    R="k_expmv_rows"
+    ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$R" -d $O/pmc_fetch -o f --output-format csv -- python3 $B > $O/pmc_fetch.log 2>&1 ) || { tail -20 $O/pmc_fetch.log; exit 1; }
+    ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$R" -d $O/pmc_write -o w --output-format csv -- python3 $B > $O/pmc_write.log 2>&1 ) || { tail -20 $O/pmc_write.log; exit 1; }
+    ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "$R" -d $O/pmc_hit -o h --output-format csv -- python3 $B > $O/pmc_hit.log 2>&1 ) || { tail -20 $O/pmc_hit.log; exit 1; }
+    python3 tools/pmc_traffic.py $(find $O/pmc_fetch -name "*counter_collection.csv") $(find $O/pmc_write -name "*counter_collection.csv") $O/traffic.json expmv_c4 \
+        $(find $O/pmc_hit -name "*counter_collection.csv") || exit 1
+    rm -f $(find $O/pmc_fetch $O/pmc_write $O/pmc_hit -name "*counter_collection.csv")
+    cat $O/traffic.json ;;
 *)
     echo "unknown task $TASK"; exit 2 ;;
 esac
