@@ -209,10 +209,26 @@ def _pmc_traffic(kernel, P, config="sf1m", weighted=False):
     if not isinstance(sec, dict):
         return None
     for k, v in sec.items():
+        if k.startswith("_"):
+            continue
         base, targs = _kernel_template_args(k)
         if base == kernel and targs[:1] == [str(P)] and isinstance(v, dict):
             return v.get("hbm_bytes_per_launch")
     return None
+
+
+def _pmc_traffic_build(config="sf1m", weighted=False):
+    """{csrc digest the section's counters were measured on, whether it is
+    this tree's} -- a kernel change since the last PMC pass shows as False."""
+    from krylov_robustness_amd._lib import source_digest
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            sec = json.load(f).get(config + ("_weighted" if weighted else ""), {})
+    except (OSError, ValueError):
+        sec = {}
+    rec = (sec.get("_build") or {}).get("csrc_sha256") if isinstance(sec, dict) else None
+    cur = source_digest()
+    return {"traffic_csrc_sha256": rec, "csrc_sha256": cur, "traffic_build_current": rec == cur}
 
 
 def _metric_name(n, nnz):
@@ -449,6 +465,7 @@ def main():
                 traffic = _pmc_traffic(kbase, P, args.config, args.weighted)
                 roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        **_pmc_traffic_build(args.config, args.weighted),
                         "kernel": kname + ">", "avg_launch_us": round(k1_ms * 1e3, 2),
                         "launches": tl, "algorithmic_bytes_per_launch": k1_bytes,
                         "algorithmic_bytes_basis": ("unit-weight matrix: 4 nnz (int32 columns; values "
@@ -592,10 +609,15 @@ def _reference_composition(kra, D, ctx, A, ref, budget_s):
     os.environ["KT_MC_SPEC"] = "0"
     try:
         c0, k0 = ctx.stat(3), ctx.stat(4)
+        ctx.profile_reset()
+        ctx.profile(True)  # HIP events around every Taylor-term launch (slot 4)
         t0 = time.perf_counter()
         tr, res, it = kra.mc_trace("expmv", None, 1e-4, 1000, 1, 0, seed=0, A=D, ctx=ctx)
         gpu_s = time.perf_counter() - t0
+        ctx.profile(False)
         calls, terms = ctx.stat(3) - c0, ctx.stat(4) - k0
+        t_launches, t_ms = ctx.profile_read(4)
+        t_busy = ctx.profile_busy(4)
     finally:
         for k, v in saved.items():
             if v is None:
@@ -608,6 +630,32 @@ def _reference_composition(kra, D, ctx, A, ref, budget_s):
            "gpu_mode": "serial: every expmv call on one stream (KT_TWIN=0, KT_MC_SPEC=0)"}
     if ref:
         out["rel_err"] = (tr - ref["value"]) / ref["value"]
+    # the term kernel's roofline: one active term = expmv.m:75-78 on the
+    # n x 10 block, P = 16 padded: CSR (4 nnz + 4 (n+1), unit weights) + the
+    # gathered block b (8 n P, each row once) + f read and written + b_next
+    # written (3 x 8 n P); "useful" prices the 10 live columns only
+    n, nnz = A.shape[0], A.nnz
+    unit = bool(A.nnz) and bool(np.all(A.data == 1.0))
+    csr_b = (4 if unit else 12) * nnz + 4 * (n + 1)
+    P, nc = 16, 10
+    padded, useful = csr_b + 32 * n * P, csr_b + 32 * n * nc
+    if terms and t_launches:
+        us = t_busy * 1e3 / terms  # launch time (no-op launches included) per active term
+        gbs = padded / (us * 1e-6) / 1e9
+        traffic = _pmc_traffic("k_expmv_rows", P, "expmv_c4")
+        roof = {"kernel": "k_expmv_rows<16>", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                "active_terms": terms, "launches": t_launches, "busy_ms": round(t_busy, 2),
+                "us_per_active_term": round(us, 2),
+                "bytes_per_term_padded": padded, "bytes_per_term_useful": useful,
+                "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                "useful_frac": round(useful / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "traffic": traffic, **_pmc_traffic_build("expmv_c4"),
+                "measured": "HIP events around every term launch on the context's stream (one stream: "
+                            "the union is the sum); us_per_active_term = busy / active terms, the "
+                            "~4 us no-op launches past a stage's stop included"}
+        if traffic:
+            roof["traffic_GBs"] = round(traffic / (us * 1e-6) / 1e9, 1)
+        out["roofline"] = roof
     Acsr = A.tocsr()
     n = Acsr.shape[0]
     # (1) the C + OpenMP restatement of the same algorithm (oracle/mctrace_ref.c)

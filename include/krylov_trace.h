@@ -319,7 +319,9 @@ int kt_eigs_leading(kt_matrix_t A, double tol, int maxit, double* lambda, double
  * gather pass (k_spmm_lanczos in the y-form sweep, k_spmm_dot = K1 in the
  * explicit sweep), 1 = K2 (k_update, explicit sweep only), 2 = the y-form
  * start pass (k_spmm_lanczos_start), 3 = the y-form pass of a sweep seeded
- * by a given block (k_spmm_lanczos in mc_trace's quadrature-only columns).
+ * by a given block (k_spmm_lanczos in mc_trace's quadrature-only columns),
+ * 4 = the expmv Taylor-term kernel (k_expmv_rows / k_expmv_step, one launch
+ * per term; a term queued past its stage's stop is a short no-op launch).
  * Returns launch count and summed milliseconds. */
 int kt_profile_enable(kt_context_t ctx, int enable);
 int kt_profile_read(kt_context_t ctx, int kernel, int64_t* launches, double* total_ms);

@@ -142,3 +142,21 @@ def check(status: int):
     if status != KT_OK:
         msg = load().kt_last_error()
         raise KrylovError(status, msg.decode() if msg else f"kt status {status}")
+
+
+def source_digest() -> str:
+    """sha256 (16 hex digits) of the sources libkrylov_hip.so is built from
+    (krylov_robustness_amd/csrc/*.hip|*.cpp|*.h, include/krylov_trace.h):
+    names the library build a profile was measured on (profiles/traffic.json
+    records it; bench.py compares it with the tree it runs from)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    root = os.path.dirname(_HERE)
+    files = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")) + glob.glob(os.path.join(_HERE, "csrc", "*.cpp")) +
+                   glob.glob(os.path.join(_HERE, "csrc", "*.h"))) + [os.path.join(root, "include", "krylov_trace.h")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]

@@ -132,7 +132,7 @@ struct ProfSlot {
     std::vector<std::pair<int, std::pair<int64_t, double>>> by_tag;
 };
 
-enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_START = 2, PROF_YBLOCK = 3, PROF_NSLOTS = 4 };
+enum { PROF_SPMM = 0, PROF_UPDATE = 1, PROF_START = 2, PROF_YBLOCK = 3, PROF_EXPMV = 4, PROF_NSLOTS = 5 };
 
 // Buffers of one probe-sweep lane (kt_slq.cpp); two lanes let two sweeps
 // run on two streams.

@@ -1430,7 +1430,10 @@ __device__ __forceinline__ void expmv_row_prefetch(int row, int p0, int nc, int 
         bo[e] = (c < nc && mu != 0.0) ? bin[o] : 0.0;
     }
 }
-template <int VEC>
+// PADW = false: the padding columns nc..P-1 of bout are not written (the
+// row-blocked kernel: both ping-pong blocks are zeroed when allocated and
+// never written there)
+template <int VEC, bool PADW = true>
 __device__ __forceinline__ void expmv_row_update(int row, int p0, const double* s, const double* fo,
                                                  const double* bo, int nc, int ld, double mu, double coef,
                                                  double* __restrict__ bout, double* __restrict__ F,
@@ -1448,7 +1451,7 @@ __device__ __forceinline__ void expmv_row_update(int row, int p0, const double* 
             F[o] = f;
             sb += fabs(bn);
             sf += fabs(f);
-        } else {
+        } else if constexpr (PADW) {
             bout[o] = 0.0;
         }
     }
@@ -1676,53 +1679,34 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
 // medium rows and one per 32 short rows: 66k workgroups at config 4 (12.6k
 // rows of degree > 64, 90k of 17-64), each paying an `active` read behind a
 // barrier, an LDS reduction, a barrier and two atomics for one gather round
-// trip.  Here resident workgroups stride over the rows with WAVES as the unit
-// of work, as the probe passes do (k_spmm_lanczos):
-//   long rows  (degree > long_thresh, heaviest first): one wave per row;
-//   medium rows (kMedThresh < degree <= long_thresh): one wave per row;
-//   short rows: row blocks of GPW (= 8 at P = 16) consecutive rows per wave,
-//               one row group of 16 B per lane per row, the next block's
-//               row_ptr loaded while this block gathers.
+// trip.  Here resident workgroups stride over the rows with waves as the
+// unit of work, as the probe passes do (k_spmm_lanczos):
+//   (0) long rows of degree > kExpmvCoopThresh: one workgroup per row;
+//   (1) the other long rows (degree > long_thresh): one wave per row;
+//   (2) medium rows (kMedThresh < degree <= long_thresh): one wave per row,
+//       the next row's task, chain columns and own f in flight meanwhile;
+//   (3) short rows (degree <= kMedThresh) from a task list sorted by degree
+//       within windows of 4,096 rows (kt_runtime.cpp build_csr), GPW (= 8 at
+//       P = 16) per wave with one row group of 16 B per lane each, pipelined
+//       the same way.
 // Every row's sum is formed in exactly the order of the split / fused
 // kernels, so F, s, m and mv are bit-identical to them:
 //   short:  one sequential chain over the row in CSR order (row_gather8, stride 1);
 //   medium: 16 chains k = beg + g + 16 i (g < 16), each in i order, summed by
 //           the xor butterfly over g (g ^ 1, g ^ 2, g ^ 4, g ^ 8);
 //   long:   the fused kernel's 4 waves x 16 chains k = beg + 16 w + g + 64 i,
-//           here the 4 chain sets w taken in turn by one wave, each
-//           butterflied over g, then ((t0 + t1) + t2) + t3 as the fused
-//           kernel's LDS sum.
+//           each set butterflied over g, then ((t0 + t1) + t2) + t3 as the
+//           fused kernel's LDS sum (one wave per set in (0), the 4 sets in
+//           turn in one wave in (1)).
 // The row sums of |b| and |F| and their maxima are the split kernel's too
 // (the same lane geometry per row class; max is exact in any order).
-// 4 waves per workgroup: 92 VGPRs = 5 waves per SIMD (8-wave workgroups
-// would fit only 2 per CU, 4 waves per SIMD)
-#ifndef KT_XR_WAVES
-#define KT_XR_WAVES 4
-#endif
-#ifndef KT_XR_WPE
-#define KT_XR_WPE 0
-#endif
-#ifndef KT_XR_SD
-#define KT_XR_SD 8
-#endif
-#ifndef KT_XR_TASKS
-#define KT_XR_TASKS 1
-#endif
-#ifndef KT_XR_FPS
-#define KT_XR_FPS 1
-#endif
-#ifndef KT_XR_FPM
-#define KT_XR_FPM 1
-#endif
-#ifndef KT_XR_MD
-#define KT_XR_MD 4
-#endif
-#ifndef KT_XR_LD
-#define KT_XR_LD 4
-#endif
-constexpr int kExpmvRowsWaves = KT_XR_WAVES;
+// Config 4, one MI355X (profiles/r06/expmv_rows_ab): active term 394 us
+// (split kernel) -> 293 us; the reference composition 1.58 -> 1.22 s.
+// 4 waves per workgroup (108 VGPRs, 4 waves per SIMD); measured flat against
+// 5 waves per SIMD at shallower gathers (4-deep short rows, 2-deep medium).
+constexpr int kExpmvRowsWaves = 4;
 template <int P, int FLAGS>
-__global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
+__global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
     const int* __restrict__ rp, const int* __restrict__ ci, const double* __restrict__ va, int n,
     const int* __restrict__ long_rows, int n_long, int n_heavy, const int4* __restrict__ med_tasks, int n_med,
     const int4* __restrict__ short_tasks, int n_short,
@@ -1743,11 +1727,6 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
     __syncthreads();
     if (!decide) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) st->mv += 1;
-#ifdef KT_XR_SKIP  // resource-usage probes only: drop row classes
-    if (KT_XR_SKIP & 1) n_long = n_heavy = 0;
-    if (KT_XR_SKIP & 2) n_med = 0;
-    if (KT_XR_SKIP & 4) n_short = 0;
-#endif
     const int gw = blockIdx.x * WAVES + wave, TW = gridDim.x * WAVES;
     __builtin_assume(gw >= 0);
     __builtin_assume(TW > 0);
@@ -1773,8 +1752,8 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
         double acc[GL::VEC];
 #pragma unroll
         for (int e = 0; e < GL::VEC; ++e) acc[e] = 0.0;
-        row_gather8<P, FLAGS, GL, KT_XR_LD>(rp[row] + wave * GL::GPW + grpL, rp[row + 1], VW * GL::GPW, p0L, ci, va,
-                                           bin, acc, ld);
+        row_gather8<P, FLAGS, GL, 4>(rp[row] + wave * GL::GPW + grpL, rp[row + 1], VW * GL::GPW, p0L, ci, va, bin,
+                                    acc, ld);
 #pragma unroll
         for (int o = GL::LPR; o < 64; o <<= 1)
 #pragma unroll
@@ -1794,7 +1773,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
                     for (int w = 1; w < VW; ++w) t[e] += lsum[w][p0L + e];
                 }
                 expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
-                expmv_row_update<GL::VEC>(row, p0L, t, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+                expmv_row_update<GL::VEC, false>(row, p0L, t, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
             }
             fold(sb, sf, GL::LPR);
         }
@@ -1812,7 +1791,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
             double acc[GL::VEC];
 #pragma unroll
             for (int e = 0; e < GL::VEC; ++e) acc[e] = 0.0;
-            row_gather8<P, FLAGS, GL, KT_XR_LD>(beg + w * GL::GPW + grpL, end, VW * GL::GPW, p0L, ci, va, bin, acc, ld);
+            row_gather8<P, FLAGS, GL, 4>(beg + w * GL::GPW + grpL, end, VW * GL::GPW, p0L, ci, va, bin, acc, ld);
 #pragma unroll
             for (int o = GL::LPR; o < 64; o <<= 1)
 #pragma unroll
@@ -1824,7 +1803,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
         if (grpL == 0) {
             double fo[GL::VEC], bo[GL::VEC];
             expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
-            expmv_row_update<GL::VEC>(row, p0L, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+            expmv_row_update<GL::VEC, false>(row, p0L, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
         }
         fold(sb, sf, GL::LPR);
     }
@@ -1832,7 +1811,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
     //     degree <= 64 is one round), pipelined: while row mi gathers, the
     //     chain columns of row mi + TW and the task of row mi + 2 TW are in
     //     flight
-    constexpr int MD = KT_XR_MD;
+    constexpr int MD = 4;
     auto load_mtask = [&](int ii, int& r, int& bg, int& en) {
         r = -1;
         bg = en = 0;
@@ -1856,7 +1835,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
 #pragma unroll
             for (int e = 0; e < GL::VEC; ++e) {
                 const int c = p0L + e;
-                f[e] = (MU0 && KT_XR_FPM && grpL == 0 && r >= 0 && c < nc) ? F[(int64_t)r * ld + c] : 0.0;
+                f[e] = (MU0 && grpL == 0 && r >= 0 && c < nc) ? F[(int64_t)r * ld + c] : 0.0;
             }
         };
         int mi = gw;
@@ -1907,13 +1886,13 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
             double sb = 0.0, sf = 0.0;
             if (grpL == 0) {
                 double fo[GL::VEC], bo[GL::VEC];
-                if constexpr (MU0 && KT_XR_FPM) {
+                if constexpr (MU0) {
 #pragma unroll
                     for (int e = 0; e < GL::VEC; ++e) fo[e] = mfc[e];
                 } else {
                     expmv_row_prefetch<GL::VEC>(row, p0L, nc, ld, mu, bin, F, fo, bo);
                 }
-                expmv_row_update<GL::VEC>(row, p0L, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+                expmv_row_update<GL::VEC, false>(row, p0L, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
             }
             fold(sb, sf, GL::LPR);
 #pragma unroll
@@ -1928,13 +1907,12 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
             for (int i = 0; i < MD; ++i) mc[i] = mn[i];
         }
     }
-    constexpr int SD = KT_XR_SD;  // short rows: gathers in flight per row group
+    constexpr int SD = 8;  // short rows: gathers in flight per row group
     // (3) short rows, in the task list's order (degree-descending, so the
     //     GPW rows of a wave take the same number of gather rounds), GPW
     //     tasks per wave, software-pipelined: while block b gathers, the
     //     first SD column indices of block b + TW and the tasks of block
     //     b + 2 TW are in flight
-#if KT_XR_TASKS
     const int nblk = (n_short + G::GPW - 1) / G::GPW;
     auto load_task = [&](int bb, int& r, int& bg, int& en) {
         const int t = bb * G::GPW + grp;
@@ -1947,20 +1925,6 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
             en = v.z;
         }
     };
-#else  // natural row blocks from row_ptr (medium / long rows skipped)
-    const int nblk = (n + G::GPW - 1) / G::GPW;
-    auto load_task = [&](int bb, int& r, int& bg, int& en) {
-        const int t = bb * G::GPW + grp;
-        r = -1;
-        bg = en = 0;
-        if (bb < nblk && t < n) {
-            bg = ld_stream<FLAGS>(rp + t);
-            en = ld_stream<FLAGS>(rp + t + 1);
-            if (en - bg <= kMedThresh) r = t;
-            else en = bg;
-        }
-    };
-#endif
     auto load_chunk = [&](int bg, int en, int* c) {  // a row's first SD columns (tail: its first)
         const int c0 = bg < en ? ld_stream<FLAGS>(ci + bg) : 0;
         c[0] = c0;
@@ -1972,7 +1936,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
 #pragma unroll
         for (int e = 0; e < G::VEC; ++e) {
             const int c = p0 + e;
-            f[e] = (MU0 && KT_XR_FPS && r >= 0 && c < nc) ? F[(int64_t)r * ld + c] : 0.0;
+            f[e] = (MU0 && r >= 0 && c < nc) ? F[(int64_t)r * ld + c] : 0.0;
         }
     };
     int b = gw;
@@ -2016,13 +1980,13 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves, KT_XR_WPE) void k_expmv_rows(
                     }
             }
             row_gather8<P, FLAGS, G, SD>(beg + SD, end, 1, p0, ci, va, bin, s, ld);
-            if constexpr (MU0 && KT_XR_FPS) {
+            if constexpr (MU0) {
 #pragma unroll
                 for (int e = 0; e < G::VEC; ++e) fo[e] = fc[e];
             } else {
                 expmv_row_prefetch<G::VEC>(row, p0, nc, ld, mu, bin, F, fo, bo);
             }
-            expmv_row_update<G::VEC>(row, p0, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
+            expmv_row_update<G::VEC, false>(row, p0, s, fo, bo, nc, ld, mu, coef, bout, F, sb, sf);
         }
         fold(sb, sf, G::LPR);
 #pragma unroll

@@ -374,8 +374,10 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
             for (int k = 1; k <= r.m; ++k) {
                 if (ahead && queued >= ahead) KT_HIP(hipEventSynchronize(ring[queued % ahead]));
                 if (use_flag && k > 2 && __atomic_load_n(ctx->ws.expmv_stop.host, __ATOMIC_ACQUIRE) >= i) break;
+                prof_begin(ctx, PROF_EXPMV, st, form);
                 KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu,
                                          t / ((double)r.s * k), tol, k, cur, nxt, F, state, st, form, hflag, i));
+                prof_end(ctx, PROF_EXPMV, st);
                 if (split && k < r.m) KT_HIP(launch_expmv_slot_check(state, k, tol, st, hflag, i));
                 if (ahead) KT_HIP(hipEventRecord(ring[queued % ahead], st));
                 ++queued;
@@ -502,6 +504,13 @@ static void project(kt_context_s* ctx, int64_t n, const double* Q, int ld, int n
 // depend only on the slot layout and on the guess (made from all-reduced
 // sums, the same on every rank), never on the rank count, so every world size
 // gives the world-1 estimate bit for bit.
+// y-form sweep chunk of a round that does not compute the next S term (its
+// 10 Q and 10 G columns, forms only): KT_MC_YCHUNK (A/B), default 16 (16 + 4)
+static int mc_final_chunk() {
+    const char* e = getenv("KT_MC_YCHUNK");
+    return e ? std::max(1, std::min(16, atoi(e))) : 16;
+}
+
 static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int maxit, uint64_t seed,
                              double* tr_out, double* res_out, int* it_out, const Shard& sh) {
     kt_context_s* ctx = A->ctx;
@@ -511,10 +520,9 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
     const int K = (maxit + 3 * mb - 1) / (3 * mb);  // :41
     double tr = 0.0, tr_old = 0.0, tr_new = 0.0, res = 1.0;
     std::vector<DevMat> Qs;
-    DevMat Bk, Yb, T;
+    DevMat Bk, Yb;
     Bk.alloc(ctx, n, LB);  // [S_{it+1} | P..P Q_it | P..P G_it (10 slots) | 0 0]
     Yb.alloc(ctx, n, ld);  // Afun_it(S_it), then Q_it in place
-    if (sh.world > 1) T.alloc(ctx, n, ld);  // a rank's G columns before they enter their slots
     auto rademacher_into = [&](int64_t base, double* dst) {  // probes base .. base + 9 into their slots
         KT_HIP(launch_rademacher_cols((int)n, mb, seed, base, dst, LB, st));
     };
@@ -542,17 +550,16 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
         Qs.emplace_back();                                                 // :47-48
         Qs.back().alloc(ctx, n, ld);
         copy_cols(ctx, n, Yb.col(0), ld, Qs.back().col(0), ld, mb);
-        // G term input: P_it..P_1 G_it, this rank's columns c % world == rank  :44, :49
-        int ng = 0;
-        if (sh.world == 1) {  // every G column, straight into its slot
-            rademacher_into(base + mb, Bk.col(2 * mb));
-            ng = mb;
-        } else {
-            KT_HIP(launch_rademacher(ld, (int)n, seed, base + mb, nullptr, T.col(0), st));
-            for (int c = sh.rank; c < mb; c += sh.world) copy_cols(ctx, n, T.col(c), ld, Bk.col(2 * mb + ng++), LB, 1);
-        }
-        for (int k = (int)Qs.size() - 1; k >= 0 && ng > 0; --k)
-            project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(2 * mb), LB, ng);
+        // G term input: P_it..P_1 G_it.  G column c sits in slot 2 mb + c at
+        // every world size; a rank zeroes the slots of the other ranks' columns
+        // (c % world != rank; a zero column's form is 0), so every column runs
+        // in the same sweep at the same width whatever the rank count   :44, :49
+        rademacher_into(base + mb, Bk.col(2 * mb));
+        if (sh.world > 1)
+            for (int c = 0; c < mb; ++c)
+                if (c % sh.world != sh.rank) zero_cols(ctx, n, Bk.col(2 * mb + c), LB, 1);
+        for (int k = (int)Qs.size() - 1; k >= 0; --k)
+            project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(2 * mb), LB, mb);
         // next round's S term input: P_it..P_1 S_{it+1}, unless this round is
         // expected to stop
         const bool ahead = it < K && (ahead_mode == 1 || (ahead_mode < 0 && (it == 1 || !(gprev < tol * std::fabs(tr_new)))));
@@ -569,10 +576,11 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
             // rounding -- a lucky breakdown at step 1 that the y-form guard
             // sends to the explicit redo -- but round 1 always computes the
             // S term ahead, so its Q columns ride the explicit sweeps.)
-            lanczos_columns_split(A, Bk.col(mb), LB, 2 * mb, 0, 0, F.m, F.fun, q.data() + mb, nullptr, 0, 16);
+            lanczos_columns_split(A, Bk.col(mb), LB, 2 * mb, 0, 0, F.m, F.fun, q.data() + mb, nullptr, 0, 16,
+                                  mc_final_chunk());
         }
         std::vector<double> qv(mb, 0.0);
-        for (int c = sh.rank, t = 0; c < mb; c += sh.world, ++t) qv[c] = q[2 * mb + t];
+        for (int c = sh.rank; c < mb; c += sh.world) qv[c] = q[2 * mb + c];
         if (sh.allreduce && sh.allreduce(qv.data(), mb, sh.user) != 0)
             fail(KT_ERR_CALLBACK, "mc_trace: all-reduce callback failed");
         double qsum = 0.0, gsum = 0.0;  // column order, as trace_quad sums

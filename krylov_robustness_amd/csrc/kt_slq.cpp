@@ -338,21 +338,22 @@ void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m,
 // second lane was queued only after the whole first sweep).  The explicit
 // sweep does not take narrow chunks: 10 + 30 columns as greedy power-of-two
 // sweeps (8 + 2, 16 + 8 + 4 + 2) cost 53 ms.
-static std::vector<int> quad_plan(int cols) {
-    std::vector<int> wv;
-    for (int left = cols; left > 0; left -= 16) {
-        int P = 16;
-        if (left < 16) {
-            P = 1;
-            while (P < left) P <<= 1;
-        }
-        wv.push_back(P);
+// A smaller `chunk` cuts the columns into sweeps of `chunk` (the last one
+// shorter), each at the power of two that holds it: {(columns, width)}.
+static std::vector<std::pair<int, int>> quad_plan(int cols, int chunk = 16) {
+    std::vector<std::pair<int, int>> wv;
+    chunk = std::max(1, std::min(chunk, 16));
+    for (int left = cols; left > 0; left -= chunk) {
+        const int c = std::min(left, chunk);
+        int P = 1;
+        while (P < c) P <<= 1;
+        wv.push_back({c, P});
     }
     return wv;
 }
 
 void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, int ny, int ne, int m, int fun,
-                           double* quad, double* Y, int ldy, int px) {
+                           double* quad, double* Y, int ldy, int px, int ychunk) {
     kt_context_s* ctx = A->ctx;
     const int64_t n = A->n;
     if (!Y) ny = 0;
@@ -406,9 +407,9 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     for (int c0 = 0; c0 < ne; c0 += Pe) sw.push_back({c0, std::min(Pe, ne - c0), Pe, k++ % 4, false});
     {
         int c0 = ne;
-        for (int P : quad_plan(ncols - ne)) {
-            sw.push_back({c0, std::min(P, ncols - c0), P, k++ % 4, true});
-            c0 += P;
+        for (const auto& cp : quad_plan(ncols - ne, ychunk)) {
+            sw.push_back({c0, cp.first, cp.second, k++ % 4, true});
+            c0 += cp.first;
         }
     }
     const size_t rec_max = (size_t)3 * m * 32 + 32;

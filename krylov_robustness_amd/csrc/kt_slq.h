@@ -121,8 +121,11 @@ void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m,
 // on the values (zero columns included).  The y-form suits random probes;
 // columns that start close to an invariant subspace (mc_trace's Q) trip its
 // cancellation guard and belong in [0, ne).
+// ychunk: columns per y-form sweep (each sweep at the power of two >= its
+// columns, <= 16): 16 packs them; a smaller chunk splits them evenly (mc_trace's
+// final round: [Q | pad] and [G | pad] instead of 16 + 4).
 void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, int ny, int ne, int m, int fun,
-                           double* quad, double* Y, int ldy, int px = 0);
+                           double* quad, double* Y, int ldy, int px = 0, int ychunk = 16);
 
 // y-form sweep seeded by a device block (see kt_slq.cpp)
 void lanczos_sweep_y_block(kt_matrix_s* A, const DevCSR& M, int P, int m, const double* x, int ldx, int ncols,

@@ -43,6 +43,7 @@ class _ThreadReduce:
         self.bar = threading.Barrier(world)
         self.bufs = [None] * world
         self.calls = 0
+        self.totals = []  # the all-reduced vector of every round (rank 0's view)
 
     def fn(self, rank):
         from krylov_robustness_amd import _lib
@@ -58,6 +59,7 @@ class _ThreadReduce:
             arr[:] = tot
             if rank == 0:
                 self.calls += 1
+                self.totals.append(tot.copy())
             return 0
         return _lib.REDUCE_FN(cb)
 
@@ -85,6 +87,31 @@ def _run_world(kra, A, world, afun, **kw):
         t.join(timeout=300)
     assert not errs, errs
     return out, red.calls
+
+
+def _run_world_forms(kra, A, world, afun, **kw):
+    """As _run_world, plus every round's all-reduced G-form vector."""
+    red = _ThreadReduce(world)
+    out = [None] * world
+    errs = []
+
+    def worker(r):
+        try:
+            ctx = kra.Context(0)
+            D = kra.DeviceMatrix(A, ctx)
+            out[r] = kra.mc_trace_sharded(afun, None, A=D, rank=r, world=world, allreduce=red.fn(r),
+                                          ctx=ctx, **kw)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+            red.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    return out, red.totals
 
 
 @pytest.mark.parametrize("afun", ["lanczos", "matrix"])
@@ -131,6 +158,32 @@ def test_threads_world_guard_redo_bit_identical(kra, gpu_ctx, monkeypatch, world
     for r in out:
         assert r == ref
     assert calls == ref[2]
+
+
+@pytest.mark.parametrize("ahead", ["0", "1"])
+def test_threads_world_g_forms_bit_identical(kra, monkeypatch, ahead):
+    """The G forms themselves, not only the estimate: on an ER graph (exp(A)
+    far from rank one, so the deflated G term is not negligible against the
+    trace) every round's all-reduced 10-vector of G quadratic forms is the
+    same bits at worlds 1-4 -- G column c sits in slot 2 mb + c of the same
+    16-wide sweep whatever the rank count, the other ranks' slots zero.
+    KT_MC_AHEAD=0: every round without the S term (the final-round sweep
+    plan); 1: every round with it; tol = 0 runs all K rounds."""
+    from krylov_robustness_amd import graphs
+    monkeypatch.setenv("KT_MC_AHEAD", ahead)
+    A = graphs.erdos_renyi(20_000, 100_000, seed=2)
+    kw = dict(tol=0.0, maxit=90, isAreal=1, seed=5, fun="exp", m=20)
+    ref, g1 = _run_world_forms(kra, A, 1, "lanczos", **kw)
+    assert len(g1) == 3 and all(np.all(g != 0) for g in g1)
+    gsum = sum(abs(float(np.sum(g))) / 10 for g in g1)
+    assert gsum > 1e-6 * abs(ref[0][0])  # the G term moves the estimate
+    for world in (2, 3, 4):
+        out, gw = _run_world_forms(kra, A, world, "lanczos", **kw)
+        assert len(gw) == len(g1)
+        for a, b in zip(gw, g1):
+            assert np.array_equal(a, b)
+        for r in out:
+            assert r == ref[0]
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -53,6 +53,12 @@ def main(fetch_csv, write_csv, out_json, section=None, hit_csv=None):
     doc = ("median per launch; FETCH_SIZE doubled per the gfx950 calibration "
            "(MI355X_MICROARCH.md §HBM); Infinity-Cache hits are counted by these "
            "memory-side counters")
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from krylov_robustness_amd._lib import source_digest
+    res["_build"] = {"csrc_sha256": source_digest(),
+                     "note": "digest of the library sources these counters were measured on "
+                             "(krylov_robustness_amd._lib.source_digest)"}
     if section:
         try:
             allr = json.load(open(out_json))
