@@ -47,6 +47,9 @@ struct Rot {
 // first eigenvector components in z (implicit-shift QL rotating only the first
 // row of the eigenvector matrix Z).  With `log`, every rotation applied to z
 // is recorded in order: Z = R_1 R_2 ... R_k, R_j acting on columns (i, i+1).
+// (The QL iteration is EISPACK IMTQL2's, public domain: Bowdler, Martin,
+// Reinsch & Wilkinson, Numer. Math. 11 (1968); first-row form after Golub &
+// Welsch, Math. Comp. 23 (1969).)
 static void ql_first_row(int m, double* d, double* e, double* z, std::vector<Rot>* log = nullptr) {
     e[m - 1] = 0.0;
     for (int i = 0; i < m; ++i) z[i] = (i == 0) ? 1.0 : 0.0;
@@ -175,7 +178,14 @@ void tri_upper_inv(const double* R, int n, double* X) {
 // Householder reduction of a symmetric matrix to tridiagonal form (d, e) with
 // the accumulated orthogonal transform in Z (if want_vectors), followed by
 // implicit-shift QL.  On exit: w ascending eigenvalues, Z (col-major) the
-// eigenvectors.  Classic tred2/tql2 structure, written for column-major.
+// eigenvectors, written for column-major.
+// Source: the EISPACK routines TRED2 (Householder tridiagonalisation, with
+// the transform accumulated) and IMTQL2 / TQL2 (implicit-shift QL), public
+// domain -- Martin, Reinsch & Wilkinson, "Householder's tridiagonalization of a
+// symmetric matrix" and Bowdler, Martin, Reinsch & Wilkinson, "The QR and QL
+// algorithms for symmetric matrices", Numer. Math. 11 (1968), Handbook for
+// Automatic Computation vol. II (Wilkinson & Reinsch 1971), contributions II/2
+// and II/3; Smith et al., EISPACK Guide (1976).
 static void tred2(int n, double* a /* in: sym, out: Q */, double* d, double* e, bool vecs) {
     for (int i = n - 1; i > 0; --i) {
         const int l = i - 1;
@@ -380,7 +390,7 @@ static void tridiag_lower_cols_base(int n, double* a, double* d, double* e, doub
     tridiag_lower_cols<0>(n, a, d, e, v, p);
 }
 
-// tql2 without eigenvectors for the column path
+// tql2 without eigenvectors for the column path (EISPACK TQL1 / IMTQL1 form)
 static void tql_values(int n, double* d, double* e) {
     for (int i = 1; i < n; ++i) e[i - 1] = e[i];
     e[n - 1] = 0.0;

@@ -286,7 +286,14 @@ __device__ double dev_fscalar(int fun, double x) {
 }
 
 // eigenvalues (ascending, in d) of the symmetric n x n column-major `a`
-// (destroyed); e: n scratch
+// (destroyed); e: n scratch.  The device copy of kt_dense.cpp's host routine:
+// Source: the EISPACK routines TRED2 (Householder tridiagonalisation, with
+// the transform accumulated) and IMTQL2 / TQL2 (implicit-shift QL), public
+// domain -- Martin, Reinsch & Wilkinson, "Householder's tridiagonalization of a
+// symmetric matrix" and Bowdler, Martin, Reinsch & Wilkinson, "The QR and QL
+// algorithms for symmetric matrices", Numer. Math. 11 (1968), Handbook for
+// Automatic Computation vol. II (Wilkinson & Reinsch 1971), contributions II/2
+// and II/3; Smith et al., EISPACK Guide (1976).
 __device__ void dev_sym_eigvals(int n, double* a, double* d, double* e) {
     for (int i = n - 1; i > 0; --i) {  // tred2, values only
         const int l = i - 1;

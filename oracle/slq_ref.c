@@ -51,6 +51,9 @@ static double fscalar(int fun, double x) {
 }
 
 /* Implicit-shift QL on a symmetric tridiagonal (d[0..m-1], e[0..m-2]).
+ * Source: EISPACK IMTQL2 / TQL2 (public domain; Bowdler, Martin, Reinsch &
+ * Wilkinson, Numer. Math. 11 (1968), Handbook vol. II contribution II/3),
+ * rotating only the first row of the eigenvector matrix (Golub & Welsch 1969).
  * On exit d holds the eigenvalues and z the FIRST components of the
  * normalised eigenvectors (only row 0 of the eigenvector matrix is rotated). */
 static void tql_first_row(int m, double *d, const double *e_in, double *z) {

@@ -8,7 +8,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_PATH = os.path.join(_HERE, "libslq_ref.so")
+_PATH = os.path.join(os.environ.get("KT_ORACLE_DIR") or _HERE, "libslq_ref.so")  # (sanitizer builds: tools/sanitize.sh)
 _lib = None
 
 

@@ -29,7 +29,8 @@ from conftest import ROOT, load_graph
 from oracle import krylov_oracle as ko
 
 pytestmark = pytest.mark.gpu
-BUILD = os.path.join(ROOT, "tests", "mexstub", "_build")
+# KT_MEXSTUB_BUILD: the sanitizer build's directory (tools/sanitize.sh)
+BUILD = os.environ.get("KT_MEXSTUB_BUILD") or os.path.join(ROOT, "tests", "mexstub", "_build")
 ENTRIES = ["TRACE_EXP", "MC_TRACE", "TRACE_FUN_UPDATE", "FUN_UPDATE", "FG_EXP", "FG_FUN",
            "KRYLOV_MIOBI", "FME", "HESS_EXP", "HESS_FUN"]
 P = C.c_void_p

@@ -34,7 +34,8 @@ def test_mex_entry_library_exports_mexfunction(entry):
     made here (no GPU); tests/test_mex_exec.py runs them on the GPU box."""
     import ctypes
     from krylov_robustness_amd import _lib
-    build = os.path.join(ROOT, "tests", "mexstub", "_build")
+    # KT_MEXSTUB_BUILD: the sanitizer build's directory (tools/sanitize.sh)
+    build = os.environ.get("KT_MEXSTUB_BUILD") or os.path.join(ROOT, "tests", "mexstub", "_build")
     if not os.path.exists(os.path.join(build, f"kt_mex_{entry}.so")):
         subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "mexstub")], check=True,
                        capture_output=True)
