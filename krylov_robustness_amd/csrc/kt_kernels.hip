@@ -93,7 +93,9 @@ template <int P> using GeoB = GeoW<P, (P >= 16) ? KT_BLK_VW : (P >= 2) ? 2 : 1>;
 // gathered table.
 // FLAGS bit 5 (expmv terms): mu = 0 (no self loops: trace(A) = 0), so a row's
 // own b is never read and (A - mu I) b is A b.
-enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4, KF_NTY = 8, KF_SC1 = 16, KF_MU0 = 32 };
+// FLAGS bit 6 (y-form passes): also form the Lanczos vector v_{j+1} (the
+// basis of f(A) x = ||x|| V f(T) e1) from the pass's own rows.
+enum : int { KF_NT = 1, KF_UNIT = 2, KF_MLP = 4, KF_NTY = 8, KF_SC1 = 16, KF_MU0 = 32, KF_VB = 64 };
 
 // KT_KY_DIAG (diagnostic builds of the y-form pass only, tools/ky_diag.sh; their
 // results are wrong): 1 = gathers + own row, 2 = gathers only, 3 = row streams only
@@ -523,6 +525,15 @@ __device__ __forceinline__ void ycoef_probe(int p, int P, double d0, double d1, 
 // y_0 = A v_0.  partial slabs [3][P][grid]: X.t, X.Out, Out.Out.  Out ==
 // nullptr (the last pass of a sweep): only X.t is formed -- Yold is not read
 // and nothing is stored.
+// KF_VB (round 6): the pass also forms the normalised Lanczos vector
+//   v_{j+1} = g y_j - a v_j - b v_{j-1}
+// with the SAME per-probe (g, a, b): y_i = A v_i for every i (v_0 is the start
+// table, y_0 = A v_0), so A applied to the right side is y_{j+1}'s
+// recurrence.  y_j[r] is the own row already loaded for alpha; v_j[r] and
+// v_{j-1}[r] are read from basis slots Vc, Vo (Vo == nullptr at j = 0) and
+// v_{j+1}[r] is written to slot Vn, columns < bcols only -- also in the last
+// pass, which still owes v_{m-1}.  No extra gathers: +24 n bcols bytes per
+// pass where the explicit sweep's K1 + K2 move 32 n P more.
 // ---------------------------------------------------------------------------
 template <int P, int FLAGS, class G = Geo<P>, class C = const double*>
 __device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s, C cg,
@@ -530,7 +541,10 @@ __device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s,
                                                const double* __restrict__ X,
                                                const double* __restrict__ Yold,
                                                double* __restrict__ Out, double* d0, double* d1,
-                                               double* d2, __amdgpu_buffer_rsrc_t orsrc) {
+                                               double* d2, __amdgpu_buffer_rsrc_t orsrc,
+                                               const double* __restrict__ Vc = nullptr,
+                                               const double* __restrict__ Vo = nullptr,
+                                               double* __restrict__ Vn = nullptr, int bcols = 0) {
     using V = VecT<G::VEC>;
     const int64_t off = (int64_t)row * P + p0;
 #if KT_KY_DIAG == 2
@@ -541,6 +555,19 @@ __device__ __forceinline__ void row_epilogue_y(int row, int p0, const double* s,
     return;
 #endif
     const typename V::T xi = V::load(X + off);
+    if constexpr (FLAGS & KF_VB) {
+        if (p0 < bcols) {
+            const typename V::T vc = V::load(Vc + off);
+            typename V::T vo;
+            if (Vo) vo = V::load(Vo + off);
+#pragma unroll
+            for (int e = 0; e < G::VEC; ++e) {
+                double v = fma(-ca[e], V::get(vc, e), cg[e] * V::get(xi, e));
+                if (Vo) v = fma(-cb[e], V::get(vo, e), v);
+                if (p0 + e < bcols) Vn[off + e] = v;
+            }
+        }
+    }
 #if KT_KY_DIAG == 1
     // diagnostic build: gathers + the own-row read (alpha's y_j . t), no
     // y_{j-1} read and no y_{j+1} store
@@ -728,7 +755,8 @@ __global__ KT_KY_BOUNDS(BLOCK) void k_spmm_lanczos(
     const int* __restrict__ row_ptr, const int* __restrict__ col, const double* __restrict__ val,
     int n, const double* __restrict__ X, const double* __restrict__ Yold, double* __restrict__ Out,
     const double* __restrict__ coef, double* __restrict__ partial,
-    const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks) {
+    const int* __restrict__ long_rows, int n_long, int long_thresh, int long_blocks,
+    const double* __restrict__ Vc, const double* __restrict__ Vo, double* __restrict__ Vn, int bcols) {
     using G = GeoKY<P>;
     constexpr int WAVES = BLOCK / 64;
     const int lane = threadIdx.x & 63;
@@ -780,7 +808,7 @@ __global__ KT_KY_BOUNDS(BLOCK) void k_spmm_lanczos(
                 for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
             if (grp == 0)
                 row_epilogue_y<P, FLAGS, G, decltype(cg)>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2,
-                                           orsrc);
+                                           orsrc, Vc, Vo, Vn, bcols);
         }
     } else {
         const int sb = blockIdx.x - long_blocks;
@@ -796,7 +824,7 @@ __global__ KT_KY_BOUNDS(BLOCK) void k_spmm_lanczos(
             gather_row<P, FLAGS, G>(beg, end, 1, p0, col, val, X, s);
 #endif
             row_epilogue_y<P, FLAGS, G, decltype(cg)>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2,
-                                           orsrc);
+                                           orsrc, Vc, Vo, Vn, bcols);
         }
     }
 
@@ -2237,12 +2265,23 @@ hipError_t launch_spmm_lanczos(int P, int flags, int grid, const int* rp, const 
                                const double* va, int n, const double* X, const double* Yold,
                                double* Out, const double* coef, double* partial,
                                const int* long_rows, int n_long, int long_thresh, int long_blocks,
-                               hipStream_t st) {
+                               hipStream_t st, const double* Vc, const double* Vo, double* Vn, int bcols) {
     return dispatch_p(P, [&](auto c) {
         constexpr int PP = decltype(c)::value;
 #define KT_KY(F)                                                                                   \
     k_spmm_lanczos<PP, kBlock, F><<<grid, kBlock, 0, st>>>(rp, ci, va, n, X, Yold, Out, coef, partial, \
-                                                           long_rows, n_long, long_thresh, long_blocks)
+                                                           long_rows, n_long, long_thresh, long_blocks, \
+                                                           Vc, Vo, Vn, bcols)
+        if (Vn) {  // the basis-forming pass (KF_VB)
+            if (flags & KF_UNIT) {
+                if (flags & KF_SC1) KT_KY(KF_UNIT | KF_SC1 | KF_VB);
+                else KT_KY(KF_UNIT | KF_VB);
+            } else {
+                if (flags & KF_SC1) KT_KY(KF_SC1 | KF_VB);
+                else KT_KY(KF_VB);
+            }
+            return;
+        }
         switch (flags & (KF_UNIT | KF_NTY | KF_SC1)) {
         case 0: KT_KY(0); break;
         case KF_UNIT: KT_KY(KF_UNIT); break;

@@ -83,11 +83,15 @@ hipError_t launch_norm(int P, const double* partial, int nblk, double* k2s, doub
                        double* t_low, hipStream_t st);
 // y-form probe Lanczos (one pass per step; slot-major partials [3P][grid]
 // for launch_ycoef, the per-probe coefficient step).
+// Vn != nullptr: also v_{j+1} = g y_j - a v_j - b v_{j-1} into basis slot Vn
+// from slots Vc (v_j) and Vo (v_{j-1}, nullptr at j = 0), columns < bcols
+// (every slot n x P, row-major)
 hipError_t launch_spmm_lanczos(int P, int flags, int grid, const int* rp, const int* ci,
                                const double* va, int n, const double* X, const double* Yold,
                                double* Out, const double* coef, double* partial,
                                const int* long_rows, int n_long, int long_thresh, int long_blocks,
-                               hipStream_t st);
+                               hipStream_t st, const double* Vc = nullptr, const double* Vo = nullptr,
+                               double* Vn = nullptr, int bcols = 0);
 hipError_t launch_rademacher_signs(int P, int n, uint64_t seed, int64_t probe_base,
                                   const int* perm, uint32_t* S, hipStream_t st);
 hipError_t launch_spmm_lanczos_start(int P, int flags, int grid, const int* rp, const int* ci,

@@ -527,10 +527,20 @@ static void mc_trace_batched(kt_matrix_s* A, const AfunDev& F, double tol, int m
         KT_HIP(launch_rademacher_cols((int)n, mb, seed, base, dst, LB, st));
     };
     // S term of round itx: Y = F(P_{itx-1}..P_1 S_itx) into Yb (unprojected)
+    // The S term alone (round 1, or a round whose guess was wrong): its 10
+    // columns need f(A) x, so their sweep keeps the Lanczos basis.
+    // KT_MC_YBASIS=1 forms it with the y-form pass itself (KF_VB: one gather
+    // pass per step instead of K1 + K2; a tripped column redoes the sweep
+    // explicitly).  Measured at config 4 (round 6, profiles/r06/mc_ybasis_ab):
+    // 42.1 vs 41.7 ms per trace_exp -- the three basis streams and the
+    // P-wide slots' weighted sum cost what K2 saved on a lone sweep -- so the
+    // explicit sweep stays the default.
+    const char* ybe = getenv("KT_MC_YBASIS");
+    const int yb_cols = (ybe && ybe[0] == '1') ? mb : 0;
     auto s_term = [&](int itx) {
         rademacher_into((int64_t)(itx - 1) * 2 * mb, Bk.col(0));
         for (int k = (int)Qs.size() - 1; k >= 0; --k) project_ld(ctx, n, Qs[k].col(0), ld, mb, Bk.col(0), LB, mb);
-        lanczos_columns_split(A, Bk.col(0), LB, mb, mb, mb, F.m, F.fun, nullptr, Yb.col(0), ld, 16);
+        lanczos_columns_split(A, Bk.col(0), LB, mb, mb, mb, F.m, F.fun, nullptr, Yb.col(0), ld, 16, 16, yb_cols);
     };
     s_term(1);                                                             // :43-45
     std::vector<double> q(3 * mb);

@@ -230,9 +230,9 @@ void YSweep::finish() {
 // receives [alpha | up | low][m][P] followed by guard[P].  No basis:
 // quadratic forms only.
 YBlockSweep::YBlockSweep(kt_matrix_s* A_, const DevCSR& M_, int P_, int m_, const double* x_, int ldx_, int ncols_,
-                         const double* dnorms2_, double* rec_host_, int lane_)
+                         const double* dnorms2_, double* rec_host_, int lane_, double* basis_, int bcols_)
     : A(A_), M(M_), P(P_), m(m_), x(x_), ldx(ldx_), ncols(ncols_), dnorms2(dnorms2_), rec_host(rec_host_),
-      lane(lane_) {
+      lane(lane_), basis(basis_), bcols(basis_ ? bcols_ : 0) {
     kt_context_s* ctx = A->ctx;
     n = (int)A->n;
     if (lane < 0 || lane > 3) fail(KT_ERR_ARG, "sweep lane out of range");
@@ -257,7 +257,7 @@ YBlockSweep::YBlockSweep(kt_matrix_s* A_, const DevCSR& M_, int P_, int m_, cons
     guard = trec + (size_t)3 * m * P;
     flags = ctx->ky_flags | (A->unit_values ? 2 : 0);
     if (blk_bytes >= ((size_t)1 << 31)) flags &= ~16;  // sc1 buffer stores take 32-bit offsets
-    V0 = w.X1.as<double>();  // the start pass's gathered table v_0
+    V0 = basis ? slot(0) : w.X1.as<double>();  // the start pass's gathered table v_0 (basis slot 0)
     Xc = w.Y.as<double>();   // y_j
     Yo = nullptr;            // y_{j-1}
     Ot = w.X0.as<double>();  // y_{j+1}
@@ -282,7 +282,8 @@ void YBlockSweep::step(int j) {
     prof_begin(A->ctx, PROF_YBLOCK, st, P);
     KT_HIP(launch_spmm_lanczos(P, flags, grid1, M.rowptr, M.col, M.val, n, Xc, last ? nullptr : Yo,
                                last ? nullptr : Ot, ys + 6 * P, part, M.long_rows, M.n_long, A->long_thresh, lblocks,
-                               st));
+                               st, basis ? slot(j) : nullptr, (basis && j > 0) ? slot(j - 1) : nullptr,
+                               basis ? slot(j + 1) : nullptr, bcols));
     prof_end(A->ctx, PROF_YBLOCK, st);
     KT_HIP(launch_ycoef(P, part, grid1, 0, last, 0.0, ys, rec_at(0, j + 1), rec_at(1, j + 1), rec_at(2, j + 1), guard,
                         st));
@@ -326,8 +327,11 @@ int record_tridiag(const double* R, int m, int P, int c, double* al, double* off
 
 void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m, int fun,
                      double* quad, double* Y, int ldy) {
-    // every column by the explicit sweep (P = pow2 >= ncols, <= 16)
-    lanczos_columns_split(A, X, ldx, ncols, Y ? ncols : 0, ncols, m, fun, quad, Y, ldy, 0);
+    // every column by the explicit sweep (P = pow2 >= ncols, <= 16);
+    // KT_LC_YBASIS=1 (tests): the f(A) x columns by basis-forming y-form sweeps
+    const char* e = getenv("KT_LC_YBASIS");
+    const int yb = (e && e[0] == '1' && Y) ? ncols : 0;
+    lanczos_columns_split(A, X, ldx, ncols, Y ? ncols : 0, ncols, m, fun, quad, Y, ldy, 0, 16, yb);
 }
 
 // Widths of the y-form sweeps for `cols` quadrature-only columns: sweeps of
@@ -353,11 +357,12 @@ static std::vector<std::pair<int, int>> quad_plan(int cols, int chunk = 16) {
 }
 
 void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, int ny, int ne, int m, int fun,
-                           double* quad, double* Y, int ldy, int px, int ychunk) {
+                           double* quad, double* Y, int ldy, int px, int ychunk, int yb) {
     kt_context_s* ctx = A->ctx;
     const int64_t n = A->n;
     if (!Y) ny = 0;
     if (ny < 0 || ny > ne || ne > ncols) fail(KT_ERR_ARG, "lanczos_columns_split: 0 <= ny <= ne <= ncols");
+    yb = std::max(0, std::min(yb, ny));
     // squared column norms on the device (the sweeps' start scales are formed
     // from them there); the host reads them with the sweep records
     ctx->ws.colnorm.ensure(sizeof(double) * ncols);
@@ -393,22 +398,33 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     struct Sw {
         int c0, nc, P, lane;
         bool yform;
+        bool ybasis;  // a y-form sweep that also forms its Lanczos basis (KF_VB)
     };
     std::vector<Sw> sw;
     const char* ye = getenv("KT_LC_YFORM");  // 0: every column by the explicit sweep
-    if (ye && ye[0] == '0') ne = ncols;
+    if (ye && ye[0] == '0') {
+        ne = ncols;
+        yb = 0;
+    }
     int Pe = 1;
-    while (Pe < ne && Pe < 16) Pe <<= 1;
+    while (Pe < ne - yb && Pe < 16) Pe <<= 1;
     if (px > 0) Pe = px;
     if (Pe > 32 || (Pe & (Pe - 1))) fail(KT_ERR_ARG, "lanczos_columns_split: sweep width must be a power of two <= 32");
-    // sweeps dealt over the four lanes in order (explicit first), so up to
-    // four run side by side; a lane's later sweeps follow its earlier ones
+    // sweeps dealt over the four lanes in order (basis-forming y-form, then
+    // explicit, then forms-only y-form), so up to four run side by side; a
+    // lane's later sweeps follow its earlier ones
     int k = 0;
-    for (int c0 = 0; c0 < ne; c0 += Pe) sw.push_back({c0, std::min(Pe, ne - c0), Pe, k++ % 4, false});
+    for (int c0 = 0; c0 < yb; c0 += 16) {
+        const int c = std::min(16, yb - c0);
+        int P = 1;
+        while (P < c) P <<= 1;
+        sw.push_back({c0, c, P, k++ % 4, true, true});
+    }
+    for (int c0 = yb; c0 < ne; c0 += Pe) sw.push_back({c0, std::min(Pe, ne - c0), Pe, k++ % 4, false, false});
     {
         int c0 = ne;
         for (const auto& cp : quad_plan(ncols - ne, ychunk)) {
-            sw.push_back({c0, cp.first, cp.second, k++ % 4, true});
+            sw.push_back({c0, cp.first, cp.second, k++ % 4, true, false});
             c0 += cp.first;
         }
     }
@@ -433,11 +449,17 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
         KT_HIP(hipStreamWaitEvent(as, ready, 0));
         used[q.lane] = true;
     }
-    // the explicit sweeps keep their bases
+    // the explicit sweeps keep their bases (slot j: n x nyc); the basis-forming
+    // y-form sweeps theirs as m slots of n x P (normalised vectors: no scale
+    // history)
     std::vector<DevMat> bases(sw.size());
     std::vector<std::vector<double>> hists(sw.size());
     for (size_t i = 0; i < sw.size(); ++i) {
         const Sw& q = sw[i];
+        if (q.ybasis) {
+            bases[i].alloc(ctx, (int64_t)m * n, q.P, false);  // slot j = rows [j n, (j + 1) n)
+            continue;
+        }
         if (q.yform) continue;
         const int nyc = std::max(0, std::min(q.nc, ny - q.c0));
         if (nyc) bases[i].alloc(ctx, n, m * nyc, false);  // every slot is written by the sweep
@@ -449,14 +471,15 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     for (size_t i = 0; i < sw.size(); ++i) by_lane[sw[i].lane].push_back((int)i);
     for (;;) {
         std::vector<std::unique_ptr<ExplicitSweep>> ex;
-        std::vector<std::unique_ptr<YBlockSweep>> yb;
+        std::vector<std::unique_ptr<YBlockSweep>> ybs;
         for (int l = 0; l < 4; ++l) {
             if (next[l] >= (int)by_lane[l].size()) continue;
             const int i = by_lane[l][next[l]++];
             const Sw& q = sw[i];
             double* R = hr.as<double>() + rec_max * i;
             if (q.yform) {
-                yb.emplace_back(new YBlockSweep(A, M, q.P, m, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, R, q.lane));
+                ybs.emplace_back(new YBlockSweep(A, M, q.P, m, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, R, q.lane,
+                                                 q.ybasis ? bases[i].col(0) : nullptr, q.nc));
             } else {
                 const int nyc = std::max(0, std::min(q.nc, ny - q.c0));
                 ex.emplace_back(new ExplicitSweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, R,
@@ -464,15 +487,15 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
                                                   nyc));
             }
         }
-        if (ex.empty() && yb.empty()) break;
-        for (auto& y : yb) y->start();
+        if (ex.empty() && ybs.empty()) break;
+        for (auto& y : ybs) y->start();
         for (auto& e : ex) e->start();
         for (int j = 0; j < m; ++j) {
-            for (auto& y : yb)
+            for (auto& y : ybs)
                 if (j + 1 < m) y->step(j);
             for (auto& e : ex) e->step(j);
         }
-        for (auto& y : yb) y->finish();
+        for (auto& y : ybs) y->finish();
         for (auto& e : ex) e->finish();
     }
     KT_HIP(hipStreamSynchronize(ctx->stream));
@@ -483,7 +506,13 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     // redone by the explicit CGS2 sweep at the same width; only the tripped
     // columns take the redo's records, so a column's form never depends on
     // which columns share its sweep (mc_trace's world-size bit identity)
+    // A basis-forming sweep with a tripped column is redone WHOLE by the
+    // explicit sweep with its basis (its columns are f(A) x inputs, not
+    // sharded forms): the sweep then takes the explicit path's records,
+    // basis and scale history.
     std::vector<double> redo;
+    std::vector<char> ex_basis(sw.size(), 0);  // the sweep's basis is the explicit layout
+    for (size_t i = 0; i < sw.size(); ++i) ex_basis[i] = !sw[i].yform;
     for (size_t i = 0; i < sw.size(); ++i) {
         const Sw& q = sw[i];
         if (!q.yform) continue;
@@ -493,6 +522,18 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
         for (int c = 0; c < q.nc; ++c)
             if (norms2[q.c0 + c] > 0.0 && !(g[c] >= kYformGuard)) bad.push_back(c);
         if (bad.empty()) continue;
+        if (q.ybasis) {
+            const int nyc = std::max(0, std::min(q.nc, ny - q.c0));
+            DevMat eb;
+            if (nyc) eb.alloc(ctx, n, m * nyc, false);
+            lanczos_sweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, R, nyc ? &eb : nullptr,
+                          nyc ? &hists[i] : nullptr, 0, nyc);
+            KT_HIP(hipStreamSynchronize(ctx->stream));
+            bases[i] = std::move(eb);
+            ex_basis[i] = 1;
+            ctx->yform_redone += 1;
+            continue;
+        }
         redo.assign((size_t)3 * m * q.P, 0.0);
         lanczos_sweep(A, M, q.P, m, 0, 0, Xs + q.c0, ldxs, q.nc, dn2 + q.c0, redo.data(), nullptr, nullptr, 0);
         KT_HIP(hipStreamSynchronize(ctx->stream));
@@ -506,7 +547,7 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
     std::vector<std::vector<double>> Ws(sw.size());  // Y = sum_j u_j w_j, [j * nyc + c]
     for (size_t i = 0; i < sw.size(); ++i) {
         const Sw& q = sw[i];
-        nycs[i] = q.yform ? 0 : std::max(0, std::min(q.nc, ny - q.c0));
+        nycs[i] = (q.yform && !q.ybasis) ? 0 : std::max(0, std::min(q.nc, ny - q.c0));
         Ws[i].assign((size_t)m * std::max(nycs[i], 1), 0.0);
         for (int c = 0; c < q.nc; ++c) {
             col_sw.push_back((int)i);
@@ -530,8 +571,12 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
         const double qd = tridiag_fun_e1(steps, al.data(), off.data(), fun, fe1.data());
         if (quad) quad[q.c0 + c] = norms2[q.c0 + c] * qd;
         const double nx = std::sqrt(norms2[q.c0 + c]);
-        for (int j = 0; j < steps; ++j)
-            Ws[i][(size_t)j * nyc + c] = nx * hists[i][(size_t)j * q.P + c] * fe1[j];  // v_j = s_j u_j
+        if (ex_basis[i]) {
+            for (int j = 0; j < steps; ++j)
+                Ws[i][(size_t)j * nyc + c] = nx * hists[i][(size_t)j * q.P + c] * fe1[j];  // v_j = s_j u_j
+        } else {  // the y-form basis holds the normalised v_j
+            for (int j = 0; j < steps; ++j) Ws[i][(size_t)j * nyc + c] = nx * fe1[j];
+        }
     }, 4);
     for (size_t i = 0; i < sw.size(); ++i) {
         const Sw& q = sw[i];
@@ -541,7 +586,9 @@ void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, 
             DevBuf& dw = ctx->ws.small2;
             dw.ensure(sizeof(double) * W.size());
             KT_HIP(hipMemcpyAsync(dw.ptr, W.data(), sizeof(double) * W.size(), hipMemcpyHostToDevice, ctx->stream));
-            KT_HIP(launch_weighted_sum((int)n, m, nyc, nyc, bases[i].col(0), nyc, (int64_t)n * nyc, dw.as<double>(),
+            // explicit basis: slot j = n x nyc; y-form basis: slot j = n x P
+            const int ldu = ex_basis[i] ? nyc : q.P;
+            KT_HIP(launch_weighted_sum((int)n, m, nyc, nyc, bases[i].col(0), ldu, (int64_t)n * ldu, dw.as<double>(),
                                        Ys + q.c0, ldys, ctx->stream));
             KT_HIP(hipStreamSynchronize(ctx->stream));
         }

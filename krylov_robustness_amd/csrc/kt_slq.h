@@ -78,10 +78,13 @@ class YSweep {
 
 // lanczos_sweep_y_block enqueued step by step: start(), step(j) for j < m - 1,
 // finish(); same interleaving rule as ExplicitSweep.
+// With `basis` (m slots of n x P, slot j at basis + j n P; bcols > 0) the
+// sweep also forms the normalised Lanczos vectors v_0 .. v_{m-1} of its
+// first bcols columns there (KF_VB passes; v_0 is the start table itself).
 class YBlockSweep {
    public:
     YBlockSweep(kt_matrix_s* A, const DevCSR& M, int P, int m, const double* x, int ldx, int ncols,
-                const double* dnorms2, double* rec_host, int lane);
+                const double* dnorms2, double* rec_host, int lane, double* basis = nullptr, int bcols = 0);
     void start();
     void step(int j);
     void finish();
@@ -101,6 +104,9 @@ class YBlockSweep {
     hipStream_t st = nullptr;
     double *part = nullptr, *ys = nullptr, *trec = nullptr, *guard = nullptr;
     double *V0 = nullptr, *Xc = nullptr, *Yo = nullptr, *Ot = nullptr;
+    double* basis = nullptr;
+    int bcols = 0;
+    double* slot(int j) { return basis + (size_t)j * n * P; }
 };
 
 int record_tridiag(const double* R, int m, int P, int c, double* al, double* off);
@@ -124,8 +130,12 @@ void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m,
 // ychunk: columns per y-form sweep (each sweep at the power of two >= its
 // columns, <= 16): 16 packs them; a smaller chunk splits them evenly (mc_trace's
 // final round: [Q | pad] and [G | pad] instead of 16 + 4).
+// yb (<= ny): the first yb columns run as y-form sweeps that also form their
+// Lanczos basis (KF_VB) instead of the explicit sweep: columns [0, yb) y-form
+// with basis, [yb, ne) explicit, [ne, ncols) y-form forms only.  A y-form
+// basis sweep whose guard trips is redone whole by the explicit sweep.
 void lanczos_columns_split(kt_matrix_s* A, const double* X, int ldx, int ncols, int ny, int ne, int m, int fun,
-                           double* quad, double* Y, int ldy, int px = 0, int ychunk = 16);
+                           double* quad, double* Y, int ldy, int px = 0, int ychunk = 16, int yb = 0);
 
 // y-form sweep seeded by a device block (see kt_slq.cpp)
 void lanczos_sweep_y_block(kt_matrix_s* A, const DevCSR& M, int P, int m, const double* x, int ldx, int ncols,

@@ -152,6 +152,53 @@ def test_lanczos_fmv_matches_oracle(kra, gpu_ctx):
     np.testing.assert_allclose(Y, Yo, rtol=1e-8, atol=1e-10 * np.abs(Yo).max())
 
 
+def test_lanczos_fmv_yform_basis_matches_oracle(kra, gpu_ctx, monkeypatch):
+    """f(A) x with the Lanczos basis formed by the y-form pass itself (KF_VB:
+    v_{j+1} = g y_j - a v_j - b v_{j-1} with the pass's own coefficients;
+    KT_LC_YBASIS=1 routes lanczos_fmv through it): 4 columns and 40 columns
+    (three 16-wide sweeps, the last padded) match the oracle and the explicit
+    CGS2 sweep's result.  A column that is an eigenvector of A (a lucky
+    breakdown at step 1) trips the y-form guard: its sweep is redone whole by
+    the explicit sweep with its basis, still matching the oracle."""
+    import scipy.sparse.linalg as sla
+    A = load_graph("rome")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    for ncol, seed in ((4, 2), (40, 5)):
+        X = np.random.default_rng(seed).normal(size=(A.shape[0], ncol))
+        Ye = kra.lanczos_fmv(D, X, m=20, fun="exp", ctx=gpu_ctx)
+        monkeypatch.setenv("KT_LC_YBASIS", "1")
+        Y = kra.lanczos_fmv(D, X, m=20, fun="exp", ctx=gpu_ctx)
+        monkeypatch.delenv("KT_LC_YBASIS")
+        Yo = ko.lanczos_fmv(A, X, 20, "exp")
+        np.testing.assert_allclose(Y, Yo, rtol=1e-8, atol=1e-10 * np.abs(Yo).max())
+        np.testing.assert_allclose(Y, Ye, rtol=1e-9, atol=1e-11 * np.abs(Ye).max())
+    w, v = sla.eigsh(A.astype(np.float64), k=1, which="LA")
+    X = np.random.default_rng(9).normal(size=(A.shape[0], 3))
+    X[:, 1] = v[:, 0]
+    before = gpu_ctx.stat(0)
+    monkeypatch.setenv("KT_LC_YBASIS", "1")
+    Y = kra.lanczos_fmv(D, X, m=20, fun="exp", ctx=gpu_ctx)
+    monkeypatch.delenv("KT_LC_YBASIS")
+    assert gpu_ctx.stat(0) > before  # the explicit redo ran
+    Yo = ko.lanczos_fmv(A, X, 20, "exp")
+    np.testing.assert_allclose(Y, Yo, rtol=1e-8, atol=1e-10 * np.abs(Yo).max())
+
+
+def test_mc_trace_s_term_yform_basis(kra, gpu_ctx, monkeypatch):
+    """mc_trace with the Lanczos Afun can form the lone S term's f(A) S with
+    the basis-forming y-form sweep (KT_MC_YBASIS=1) instead of the explicit
+    sweep (the default): the same rounds and the estimate to 1e-11."""
+    A = load_graph("oregon_A0")
+    D = kra.DeviceMatrix(A, gpu_ctx)
+    kw = dict(tol=1e-6, maxit=120, isAreal=1, seed=3, fun="exp", m=20)
+    ref = kra.mc_trace("lanczos", None, A=D, ctx=gpu_ctx, **kw)
+    monkeypatch.setenv("KT_MC_YBASIS", "1")
+    got = kra.mc_trace("lanczos", None, A=D, ctx=gpu_ctx, **kw)
+    monkeypatch.delenv("KT_MC_YBASIS")
+    assert got[2] == ref[2]
+    assert got[0] == pytest.approx(ref[0], rel=1e-11)
+
+
 def test_lanczos_fmv_many_columns_over_lanes(kra, gpu_ctx):
     """40 columns: three 16-wide explicit sweeps (the last zero-padded) queued
     step by step on three sweep lanes (kt_slq.cpp lanczos_columns_split).
