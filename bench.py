@@ -659,33 +659,26 @@ def _reference_composition(kra, D, ctx, A, ref, budget_s):
     Acsr = A.tocsr()
     n = Acsr.shape[0]
     # (1) the C + OpenMP restatement of the same algorithm (oracle/mctrace_ref.c)
-    # on every CPU this process may use: round 1's first Afun call -- one
-    # whole expmv call, every stage and term, on S_1 (mc_trace.m:43-45) --
-    # and the host work of a round (qr(., 0), one projection), extrapolated
-    # to the GPU run's calls, terms, rounds and projections
+    # on every CPU this process may use: ONE WHOLE trace_exp evaluation
+    # (trace_exp.m:5-6, seed 0: every mc_trace round, qr, projection, expmv
+    # call and Taylor term), timed -- a measurement, not an extrapolation
+    # (about a minute on 16 cores; --ref-cpu-seconds 0 skips the CPU legs)
     from oracle import mctrace_ref as MR
     cores, detail = cpu_share()
-    S1 = O.rademacher(n, range(10), 0)
     t0 = time.perf_counter()
-    _, s_c, m_c, mv_c, st = MR.expmv(1.0, Acsr, S1, nthreads=cores)
-    call_s = time.perf_counter() - t0
-    t_qr, t_proj = MR.round_host_times(n, seed=0, nthreads=cores)
-    t_term = st["t_terms"] / max(st["terms"], 1)
-    nproj = sum(6 * r - 4 for r in range(1, it + 1))  # block projections of `it` nested rounds
-    est = calls * st["t_select"] + terms * t_term + it * t_qr + nproj * t_proj
+    tr_c, res_c, it_c, st = MR.trace_exp(Acsr, seed=0, tol=1e-4, maxit=1000, nthreads=cores)
+    cpu_s = time.perf_counter() - t0
     out["cpu_baseline"] = {
-        "value": 1.0 / est if est > 0 else None, "unit": "evals/s", "cores": cores, "kind": "port",
+        "value": 1.0 / cpu_s, "unit": "evals/s", "cores": cores, "kind": "port",
         "algorithm": "the reference's: mc_trace + expmv + select_taylor_degree + normAm "
                      "(oracle/mctrace_ref.c, C + OpenMP over rows; equals the numpy restatement)",
-        "seconds_per_eval": round(est, 2),
-        "sample": f"one whole expmv call (round 1's S block: s = {s_c}, m = {m_c}, {st['terms']} Taylor terms, "
-                  f"select_taylor_degree {st['t_select']:.2f} s, {call_s:.1f} s in all) and one qr(., 0) "
-                  f"({t_qr:.3f} s) + one projection ({t_proj:.3f} s) of an n x 10 block on {cores} OpenMP "
-                  f"threads, extrapolated from that whole call to the GPU run's {calls} expmv calls, {terms} "
-                  f"Taylor terms, {it} rounds and {nproj} projections",
-        "sample_call": {"s": s_c, "m": m_c, "terms": st["terms"], "mv": mv_c, "seconds": round(call_s, 3),
-                        "select_taylor_degree_s": round(st["t_select"], 3), "term_s": round(t_term, 5)},
-        "qr_s": round(t_qr, 4), "projection_s": round(t_proj, 4), **detail}
+        "seconds_per_eval": round(cpu_s, 2),
+        "sample": f"one whole evaluation (seed 0, the GPU run's seed: {it_c} rounds, every expmv call and "
+                  f"Taylor term, qr and projection) on {cores} OpenMP threads, timed",
+        "trace_estimate": tr_c, "rounds": it_c,
+        "rel_diff_vs_gpu": (tr_c - tr) / tr if tr else None,
+        "stats": st, **detail}
+    S1 = O.rademacher(n, range(10), 0)
     # (2) beside it, the numpy/SciPy restatement (oracle/krylov_oracle.py) on ONE
     # thread (SciPy's sparse @ dense is single-threaded), a shorter sample: one
     # select_taylor_degree call and the first Taylor terms of one 10-column call

@@ -344,13 +344,17 @@ void lanczos_columns(kt_matrix_s* A, const double* X, int ldx, int ncols, int m,
 // sweeps (8 + 2, 16 + 8 + 4 + 2) cost 53 ms.
 // A smaller `chunk` cuts the columns into sweeps of `chunk` (the last one
 // shorter), each at the power of two that holds it: {(columns, width)}.
+// KT_LC_YMINP (A/B): the narrowest y-form sweep width (a remainder of 4
+// columns padded to 8 or 16 instead of a 4-wide sweep).
 static std::vector<std::pair<int, int>> quad_plan(int cols, int chunk = 16) {
     std::vector<std::pair<int, int>> wv;
     chunk = std::max(1, std::min(chunk, 16));
+    const char* e = getenv("KT_LC_YMINP");
+    const int pmin = e ? std::max(1, std::min(16, atoi(e))) : 1;
     for (int left = cols; left > 0; left -= chunk) {
         const int c = std::min(left, chunk);
         int P = 1;
-        while (P < c) P <<= 1;
+        while (P < c || P < pmin) P <<= 1;
         wv.push_back({c, P});
     }
     return wv;
