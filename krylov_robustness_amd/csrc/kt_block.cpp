@@ -551,6 +551,10 @@ void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vect
         dmax = std::max(dmax, R1[k + (size_t)k * bs]);
         dmin = std::min(dmin, R1[k + (size_t)k * bs]);
     }
+    static const bool qr_log = std::getenv("KT_QR_LOG") != nullptr;  // diagnostics: the QR path per block
+    if (qr_log)
+        std::fprintf(stderr, "kt_qr n=%lld bs=%d chol=%d dmin=%.3e dmax=%.3e allow_shifted=%d\n", (long long)n, bs,
+                     (int)ok, ok ? dmin : -1.0, ok ? dmax : -1.0, (int)allow_shifted);
     if (!ok || !(dmin >= 1e-4 * dmax) || !(dmax > 1e-6)) {
         // block Arnoldi (allow_shifted): an
         // ill-conditioned block that is not at a breakdown takes shifted
@@ -591,6 +595,8 @@ void block_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vect
 // kernels of kt_tsqr.hip.  Exactly rank-deficient W takes dlarfg's tau = 0
 // branch, so its completion matches LAPACK's.
 void householder_qr(kt_context_s* ctx, int64_t n, double* W, int ld, int bs, std::vector<double>& R) {
+    static const bool qr_log = std::getenv("KT_QR_LOG") != nullptr;
+    if (qr_log) std::fprintf(stderr, "kt_hh n=%lld bs=%d\n", (long long)n, bs);
     R.assign((size_t)bs * bs, 0.0);
     if (n == 0 || bs == 0) return;
     if (n < bs) fail(KT_ERR_UNSUPPORTED, "thin QR needs n >= block size");
