@@ -608,6 +608,13 @@ def _reference_composition(kra, D, ctx, A, ref, budget_s):
     os.environ["KT_TWIN"] = "0"
     os.environ["KT_MC_SPEC"] = "0"
     try:
+        # one untimed call first (seed 1), as the headline's warm-up: the
+        # natural-order CSR and its task lists are built on first use and
+        # select_taylor_degree's result is cached per matrix version (the
+        # same inputs give the same (s, m) every call), so the timed call is
+        # a steady-state trace_exp on a resident A -- the drop-in's
+        # situation across MATLAB calls (kt_mex.cpp keeps A on the device)
+        kra.mc_trace("expmv", None, 1e-4, 1000, 1, 0, seed=1, A=D, ctx=ctx)
         c0, k0 = ctx.stat(3), ctx.stat(4)
         ctx.profile_reset()
         ctx.profile(True)  # HIP events around every Taylor-term launch (slot 4)
@@ -627,7 +634,8 @@ def _reference_composition(kra, D, ctx, A, ref, budget_s):
     out = {"afun": "expmv (trace_exp.m:5-6 as the reference composes it), tol 1e-4, maxit 1000, seed 0",
            "gpu_ms": round(gpu_s * 1e3, 2), "gpu_evals_per_s": round(1.0 / gpu_s, 4), "rounds": it,
            "trace_estimate": tr, "expmv_calls": calls, "taylor_terms": terms,
-           "gpu_mode": "serial: every expmv call on one stream (KT_TWIN=0, KT_MC_SPEC=0)"}
+           "gpu_mode": "serial: every expmv call on one stream (KT_TWIN=0, KT_MC_SPEC=0); after one "
+                       "untimed warm-up call (seed 1: CSR build, cached Taylor-degree selection)"}
     if ref:
         out["rel_err"] = (tr - ref["value"]) / ref["value"]
     # the term kernel's roofline: one active term = expmv.m:75-78 on the

@@ -1733,13 +1733,13 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
 // 4 waves per workgroup (108 VGPRs, 4 waves per SIMD); measured flat against
 // 5 waves per SIMD at shallower gathers (4-deep short rows, 2-deep medium).
 constexpr int kExpmvRowsWaves = 4;
-template <int P, int FLAGS>
+template <int P, int FLAGS, bool CHECK>
 __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
     const int* __restrict__ rp, const int* __restrict__ ci, const double* __restrict__ va, int n,
     const int* __restrict__ long_rows, int n_long, int n_heavy, const int4* __restrict__ med_tasks, int n_med,
     const int4* __restrict__ short_tasks, int n_short,
     int nc, int ld, double mu, double coef, int k, const double* __restrict__ bin,
-    double* __restrict__ bout, double* __restrict__ F, ExpmvState* st) {
+    double* __restrict__ bout, double* __restrict__ F, ExpmvState* st, double tol, int* hflag, int stage) {
     constexpr int WAVES = kExpmvRowsWaves;
     constexpr int VW = 4;                                          // the fused kernel's waves per long row
     using G = GeoW<P, (P >= 2) ? 2 : 1>;                          // short rows
@@ -1751,10 +1751,49 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
     __shared__ double lsum[WAVES][P];  // a heavy row's chain-set sums
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) decide = st->active;
+    if (wave == 0) {
+        // CHECK (fused, round 6): the stop test of term k - 1 (expmv.m:79-82)
+        // from its 64 slots, evaluated by every workgroup before any gather
+        // (so a term past the stop costs one round trip, not a pass) --
+        // the same test k_expmv_slot_check runs as its own launch.  Every
+        // workgroup reads the same slots (written by the previous launch) and
+        // reaches the same decision; block 0 alone records it (active = 0 and
+        // the host flag, or c1s[k & 1] = c2), counts the term and zeroes the
+        // next term's slot set (k + 1) % 3, last read by the check of term
+        // k - 2 in the previous launch.  Without CHECK the separate launch
+        // did all of that and `active` decides.
+        int run = st->active;
+        if (CHECK && k > 1 && run) {
+            unsigned long long pmb = st->term_max[(k - 1) % 3][lane][0], pmf = st->term_max[(k - 1) % 3][lane][1];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const unsigned long long xb = __shfl_xor(pmb, o, 64), xf = __shfl_xor(pmf, o, 64);
+                pmb = xb > pmb ? xb : pmb;
+                pmf = xf > pmf ? xf : pmf;
+            }
+            const double c1 = st->c1s[(k - 1) & 1];
+            const double c2 = __longlong_as_double((long long)pmb), nf = __longlong_as_double((long long)pmf);
+            if (c1 + c2 <= tol * nf) {
+                run = 0;
+                if (blockIdx.x == 0 && lane == 0) {
+                    st->active = 0;
+                    if (hflag) __hip_atomic_store(hflag, stage, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            } else if (blockIdx.x == 0 && lane == 0) {
+                st->c1s[k & 1] = c2;
+            }
+        }
+        if (run && blockIdx.x == 0) {
+            if (lane == 0) st->mv += 1;
+            if (CHECK) {
+                st->term_max[(k + 1) % 3][lane][0] = 0ull;
+                st->term_max[(k + 1) % 3][lane][1] = 0ull;
+            }
+        }
+        if (lane == 0) decide = run;
+    }
     __syncthreads();
     if (!decide) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->mv += 1;
     const int gw = blockIdx.x * WAVES + wave, TW = gridDim.x * WAVES;
     __builtin_assume(gw >= 0);
     __builtin_assume(TW > 0);
@@ -1935,12 +1974,16 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
             for (int i = 0; i < MD; ++i) mc[i] = mn[i];
         }
     }
-    constexpr int SD = 8;  // short rows: gathers in flight per row group
+    constexpr int SD = 8;            // short rows: gathers in flight per row group
+    // short rows: column indices loaded one block ahead (all 16 of a short
+    // row measured equal to 8: 1,070-1,076 vs 1,067-1,070 ms per warm
+    // trace_exp, profiles/r06/expmv_rows_ab)
+    constexpr int SCOL = 8;
     // (3) short rows, in the task list's order (degree-descending, so the
     //     GPW rows of a wave take the same number of gather rounds), GPW
     //     tasks per wave, software-pipelined: while block b gathers, the
-    //     first SD column indices of block b + TW and the tasks of block
-    //     b + 2 TW are in flight
+    //     first SCOL column indices of block b + TW (every column of a short
+    //     row at SCOL = 16) and the tasks of block b + 2 TW are in flight
     const int nblk = (n_short + G::GPW - 1) / G::GPW;
     auto load_task = [&](int bb, int& r, int& bg, int& en) {
         const int t = bb * G::GPW + grp;
@@ -1953,11 +1996,11 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
             en = v.z;
         }
     };
-    auto load_chunk = [&](int bg, int en, int* c) {  // a row's first SD columns (tail: its first)
+    auto load_chunk = [&](int bg, int en, int* c) {  // a row's first SCOL columns (tail: its first)
         const int c0 = bg < en ? ld_stream<FLAGS>(ci + bg) : 0;
         c[0] = c0;
 #pragma unroll
-        for (int i = 1; i < SD; ++i) c[i] = (bg + i < en) ? ld_stream<FLAGS>(ci + bg + i) : c0;
+        for (int i = 1; i < SCOL; ++i) c[i] = (bg + i < en) ? ld_stream<FLAGS>(ci + bg + i) : c0;
     };
     // mu = 0: the rows' own f is loaded one block ahead too
     auto load_f = [&](int r, double* f) {
@@ -1970,7 +2013,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
     int b = gw;
     int row, beg, end, nrow, nbeg, nend;
     load_task(b, row, beg, end);
-    int cc[SD];
+    int cc[SCOL];
     load_chunk(beg, end, cc);
     double fc[G::VEC];
     load_f(row, fc);
@@ -1978,7 +2021,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
     for (; b < nblk; b += TW) {
         int nnrow, nnbeg, nnend;
         load_task(b + 2 * TW, nnrow, nnbeg, nnend);
-        int cn[SD];
+        int cn[SCOL];
         load_chunk(nbeg, nend, cn);
         double fn[G::VEC];
         load_f(nrow, fn);
@@ -1988,26 +2031,31 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
             double s[G::VEC], fo[G::VEC], bo[G::VEC];
 #pragma unroll
             for (int e = 0; e < G::VEC; ++e) s[e] = 0.0;
-            {   // first chunk (the prefetched columns), then the rest as row_gather8
+            // the prefetched columns in rounds of SD gathers, then (rows longer
+            // than SCOL) the rest as row_gather8 -- one chain in CSR order
+#pragma unroll
+            for (int h = 0; h < SCOL / SD; ++h) {
+                const int k0 = beg + h * SD;
+                if (h > 0 && k0 >= end) break;
                 // unit weights: fma(1, x, s) = s + x and fma(0, x, s) = s (a
                 // masked tail entry), so the weights are predicates, not registers
                 double a[(FLAGS & KF_UNIT) ? 1 : SD];
                 if constexpr (!(FLAGS & KF_UNIT)) {
 #pragma unroll
-                    for (int i = 0; i < SD; ++i) a[i] = (beg + i < end) ? ld_stream<FLAGS>(va + beg + i) : 0.0;
+                    for (int i = 0; i < SD; ++i) a[i] = (k0 + i < end) ? ld_stream<FLAGS>(va + k0 + i) : 0.0;
                 }
                 typename VV::T x[SD];
 #pragma unroll
-                for (int i = 0; i < SD; ++i) x[i] = VV::load(bin + (int64_t)cc[i] * ld + p0);
+                for (int i = 0; i < SD; ++i) x[i] = VV::load(bin + (int64_t)cc[h * SD + i] * ld + p0);
 #pragma unroll
                 for (int i = 0; i < SD; ++i)
 #pragma unroll
                     for (int e = 0; e < G::VEC; ++e) {
-                        if constexpr (FLAGS & KF_UNIT) s[e] = (beg + i < end) ? s[e] + VV::get(x[i], e) : s[e];
+                        if constexpr (FLAGS & KF_UNIT) s[e] = (k0 + i < end) ? s[e] + VV::get(x[i], e) : s[e];
                         else s[e] = fma(a[i], VV::get(x[i], e), s[e]);
                     }
             }
-            row_gather8<P, FLAGS, G, SD>(beg + SD, end, 1, p0, ci, va, bin, s, ld);
+            row_gather8<P, FLAGS, G, SD>(beg + SCOL, end, 1, p0, ci, va, bin, s, ld);
             if constexpr (MU0) {
 #pragma unroll
                 for (int e = 0; e < G::VEC; ++e) fo[e] = fc[e];
@@ -2026,7 +2074,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
         nbeg = nnbeg;
         nend = nnend;
 #pragma unroll
-        for (int i = 0; i < SD; ++i) cc[i] = cn[i];
+        for (int i = 0; i < SCOL; ++i) cc[i] = cn[i];
     }
     // (4) this workgroup's maxima into slot blockIdx % 64 of set k % 3
 #pragma unroll
@@ -2422,7 +2470,7 @@ static int expmv_rows_grid(int n_tasks_hint) {
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         int occ = 0;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_expmv_rows<16, KF_UNIT | KF_MU0>,
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_expmv_rows<16, KF_UNIT | KF_MU0, true>,
                                                            64 * kExpmvRowsWaves, 0);
         per_cu = occ > 0 ? occ : 2;
         if (cus <= 0) cus = 256;
@@ -2437,8 +2485,9 @@ hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_
                              double* bout, double* F, void* state, hipStream_t st, int form, int* hflag,
                              int stage) {
     ExpmvState* s = static_cast<ExpmvState*>(state);
-    if (form == 2 && !(M.short_tasks && M.med_tasks)) form = 1;  // no task lists: the split kernel
-    if (form == 2) {
+    if ((form == 2 || form == 3) && !(M.short_tasks && M.med_tasks)) form = 1;  // no task lists: the split kernel
+    if (form == 2 || form == 3) {
+        const bool fused_check = form == 3;
         // KT_EXPMV_CLASSES (timing diagnostics only; the results are WRONG):
         // bit mask of the row classes the term processes, 1 long, 2 medium, 4 short
         static const int classes = [] {
@@ -2451,9 +2500,14 @@ hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_
         const int tasks = nl + nm + (ns + 7) / 8;
         const int grid = expmv_rows_grid((tasks + kExpmvRowsWaves - 1) / kExpmvRowsWaves);
 #define KT_EXPMV_ROWS(PP, F_)                                                                      \
-    k_expmv_rows<PP, F_><<<grid, 64 * kExpmvRowsWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, nl, nh, \
-        reinterpret_cast<const int4*>(M.med_tasks), nm, reinterpret_cast<const int4*>(M.short_tasks), ns, \
-        nc, ld, mu, coef, k, bin, bout, F, s)
+    if (fused_check)                                                                               \
+        k_expmv_rows<PP, F_, true><<<grid, 64 * kExpmvRowsWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, \
+            nl, nh, reinterpret_cast<const int4*>(M.med_tasks), nm, reinterpret_cast<const int4*>(M.short_tasks), \
+            ns, nc, ld, mu, coef, k, bin, bout, F, s, tol, hflag, stage);                          \
+    else                                                                                           \
+        k_expmv_rows<PP, F_, false><<<grid, 64 * kExpmvRowsWaves, 0, st>>>(M.rp, M.ci, M.va, M.n, M.long_rows, \
+            nl, nh, reinterpret_cast<const int4*>(M.med_tasks), nm, reinterpret_cast<const int4*>(M.short_tasks), \
+            ns, nc, ld, mu, coef, k, bin, bout, F, s, tol, hflag, stage)
 #define KT_EXPMV_ROWS_P(PP)                                                                        \
     if (mu == 0.0) {                                                                               \
         if (unit) KT_EXPMV_ROWS(PP, KF_UNIT | KF_MU0);                                             \

@@ -200,7 +200,9 @@ int expmv_step_blocks(int n, int P, int n_long, int n_med, int waves = 0);
 // above 1,024 workgroups); with split the host launches
 // launch_expmv_slot_check after every term but a stage's last.
 // launch_expmv_step form: 0 fused, 1 split (a workgroup per row class unit),
-// 2 split, row-blocked (k_expmv_rows: resident workgroups; the default split form)
+// 2 row-blocked (k_expmv_rows: resident workgroups) with the stop test in
+// k_expmv_slot_check, 3 row-blocked with the stop test of term k - 1 at the
+// start of term k (no slot-check launch; the default on large grids)
 bool expmv_split_check(int n, int P, int n_long, int n_med);
 hipError_t launch_expmv_slot_check(void* state, int k, double tol, hipStream_t st, int* hflag, int stage);
 hipError_t launch_expmv_step(int P, bool unit, const CsrView& M, const int* med_rows, int n_med, int nc,

@@ -326,10 +326,15 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
         // KT_EXPMV_SPLIT=0 / 1 forces the fused / split term form (read per call)
         const char* spe = std::getenv("KT_EXPMV_SPLIT");
         const bool split = spe ? spe[0] == '1' : expmv_split_check((int)n, P, M0.n_long, M0.n_med);
-        // the split form runs row-blocked (k_expmv_rows, resident workgroups);
-        // KT_EXPMV_ROWS=0 selects the workgroup-per-row-class split kernel (A/B)
+        // the split form runs row-blocked (k_expmv_rows, resident workgroups)
+        // with each term's kernel first testing the previous term's stop
+        // (form 3); KT_EXPMV_ROWS=0 selects the workgroup-per-row-class split
+        // kernel, KT_EXPMV_ROWCHECK=0 the row-blocked one with the separate
+        // slot-check launch (A/B)
         const char* rwe = std::getenv("KT_EXPMV_ROWS");
-        const int form = !split ? 0 : (rwe && rwe[0] == '0') ? 1 : 2;
+        const char* rce = std::getenv("KT_EXPMV_ROWCHECK");
+        int form = !split ? 0 : (rwe && rwe[0] == '0') ? 1 : (rce && rce[0] == '0') ? 2 : 3;
+        if (form >= 2 && !(M0.short_tasks && M0.med_tasks)) form = 1;  // (the launcher's own fallback)
         // (Measured and dropped, round 6: the Taylor loop on hubs-first copies
         // of b and f with each row in natural column order -- bit-identical --
         // ran 16 % slower than the natural table, profiles/r06/expmv_rows_ab.)
@@ -378,7 +383,7 @@ static Expmv expmv_device(kt_matrix_s* A, double t, const double* Bsrc, int ld, 
                 KT_HIP(launch_expmv_step(P, A->unit_values, V, M.med_rows, M.n_med, nc, ld, mu,
                                          t / ((double)r.s * k), tol, k, cur, nxt, F, state, st, form, hflag, i));
                 prof_end(ctx, PROF_EXPMV, st);
-                if (split && k < r.m) KT_HIP(launch_expmv_slot_check(state, k, tol, st, hflag, i));
+                if ((form == 1 || form == 2) && k < r.m) KT_HIP(launch_expmv_slot_check(state, k, tol, st, hflag, i));
                 if (ahead) KT_HIP(hipEventRecord(ring[queued % ahead], st));
                 ++queued;
                 std::swap(cur, nxt);

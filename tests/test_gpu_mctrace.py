@@ -84,11 +84,14 @@ def test_expmv_split_check_form(kra, gpu_ctx, monkeypatch, graph):
     and agree with the oracle; the first column alone (P = 1) too."""
     A = _expmv_graph(graph)
     b = np.random.default_rng(7).normal(size=(A.shape[0], 10))
-    # (KT_EXPMV_SPLIT, KT_EXPMV_ROWS, KT_EXPMV_SORTWIN): fused; split;
-    # row-blocked (short rows degree-sorted in windows of 4,096 rows, the
-    # default); row-blocked with the whole matrix's short rows degree-sorted
-    forms = (("0", None, None), ("1", "0", None), ("1", None, None), ("1", None, "0"))
-    keys = ("KT_EXPMV_SPLIT", "KT_EXPMV_ROWS", "KT_EXPMV_SORTWIN")
+    # (KT_EXPMV_SPLIT, KT_EXPMV_ROWS, KT_EXPMV_SORTWIN, KT_EXPMV_ROWCHECK):
+    # fused; split; row-blocked (short rows degree-sorted in windows of 4,096
+    # rows, each term testing the previous term's stop: the default);
+    # row-blocked with the whole matrix's short rows degree-sorted; row-blocked
+    # with the separate slot-check launch
+    forms = (("0", None, None, None), ("1", "0", None, None), ("1", None, None, None), ("1", None, "0", None),
+             ("1", None, None, "0"))
+    keys = ("KT_EXPMV_SPLIT", "KT_EXPMV_ROWS", "KT_EXPMV_SORTWIN", "KT_EXPMV_ROWCHECK")
     for B in (b, b[:, :1]):
         outs = []
         for f in forms:

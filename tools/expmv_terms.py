@@ -11,6 +11,27 @@ import re
 import sys
 
 
+def gaps(path, top=12):
+    """Idle time of the device between consecutive kernels (all kernels of
+    the trace), the largest gaps with the kernels either side."""
+    ks = []
+    for r in csv.DictReader(open(path)):
+        m = re.search(r"kt::(k_\w+)", r["Kernel_Name"])
+        ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), m.group(1) if m else r["Kernel_Name"][:40]))
+    ks.sort()
+    g, end, prev = [], None, None
+    for s0, e0, nm in ks:
+        if end is not None and s0 > end:
+            g.append(((s0 - end) / 1e3, prev, nm))
+        if end is None or e0 > end:
+            end, prev = e0, nm
+    g.sort(reverse=True)
+    span = (max(e for _, e, _ in ks) - min(s for s, _, _ in ks)) / 1e3 if ks else 0.0
+    return {"span_us": round(span, 1), "idle_us": round(sum(x[0] for x in g), 1),
+            "idle_over_50us": round(sum(x[0] for x in g if x[0] > 50), 1),
+            "largest": [(round(a, 1), b, c) for a, b, c in g[:top]]}
+
+
 def main(path, out=None):
     d = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
@@ -27,6 +48,7 @@ def main(path, out=None):
                   "active_median_us": round(act[len(act) // 2], 2) if act else None,
                   "active_total_ms": round(sum(act) / 1e3, 2),
                   "noop": len(idle), "noop_mean_us": round(sum(idle) / len(idle), 2) if idle else None}
+    res["_gaps"] = gaps(path)
     print(json.dumps(res, indent=1))
     if out:
         json.dump(res, open(out, "w"), indent=1)
