@@ -470,9 +470,101 @@ __global__ void k_pair_eig(int C, int j, int it, int fun, double tol,
 
 // ---- one workgroup per candidate (2j <= 56): wave 0 solves the updated
 // projection T, wave 1 the plain one G, concurrently; both live in LDS ----
+// The xor butterfly v += v[lane ^ o], o = 32, 16, ..., 1, in every lane.
+// KT_WAVE_DPP=1 (default) moves the partners without the LDS crossbar
+// (__shfl_xor compiles to two ds_bpermute_b32 per double and step, ~400 of
+// them in k_pair_reg, each an LDS round trip): o = 32, 16 by gfx950's
+// v_permlane32/16_swap (the swap hands every lane its partner half: the sum
+// lo + hi is own + partner up to the order of the operands, which fp64
+// addition ignores), o = 8 by DPP row_ror:8 (= lane ^ 8 within a row of 16),
+// o = 4 by row_ror:4 (lane (i - 4) mod 16 holds the same value as lane i ^ 4
+// once the o = 8 step made lanes i and i ^ 8 equal), o = 2, 1 by quad_perm.
+// Every lane adds the same pairs as the shuffle form: bit-identical sums.
+// Wave-uniform control flow only (every call site: the DPP moves read the
+// other lanes' registers).
+#ifndef KT_WAVE_DPP
+#define KT_WAVE_DPP 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ double mov_dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <bool B32>
+__device__ __forceinline__ double swap_sum_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+    const auto rl = B32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                        : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = B32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                        : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const double x0 = __longlong_as_double(((long long)rh[0] << 32) | (unsigned int)rl[0]);
+    const double x1 = __longlong_as_double(((long long)rh[1] << 32) | (unsigned int)rl[1]);
+    return x0 + x1;
+}
+// min / max over the wave (exact and commutative: any pairing gives the
+// shuffle butterfly's value), same moves as wave_sum64
+template <bool MAX, bool B32>
+__device__ __forceinline__ double swap_mm_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+    const auto rl = B32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                        : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = B32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                        : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const double x0 = __longlong_as_double(((long long)rh[0] << 32) | (unsigned int)rl[0]);
+    const double x1 = __longlong_as_double(((long long)rh[1] << 32) | (unsigned int)rl[1]);
+    return MAX ? fmax(x0, x1) : fmin(x0, x1);
+}
+template <bool MAX>
+__device__ __forceinline__ double wave_minmax64(double v) {
+#if KT_WAVE_DPP
+    v = swap_mm_d<MAX, true>(v);
+    v = swap_mm_d<MAX, false>(v);
+    v = MAX ? fmax(v, mov_dpp_d<0x128>(v)) : fmin(v, mov_dpp_d<0x128>(v));
+    v = MAX ? fmax(v, mov_dpp_d<0x124>(v)) : fmin(v, mov_dpp_d<0x124>(v));
+    v = MAX ? fmax(v, mov_dpp_d<0x4E>(v)) : fmin(v, mov_dpp_d<0x4E>(v));
+    v = MAX ? fmax(v, mov_dpp_d<0xB1>(v)) : fmin(v, mov_dpp_d<0xB1>(v));
+#else
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = MAX ? fmax(v, __shfl_xor(v, o, 64)) : fmin(v, __shfl_xor(v, o, 64));
+#endif
+    return v;
+}
+// min over the aligned group of g lanes (g a power of two <= 64, wave-uniform)
+__device__ __forceinline__ int group_min_i(int v, int g) {
+#if KT_WAVE_DPP
+    if (g > 1) v = min(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));  // lane ^ 1
+    if (g > 2) v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));  // lane ^ 2
+    if (g > 4) v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false)); // 7 - i: the other quad
+    if (g > 8) v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false)); // 15 - i: the other 8
+    if (g > 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+        v = min((int)r[0], (int)r[1]);
+    }
+    if (g > 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+        v = min((int)r[0], (int)r[1]);
+    }
+#else
+    for (int o = 1; o < g; o <<= 1) v = min(v, __shfl_xor(v, o, 64));
+#endif
+    return v;
+}
 __device__ __forceinline__ double wave_sum64(double v) {
+#if KT_WAVE_DPP
+    v = swap_sum_d<true>(v);
+    v = swap_sum_d<false>(v);
+    v += mov_dpp_d<0x128>(v);  // row_ror:8
+    v += mov_dpp_d<0x124>(v);  // row_ror:4
+    v += mov_dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += mov_dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+#else
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+#endif
     return v;
 }
 
@@ -1144,9 +1236,9 @@ __device__ __forceinline__ void block_count_ms(int j, const Blk2* __restrict__ B
                                                double pivmin, double eps, int (&cnt)[MS],
                                                const double* m0 = nullptr) {
     double a[MS], b[MS], c[MS];
+    Blk2 cur = B[0];
     {
-        const Blk2 m = B[0];
-        const double ma = HAS_M0 ? m0[0] : m.a, mb = HAS_M0 ? m0[1] : m.b, mc = HAS_M0 ? m0[2] : m.c;
+        const double ma = HAS_M0 ? m0[0] : cur.a, mb = HAS_M0 ? m0[1] : cur.b, mc = HAS_M0 ? m0[2] : cur.c;
 #pragma unroll
         for (int s = 0; s < MS; ++s) {
             a[s] = ma - x[s];
@@ -1156,6 +1248,9 @@ __device__ __forceinline__ void block_count_ms(int j, const Blk2* __restrict__ B
         }
     }
     for (int k = 0;; ++k) {
+        // the next block's load issued ahead of this block's dependent chain
+        // (after the loop's exit test it would wait a whole LDS round trip)
+        const Blk2 nx = B[min(k + 1, j - 1)];
         double det[MS];
 #pragma unroll
         for (int s = 0; s < MS; ++s) {
@@ -1174,8 +1269,7 @@ __device__ __forceinline__ void block_count_ms(int j, const Blk2* __restrict__ B
             cnt[s] += det[s] < 0.0 ? 1 : (a[s] < 0.0 ? 2 : 0);
         }
         if (k + 1 >= j) break;
-        const Blk2 q = B[k];  // U_k
-        const Blk2 nx = B[k + 1];
+        const Blk2& q = cur;  // U_k
 #pragma unroll
         for (int s = 0; s < MS; ++s) {
             double r = __builtin_amdgcn_rcp(det[s]);
@@ -1191,6 +1285,7 @@ __device__ __forceinline__ void block_count_ms(int j, const Blk2* __restrict__ B
             b[s] = nx.b - s01;
             c[s] = nx.c - x[s] - s11;
         }
+        cur = nx;
     }
 }
 
@@ -1202,12 +1297,13 @@ template <bool HAS_M0 = false>
 __device__ __forceinline__ void block_count_newton(int j, const Blk2* __restrict__ B, double x,
                                                    double pivmin, double eps, int& cnt, double& S,
                                                    const double* m0 = nullptr) {
-    const Blk2 b0 = B[0];
-    double a = (HAS_M0 ? m0[0] : b0.a) - x, b = HAS_M0 ? m0[1] : b0.b, c = (HAS_M0 ? m0[2] : b0.c) - x;
+    Blk2 cur = B[0];
+    double a = (HAS_M0 ? m0[0] : cur.a) - x, b = HAS_M0 ? m0[1] : cur.b, c = (HAS_M0 ? m0[2] : cur.c) - x;
     double p = -1.0, q = 0.0, r = -1.0;  // D_k'
     cnt = 0;
     S = 0.0;
     for (int k = 0;; ++k) {
+        const Blk2 nx = B[min(k + 1, j - 1)];  // ahead of the chain (block_count_ms)
         double det = fma(a, c, -b * b);
         if (fabs(det) < pivmin) {  // as block_count_ms
             a -= eps;
@@ -1221,8 +1317,7 @@ __device__ __forceinline__ void block_count_newton(int j, const Blk2* __restrict
         const double i00 = c * rr, i01 = -b * rr, i11 = a * rr;
         S = fma(i00, p, fma(2.0 * i01, q, fma(i11, r, S)));
         if (k + 1 >= j) break;
-        const Blk2 u = B[k];
-        const Blk2 nx = B[k + 1];
+        const Blk2& u = cur;
         const double t00 = i00 * u.u0 + i01 * u.u2, t01 = i00 * u.u1 + i01 * u.u3;
         const double t10 = i01 * u.u0 + i11 * u.u2, t11 = i01 * u.u1 + i11 * u.u3;
         const double s00 = u.u0 * t00 + u.u2 * t10;
@@ -1236,6 +1331,7 @@ __device__ __forceinline__ void block_count_newton(int j, const Blk2* __restrict
         a = nx.a - x - s00;
         b = nx.b - s01;
         c = nx.c - x - s11;
+        cur = nx;
     }
 }
 
@@ -1314,12 +1410,9 @@ __device__ __forceinline__ double wave_multisect_blk(int j, const Blk2* B, int k
         hi = fmax(hi, d + off);
         smax = fmax(smax, fmax(fabs(d), off));
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        lo = fmin(lo, __shfl_xor(lo, o, 64));
-        hi = fmax(hi, __shfl_xor(hi, o, 64));
-        smax = fmax(smax, __shfl_xor(smax, o, 64));
-    }
+    lo = wave_minmax64<false>(lo);
+    hi = wave_minmax64<true>(hi);
+    smax = wave_minmax64<true>(smax);
     const double span = fmax(hi - lo, 1e-300);
     lo -= 2.2e-16 * span + 1e-300;
     hi += 2.2e-16 * span + 1e-300;
@@ -1347,8 +1440,7 @@ __device__ __forceinline__ double wave_multisect_blk(int j, const Blk2* B, int k
             for (int s2 = MS - 1; s2 >= 0; --s2)
                 if (cnt[s2] > k) mine = sub * MS + s2;
         }
-        int first = mine;  // group minimum (aligned butterfly)
-        for (int o = 1; o < g; o <<= 1) first = min(first, __shfl_xor(first, o, 64));
+        const int first = group_min_i(mine, g);  // group minimum
         if (!done) {
             const double na = first == 0 ? a : a + h * (double)first;
             const double nb = first == M ? b : fmin(b, a + h * (double)(first + 1));
@@ -1791,7 +1883,7 @@ __device__ __forceinline__ void reg_orth(int n, bool has_p, bool has_win, const 
 }
 
 // The register kernel's LDS (bytes, in this order; doubles first):
-//   X [n][2] (gather block C) | G blocks [it] Blk2
+//   X [n+1][2] (gather block C; row n = 0, the SpMM's unused slots) | G blocks [it] Blk2
 //   | ev [2][2 it] | (has_long) wl [kRegLongCap][2] | (csr >= 2) val [nnz]
 //   | (has_long) slot [n] int | (csr >= 1) rp [n+1] int, ci [nnz] u16
 struct RegLds {
@@ -1801,7 +1893,7 @@ __host__ __device__ inline RegLds reg_lds_layout(int n, int64_t nnz, int it, boo
     RegLds L;
     size_t o = 0;
     L.x = o;
-    o += sizeof(double) * 2 * (size_t)n;
+    o += sizeof(double) * 2 * ((size_t)n + 1);
     L.gblk = o;
     o += sizeof(Blk2) * (size_t)it;
     L.ev = o;
@@ -1863,6 +1955,11 @@ double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev
     return xm;
 }
 
+// KT_REG_ZROW=0: unused chunk slots repeat the row's last column (round 5)
+#ifndef KT_REG_ZROW
+#define KT_REG_ZROW 1
+#endif
+
 // One gathered row (2 doubles) of the LDS block X; the KT_REG_DIAG=1
 // diagnostic build replaces it by a register value (no gather; its results
 // are wrong by construction, only its clocks mean anything)
@@ -1907,6 +2004,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
     int* lrp = reinterpret_cast<int*>(base + L.rp);
     unsigned short* lci = reinterpret_cast<unsigned short*>(base + L.ci);
     double* lva = reinterpret_cast<double*>(base + L.va);
+    if (tid == 0) X[2 * n] = X[2 * n + 1] = 0.0;  // the zero row (SpMM's unused chunk slots)
     // the CSR (shared by every candidate, L2-resident) copied once into LDS
     if (CSR >= 1) {
         for (int t = tid; t <= n; t += kFusedThreads) lrp[t] = M.rp[t];
@@ -1968,18 +2066,29 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
             const int r = tid + q * kFusedThreads;
             Cv[q] = r < n ? *reinterpret_cast<const double2*>(X + 2 * r) : make_double2(0.0, 0.0);
             double s0 = 0.0, s1 = 0.0;
+#if defined(KT_REG_DIAG) && KT_REG_DIAG >= 2
+            if (false) {  // diagnostic: no row sums at all (the phase's fixed cost)
+#else
             if (r < n && (nl == 0 || slot[r] < 0)) {
+#endif
                 const int rb = rp[r], re = rp[r + 1];
                 // four nonzeros per round; the indices are clamped into the row
                 // (a masked weight drops the repeats) so that every load is
                 // unconditional: the four column reads issue together, then the
                 // four gathers -- predicated loads compiled to one branch and
-                // one LDS round trip EACH (the SpMM took ~13 us per Lanczos step)
+                // one LDS round trip EACH (the SpMM took ~13 us per Lanczos step).
+                // A slot past the row's end gathers the zero row n instead of
+                // repeating the last column: every such lane of the wave reads
+                // one address (an LDS broadcast, not one more random access
+                // in the instruction's bank conflicts); x + 1 * 0 = x + 0 * v.
                 if (M.unit) {
                     for (int k0 = rb; k0 < re; k0 += 4) {
                         int cc[4];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) cc[u] = col(min(k0 + u, re - 1));
+                        for (int u = 0; u < 4; ++u) {
+                            const int c0 = col(min(k0 + u, re - 1));
+                            cc[u] = (KT_REG_ZROW && k0 + u >= re) ? n : c0;
+                        }
                         double2 v[4];
 #pragma unroll
                         for (int u = 0; u < 4; ++u) v[u] = reg_gather(X, cc[u]);
@@ -1997,7 +2106,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
                             const int k = min(k0 + u, re - 1);
-                            cc[u] = col(k);
+                            const int c0 = col(k);
+                            cc[u] = (KT_REG_ZROW && k0 + u >= re) ? n : c0;
                             a[u] = va[k];
                         }
                         double2 v[4];
@@ -2232,6 +2342,19 @@ __global__ __launch_bounds__(1024) void k_greedy_edit(int C, const double* __res
     }
 }
 
+// Rows per thread of k_pair_reg: 2, 4, then exact from 6 (one row more costs
+// ~12 VGPRs: at R = 8 the kernel spills 6-18 VGPRs to scratch at 2 waves per
+// SIMD, R = 7 and below do not -- India, n = 3,228, takes R = 7).
+// KT_REG_R_POW2=1 builds the round-5 choice (2, 4, 8) for A/Bs.
+#ifndef KT_REG_R_POW2
+#define KT_REG_R_POW2 0
+#endif
+static int reg_rows(int n) {
+    const int rows = (n + kFusedThreads - 1) / kFusedThreads;
+    if (KT_REG_R_POW2) return rows <= 2 ? 2 : rows <= 4 ? 4 : 8;
+    return rows <= 2 ? 2 : rows <= 4 ? 4 : rows <= 6 ? 6 : rows;
+}
+
 bool pair_reg_applies(int n, int64_t nnz, int it, int n_long, bool unit) {
     const char* de = getenv("KT_PAIRS_DENSE_EIG");
     const char* rg = getenv("KT_PAIRS_REG");
@@ -2258,8 +2381,7 @@ hipError_t launch_pair_reg_dyn(int C, int n, int64_t nnz_max, const CsrView& A, 
             break;
         }
     const size_t lds = reg_lds_layout(n, nnz_max, it, has_long, csr).total;
-    const int rows = (n + kFusedThreads - 1) / kFusedThreads;
-    const int rr = rows <= 2 ? 2 : rows <= 4 ? 4 : 8;
+    const int rr = reg_rows(n);
 #define KT_REG_LAUNCH(RR, CC)                                                                                  \
     k_pair_reg<RR, CC><<<C, kFusedThreads, lds, st>>>(C, n, (int)nnz_max, M, ii, jj, B[0], B[1], B[2], B[3], it, \
                                                       fun, tol, state, dyn)
@@ -2269,6 +2391,8 @@ hipError_t launch_pair_reg_dyn(int C, int n, int64_t nnz_max, const CsrView& A, 
     else KT_REG_LAUNCH(RR, 2)
     if (rr == 2) { KT_REG_CSR(2); }
     else if (rr == 4) { KT_REG_CSR(4); }
+    else if (rr == 6) { KT_REG_CSR(6); }
+    else if (rr == 7) { KT_REG_CSR(7); }
     else { KT_REG_CSR(8); }
 #undef KT_REG_CSR
 #undef KT_REG_LAUNCH
@@ -2309,8 +2433,7 @@ hipError_t launch_pair_fused(int C, int n, int64_t nnz, const CsrView& A, bool u
                 break;
             }
         const size_t lds = reg_lds_layout(n, nnz, it, has_long, csr).total;
-        const int rows = (n + kFusedThreads - 1) / kFusedThreads;
-        const int rr = rows <= 2 ? 2 : rows <= 4 ? 4 : 8;
+        const int rr = reg_rows(n);
 #define KT_REG_LAUNCH(RR, CC)                                                                                  \
     k_pair_reg<RR, CC><<<C, kFusedThreads, lds, st>>>(C, n, (int)nnz, M, ii, jj, B[0], B[1], B[2], B[3], it, fun, \
                                                       tol, state)
@@ -2320,6 +2443,8 @@ hipError_t launch_pair_fused(int C, int n, int64_t nnz, const CsrView& A, bool u
     else KT_REG_LAUNCH(RR, 2)
         if (rr == 2) { KT_REG_CSR(2); }
         else if (rr == 4) { KT_REG_CSR(4); }
+        else if (rr == 6) { KT_REG_CSR(6); }
+        else if (rr == 7) { KT_REG_CSR(7); }
         else { KT_REG_CSR(8); }
 #undef KT_REG_CSR
 #undef KT_REG_LAUNCH

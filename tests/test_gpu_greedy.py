@@ -240,10 +240,11 @@ def test_pairs_fused_matches_batched(kra, gpu_ctx, monkeypatch, tol, it):
 
 
 def _reg_graphs(kra):
-    """Graphs for the register-resident kernel: India (8 rows per thread),
+    """Graphs for the register-resident kernel: India (7 rows per thread),
     a small slice (1 row per thread), a weighted scale-free graph with rows
-    longer than 64 (wave-per-row SpMM), and a dense random graph with more long
-    rows than the kernel's wave list holds (the rest go to their owners)."""
+    longer than 64 (wave-per-row SpMM; 6 rows per thread), a dense random graph
+    with more long rows than the kernel's wave list holds (the rest go to their
+    owners), and a unit scale-free graph at 8 rows per thread."""
     from krylov_robustness_amd import graphs
     india = load_graph("india")
     small = india[:400, :400].tocsr()
@@ -258,10 +259,13 @@ def _reg_graphs(kra):
     R = sp.triu(R, 1)
     R.data[:] = 1.0
     dense = (R + R.T).tocsr()
-    return {"india": india, "small": small, "hub": hub, "dense": dense}
+    B = sp.triu(graphs.chung_lu(4000, 14000, seed=5), 1)
+    B.data[:] = 1.0
+    big = (B + B.T).tocsr()
+    return {"india": india, "small": small, "hub": hub, "dense": dense, "big": big}
 
 
-@pytest.mark.parametrize("name", ["india", "small", "hub", "dense"])
+@pytest.mark.parametrize("name", ["india", "small", "hub", "dense", "big"])
 def test_pairs_register_kernel_matches_fused(kra, gpu_ctx, monkeypatch, name):
     """k_pair_reg (each thread owns its rows of the window and the new block in
     registers, gathers from LDS) forms every sum in k_pair_fused's order; the
