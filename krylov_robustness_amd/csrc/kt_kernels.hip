@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kt_launch.h"
+#include "kt_wave.h"
 #include <stdint.h>
 
 #include <cstdlib>
@@ -425,7 +426,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
-                for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
+                for (int e = 0; e < G::VEC; ++e) s[e] += kt::shfl_xor(s[e], o);
             if (grp == 0) row_epilogue<P, FLAGS, G>(row, p0, s, sc, ucur, y, acc);
         }
     } else {
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_dot(
 #pragma unroll
     for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
-        for (int e = 0; e < G::VEC; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
+        for (int e = 0; e < G::VEC; ++e) acc[e] += kt::shfl_xor(acc[e], o);
     __shared__ double red[WAVES][P];
     if (grp == 0) {
 #pragma unroll
@@ -693,7 +694,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos_start(
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
-                for (int e = 0; e < G::VEC; ++e) sm[e] += __shfl_xor(sm[e], o, 64);
+                for (int e = 0; e < G::VEC; ++e) sm[e] += kt::shfl_xor(sm[e], o);
             if (grp == 0) epilogue(row, sm);
         }
     } else {
@@ -714,9 +715,9 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_lanczos_start(
     for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
         for (int e = 0; e < G::VEC; ++e) {
-            d0[e] += __shfl_xor(d0[e], o, 64);
-            d1[e] += __shfl_xor(d1[e], o, 64);
-            d2[e] += __shfl_xor(d2[e], o, 64);
+            d0[e] += kt::shfl_xor(d0[e], o);
+            d1[e] += kt::shfl_xor(d1[e], o);
+            d2[e] += kt::shfl_xor(d2[e], o);
         }
     __shared__ double red[WAVES][3][P];
     if (grp == 0) {
@@ -805,7 +806,7 @@ __global__ KT_KY_BOUNDS(BLOCK) void k_spmm_lanczos(
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
-                for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
+                for (int e = 0; e < G::VEC; ++e) s[e] += kt::shfl_xor(s[e], o);
             if (grp == 0)
                 row_epilogue_y<P, FLAGS, G, decltype(cg)>(row, p0, s, cg, ca, cb, has_old, X, Yold, Out, d0, d1, d2,
                                            orsrc, Vc, Vo, Vn, bcols);
@@ -832,9 +833,9 @@ __global__ KT_KY_BOUNDS(BLOCK) void k_spmm_lanczos(
     for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
         for (int e = 0; e < G::VEC; ++e) {
-            d0[e] += __shfl_xor(d0[e], o, 64);
-            d1[e] += __shfl_xor(d1[e], o, 64);
-            d2[e] += __shfl_xor(d2[e], o, 64);
+            d0[e] += kt::shfl_xor(d0[e], o);
+            d1[e] += kt::shfl_xor(d1[e], o);
+            d2[e] += kt::shfl_xor(d2[e], o);
         }
     __shared__ double red[WAVES][3][P];
     if (grp == 0) {
@@ -894,7 +895,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_block(
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
-                for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
+                for (int e = 0; e < G::VEC; ++e) s[e] += kt::shfl_xor(s[e], o);
             if (grp == 0) {
 #pragma unroll
                 for (int e = 0; e < G::VEC; ++e) part[(int64_t)ci * P + p0 + e] = s[e];
@@ -913,7 +914,7 @@ __global__ __launch_bounds__(BLOCK) void k_spmm_block(
 #pragma unroll
             for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
-                for (int e = 0; e < G::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
+                for (int e = 0; e < G::VEC; ++e) s[e] += kt::shfl_xor(s[e], o);
             if (grp == 0) {
                 typename V::T yo;
                 double* yp = reinterpret_cast<double*>(&yo);
@@ -1001,7 +1002,7 @@ __device__ __forceinline__ double wave_reduce_slot(const double* __restrict__ pa
         for (int i = 0; i < kReduceDepth; ++i) v += x[i];
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    for (int o = 32; o > 0; o >>= 1) v += kt::shfl_xor(v, o);
     return v;
 }
 
@@ -1104,9 +1105,9 @@ __global__ __launch_bounds__(BLOCK) void k_update(
     for (int o = G::LPR; o < 64; o <<= 1)
 #pragma unroll
         for (int e = 0; e < G::VEC; ++e) {
-            nn[e] += __shfl_xor(nn[e], o, 64);
-            yu[e] += __shfl_xor(yu[e], o, 64);
-            cu[e] += __shfl_xor(cu[e], o, 64);
+            nn[e] += kt::shfl_xor(nn[e], o);
+            yu[e] += kt::shfl_xor(yu[e], o);
+            cu[e] += kt::shfl_xor(cu[e], o);
         }
     __shared__ double red[WAVES][3][P];
     if (grp == 0) {
@@ -1256,7 +1257,7 @@ __global__ __launch_bounds__(256) void k_inf_norm(int n, int nc, const double* _
         for (int c = 0; c < nc; ++c) s += fabs(X[(int64_t)r * ldx + c]);
         mx = fmax(mx, s);
     }
-    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, kt::shfl_xor(mx, o));
     __shared__ double red[4];
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
     __syncthreads();
@@ -1280,8 +1281,8 @@ __global__ __launch_bounds__(256) void k_normest1_y(int n, const double* __restr
         S[r] = s;
     }
     for (int o = 32; o > 0; o >>= 1) {
-        a += __shfl_xor(a, o, 64);
-        d += __shfl_xor(d, o, 64);
+        a += kt::shfl_xor(a, o);
+        d += kt::shfl_xor(d, o);
     }
     __shared__ double red[2][4];
     if ((threadIdx.x & 63) == 0) {
@@ -1309,7 +1310,7 @@ __global__ __launch_bounds__(256) void k_absmax_idx(int n, const double* __restr
     int i = 0x7fffffff;
     for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x)
         absmax_merge(v, i, fabs(Z[r]), r);
-    for (int o = 32; o > 0; o >>= 1) absmax_merge(v, i, __shfl_xor(v, o, 64), __shfl_xor(i, o, 64));
+    for (int o = 32; o > 0; o >>= 1) absmax_merge(v, i, kt::shfl_xor(v, o), kt::shfl_xor(i, o));
     __shared__ double sv[4];
     __shared__ int si[4];
     if ((threadIdx.x & 63) == 0) {
@@ -1387,7 +1388,7 @@ __global__ __launch_bounds__(256) void k_expmv_begin(const double* __restrict__ 
                                                      ExpmvState* st) {
     double mx = 0.0;
     for (int i = threadIdx.x; i < nb; i += blockDim.x) mx = fmax(mx, partial[i]);
-    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, kt::shfl_xor(mx, o));
     __shared__ double red[4];
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
     __syncthreads();
@@ -1428,8 +1429,8 @@ __global__ __launch_bounds__(256) void k_expmv_term(int n, int nc, double mu, do
         mf = fmax(mf, sf);
     }
     for (int o = 32; o > 0; o >>= 1) {
-        mb = fmax(mb, __shfl_xor(mb, o, 64));
-        mf = fmax(mf, __shfl_xor(mf, o, 64));
+        mb = fmax(mb, kt::shfl_xor(mb, o));
+        mf = fmax(mf, kt::shfl_xor(mf, o));
     }
     __shared__ double red[2][4];
     if ((threadIdx.x & 63) == 0) {
@@ -1600,7 +1601,7 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
 #pragma unroll
         for (int o = GL::LPR; o < 64; o <<= 1)
 #pragma unroll
-            for (int e = 0; e < GL::VEC; ++e) sl[e] += __shfl_xor(sl[e], o, 64);
+            for (int e = 0; e < GL::VEC; ++e) sl[e] += kt::shfl_xor(sl[e], o);
     }
     if (kind == 2 && grpL == 0)
 #pragma unroll
@@ -1610,7 +1611,7 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
     if (wave == 0) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long xb = __shfl_xor(pmb, o, 64), xf = __shfl_xor(pmf, o, 64);
+            const unsigned long long xb = kt::shfl_xor(pmb, o), xf = kt::shfl_xor(pmf, o);
             pmb = xb > pmb ? xb : pmb;
             pmf = xf > pmf ? xf : pmf;
         }
@@ -1651,8 +1652,8 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
         }
 #pragma unroll
         for (int o = 1; o < G::LPR; o <<= 1) {
-            sb += __shfl_xor(sb, o, 64);
-            sf += __shfl_xor(sf, o, 64);
+            sb += kt::shfl_xor(sb, o);
+            sf += kt::shfl_xor(sf, o);
         }
     } else {
         if (kind == 2 && wave == 0 && grpL == 0) {
@@ -1672,15 +1673,15 @@ __global__ __launch_bounds__(64 * kExpmvWaves) void k_expmv_step(
         }
 #pragma unroll
         for (int o = 1; o < GL::LPR; o <<= 1) {
-            sb += __shfl_xor(sb, o, 64);
-            sf += __shfl_xor(sf, o, 64);
+            sb += kt::shfl_xor(sb, o);
+            sf += kt::shfl_xor(sf, o);
         }
     }
     double mb = sb, mf = sf;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        mb = fmax(mb, __shfl_xor(mb, o, 64));
-        mf = fmax(mf, __shfl_xor(mf, o, 64));
+        mb = fmax(mb, kt::shfl_xor(mb, o));
+        mf = fmax(mf, kt::shfl_xor(mf, o));
     }
     if (lane == 0) {
         red[0][wave] = mb;
@@ -1767,7 +1768,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
             unsigned long long pmb = st->term_max[(k - 1) % 3][lane][0], pmf = st->term_max[(k - 1) % 3][lane][1];
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
-                const unsigned long long xb = __shfl_xor(pmb, o, 64), xf = __shfl_xor(pmf, o, 64);
+                const unsigned long long xb = kt::shfl_xor(pmb, o), xf = kt::shfl_xor(pmf, o);
                 pmb = xb > pmb ? xb : pmb;
                 pmf = xf > pmf ? xf : pmf;
             }
@@ -1802,8 +1803,8 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
     double mb = 0.0, mf = 0.0;  // running maxima of this lane's row sums
     auto fold = [&](double sb, double sf, int lpr) {
         for (int o = 1; o < lpr; o <<= 1) {
-            sb += __shfl_xor(sb, o, 64);
-            sf += __shfl_xor(sf, o, 64);
+            sb += kt::shfl_xor(sb, o);
+            sf += kt::shfl_xor(sf, o);
         }
         mb = fmax(mb, sb);
         mf = fmax(mf, sf);
@@ -1824,7 +1825,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
 #pragma unroll
         for (int o = GL::LPR; o < 64; o <<= 1)
 #pragma unroll
-            for (int e = 0; e < GL::VEC; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
+            for (int e = 0; e < GL::VEC; ++e) acc[e] += kt::shfl_xor(acc[e], o);
         if (grpL == 0)
 #pragma unroll
             for (int e = 0; e < GL::VEC; ++e) lsum[wave][p0L + e] = acc[e];
@@ -1862,7 +1863,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
 #pragma unroll
             for (int o = GL::LPR; o < 64; o <<= 1)
 #pragma unroll
-                for (int e = 0; e < GL::VEC; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
+                for (int e = 0; e < GL::VEC; ++e) acc[e] += kt::shfl_xor(acc[e], o);
 #pragma unroll
             for (int e = 0; e < GL::VEC; ++e) s[e] = w == 0 ? acc[e] : s[e] + acc[e];
         }
@@ -1949,7 +1950,7 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
 #pragma unroll
             for (int o = GL::LPR; o < 64; o <<= 1)
 #pragma unroll
-                for (int e = 0; e < GL::VEC; ++e) s[e] += __shfl_xor(s[e], o, 64);
+                for (int e = 0; e < GL::VEC; ++e) s[e] += kt::shfl_xor(s[e], o);
             double sb = 0.0, sf = 0.0;
             if (grpL == 0) {
                 double fo[GL::VEC], bo[GL::VEC];
@@ -2079,8 +2080,8 @@ __global__ __launch_bounds__(64 * kExpmvRowsWaves) void k_expmv_rows(
     // (4) this workgroup's maxima into slot blockIdx % 64 of set k % 3
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        mb = fmax(mb, __shfl_xor(mb, o, 64));
-        mf = fmax(mf, __shfl_xor(mf, o, 64));
+        mb = fmax(mb, kt::shfl_xor(mb, o));
+        mf = fmax(mf, kt::shfl_xor(mf, o));
     }
     if (lane == 0) {
         red[0][wave] = mb;
@@ -2115,7 +2116,7 @@ __global__ __launch_bounds__(64) void k_expmv_slot_check(ExpmvState* st, int k, 
     unsigned long long mb = st->term_max[k % 3][lane][0], mf = st->term_max[k % 3][lane][1];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long xb = __shfl_xor(mb, o, 64), xf = __shfl_xor(mf, o, 64);
+        const unsigned long long xb = kt::shfl_xor(mb, o), xf = kt::shfl_xor(mf, o);
         mb = xb > mb ? xb : mb;
         mf = xf > mf ? xf : mf;
     }
@@ -2140,8 +2141,8 @@ __global__ __launch_bounds__(256) void k_expmv_check(const double* __restrict__ 
         mf = fmax(mf, partial[nb + i]);
     }
     for (int o = 32; o > 0; o >>= 1) {
-        mb = fmax(mb, __shfl_xor(mb, o, 64));
-        mf = fmax(mf, __shfl_xor(mf, o, 64));
+        mb = fmax(mb, kt::shfl_xor(mb, o));
+        mf = fmax(mf, kt::shfl_xor(mf, o));
     }
     __shared__ double red[2][4];
     if ((threadIdx.x & 63) == 0) {
