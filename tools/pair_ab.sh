@@ -5,12 +5,12 @@
 # library); each is timed by tests/perf/bench_greedy.py twice, interleaved.
 # PROF names are -DKT_FUSED_PROF builds: their per-phase device clocks
 # (one reg_prof line per launch of tools/pair_prof.py) go to PROF.log.  The greedy / pair tests run
-# first on the in-tree library.
+# first on the in-tree library (NOTEST=1: timing only).
 set -o pipefail
 TAG=$1; NAMES=$2; PROFS=$3
 O=$PWD/gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_greedy.py tests/test_gpu_configs.py -k "greedy or pairs" \
+[ -n "$NOTEST" ] || timeout -k 10 600 python -u -m pytest tests/test_gpu_greedy.py tests/test_gpu_configs.py -k "greedy or pairs" \
     -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 lib() { [ "$1" = lib ] && echo "$PWD/krylov_robustness_amd/libkrylov_hip.so" || echo "$PWD/var/$1/libkrylov_hip.so"; }
