@@ -1886,14 +1886,18 @@ __device__ __forceinline__ void reg_orth(int n, bool has_p, bool has_win, const 
 //   X [n+1][2] (gather block C; row n = 0, the SpMM's unused slots) | G blocks [it] Blk2
 //   | ev [2][2 it] | (has_long) wl [kRegLongCap][2] | (csr >= 2) val [nnz]
 //   | (has_long) slot [n] int | (csr >= 1) rp [n+1] int, ci [nnz] u16
+//   (spec: ws [n][2], the next step's row sums formed during the eigenvalues)
 struct RegLds {
-    size_t x, gblk, ev, wl, va, slot, rp, ci, total;
+    size_t x, ws, gblk, ev, wl, va, slot, rp, ci, total;
 };
-__host__ __device__ inline RegLds reg_lds_layout(int n, int64_t nnz, int it, bool has_long, int csr) {
+__host__ __device__ inline RegLds reg_lds_layout(int n, int64_t nnz, int it, bool has_long, int csr,
+                                                 bool spec = false) {
     RegLds L;
     size_t o = 0;
     L.x = o;
     o += sizeof(double) * 2 * ((size_t)n + 1);
+    L.ws = o;
+    if (spec) o += sizeof(double) * 2 * (size_t)n;
     L.gblk = o;
     o += sizeof(Blk2) * (size_t)it;
     L.ev = o;
@@ -1955,6 +1959,11 @@ double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev
     return xm;
 }
 
+// KT_REG_SPEC=0: no row sums formed ahead during the eigenvalues (round 5)
+#ifndef KT_REG_SPEC
+#define KT_REG_SPEC 1
+#endif
+
 // KT_REG_ZROW=0: unused chunk slots repeat the row's last column (round 5)
 #ifndef KT_REG_ZROW
 #define KT_REG_ZROW 1
@@ -1981,7 +1990,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
                                                             double b00, double b10, double b01, double b11,
                                                             int it, int fun, double tol,
                                                             double* __restrict__ state,
-                                                            const int* __restrict__ dyn = nullptr) {
+                                                            const int* __restrict__ dyn = nullptr,
+                                                            int spec = 0) {
     extern __shared__ double sm[];
     __shared__ double red[2 * kFusedWaves * 8];
     __shared__ double bc[4];
@@ -1994,7 +2004,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
     // first step's (larger) matrix
     const int nnz = dyn ? dyn[0] : nnz_host;
     const int nl = min(dyn ? dyn[1] : M.n_long, kRegLongCap);
-    const RegLds L = reg_lds_layout(n, nnz, it, nl > 0, CSR);
+    const RegLds L = reg_lds_layout(n, nnz, it, nl > 0, CSR, spec != 0);
     char* base = reinterpret_cast<char*>(sm);
     double* X = reinterpret_cast<double*>(base + L.x);
     Blk2* gblk = reinterpret_cast<Blk2*>(base + L.gblk);
@@ -2004,6 +2014,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
     int* lrp = reinterpret_cast<int*>(base + L.rp);
     unsigned short* lci = reinterpret_cast<unsigned short*>(base + L.ci);
     double* lva = reinterpret_cast<double*>(base + L.va);
+    double* ws = reinterpret_cast<double*>(base + L.ws);
     if (tid == 0) X[2 * n] = X[2 * n + 1] = 0.0;  // the zero row (SpMM's unused chunk slots)
     // the CSR (shared by every candidate, L2-resident) copied once into LDS
     if (CSR >= 1) {
@@ -2059,7 +2070,65 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
     FPROF(0);
     double x0 = 0.0, x1 = 0.0, xm = 0.0;
     int iter = it, lucky = 0;
+    // one row's sum of W = A C, in CSR order (the owners' loop below, for the
+    // rows waves 4-7 sum ahead into ws)
+    auto row_sum = [&](int r, double& s0, double& s1) {
+        const int rb = rp[r], re = rp[r + 1];
+        if (M.unit) {
+            for (int k0 = rb; k0 < re; k0 += 4) {
+                int cc[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int c0 = col(min(k0 + u, re - 1));
+                    cc[u] = (KT_REG_ZROW && k0 + u >= re) ? n : c0;
+                }
+                double2 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = reg_gather(X, cc[u]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double a = (k0 + u < re) ? 1.0 : 0.0;
+                    s0 = fma(a, v[u].x, s0);
+                    s1 = fma(a, v[u].y, s1);
+                }
+            }
+        } else {
+            for (int k0 = rb; k0 < re; k0 += 4) {
+                int cc[4];
+                double a[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = min(k0 + u, re - 1);
+                    const int c0 = col(k);
+                    cc[u] = (KT_REG_ZROW && k0 + u >= re) ? n : c0;
+                    a[u] = va[k];
+                }
+                double2 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = reg_gather(X, cc[u]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const double w = (k0 + u < re) ? a[u] : 0.0;
+                    s0 = fma(w, v[u].x, s0);
+                    s1 = fma(w, v[u].y, s1);
+                }
+            }
+        }
+    };
+    bool have_spec = false;  // this step's W = A C already in ws / wl (formed by waves 4-7)
     for (int j = 1; j <= it; ++j) {
+        if (have_spec) {
+            // the sums waves 4-7 formed during the previous step's eigenvalues
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                const int r = tid + q * kFusedThreads;
+                Cv[q] = r < n ? *reinterpret_cast<const double2*>(X + 2 * r) : make_double2(0.0, 0.0);
+                const int ls = (nl > 0 && r < n) ? slot[r] : -1;
+                W[q] = r >= n ? make_double2(0.0, 0.0)
+                     : ls >= 0 ? make_double2(wl[2 * ls], wl[2 * ls + 1])
+                               : *reinterpret_cast<const double2*>(ws + 2 * r);
+            }
+        } else {
         // W = A C   (lanczos_krylov.m:81): short rows by their owner, gathers from LDS
 #pragma unroll
         for (int q = 0; q < R; ++q) {
@@ -2151,6 +2220,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
                 if (ls >= 0) W[q] = make_double2(wl[2 * ls], wl[2 * ls + 1]);
             }
         }
+        }  // !have_spec
         FPROF(1);
         // X is overwritten by Q in sweep E: every SpMM read is behind the sweeps' barriers
         reg_orth<R>(n, j > 1, true, P, Cv, W, X, red, bc, par, o);
@@ -2187,10 +2257,46 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
         }
         __syncthreads();  // X = V_{j+1}, blocks of step j visible
         FPROF(6);
+        // While waves 0-3 solve step j's eigenvalues (xm_waves: <= 2 waves per
+        // projection up to 2j = 32), waves 4-7 would wait at its barrier: they
+        // form step j+1's W = A C meanwhile (X = V_{j+1} is final), every row
+        // by row_sum in CSR order -- the owners' sums, bit for bit -- into ws
+        // and wl.  If step j stops, the sums are simply not used.
+        have_spec = spec && j < it && 2 * xm_waves(2 * j) <= kFusedWaves / 2;
+        if (have_spec && wave >= kFusedWaves / 2) {
+            const int t2 = tid - kFusedThreads / 2;
+#pragma unroll 1
+            for (int r = t2; r < n; r += kFusedThreads / 2) {
+                if (nl == 0 || slot[r] < 0) {
+                    double s0 = 0.0, s1 = 0.0;
+                    row_sum(r, s0, s1);
+                    *reinterpret_cast<double2*>(ws + 2 * r) = make_double2(s0, s1);
+                }
+            }
+            for (int li = wave - kFusedWaves / 2; li < nl; li += kFusedWaves / 2) {
+                const int r = M.long_rows[li];
+                const int b = rp[r], e = rp[r + 1];
+                double s0 = 0.0, s1 = 0.0;
+                for (int k = b + lane; k < e; k += 64) {
+                    const int cc = col(k);
+                    const double a = M.unit ? 1.0 : va[k];
+                    const double2 v = *reinterpret_cast<const double2*>(X + 2 * cc);
+                    s0 = fma(a, v.x, s0);
+                    s1 = fma(a, v.y, s1);
+                }
+                s0 = wave_sum64(s0);
+                s1 = wave_sum64(s1);
+                if (lane == 0) {
+                    wl[2 * li] = s0;
+                    wl[2 * li + 1] = s1;
+                }
+            }
+        }
 #ifdef KT_FUSED_NOEIG
+        __syncthreads();
         xm = (double)j;
 #else
-        xm = reg_xm_blk(j, fun, gblk, t0, ev);
+        xm = reg_xm_blk(j, fun, gblk, t0, ev);  // its first barrier: ws / wl complete
 #endif
         FPROF(7);
         lucky = sqrt(o.beta1 * o.beta1 + o.r12 * o.r12 + o.beta2 * o.beta2) < 1e-8;  // :91-93
@@ -2215,8 +2321,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
     }
 #ifdef KT_FUSED_PROF
     if (c == 0 && tid == 0)
-        printf("reg_prof n=%d it=%d iter=%d start=%llu spmm=%llu A=%llu B=%llu C=%llu D=%llu E=%llu eig=%llu stop=%llu (x10ns) shader_MHz=%.0f\n",
-               n, it, iter, g_fprof[0], g_fprof[1], g_fprof[2], g_fprof[3], g_fprof[4], g_fprof[5], g_fprof[6],
+        printf("reg_prof spec=%d lds=%d n=%d it=%d iter=%d start=%llu spmm=%llu A=%llu B=%llu C=%llu D=%llu E=%llu eig=%llu stop=%llu (x10ns) shader_MHz=%.0f\n",
+               spec, (int)L.total, n, it, iter, g_fprof[0], g_fprof[1], g_fprof[2], g_fprof[3], g_fprof[4], g_fprof[5], g_fprof[6],
                g_fprof[7], g_fprof[8], 100.0 * (double)(clock64() - clk0) / (double)(wall_clock64() - wclk0));
 #endif
     if (tid == 0) {
@@ -2355,6 +2461,19 @@ static int reg_rows(int n) {
     return rows <= 2 ? 2 : rows <= 4 ? 4 : rows <= 6 ? 6 : rows;
 }
 
+// Whether k_pair_reg forms the next step's row sums during the eigenvalues
+// (spec: one more n x 2 LDS block); the weights leave the LDS for it (csr 2
+// -> 1: read from global memory, L2-resident) when both do not fit.
+static int reg_spec_fits(int n, int64_t nnz, int it, bool has_long, int& csr, size_t lds_max) {
+    if (!KT_REG_SPEC) return 0;
+    if (reg_lds_layout(n, nnz, it, has_long, csr, true).total <= lds_max) return 1;
+    if (csr == 2 && reg_lds_layout(n, nnz, it, has_long, 1, true).total <= lds_max) {
+        csr = 1;
+        return 1;
+    }
+    return 0;
+}
+
 bool pair_reg_applies(int n, int64_t nnz, int it, int n_long, bool unit) {
     const char* de = getenv("KT_PAIRS_DENSE_EIG");
     const char* rg = getenv("KT_PAIRS_REG");
@@ -2380,11 +2499,12 @@ hipError_t launch_pair_reg_dyn(int C, int n, int64_t nnz_max, const CsrView& A, 
             csr = cand;
             break;
         }
-    const size_t lds = reg_lds_layout(n, nnz_max, it, has_long, csr).total;
+    const int spec = reg_spec_fits(n, nnz_max, it, has_long, csr, kLdsMax);
+    const size_t lds = reg_lds_layout(n, nnz_max, it, has_long, csr, spec).total;
     const int rr = reg_rows(n);
 #define KT_REG_LAUNCH(RR, CC)                                                                                  \
     k_pair_reg<RR, CC><<<C, kFusedThreads, lds, st>>>(C, n, (int)nnz_max, M, ii, jj, B[0], B[1], B[2], B[3], it, \
-                                                      fun, tol, state, dyn)
+                                                      fun, tol, state, dyn, spec)
 #define KT_REG_CSR(RR)                       \
     if (csr == 0) KT_REG_LAUNCH(RR, 0);      \
     else if (csr == 1) KT_REG_LAUNCH(RR, 1); \
@@ -2432,11 +2552,12 @@ hipError_t launch_pair_fused(int C, int n, int64_t nnz, const CsrView& A, bool u
                 csr = cand;
                 break;
             }
-        const size_t lds = reg_lds_layout(n, nnz, it, has_long, csr).total;
+        const int spec = reg_spec_fits(n, nnz, it, has_long, csr, kLdsMax);
+        const size_t lds = reg_lds_layout(n, nnz, it, has_long, csr, spec).total;
         const int rr = reg_rows(n);
 #define KT_REG_LAUNCH(RR, CC)                                                                                  \
     k_pair_reg<RR, CC><<<C, kFusedThreads, lds, st>>>(C, n, (int)nnz, M, ii, jj, B[0], B[1], B[2], B[3], it, fun, \
-                                                      tol, state)
+                                                      tol, state, nullptr, spec)
 #define KT_REG_CSR(RR)                       \
     if (csr == 0) KT_REG_LAUNCH(RR, 0);      \
     else if (csr == 1) KT_REG_LAUNCH(RR, 1); \
