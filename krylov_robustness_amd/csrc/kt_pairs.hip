@@ -1924,12 +1924,18 @@ __host__ __device__ inline RegLds reg_lds_layout(int n, int64_t nnz, int it, boo
 #ifndef KT_REG_XM_INLINE
 #define KT_REG_XM_INLINE 1
 #endif
+// help(): called by every wave once its share of the eigenvalues is done,
+// before the phase's first barrier (k_pair_reg: the next step's row sums)
+struct NoHelp {
+    __device__ void operator()() const {}
+};
+template <class Help = NoHelp>
 #if KT_REG_XM_INLINE
 __device__ __forceinline__
 #else
 __device__ __noinline__
 #endif
-double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev) {
+double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev, const Help& help = Help()) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nn = 2 * j;
     const int W = xm_waves(nn);  // waves per projection; the rest wait at the barrier
@@ -1944,6 +1950,7 @@ double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev
         const int g = group_lanes(cnt);
         if (lane % g == 0 && lane / g < cnt) ev[mat * nn + k0 + e0 + lane / g] = lam;
     }
+    help();
     __syncthreads();
     double term = 0.0;  // trace_fun_update.m:85-89 (k-th smallest of each)
     if (wave == 0)
@@ -1962,6 +1969,11 @@ double reg_xm_blk(int j, int fun, const Blk2* gblk, const double* t0, double* ev
 // KT_REG_SPEC=0: no row sums formed ahead during the eigenvalues (round 5)
 #ifndef KT_REG_SPEC
 #define KT_REG_SPEC 1
+#endif
+
+// KT_REG_SPEC_DYN=0: only waves 4-7 form the rows ahead (static stride)
+#ifndef KT_REG_SPEC_DYN
+#define KT_REG_SPEC_DYN 1
 #endif
 
 // KT_REG_ZROW=0: unused chunk slots repeat the row's last column (round 5)
@@ -1998,6 +2010,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
     __shared__ double t0[3];     // T's first diagonal block (a, b, c): G's + Cm
     __shared__ double cm[4];     // Cm = R B R' (column-major)
     __shared__ double lastr[3];  // the previous record's R (beta1, r12, beta2)
+    __shared__ int s_spec_next;  // the next block of 64 rows to sum ahead (spec)
     const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // dyn (device-resident greedy loop): {nnz, n_long} of the current CSR,
     // written by the previous step's k_greedy_edit; the LDS was sized for the
@@ -2255,6 +2268,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
             lastr[1] = h[9];
             lastr[2] = h[10];
         }
+        if (tid == 0) s_spec_next = 0;
         __syncthreads();  // X = V_{j+1}, blocks of step j visible
         FPROF(6);
         // While waves 0-3 solve step j's eigenvalues (xm_waves: <= 2 waves per
@@ -2263,14 +2277,33 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
         // by row_sum in CSR order -- the owners' sums, bit for bit -- into ws
         // and wl.  If step j stops, the sums are simply not used.
         have_spec = spec && j < it && 2 * xm_waves(2 * j) <= kFusedWaves / 2;
-        if (have_spec && wave >= kFusedWaves / 2) {
-            const int t2 = tid - kFusedThreads / 2;
-#pragma unroll 1
-            for (int r = t2; r < n; r += kFusedThreads / 2) {
-                if (nl == 0 || slot[r] < 0) {
+        // the short rows in blocks of 64 taken from an LDS counter: waves 4-7
+        // start at once, waves 0-3 join as their eigenvalues finish (help())
+        auto spec_rows = [&]() {
+            if (!have_spec || !KT_REG_SPEC_DYN) return;
+            for (;;) {
+                int cb = 0;
+                if (lane == 0) cb = atomicAdd(&s_spec_next, 1);
+                cb = __builtin_amdgcn_readfirstlane(cb);
+                if (cb * 64 >= n) break;
+                const int r = cb * 64 + lane;
+                if (r < n && (nl == 0 || slot[r] < 0)) {
                     double s0 = 0.0, s1 = 0.0;
                     row_sum(r, s0, s1);
                     *reinterpret_cast<double2*>(ws + 2 * r) = make_double2(s0, s1);
+                }
+            }
+        };
+        if (have_spec && wave >= kFusedWaves / 2) {
+            if (!KT_REG_SPEC_DYN) {  // round-6 first form: waves 4-7 alone, rows strided
+                const int t2 = tid - kFusedThreads / 2;
+#pragma unroll 1
+                for (int r = t2; r < n; r += kFusedThreads / 2) {
+                    if (nl == 0 || slot[r] < 0) {
+                        double s0 = 0.0, s1 = 0.0;
+                        row_sum(r, s0, s1);
+                        *reinterpret_cast<double2*>(ws + 2 * r) = make_double2(s0, s1);
+                    }
                 }
             }
             for (int li = wave - kFusedWaves / 2; li < nl; li += kFusedWaves / 2) {
@@ -2293,10 +2326,11 @@ __global__ __launch_bounds__(kFusedThreads) void k_pair_reg(int C, int n, int nn
             }
         }
 #ifdef KT_FUSED_NOEIG
+        spec_rows();
         __syncthreads();
         xm = (double)j;
 #else
-        xm = reg_xm_blk(j, fun, gblk, t0, ev);  // its first barrier: ws / wl complete
+        xm = reg_xm_blk(j, fun, gblk, t0, ev, spec_rows);  // its first barrier: ws / wl complete
 #endif
         FPROF(7);
         lucky = sqrt(o.beta1 * o.beta1 + o.r12 * o.r12 + o.beta2 * o.beta2) < 1e-8;  // :91-93
